@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py -- fp64 CG iterations/s on MI355X, with the SpMV roofline and the
+CPU baseline beside it (BASELINE.json metric).
+
+A "step" is one CG iteration of the device-resident solver (SpMV + dot
+products + vector updates) on a synthetic SPD system already resident in
+HBM.  Default workload (N = 1): C3, the 7-point 3-D Laplacian 216^3
+(10,077,696 rows, 70,263,936 nnz, fp64, b = 1) -- BASELINE.json's HBM
+roofline configuration.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c5]
+
+N > 1 is launched by torch.distributed.run (one process per GPU); each rank
+owns a 216^3-row slab of a 216 x 216 x (216 N) Laplacian (weak scaling), the
+solver exchanges halo planes and all-reduces its dot products over RCCL.
+
+Output: ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "conjugate-gradient_amd"))
+sys.path.insert(0, str(REPO / "tests"))
+
+METRIC = "fp64 CG iterations/sec + SpMV HBM GB/s (% of roofline), 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+WORKLOADS = {
+    "c3": dict(desc="C3: 7-point 3-D Laplacian 216^3 (10,077,696 rows), fp64, b = 1",
+               kind="lap3d", dims=(216, 216, 216), dtype="f64"),
+    "c2": dict(desc="C2: 5-point 2-D Laplacian 1000^2 (1,000,000 rows), fp64, b = 1 "
+                    "(working set fits the 256 MiB Infinity Cache)",
+               kind="lap2d", dims=(1000, 1000), dtype="f64"),
+    "c5": dict(desc="C5: random SPD 5,000,000 rows, 32 partners/row symmetrised "
+                    "(~64 nnz/row), splitmix64 seed 42, fp32",
+               kind="rand", n=5_000_000, partners=32, seed=42, dtype="f32"),
+}
+
+
+def make_system(wl, rank=0, world=1):
+    import numpy as np
+    import cgx
+    if wl["kind"] == "lap3d":
+        nx, ny, nz = wl["dims"]
+        nz_g = nz * world
+        n_g = nx * ny * nz_g
+        rb, re_ = n_g * rank // world, n_g * (rank + 1) // world
+        rp, col, val = cgx.laplacian3d(nx, ny, nz_g, rb, re_)
+        return dict(rp=rp, col=col, val=val, b=np.ones(re_ - rb), n_global=n_g,
+                    row_begin=rb, row_end=re_)
+    if wl["kind"] == "lap2d":
+        nx, ny = wl["dims"]
+        ny_g = ny * world
+        n_g = nx * ny_g
+        rb, re_ = n_g * rank // world, n_g * (rank + 1) // world
+        rp, col, val = cgx.laplacian2d(nx, ny_g, rb, re_)
+        return dict(rp=rp, col=col, val=val, b=np.ones(re_ - rb), n_global=n_g,
+                    row_begin=rb, row_end=re_)
+    n = wl["n"]
+    rp, col, val = cgx.random_spd(n, wl["partners"], wl["seed"], f32=True)
+    b = np.random.default_rng(1).standard_normal(n).astype(np.float32)
+    return dict(rp=rp, col=col, val=val, b=b, n_global=n, row_begin=0, row_end=n)
+
+
+def load_traffic(workload, alg):
+    """HBM bytes per SpMV launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_<workload>.json, written by profiles/collect_pmc.py), or None."""
+    p = REPO / "profiles" / f"pmc_{workload}.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get("spmv_hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(sysm, budget_s):
+    """The oracle's CSR-sequential HS-CG (bit-exact to the reference on chained
+    matrices) on ONE host core, on the same matrix, for as many iterations as
+    fit in ~budget_s seconds."""
+    import numpy as np
+    import helpers as H
+    rp, col, val, b = sysm["rp"], sysm["col"], sysm["val"], sysm["b"]
+    if val.dtype != np.float64:
+        val = val.astype(np.float64)
+        b = b.astype(np.float64)
+    t0 = time.perf_counter()
+    H.o_solve(0, 0.0, rp, col, val, b)          # 1 iteration (probe)
+    t1 = time.perf_counter() - t0
+    its = max(1, min(1000, int(budget_s / max(t1, 1e-6))))
+    t0 = time.perf_counter()
+    _, done, _ = H.o_solve(its - 1, 0.0, rp, col, val, b)
+    dt = time.perf_counter() - t0
+    return dict(value=done / dt, unit="it/s", cores=1, kind="port",
+                sample=f"{done} HS-CG iterations of the same system (oracle/cg_oracle.c "
+                       f"CSR-sequential restatement, bit-exact to the reference's "
+                       f"mv_mult on chained matrices), 1 host core, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--alg", default=None, choices=["hs", "cg1"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch  # loads the HIP runtime libcgx then shares (same SONAME)
+    import torch.distributed as dist
+    import numpy as np
+    import cgx
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    wl = WORKLOADS[args.workload]
+    alg = args.alg or ("cg1" if world > 1 else "hs")
+    sysm = make_system(wl, rank, world)
+
+    if world > 1:
+        raise SystemExit("bench.py: multi-GPU path not available in this build")
+
+    s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
+    s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+    s.set_rhs(sysm["b"])
+    info = s.info()
+
+    # ---- timed region: exactly K steps, barrier + sync on both sides
+    s.bench_prepare(args.warmup)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev_ms, _ = s.bench_run(args.steps, graph=True)
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    ms_per_step = 1e3 * wall / args.steps
+
+    # ---- roofline of the dominant kernel (SpMV): HIP events around every
+    # SpMV launch on the solver's stream over K more iterations.
+    tot2, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
+    achieved = info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.workload, alg)
+    roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
+                    unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
+                    traffic=traffic, kernel="k_spmv (CSR-stream, LDS-staged)",
+                    spmv_us=round(spmv_ms * 1e3, 2),
+                    algorithmic_bytes_per_launch=int(info["spmv_bytes"]))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(sysm, args.cpu_seconds)
+
+    value = (args.steps / wall) * world  # weak scaling: slab-iterations/s
+    out = dict(
+        metric=METRIC, value=round(value, 2), unit="it/s", n_gpus=world,
+        steps=args.steps, warmup=args.warmup, ms_per_step=round(ms_per_step, 4),
+        higher_is_better=True, scaling="weak", vs_baseline=None,
+        dtype=wl["dtype"], data="synthetic",
+        config=dict(workload=wl["desc"], n=sysm["n_global"], nnz_local=int(len(sysm["col"])),
+                    alg=alg, graph=True, parallelism=f"row-partition x{world}"),
+        device_ms_per_step=round(dev_ms / args.steps, 4),
+        iter_bytes=int(info["iter_bytes"]),
+        iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),
+        roofline=roofline, cpu_baseline=cpu,
+    )
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    s.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

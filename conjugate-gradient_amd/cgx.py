@@ -1,0 +1,347 @@
+"""ctypes binding of libcgx.so (include/cgx.h, include/mv_ops.h).
+
+This is the host-side mirror used by the Python tests and bench.py; the
+product is the C ABI itself.  The library must be built (``make -C
+conjugate-gradient_amd`` or ``__graft_entry__.build()``); there is no CPU
+fallback -- a missing library raises, and compute calls without a gfx950
+device return CGX_ENODEV, which this module raises as CgxError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "lib" / "libcgx.so"
+
+CGX_EINVAL, CGX_ENODEV, CGX_ENOMEM, CGX_ECOMM = -1, -2, -3, -4
+CGX_MODE_FAST, CGX_MODE_EXACT = 0, 1
+CGX_ALG_HS, CGX_ALG_CG1 = 0, 1
+CGX_F64, CGX_F32 = 0, 1
+CGX_BENCH_GRAPH, CGX_BENCH_SPMV_EVENTS = 1, 2
+
+_i32p = ctypes.POINTER(ctypes.c_int)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_vp = ctypes.c_void_p
+
+
+class CgxError(RuntimeError):
+    pass
+
+
+class MvSparse(ctypes.Structure):
+    """struct __mv_sparse (mv_ops.h:17-23)."""
+    _fields_ = [("size", ctypes.c_int), ("nnz", ctypes.c_int),
+                ("values", _f64p), ("col_indices", _i32p), ("row_ptr", _i32p)]
+
+
+class CgxInfo(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("nnz", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("mode", ctypes.c_int), ("alg", ctypes.c_int),
+                ("n_rowblocks", ctypes.c_int), ("spmv_grid", ctypes.c_int),
+                ("vec_grid", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
+                ("iter_bytes", ctypes.c_double), ("device_bytes", ctypes.c_size_t)]
+
+
+_MVP = ctypes.POINTER(MvSparse)
+_MVPP = ctypes.POINTER(_MVP)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    # mv_ops.h
+    "new_mv_struct": (_MVP, []),
+    "new_mv_struct_with_size": (_MVP, [ctypes.c_int]),
+    "free_mv_struct": (None, [_MVP]),
+    "mv_deep_copy": (_MVP, [_MVP]),
+    "print_sparse": (None, [_MVP]),
+    "mat_get_row": (ctypes.c_int, [_MVP, ctypes.c_int, _f64p]),
+    "dot_product": (ctypes.c_double, [_MVP, _MVP]),
+    "sv_mult": (ctypes.c_int, [ctypes.c_double, _MVP, _MVPP]),
+    "mv_mult": (ctypes.c_int, [_MVP, _MVP, _MVPP]),
+    "vec_add": (ctypes.c_int, [_MVP, _MVP, _MVPP]),
+    "vec_sub": (ctypes.c_int, [_MVP, _MVP, _MVPP]),
+    # cgx.h
+    "conj_grad": (ctypes.c_int, [ctypes.c_int, _MVP, _MVP, _MVPP]),
+    "solve": (ctypes.c_int, [_MVP, _MVP, _MVPP, ctypes.c_double, ctypes.c_int]),
+    "cgx_free_mv_deep": (None, [_MVP]),
+    "cgx_last_error": (ctypes.c_char_p, []),
+    "cgx_device_count": (ctypes.c_int, []),
+    "cgx_solver_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "cgx_solver_destroy": (None, [_vp]),
+    "cgx_solver_set_mode": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    "cgx_solver_set_matrix": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                             _i32p, _i32p, _f64p]),
+    "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                                 _i32p, _i32p, _f32p]),
+    "cgx_solver_set_rhs": (ctypes.c_int, [_vp, _f64p]),
+    "cgx_solver_set_rhs_f32": (ctypes.c_int, [_vp, _f32p]),
+    "cgx_solver_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_int)]),
+    "cgx_solver_get_x": (ctypes.c_int, [_vp, _f64p]),
+    "cgx_solver_get_x_f32": (ctypes.c_int, [_vp, _f32p]),
+    "cgx_solver_get_history": (ctypes.c_int, [_vp, _f64p, ctypes.c_int]),
+    "cgx_solver_spmv": (ctypes.c_int, [_vp, _f64p, _f64p]),
+    "cgx_solver_spmv_f32": (ctypes.c_int, [_vp, _f32p, _f32p]),
+    "cgx_solver_info": (ctypes.c_int, [_vp, ctypes.POINTER(CgxInfo)]),
+    "cgx_solver_bench": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        _f64p, _f64p]),
+    "cgx_solver_bench_prepare": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_solver_bench_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                            _f64p, _f64p]),
+    "cgx_gen_laplacian2d": (ctypes.c_longlong, [ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int,
+                                                _i32p, _i32p, _f64p]),
+    "cgx_gen_laplacian3d": (ctypes.c_longlong, [ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, _i32p, _i32p, _f64p]),
+    "cgx_gen_random_spd": (ctypes.c_longlong, [ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_ulonglong, ctypes.c_int,
+                                               ctypes.c_int, _i32p, _i32p, _f64p,
+                                               _f32p]),
+    "cgx_csr_is_chained": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libcgx.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise CgxError(f"{LIB_PATH} not built: run `make -C {HERE}` "
+                       "(or __graft_entry__.build())")
+    L = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    return (lib().cgx_last_error() or b"").decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc < 0:
+        raise CgxError(f"{what} failed ({rc}): {last_error()}")
+    return rc
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+# --------------------------------------------------------------- generators
+
+def _gen(fn, args, m, want_f32=False):
+    L = lib()
+    nnz = getattr(L, fn)(*args, None, None, None, *([None] if fn == "cgx_gen_random_spd" else []))
+    check(nnz, fn)
+    rp = np.empty(m + 1, np.int32)
+    col = np.empty(max(nnz, 1), np.int32)
+    if fn == "cgx_gen_random_spd":
+        val = None if want_f32 else np.empty(max(nnz, 1), np.float64)
+        v32 = np.empty(max(nnz, 1), np.float32) if want_f32 else None
+        got = L.cgx_gen_random_spd(*args, _p(rp, _i32p), _p(col, _i32p),
+                                   _p(val, _f64p) if val is not None else None,
+                                   _p(v32, _f32p) if v32 is not None else None)
+        check(got, fn)
+        return rp, col[:nnz], (v32 if want_f32 else val)[:nnz]
+    val = np.empty(max(nnz, 1), np.float64)
+    got = getattr(L, fn)(*args, _p(rp, _i32p), _p(col, _i32p), _p(val, _f64p))
+    check(got, fn)
+    return rp, col[:nnz], val[:nnz]
+
+
+def laplacian2d(nx, ny, row_begin=0, row_end=None):
+    row_end = nx * ny if row_end is None else row_end
+    return _gen("cgx_gen_laplacian2d", (nx, ny, row_begin, row_end), row_end - row_begin)
+
+
+def laplacian3d(nx, ny, nz, row_begin=0, row_end=None):
+    row_end = nx * ny * nz if row_end is None else row_end
+    return _gen("cgx_gen_laplacian3d", (nx, ny, nz, row_begin, row_end),
+                row_end - row_begin)
+
+
+def random_spd(n, partners, seed, row_begin=0, row_end=None, f32=False):
+    row_end = n if row_end is None else row_end
+    return _gen("cgx_gen_random_spd", (n, partners, seed, row_begin, row_end),
+                row_end - row_begin, want_f32=f32)
+
+
+def is_chained(rp, col):
+    rp = np.ascontiguousarray(rp, np.int32)
+    col = np.ascontiguousarray(col, np.int32)
+    return bool(check(lib().cgx_csr_is_chained(len(rp) - 1, _p(rp, _i32p),
+                                                _p(col, _i32p)), "is_chained"))
+
+
+# ------------------------------------------------------------------ solver
+
+class Solver:
+    """Device-resident CG solver (cgx_solver_*)."""
+
+    def __init__(self, device=0, mode=CGX_MODE_FAST, alg=CGX_ALG_HS):
+        self._h = _vp()
+        check(lib().cgx_solver_create(device, ctypes.byref(self._h)), "cgx_solver_create")
+        self.set_mode(mode, alg)
+        self.n = 0
+        self.f32 = False
+
+    def close(self):
+        if self._h:
+            lib().cgx_solver_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_mode(self, mode, alg=CGX_ALG_HS):
+        check(lib().cgx_solver_set_mode(self._h, mode, alg), "set_mode")
+
+    def set_matrix(self, rp, col, val):
+        rp = np.ascontiguousarray(rp, np.int32)
+        col = np.ascontiguousarray(col, np.int32)
+        n = len(rp) - 1
+        if np.asarray(val).dtype == np.float32:
+            val = np.ascontiguousarray(val, np.float32)
+            check(lib().cgx_solver_set_matrix_f32(self._h, n, len(col), _p(rp, _i32p),
+                                                  _p(col, _i32p), _p(val, _f32p)),
+                  "set_matrix_f32")
+            self.f32 = True
+        else:
+            val = np.ascontiguousarray(val, np.float64)
+            check(lib().cgx_solver_set_matrix(self._h, n, len(col), _p(rp, _i32p),
+                                              _p(col, _i32p), _p(val, _f64p)),
+                  "set_matrix")
+            self.f32 = False
+        self.n = n
+
+    def set_rhs(self, b):
+        if self.f32:
+            b = np.ascontiguousarray(b, np.float32)
+            check(lib().cgx_solver_set_rhs_f32(self._h, _p(b, _f32p)), "set_rhs_f32")
+        else:
+            b = np.ascontiguousarray(b, np.float64)
+            check(lib().cgx_solver_set_rhs(self._h, _p(b, _f64p)), "set_rhs")
+
+    def run(self, maxit, tol=0.0):
+        it = ctypes.c_int(0)
+        check(lib().cgx_solver_run(self._h, maxit, tol, ctypes.byref(it)), "run")
+        return it.value
+
+    def x(self):
+        if self.f32:
+            out = np.empty(self.n, np.float32)
+            check(lib().cgx_solver_get_x_f32(self._h, _p(out, _f32p)), "get_x_f32")
+        else:
+            out = np.empty(self.n, np.float64)
+            check(lib().cgx_solver_get_x(self._h, _p(out, _f64p)), "get_x")
+        return out
+
+    def history(self, cap):
+        out = np.zeros(cap, np.float64)
+        m = check(lib().cgx_solver_get_history(self._h, _p(out, _f64p), cap), "history")
+        return out[:m]
+
+    def spmv(self, x):
+        if self.f32:
+            x = np.ascontiguousarray(x, np.float32)
+            y = np.empty(self.n, np.float32)
+            check(lib().cgx_solver_spmv_f32(self._h, _p(x, _f32p), _p(y, _f32p)), "spmv")
+        else:
+            x = np.ascontiguousarray(x, np.float64)
+            y = np.empty(self.n, np.float64)
+            check(lib().cgx_solver_spmv(self._h, _p(x, _f64p), _p(y, _f64p)), "spmv")
+        return y
+
+    def info(self):
+        i = CgxInfo()
+        check(lib().cgx_solver_info(self._h, ctypes.byref(i)), "info")
+        return {k: getattr(i, k) for k, _ in CgxInfo._fields_}
+
+    def bench_prepare(self, warmup):
+        check(lib().cgx_solver_bench_prepare(self._h, warmup), "bench_prepare")
+
+    def bench_run(self, iters, graph=True, spmv_events=False):
+        """Returns (device ms for all iters, average SpMV ms or -1)."""
+        tot = ctypes.c_double(0)
+        sp = ctypes.c_double(0)
+        flags = (CGX_BENCH_GRAPH if graph else 0) | (CGX_BENCH_SPMV_EVENTS if spmv_events else 0)
+        check(lib().cgx_solver_bench_run(self._h, iters, flags, ctypes.byref(tot),
+                                         ctypes.byref(sp)), "bench_run")
+        return tot.value, sp.value
+
+    def bench(self, warmup, iters, graph=True, spmv_events=False):
+        tot = ctypes.c_double(0)
+        sp = ctypes.c_double(0)
+        flags = (CGX_BENCH_GRAPH if graph else 0) | (CGX_BENCH_SPMV_EVENTS if spmv_events else 0)
+        check(lib().cgx_solver_bench(self._h, warmup, iters, flags, ctypes.byref(tot),
+                                     ctypes.byref(sp)), "bench")
+        return tot.value, sp.value
+
+
+# ------------------------------------------------- reference struct helpers
+
+class Mv:
+    """A struct __mv_sparse whose arrays are owned by numpy (kept alive here)."""
+
+    def __init__(self, values, col=None, row_ptr=None):
+        self.values = np.ascontiguousarray(values, np.float64)
+        self.col = None if col is None else np.ascontiguousarray(col, np.int32)
+        self.row_ptr = None if row_ptr is None else np.ascontiguousarray(row_ptr, np.int32)
+        s = MvSparse()
+        if self.row_ptr is not None:
+            s.size = len(self.row_ptr) - 1
+            s.nnz = len(self.values)
+            s.col_indices = _p(self.col, _i32p)
+            s.row_ptr = _p(self.row_ptr, _i32p)
+        else:
+            s.size = s.nnz = len(self.values)
+        s.values = _p(self.values, _f64p)
+        self.struct = s
+
+    @property
+    def ptr(self):
+        return ctypes.pointer(self.struct)
+
+
+def mv_values(p):
+    """Copy the values of a libcgx-allocated struct __mv_sparse* to numpy."""
+    s = p.contents
+    return np.ctypeslib.as_array(s.values, shape=(s.size,)).copy() if s.size > 0 else np.empty(0)
+
+
+def conj_grad(max_iter, A: Mv, b: Mv):
+    out = _MVP()
+    rc = lib().conj_grad(max_iter, A.ptr, b.ptr, ctypes.byref(out))
+    check(rc, "conj_grad")
+    x = mv_values(out)
+    lib().cgx_free_mv_deep(out)
+    return x
+
+
+def solve(A: Mv, b: Mv, tol, maxit):
+    out = _MVP()
+    its = check(lib().solve(A.ptr, b.ptr, ctypes.byref(out), tol, maxit), "solve")
+    x = mv_values(out)
+    lib().cgx_free_mv_deep(out)
+    return x, its

@@ -1,0 +1,129 @@
+// cgx_internal.h -- shared between the HIP kernels (cgx_kernels.hip) and the
+// host orchestration (cgx_solver.cpp, cgx_mvops.cpp, cgx_dist.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "cgx.h"
+
+namespace cgx {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define CGX_HIP(call)                                                        \
+  do {                                                                       \
+    hipError_t e_ = (call);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      ::cgx::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call,    \
+                       hipGetErrorString(e_));                               \
+      return CGX_ENODEV;                                                     \
+    }                                                                        \
+  } while (0)
+
+// ------------------------------------------------------- device CG state
+// One per solve, device resident: every scalar of the recurrence lives here
+// so an iteration never round-trips to the host (graph-replayable).
+struct CgState {
+  double rr;      // HS: r.r of the current r;  CG1: gamma = r.r
+  double alpha;
+  double beta;
+  double bb;      // b.b
+  double tol;     // requested tolerance (<= 0: none)
+  double tol2bb;  // tol*tol*b.b
+  double delta;   // CG1: w.r
+  double ps;      // HS: p.s of the last SpMV (diagnostic)
+  int k;          // index of the current iteration (x-updates done = k+1 at stop)
+  int max_iter;
+  int done;       // set by the finalize step; every kernel early-exits on it
+  int use_tol;
+  int hist_cap;
+  int pad[3];
+};
+static_assert(sizeof(CgState) == 96, "CgState layout");
+
+// -------------------------------------------------------------- geometry
+constexpr int kSpmvBS = 256;          // rows per LDS row block (one per lane)
+constexpr int kSpmvCapF64 = 2048;     // LDS product slots per row block (16 KiB)
+constexpr int kSpmvCapF32 = 4096;     // (16 KiB)
+constexpr int kVecBS = 256;
+constexpr int kFinBS = 1024;
+constexpr int kPad = 8;               // val/col padded to a multiple of this
+
+// Finalize ops (single-workgroup scalar steps of the recurrence).
+enum FinOp {
+  FIN_INIT_HS = 0,  // bb = rr = sum(a)
+  FIN_HS_ALPHA = 1, // alpha = rr / sum(a)            (cg.c:113)
+  FIN_HS_BETA = 2,  // rr_new = sum(a); stop test; beta = rr_new/rr (cg.c:125-129)
+  FIN_INIT_CG1 = 3, // gamma = bb = sum(a), delta = sum(b), alpha = gamma/delta
+  FIN_CG1 = 4,      // gamma' = sum(a), delta = sum(b); stop test; alpha, beta
+  FIN_SUM = 5,      // out[0] = sum(a) (op-level dot)
+};
+
+template <typename T>
+struct SpmvArgs {
+  const int *rp;       // row_ptr (local rows)
+  const int *col;      // column indices into x (local numbering)
+  const T *val;
+  const T *x;
+  T *y;
+  const int *blk_row;  // row-block boundaries, nblk_total+1 entries
+  const int *blk_list; // optional subset of row blocks (nullptr: 0..nblk-1)
+  int nblk;            // row blocks processed by this launch
+  double *part;        // per-workgroup partial of x[row]*y[row] (nullptr: none)
+  const int *done;     // early-exit flag (nullptr: never)
+};
+
+// Row-block plan: consecutive rows, at most kSpmvBS rows and `cap` nonzeros
+// per block; a row longer than `cap` gets a block of its own (chunked path).
+std::vector<int> plan_rowblocks(int n, const int *rp, int cap);
+
+// ------------------------------------------------------------- launchers
+// All launchers are graph-capturable (no sync, no allocation).
+template <typename T>
+hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st);
+
+template <typename T>
+hipError_t launch_init_hs(int n, const T *b, T *x, T *r, T *p, double *part,
+                          int grid, hipStream_t st);
+template <typename T>
+hipError_t launch_init_cg1(int n, const T *b, T *x, T *r, T *p, T *s,
+                           double *part, int grid, hipStream_t st);
+template <typename T>
+hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
+                            const CgState *stt, double *part, int grid,
+                            hipStream_t st);
+template <typename T>
+hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
+                       hipStream_t st);
+template <typename T>
+hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w,
+                             const CgState *stt, double *part, int grid,
+                             hipStream_t st);
+// Sequential dot (exact mode): out[0] = sum_i a[i]*b[i] in index order.
+template <typename T>
+hipError_t launch_dot_seq(int n, const T *a, const T *b, double *out,
+                          const int *done, hipStream_t st);
+// Two-stage dot, stage 1: part[blockIdx] = partial sums.
+template <typename T>
+hipError_t launch_dot_part(int n, const T *a, const T *b, double *part,
+                           int grid, hipStream_t st);
+hipError_t launch_finalize(int op, const double *pa, int na, const double *pb,
+                           int nb, CgState *stt, double *hist, double *out,
+                           hipStream_t st);
+// Elementwise ops of the mv_ops API: op 0: r = s*a, 1: r = a+b, 2: r = a-b
+template <typename T>
+hipError_t launch_axpby(int op, int n, double s, const T *a, const T *b, T *r,
+                        int grid, hipStream_t st);
+// Halo pack: buf[i] = x[idx[i]]
+template <typename T>
+hipError_t launch_gather(int m, const int *idx, const T *x, T *buf,
+                         hipStream_t st);
+
+int vec_grid_for(int n, int cus);
+
+}  // namespace cgx

@@ -1,0 +1,642 @@
+// cgx_kernels.hip -- hand-written gfx950 kernels for the CG hot path.
+//
+// Replaces the reference's CPU loops (rnelias/Conjugate-Gradient):
+//   mv_mult + mat_get_row   mv_ops.c:160-201, :99-113  -> k_spmv (CSR-stream,
+//                           LDS-staged per-row sums, persistent grid)
+//   dot_product             mv_ops.c:117-132  -> fused block partials + k_finalize
+//                           (deterministic two-stage), k_dot_seq (exact order)
+//   sv_mult + vec_add/sub   mv_ops.c:134-259, used at cg.c:115-132
+//                           -> k_update_xr, k_xpay, k_cg1_update (fused)
+//
+// Everything is bandwidth bound (about 0.17 flop/byte), so the design goal is
+// one coalesced pass over each array per iteration at 16 bytes per lane and
+// no fp64 atomics.  Compiled with -ffp-contract=off: the reference never
+// fuses multiply-add (Makefile:2 builds -O0), and x + alpha*p must round
+// twice to stay bit-identical.
+#include <hip/hip_runtime.h>
+
+#include "cgx_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace cgx {
+
+namespace {
+
+constexpr int kWave = 64;
+
+// 16-byte vector of T.
+template <typename T> struct Vec16;
+template <> struct Vec16<double> {
+  typedef double type __attribute__((ext_vector_type(2)));
+  static constexpr int W = 2;
+};
+template <> struct Vec16<float> {
+  typedef float type __attribute__((ext_vector_type(4)));
+  static constexpr int W = 4;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_down(v, off, kWave);
+  return v;  // valid in lane 0
+}
+
+// Deterministic block reduction; result valid in thread 0.
+template <int BS>
+__device__ __forceinline__ double block_sum(double v, double *red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    s = red[0];
+#pragma unroll
+    for (int i = 1; i < BS / kWave; ++i) s = s + red[i];
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------- SpMV
+// CSR-stream: each row block (<= BS rows, <= CAP nonzeros) is streamed with
+// coalesced VEC-wide loads of val/col; the products val[k]*x[col[k]] land in
+// LDS; then lane t sums row t's products sequentially in column order from
+// 0.0 -- the reference's per-row order (mv_ops.c:190-194), so y is
+// bit-identical to it on chained matrices.  The grid is persistent: workgroup
+// g owns a contiguous chunk of row blocks (x-gather locality in L1/L2) and
+// accumulates the fused x.y epilogue over its chunk in a fixed order.
+template <typename T, int BS, int CAP, int VEC, bool EPI>
+__global__ __launch_bounds__(BS) void k_spmv(SpmvArgs<T> a) {
+  __shared__ T prod[CAP];
+  __shared__ int srp[BS + 1];
+  __shared__ double red[BS / kWave];
+  if (a.done && *a.done) return;
+
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  const int lo = (int)(((long long)a.nblk * blockIdx.x) / G);
+  const int hi = (int)(((long long)a.nblk * (blockIdx.x + 1)) / G);
+  double dot = 0.0;
+
+  for (int i = lo; i < hi; ++i) {
+    const int rb = a.blk_list ? a.blk_list[i] : i;
+    const int r0 = a.blk_row[rb];
+    const int nr = a.blk_row[rb + 1] - r0;
+    for (int t = tid; t <= nr; t += BS) srp[t] = a.rp[r0 + t];
+    __syncthreads();
+    const int k0 = srp[0], k1 = srp[nr];
+
+    if (k1 - k0 <= CAP) {
+      if (VEC == 1) {
+        for (int k = k0 + tid; k < k1; k += BS)
+          prod[k - k0] = a.val[k] * a.x[a.col[k]];
+      } else {
+        // VEC-aligned vector loads; val/col are padded to a multiple of
+        // kPad, so the aligned window never leaves the allocation.
+        typedef T tv __attribute__((ext_vector_type(VEC)));
+        typedef int iv __attribute__((ext_vector_type(VEC)));
+        const int kb = k0 & ~(VEC - 1);
+        for (int kk = kb + tid * VEC; kk < k1; kk += BS * VEC) {
+          const tv v = *reinterpret_cast<const tv *>(a.val + kk);
+          const iv c = *reinterpret_cast<const iv *>(a.col + kk);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) {
+            const int k = kk + j;
+            if (k >= k0 && k < k1) prod[k - k0] = v[j] * a.x[c[j]];
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < nr) {
+        const int j0 = srp[tid] - k0, j1 = srp[tid + 1] - k0;
+        T acc = T(0);
+        for (int j = j0; j < j1; ++j) acc = acc + prod[j];
+        a.y[r0 + tid] = acc;
+        if (EPI) {
+          const double xv = (double)a.x[r0 + tid];
+          dot = dot + xv * (double)acc;
+        }
+      }
+    } else {
+      // One row longer than CAP (planner guarantees nr == 1): stream it in
+      // CAP-sized chunks, lane 0 keeps the sequential sum.
+      T acc = T(0);
+      for (int c0 = k0; c0 < k1; c0 += CAP) {
+        const int m = min(CAP, k1 - c0);
+        for (int t = tid; t < m; t += BS)
+          prod[t] = a.val[c0 + t] * a.x[a.col[c0 + t]];
+        __syncthreads();
+        if (tid == 0)
+          for (int j = 0; j < m; ++j) acc = acc + prod[j];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        a.y[r0] = acc;
+        if (EPI) dot = dot + (double)a.x[r0] * (double)acc;
+      }
+    }
+    __syncthreads();  // srp/prod are reused by the next row block
+  }
+  if (EPI) {
+    const double s = block_sum<BS>(dot, red);
+    if (tid == 0) a.part[blockIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------- vector kernels
+// All grid-stride over 16-byte vectors; the scalar tail (n % W) is handled
+// by global thread 0.  Reductions: per-thread fixed-order sums, then
+// block_sum -> part[blockIdx.x]; finalize adds the partials in index order.
+
+// x = 0, r = b, p = b; part = b.b partials (HS prologue, cg.c:104-108)
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_init_hs(int n, const T *__restrict__ b,
+                                                T *__restrict__ x,
+                                                T *__restrict__ r,
+                                                T *__restrict__ p,
+                                                double *__restrict__ part) {
+  __shared__ double red[BS / kWave];
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    const V bv = reinterpret_cast<const V *>(b)[i];
+    reinterpret_cast<V *>(x)[i] = V(T(0));
+    reinterpret_cast<V *>(r)[i] = bv;
+    reinterpret_cast<V *>(p)[i] = bv;
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc = acc + (double)bv[j] * (double)bv[j];
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T bv = b[i];
+      x[i] = T(0); r[i] = bv; p[i] = bv;
+      acc = acc + (double)bv * (double)bv;
+    }
+  const double s = block_sum<BS>(acc, red);
+  if (threadIdx.x == 0 && part) part[blockIdx.x] = s;
+}
+
+// x = 0, r = b, p = s = 0; part = b.b partials (CG1 prologue)
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_init_cg1(int n, const T *__restrict__ b,
+                                                 T *__restrict__ x,
+                                                 T *__restrict__ r,
+                                                 T *__restrict__ p,
+                                                 T *__restrict__ s,
+                                                 double *__restrict__ part) {
+  __shared__ double red[BS / kWave];
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    const V bv = reinterpret_cast<const V *>(b)[i];
+    reinterpret_cast<V *>(x)[i] = V(T(0));
+    reinterpret_cast<V *>(p)[i] = V(T(0));
+    reinterpret_cast<V *>(s)[i] = V(T(0));
+    reinterpret_cast<V *>(r)[i] = bv;
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc = acc + (double)bv[j] * (double)bv[j];
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T bv = b[i];
+      x[i] = T(0); p[i] = T(0); s[i] = T(0); r[i] = bv;
+      acc = acc + (double)bv * (double)bv;
+    }
+  const double sum = block_sum<BS>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = sum;
+}
+
+// x += alpha*p (cg.c:115-118); r -= alpha*s (cg.c:122-123); part = r.r
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
+                                                  const T *__restrict__ p,
+                                                  T *__restrict__ r,
+                                                  const T *__restrict__ s,
+                                                  const CgState *__restrict__ st,
+                                                  double *__restrict__ part) {
+  __shared__ double red[BS / kWave];
+  if (st->done) return;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T alpha = (T)st->alpha;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    V xv = reinterpret_cast<const V *>(x)[i];
+    const V pv = reinterpret_cast<const V *>(p)[i];
+    V rv = reinterpret_cast<const V *>(r)[i];
+    const V sv = reinterpret_cast<const V *>(s)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T ap = alpha * pv[j];
+      xv[j] = xv[j] + ap;
+      const T as = alpha * sv[j];
+      rv[j] = rv[j] - as;
+      acc = acc + (double)rv[j] * (double)rv[j];
+    }
+    reinterpret_cast<V *>(x)[i] = xv;
+    reinterpret_cast<V *>(r)[i] = rv;
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T ap = alpha * p[i];
+      x[i] = x[i] + ap;
+      const T as = alpha * s[i];
+      const T ri = r[i] - as;
+      r[i] = ri;
+      acc = acc + (double)ri * (double)ri;
+    }
+  if (part) {
+    const double sum = block_sum<BS>(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = sum;
+  }
+}
+
+// p = r + beta*p (cg.c:131-132)
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_xpay(int n, T *__restrict__ p,
+                                             const T *__restrict__ r,
+                                             const CgState *__restrict__ st) {
+  if (st->done) return;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T beta = (T)st->beta;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  for (int i = gid; i < nv; i += stride) {
+    V pv = reinterpret_cast<const V *>(p)[i];
+    const V rv = reinterpret_cast<const V *>(r)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T bp = beta * pv[j];
+      pv[j] = rv[j] + bp;
+    }
+    reinterpret_cast<V *>(p)[i] = pv;
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T bp = beta * p[i];
+      p[i] = r[i] + bp;
+    }
+}
+
+// Chronopoulos-Gear update: p = r + beta p; s = w + beta s; x += alpha p;
+// r -= alpha s; part = r.r (gamma of the next iteration).
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_cg1_update(int n, T *__restrict__ x,
+                                                   T *__restrict__ p,
+                                                   T *__restrict__ r,
+                                                   T *__restrict__ s,
+                                                   const T *__restrict__ w,
+                                                   const CgState *__restrict__ st,
+                                                   double *__restrict__ part) {
+  __shared__ double red[BS / kWave];
+  if (st->done) return;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T alpha = (T)st->alpha, beta = (T)st->beta;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    V xv = reinterpret_cast<const V *>(x)[i];
+    V pv = reinterpret_cast<const V *>(p)[i];
+    V rv = reinterpret_cast<const V *>(r)[i];
+    V sv = reinterpret_cast<const V *>(s)[i];
+    const V wv = reinterpret_cast<const V *>(w)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T bp = beta * pv[j];
+      pv[j] = rv[j] + bp;
+      const T bs = beta * sv[j];
+      sv[j] = wv[j] + bs;
+      const T ap = alpha * pv[j];
+      xv[j] = xv[j] + ap;
+      const T as = alpha * sv[j];
+      rv[j] = rv[j] - as;
+      acc = acc + (double)rv[j] * (double)rv[j];
+    }
+    reinterpret_cast<V *>(x)[i] = xv;
+    reinterpret_cast<V *>(p)[i] = pv;
+    reinterpret_cast<V *>(r)[i] = rv;
+    reinterpret_cast<V *>(s)[i] = sv;
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T bp = beta * p[i];
+      const T pi = r[i] + bp;
+      const T bs = beta * s[i];
+      const T si = w[i] + bs;
+      const T ap = alpha * pi;
+      x[i] = x[i] + ap;
+      const T as = alpha * si;
+      const T ri = r[i] - as;
+      p[i] = pi; s[i] = si; r[i] = ri;
+      acc = acc + (double)ri * (double)ri;
+    }
+  const double sum = block_sum<BS>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = sum;
+}
+
+// Exact-order dot (dot_product, mv_ops.c:128-129): products are formed in
+// parallel (each rounded, as the reference does), lane 0 adds them strictly
+// in index order starting from 0.0.  O(n) serial -- parity mode only.
+template <typename T>
+__global__ __launch_bounds__(kWave) void k_dot_seq(int n, const T *__restrict__ a,
+                                                   const T *__restrict__ b,
+                                                   double *__restrict__ out,
+                                                   const int *__restrict__ done) {
+  constexpr int CH = 8 * kWave;
+  __shared__ double buf[CH];
+  if (done && *done) return;
+  const int lane = threadIdx.x;
+  double acc = 0.0;
+  for (int base = 0; base < n; base += CH) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * kWave + lane;
+      buf[j * kWave + lane] = (i < n) ? (double)(a[i] * b[i]) : 0.0;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const int m = min(CH, n - base);
+      for (int t = 0; t < m; ++t) acc = acc + buf[t];
+    }
+    __syncthreads();
+  }
+  if (lane == 0) out[0] = acc;
+}
+
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_dot_part(int n, const T *__restrict__ a,
+                                                 const T *__restrict__ b,
+                                                 double *__restrict__ part) {
+  __shared__ double red[BS / kWave];
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    const V av = reinterpret_cast<const V *>(a)[i];
+    const V bv = reinterpret_cast<const V *>(b)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc = acc + (double)av[j] * (double)bv[j];
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) acc = acc + (double)a[i] * (double)b[i];
+  const double s = block_sum<BS>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// Fixed-order sum of na partials by one workgroup (thread t adds
+// pa[t], pa[t+BS], ... in order; then the block tree).  Starts from the first
+// partial, so a single partial (exact mode) passes through unchanged.
+template <int BS>
+__device__ __forceinline__ double sum_parts(const double *pa, int na,
+                                            double *red) {
+  double acc = 0.0;
+  if ((int)threadIdx.x < na) {
+    acc = pa[threadIdx.x];
+    for (int i = threadIdx.x + BS; i < na; i += BS) acc = acc + pa[i];
+  }
+  const double s = block_sum<BS>(acc, red);
+  __syncthreads();
+  return s;
+}
+
+template <int BS>
+__global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int na,
+                                                 const double *pb, int nb,
+                                                 CgState *st, double *hist,
+                                                 double *out) {
+  __shared__ double red[BS / kWave];
+  if (op != FIN_SUM && op != FIN_INIT_HS && op != FIN_INIT_CG1 && st->done)
+    return;
+  const double sa = sum_parts<BS>(pa, na, red);
+  const double sb = pb ? sum_parts<BS>(pb, nb, red) : 0.0;
+  if (threadIdx.x != 0) return;
+  switch (op) {
+    case FIN_SUM:
+      out[0] = sa;
+      break;
+    case FIN_INIT_HS:
+      st->bb = sa;
+      st->rr = sa;  // r = b (cg.c:107), so r.r == b.b bit for bit
+      st->tol2bb = st->tol * st->tol * sa;
+      st->k = 0;
+      st->done = 0;
+      break;
+    case FIN_HS_ALPHA:
+      st->ps = sa;
+      st->alpha = st->rr / sa;  // cg.c:113
+      break;
+    case FIN_HS_BETA: {
+      const double rr_new = sa;
+      const int k = st->k;
+      if (k < st->hist_cap) hist[k] = rr_new;
+      if (k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb)) {
+        st->done = 1;  // cg.c:125 break position
+      } else {
+        st->beta = rr_new / st->rr;  // cg.c:129
+        st->rr = rr_new;
+        st->k = k + 1;
+      }
+      break;
+    }
+    case FIN_INIT_CG1:
+      st->bb = sa;
+      st->rr = sa;
+      st->delta = sb;
+      st->tol2bb = st->tol * st->tol * sa;
+      st->alpha = sa / sb;
+      st->beta = 0.0;
+      st->k = 0;
+      st->done = 0;
+      break;
+    case FIN_CG1: {
+      const double g = sa, d = sb;
+      const int k = st->k;
+      if (k < st->hist_cap) hist[k] = g;
+      if (k >= st->max_iter || (st->use_tol && g <= st->tol2bb)) {
+        st->done = 1;
+      } else {
+        const double beta = g / st->rr;
+        st->delta = d;
+        st->alpha = g / (d - beta * g / st->alpha);
+        st->beta = beta;
+        st->rr = g;
+        st->k = k + 1;
+      }
+      break;
+    }
+  }
+}
+
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_axpby(int op, int n, double sc,
+                                              const T *__restrict__ a,
+                                              const T *__restrict__ b,
+                                              T *__restrict__ r) {
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  const T s = (T)sc;
+  for (int i = gid; i < n; i += stride) {
+    T v;
+    if (op == 0) v = s * a[i];          // sv_mult, mv_ops.c:141-142
+    else if (op == 1) v = a[i] + b[i];  // vec_add, mv_ops.c:229
+    else v = a[i] - b[i];               // vec_sub, mv_ops.c:258
+    r[i] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gather(int m, const int *__restrict__ idx,
+                                                const T *__restrict__ x,
+                                                T *__restrict__ buf) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < m) buf[i] = x[idx[i]];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------- launchers
+
+template <typename T>
+hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) {
+  constexpr int CAP = sizeof(T) == 8 ? kSpmvCapF64 : kSpmvCapF32;
+  if (a.nblk <= 0) return hipSuccess;
+  grid = grid < 1 ? 1 : (grid > a.nblk ? a.nblk : grid);
+  const bool epi = a.part != nullptr;
+#define CGX_SPMV(V, E)                                                         \
+  hipLaunchKernelGGL((k_spmv<T, kSpmvBS, CAP, V, E>), dim3(grid), dim3(kSpmvBS), \
+                     0, st, a)
+  if (vec == 4) {
+    if (epi) CGX_SPMV(4, true); else CGX_SPMV(4, false);
+  } else if (vec == 2) {
+    if (epi) CGX_SPMV(2, true); else CGX_SPMV(2, false);
+  } else {
+    if (epi) CGX_SPMV(1, true); else CGX_SPMV(1, false);
+  }
+#undef CGX_SPMV
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_init_hs(int n, const T *b, T *x, T *r, T *p, double *part,
+                          int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_init_hs<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n,
+                     b, x, r, p, part);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_init_cg1(int n, const T *b, T *x, T *r, T *p, T *s,
+                           double *part, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_init_cg1<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
+                     n, b, x, r, p, s, part);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
+                            const CgState *stt, double *part, int grid,
+                            hipStream_t st) {
+  hipLaunchKernelGGL((k_update_xr<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
+                     n, x, p, r, s, stt, part);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
+                       hipStream_t st) {
+  hipLaunchKernelGGL((k_xpay<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n, p,
+                     r, stt);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w,
+                             const CgState *stt, double *part, int grid,
+                             hipStream_t st) {
+  hipLaunchKernelGGL((k_cg1_update<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
+                     n, x, p, r, s, w, stt, part);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_dot_seq(int n, const T *a, const T *b, double *out,
+                          const int *done, hipStream_t st) {
+  hipLaunchKernelGGL((k_dot_seq<T>), dim3(1), dim3(kWave), 0, st, n, a, b, out,
+                     done);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_dot_part(int n, const T *a, const T *b, double *part,
+                           int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_dot_part<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
+                     n, a, b, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(int op, const double *pa, int na, const double *pb,
+                           int nb, CgState *stt, double *hist, double *out,
+                           hipStream_t st) {
+  hipLaunchKernelGGL((k_finalize<kFinBS>), dim3(1), dim3(kFinBS), 0, st, op, pa,
+                     na, pb, nb, stt, hist, out);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_axpby(int op, int n, double s, const T *a, const T *b, T *r,
+                        int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_axpby<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, op,
+                     n, s, a, b, r);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_gather(int m, const int *idx, const T *x, T *buf,
+                         hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_gather<T>), dim3((m + 255) / 256), dim3(256), 0, st, m,
+                     idx, x, buf);
+  return hipGetLastError();
+}
+
+#define CGX_INSTANTIATE(T)                                                     \
+  template hipError_t launch_spmv<T>(const SpmvArgs<T> &, int, int,           \
+                                     hipStream_t);                             \
+  template hipError_t launch_init_hs<T>(int, const T *, T *, T *, T *,        \
+                                        double *, int, hipStream_t);           \
+  template hipError_t launch_init_cg1<T>(int, const T *, T *, T *, T *, T *,  \
+                                         double *, int, hipStream_t);          \
+  template hipError_t launch_update_xr<T>(int, T *, const T *, T *,           \
+                                          const T *, const CgState *,         \
+                                          double *, int, hipStream_t);         \
+  template hipError_t launch_xpay<T>(int, T *, const T *, const CgState *,    \
+                                     int, hipStream_t);                        \
+  template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *,           \
+                                           const T *, const CgState *,        \
+                                           double *, int, hipStream_t);        \
+  template hipError_t launch_dot_seq<T>(int, const T *, const T *, double *,  \
+                                        const int *, hipStream_t);             \
+  template hipError_t launch_dot_part<T>(int, const T *, const T *, double *, \
+                                         int, hipStream_t);                    \
+  template hipError_t launch_axpby<T>(int, int, double, const T *, const T *, \
+                                      T *, int, hipStream_t);                  \
+  template hipError_t launch_gather<T>(int, const int *, const T *, T *,      \
+                                       hipStream_t);
+
+CGX_INSTANTIATE(double)
+CGX_INSTANTIATE(float)
+
+}  // namespace cgx

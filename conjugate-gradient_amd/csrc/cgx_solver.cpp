@@ -1,0 +1,700 @@
+// cgx_solver.cpp -- device-resident CG solver: HIP-stream orchestration of the
+// iteration that replaces conj_grad's loop (rnelias/Conjugate-Gradient
+// cg.c:88-141).  The whole recurrence state (alpha, beta, r.r, k, stop flag)
+// lives on the device in a CgState, so an iteration is a fixed sequence of
+// kernel launches with no host round trip; batches of iterations are replayed
+// as hipGraphs, and the host only polls the stop flag between batches when a
+// tolerance is set.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cgx_internal.h"
+
+using cgx::CgState;
+
+namespace cgx {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+
+std::vector<int> plan_rowblocks(int n, const int *rp, int cap) {
+  std::vector<int> blk;
+  blk.reserve((size_t)n / 128 + 2);
+  blk.push_back(0);
+  int r = 0;
+  while (r < n) {
+    const int start = r;
+    const int k0 = rp[r];
+    if (rp[r + 1] - k0 > cap) {  // long row: a block of its own
+      blk.push_back(++r);
+      continue;
+    }
+    while (r < n && r - start < kSpmvBS && rp[r + 1] - k0 <= cap) ++r;
+    blk.push_back(r);
+  }
+  return blk;
+}
+
+int vec_grid_for(int n, int cus) {
+  const long long vecs = (n + 1) / 2;
+  long long g = (vecs + kVecBS - 1) / kVecBS;
+  const long long cap = (long long)cus * 4;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+static int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+}  // namespace cgx
+
+// ----------------------------------------------------------------- solver
+
+struct cgx_solver {
+  int device = 0;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  int n = 0, nnz = 0, dtype = CGX_F64;
+  int mode = CGX_MODE_FAST, alg = CGX_ALG_HS;
+  int vec = 2;
+  int nblk = 0, spmv_grid = 0, vec_grid = 0;
+  bool use_graph = true;
+  int graph_batch = 16;
+  int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr;
+  void *d_val = nullptr;
+  void *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr,
+       *d_s = nullptr, *d_w = nullptr;
+  double *d_pa = nullptr, *d_pb = nullptr;
+  int part_cap = 0;
+  CgState *d_st = nullptr, *h_st = nullptr;
+  double *d_hist = nullptr;
+  int hist_alloc = 0;
+  size_t dev_bytes = 0;
+  bool have_matrix = false, have_rhs = false, bench_ready = false;
+  int last_iters = 0;
+  hipGraphExec_t gexec = nullptr;
+  int gexec_key = -1;
+  std::vector<hipEvent_t> events;
+};
+
+namespace {
+
+using namespace cgx;
+
+size_t tsize(int dtype) { return dtype == CGX_F32 ? 4 : 8; }
+
+int dalloc(cgx_solver *s, void **p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    *p = nullptr;
+    return CGX_ENOMEM;
+  }
+  s->dev_bytes += bytes;
+  return 0;
+}
+
+void dfree(void **p) {
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+}
+
+void drop_graph(cgx_solver *s) {
+  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+  s->gexec = nullptr;
+  s->gexec_key = -1;
+}
+
+void free_matrix(cgx_solver *s) {
+  drop_graph(s);
+  dfree((void **)&s->d_rp);
+  dfree((void **)&s->d_col);
+  dfree((void **)&s->d_blk);
+  dfree(&s->d_val);
+  dfree(&s->d_b);
+  dfree(&s->d_x);
+  dfree(&s->d_r);
+  dfree(&s->d_p);
+  dfree(&s->d_s);
+  dfree(&s->d_w);
+  dfree((void **)&s->d_pa);
+  dfree((void **)&s->d_pb);
+  dfree((void **)&s->d_hist);
+  s->hist_alloc = 0;
+  s->dev_bytes = 0;
+  s->have_matrix = s->have_rhs = s->bench_ready = false;
+  s->n = s->nnz = s->nblk = 0;
+}
+
+int check_device(int device) {
+  int cnt = 0;
+  hipError_t e = hipGetDeviceCount(&cnt);
+  if (e != hipSuccess || cnt == 0) {
+    set_error("no HIP device available (%s)",
+              e != hipSuccess ? hipGetErrorString(e) : "device count is 0");
+    return CGX_ENODEV;
+  }
+  if (device < 0 || device >= cnt) {
+    set_error("device %d out of range (%d devices)", device, cnt);
+    return CGX_EINVAL;
+  }
+  hipDeviceProp_t prop;
+  CGX_HIP(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error("device %d is %s; libcgx is built for gfx950 (MI355X) only",
+              device, prop.gcnArchName);
+    return CGX_ENODEV;
+  }
+  return 0;
+}
+
+template <typename T>
+int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
+                  const T *val) {
+  if (n < 0 || nnz < 0 || (n > 0 && (!rp || (nnz > 0 && (!col || !val))))) {
+    set_error("set_matrix: invalid arguments");
+    return CGX_EINVAL;
+  }
+  if (n > 0 && (rp[0] != 0 || rp[n] != nnz)) {
+    set_error("set_matrix: row_ptr[0] must be 0 and row_ptr[n] == nnz");
+    return CGX_EINVAL;
+  }
+  CGX_HIP(hipSetDevice(s->device));
+  free_matrix(s);
+  s->dtype = sizeof(T) == 4 ? CGX_F32 : CGX_F64;
+  s->n = n;
+  s->nnz = nnz;
+  const int cap = sizeof(T) == 8 ? kSpmvCapF64 : kSpmvCapF32;
+  std::vector<int> blk;
+  if (n > 0) blk = plan_rowblocks(n, rp, cap);
+  else blk.push_back(0);
+  s->nblk = (int)blk.size() - 1;
+  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kPad;
+  const size_t nv = (size_t)n + kPad;
+  int rc;
+  if ((rc = dalloc(s, (void **)&s->d_rp, ((size_t)n + 1) * 4)) ||
+      (rc = dalloc(s, (void **)&s->d_col, nnz_pad * 4)) ||
+      (rc = dalloc(s, &s->d_val, nnz_pad * sizeof(T))) ||
+      (rc = dalloc(s, (void **)&s->d_blk, blk.size() * 4)) ||
+      (rc = dalloc(s, &s->d_b, nv * sizeof(T))) ||
+      (rc = dalloc(s, &s->d_x, nv * sizeof(T))) ||
+      (rc = dalloc(s, &s->d_r, nv * sizeof(T))) ||
+      (rc = dalloc(s, &s->d_p, nv * sizeof(T))) ||
+      (rc = dalloc(s, &s->d_s, nv * sizeof(T))) ||
+      (rc = dalloc(s, &s->d_w, nv * sizeof(T)))) {
+    free_matrix(s);
+    return rc;
+  }
+  s->spmv_grid = std::min(s->nblk, env_int("CGX_SPMV_GRID", s->cus * 8));
+  if (s->spmv_grid < 1) s->spmv_grid = 1;
+  s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
+  s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
+  if ((rc = dalloc(s, (void **)&s->d_pa, (size_t)s->part_cap * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_pb, (size_t)s->part_cap * 8))) {
+    free_matrix(s);
+    return rc;
+  }
+  CGX_HIP(hipMemsetAsync(s->d_col, 0, nnz_pad * 4, s->stream));
+  CGX_HIP(hipMemsetAsync(s->d_val, 0, nnz_pad * sizeof(T), s->stream));
+  if (n > 0) {
+    CGX_HIP(hipMemcpyAsync(s->d_rp, rp, ((size_t)n + 1) * 4,
+                           hipMemcpyHostToDevice, s->stream));
+    if (nnz > 0) {
+      CGX_HIP(hipMemcpyAsync(s->d_col, col, (size_t)nnz * 4,
+                             hipMemcpyHostToDevice, s->stream));
+      CGX_HIP(hipMemcpyAsync(s->d_val, val, (size_t)nnz * sizeof(T),
+                             hipMemcpyHostToDevice, s->stream));
+    }
+  }
+  CGX_HIP(hipMemcpyAsync(s->d_blk, blk.data(), blk.size() * 4,
+                         hipMemcpyHostToDevice, s->stream));
+  CGX_HIP(hipStreamSynchronize(s->stream));
+  s->have_matrix = true;
+  return 0;
+}
+
+template <typename T>
+int upload_rhs(cgx_solver *s, const T *b) {
+  if (!s->have_matrix || (s->n > 0 && !b)) {
+    set_error("set_rhs: no matrix loaded or NULL b");
+    return CGX_EINVAL;
+  }
+  if ((sizeof(T) == 4) != (s->dtype == CGX_F32)) {
+    set_error("set_rhs: dtype does not match the matrix");
+    return CGX_EINVAL;
+  }
+  CGX_HIP(hipSetDevice(s->device));
+  if (s->n > 0)
+    CGX_HIP(hipMemcpy(s->d_b, b, (size_t)s->n * sizeof(T),
+                      hipMemcpyHostToDevice));
+  s->have_rhs = true;
+  return 0;
+}
+
+template <typename T>
+SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
+                      bool with_done) {
+  SpmvArgs<T> a;
+  a.rp = s->d_rp;
+  a.col = s->d_col;
+  a.val = (const T *)s->d_val;
+  a.x = (const T *)x;
+  a.y = (T *)y;
+  a.blk_row = s->d_blk;
+  a.blk_list = nullptr;
+  a.nblk = s->nblk;
+  a.part = part;
+  a.done = with_done ? &s->d_st->done : nullptr;
+  return a;
+}
+
+// Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
+template <typename T>
+int enqueue_init(cgx_solver *s) {
+  hipStream_t st = s->stream;
+  T *b = (T *)s->d_b, *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p;
+  if (s->alg == CGX_ALG_HS) {
+    if (s->mode == CGX_MODE_EXACT) {
+      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, nullptr, s->vec_grid, st));
+      CGX_HIP(launch_dot_seq<T>(s->n, b, b, s->d_pa, nullptr, st));
+      CGX_HIP(launch_finalize(FIN_INIT_HS, s->d_pa, 1, nullptr, 0, s->d_st,
+                              s->d_hist, nullptr, st));
+    } else {
+      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, s->d_pa, s->vec_grid, st));
+      CGX_HIP(launch_finalize(FIN_INIT_HS, s->d_pa, s->vec_grid, nullptr, 0,
+                              s->d_st, s->d_hist, nullptr, st));
+    }
+  } else {
+    CGX_HIP(launch_init_cg1<T>(s->n, b, x, r, p, (T *)s->d_s, s->d_pa,
+                               s->vec_grid, st));
+    CGX_HIP(launch_spmv<T>(spmv_args<T>(s, r, s->d_w, s->d_pb, false),
+                           s->spmv_grid, s->vec, st));
+    CGX_HIP(launch_finalize(FIN_INIT_CG1, s->d_pa, s->vec_grid, s->d_pb,
+                            std::min(s->spmv_grid, std::max(s->nblk, 1)),
+                            s->d_st, s->d_hist, nullptr, st));
+  }
+  return 0;
+}
+
+// One CG iteration.  ev0/ev1 (optional) bracket the SpMV launch.
+template <typename T>
+int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
+  hipStream_t st = s->stream;
+  T *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p, *sv = (T *)s->d_s,
+    *w = (T *)s->d_w;
+  const int sg = std::min(s->spmv_grid, std::max(s->nblk, 1));
+  if (s->alg == CGX_ALG_HS) {
+    const bool exact = s->mode == CGX_MODE_EXACT;
+    if (ev0) CGX_HIP(hipEventRecord(ev0, st));
+    CGX_HIP(launch_spmv<T>(spmv_args<T>(s, p, sv, exact ? nullptr : s->d_pa,
+                                        true),
+                           s->spmv_grid, s->vec, st));           // cg.c:111
+    if (ev1) CGX_HIP(hipEventRecord(ev1, st));
+    if (exact) {
+      CGX_HIP(launch_dot_seq<T>(s->n, p, sv, s->d_pa, &s->d_st->done, st));
+      CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, 1, nullptr, 0, s->d_st,
+                              s->d_hist, nullptr, st));           // cg.c:113
+      CGX_HIP(launch_update_xr<T>(s->n, x, p, r, sv, s->d_st, nullptr,
+                                  s->vec_grid, st));              // cg.c:115-123
+      CGX_HIP(launch_dot_seq<T>(s->n, r, r, s->d_pa, &s->d_st->done, st));
+      CGX_HIP(launch_finalize(FIN_HS_BETA, s->d_pa, 1, nullptr, 0, s->d_st,
+                              s->d_hist, nullptr, st));           // cg.c:125-129
+    } else {
+      CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, sg, nullptr, 0, s->d_st,
+                              s->d_hist, nullptr, st));
+      CGX_HIP(launch_update_xr<T>(s->n, x, p, r, sv, s->d_st, s->d_pa,
+                                  s->vec_grid, st));
+      CGX_HIP(launch_finalize(FIN_HS_BETA, s->d_pa, s->vec_grid, nullptr, 0,
+                              s->d_st, s->d_hist, nullptr, st));
+    }
+    CGX_HIP(launch_xpay<T>(s->n, p, r, s->d_st, s->vec_grid, st));  // cg.c:131-132
+  } else {
+    CGX_HIP(launch_cg1_update<T>(s->n, x, p, r, sv, w, s->d_st, s->d_pa,
+                                 s->vec_grid, st));
+    if (ev0) CGX_HIP(hipEventRecord(ev0, st));
+    CGX_HIP(launch_spmv<T>(spmv_args<T>(s, r, w, s->d_pb, true), s->spmv_grid,
+                           s->vec, st));
+    if (ev1) CGX_HIP(hipEventRecord(ev1, st));
+    CGX_HIP(launch_finalize(FIN_CG1, s->d_pa, s->vec_grid, s->d_pb, sg,
+                            s->d_st, s->d_hist, nullptr, st));
+  }
+  return 0;
+}
+
+template <typename T>
+int enqueue_iters(cgx_solver *s, long long count) {
+  const int B = s->graph_batch;
+  const int key = s->alg * 2 + s->mode;
+  if (s->use_graph && count >= B) {
+    if (!s->gexec || s->gexec_key != key) {
+      drop_graph(s);
+      hipGraph_t g = nullptr;
+      CGX_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+      int rc = 0;
+      for (int i = 0; i < B && rc == 0; ++i)
+        rc = enqueue_iter<T>(s, nullptr, nullptr);
+      hipError_t e = hipStreamEndCapture(s->stream, &g);
+      if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      CGX_HIP(e);
+      e = hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      CGX_HIP(e);
+      s->gexec_key = key;
+    }
+    while (count >= B) {
+      CGX_HIP(hipGraphLaunch(s->gexec, s->stream));
+      count -= B;
+    }
+  }
+  for (long long i = 0; i < count; ++i) {
+    int rc = enqueue_iter<T>(s, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
+  if (hist_cap > s->hist_alloc) {
+    dfree((void **)&s->d_hist);
+    int rc = dalloc(s, (void **)&s->d_hist, (size_t)hist_cap * 8);
+    if (rc) return rc;
+    s->hist_alloc = hist_cap;
+  }
+  memset(s->h_st, 0, sizeof(CgState));
+  s->h_st->tol = tol;
+  s->h_st->use_tol = tol > 0.0 ? 1 : 0;
+  s->h_st->max_iter = maxit;
+  s->h_st->hist_cap = std::min(hist_cap, s->hist_alloc);
+  CGX_HIP(hipMemcpyAsync(s->d_st, s->h_st, sizeof(CgState),
+                         hipMemcpyHostToDevice, s->stream));
+  return 0;
+}
+
+int read_state(cgx_solver *s) {
+  CGX_HIP(hipMemcpyAsync(s->h_st, s->d_st, sizeof(CgState),
+                         hipMemcpyDeviceToHost, s->stream));
+  CGX_HIP(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+template <typename T>
+int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
+  int rc;
+  s->bench_ready = false;
+  if ((rc = prepare_state(s, maxit, tol, maxit + 1))) return rc;
+  if ((rc = enqueue_init<T>(s))) return rc;
+  const long long total = (long long)maxit + 1;
+  if (tol <= 0.0) {
+    if ((rc = enqueue_iters<T>(s, total))) return rc;
+    if ((rc = read_state(s))) return rc;
+  } else {
+    long long done_iters = 0, batch = 8;
+    for (;;) {
+      const long long b = std::min(batch, total - done_iters);
+      if ((rc = enqueue_iters<T>(s, b))) return rc;
+      done_iters += b;
+      if ((rc = read_state(s))) return rc;
+      if (s->h_st->done || done_iters >= total) break;
+      batch = std::min<long long>(batch * 2, 256);
+    }
+  }
+  if (!s->h_st->done) {
+    set_error("solver did not reach its stop condition");
+    return CGX_ENODEV;
+  }
+  s->last_iters = s->h_st->k + 1;
+  if (iters) *iters = s->last_iters;
+  return 0;
+}
+
+template <typename T>
+int bench_prepare_t(cgx_solver *s, int warmup) {
+  int rc;
+  if ((rc = prepare_state(s, INT_MAX - 1, 0.0, 0))) return rc;
+  if ((rc = enqueue_init<T>(s))) return rc;
+  if ((rc = enqueue_iters<T>(s, warmup))) return rc;
+  CGX_HIP(hipStreamSynchronize(s->stream));
+  s->bench_ready = true;
+  return 0;
+}
+
+template <typename T>
+int bench_run_t(cgx_solver *s, int iters, int flags, double *total_ms,
+                double *spmv_ms) {
+  const bool per_spmv = (flags & CGX_BENCH_SPMV_EVENTS) != 0;
+  const size_t need = 2 + (per_spmv ? 2 * (size_t)iters : 0);
+  while (s->events.size() < need) {
+    hipEvent_t e;
+    CGX_HIP(hipEventCreate(&e));
+    s->events.push_back(e);
+  }
+  hipEvent_t e0 = s->events[0], e1 = s->events[1];
+  const bool graph_saved = s->use_graph;
+  s->use_graph = (flags & CGX_BENCH_GRAPH) != 0;
+  int rc = 0;
+  CGX_HIP(hipEventRecord(e0, s->stream));
+  if (per_spmv) {
+    for (int i = 0; i < iters && !rc; ++i)
+      rc = enqueue_iter<T>(s, s->events[2 + 2 * i], s->events[3 + 2 * i]);
+  } else {
+    rc = enqueue_iters<T>(s, iters);
+  }
+  s->use_graph = graph_saved;
+  if (rc) return rc;
+  CGX_HIP(hipEventRecord(e1, s->stream));
+  CGX_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CGX_HIP(hipEventElapsedTime(&ms, e0, e1));
+  *total_ms = ms;
+  *spmv_ms = -1.0;
+  if (per_spmv) {
+    double sum = 0.0;
+    for (int i = 0; i < iters; ++i) {
+      float m = 0.f;
+      CGX_HIP(hipEventElapsedTime(&m, s->events[2 + 2 * i], s->events[3 + 2 * i]));
+      sum += m;
+    }
+    *spmv_ms = iters > 0 ? sum / iters : 0.0;
+  }
+  if ((rc = read_state(s))) return rc;
+  if (s->h_st->done) {
+    set_error("bench: solver stopped early");
+    return CGX_EINVAL;
+  }
+  return 0;
+}
+
+template <typename T>
+int spmv_t(cgx_solver *s, const T *x, T *y) {
+  if (!s->have_matrix || (s->n > 0 && (!x || !y))) {
+    set_error("spmv: no matrix or NULL vector");
+    return CGX_EINVAL;
+  }
+  if ((sizeof(T) == 4) != (s->dtype == CGX_F32)) {
+    set_error("spmv: dtype does not match the matrix");
+    return CGX_EINVAL;
+  }
+  if (s->n == 0) return 0;
+  CGX_HIP(hipSetDevice(s->device));
+  CGX_HIP(hipMemcpyAsync(s->d_p, x, (size_t)s->n * sizeof(T),
+                         hipMemcpyHostToDevice, s->stream));
+  CGX_HIP(launch_spmv<T>(spmv_args<T>(s, s->d_p, s->d_s, nullptr, false),
+                         s->spmv_grid, s->vec, s->stream));
+  CGX_HIP(hipMemcpyAsync(y, s->d_s, (size_t)s->n * sizeof(T),
+                         hipMemcpyDeviceToHost, s->stream));
+  CGX_HIP(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+
+extern "C" {
+
+const char *cgx_last_error(void) { return cgx::g_err; }
+
+int cgx_device_count(void) {
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess) return 0;
+  return cnt;
+}
+
+int cgx_solver_create(int device, cgx_solver **out) {
+  if (!out) return CGX_EINVAL;
+  *out = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  CGX_HIP(hipSetDevice(device));
+  cgx_solver *s = new cgx_solver();
+  s->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess)
+    s->cus = prop.multiProcessorCount;
+  s->vec = cgx::env_int("CGX_SPMV_VEC", 2);
+  if (s->vec != 1 && s->vec != 2 && s->vec != 4) s->vec = 2;
+  s->use_graph = cgx::env_int("CGX_GRAPH", 1) != 0;
+  s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
+      hipHostMalloc((void **)&s->h_st, sizeof(CgState), hipHostMallocDefault) !=
+          hipSuccess) {
+    cgx::set_error("cgx_solver_create: stream/state allocation failed");
+    cgx_solver_destroy(s);
+    return CGX_ENODEV;
+  }
+  *out = s;
+  return 0;
+}
+
+void cgx_solver_destroy(cgx_solver *s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  free_matrix(s);
+  for (hipEvent_t e : s->events) (void)hipEventDestroy(e);
+  if (s->d_st) (void)hipFree(s->d_st);
+  if (s->h_st) (void)hipHostFree(s->h_st);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int cgx_solver_set_mode(cgx_solver *s, int mode, int alg) {
+  if (!s || (mode != CGX_MODE_FAST && mode != CGX_MODE_EXACT) ||
+      (alg != CGX_ALG_HS && alg != CGX_ALG_CG1)) {
+    cgx::set_error("set_mode: bad arguments");
+    return CGX_EINVAL;
+  }
+  if (mode == CGX_MODE_EXACT && alg != CGX_ALG_HS) {
+    cgx::set_error("exact mode is defined for the HS recurrence only");
+    return CGX_EINVAL;
+  }
+  s->mode = mode;
+  s->alg = alg;
+  drop_graph(s);
+  return 0;
+}
+
+int cgx_solver_set_matrix(cgx_solver *s, int n, int nnz, const int *row_ptr,
+                          const int *col, const double *val) {
+  if (!s) return CGX_EINVAL;
+  return upload_matrix<double>(s, n, nnz, row_ptr, col, val);
+}
+
+int cgx_solver_set_matrix_f32(cgx_solver *s, int n, int nnz,
+                              const int *row_ptr, const int *col,
+                              const float *val) {
+  if (!s) return CGX_EINVAL;
+  return upload_matrix<float>(s, n, nnz, row_ptr, col, val);
+}
+
+int cgx_solver_set_rhs(cgx_solver *s, const double *b) {
+  return s ? upload_rhs<double>(s, b) : CGX_EINVAL;
+}
+
+int cgx_solver_set_rhs_f32(cgx_solver *s, const float *b) {
+  return s ? upload_rhs<float>(s, b) : CGX_EINVAL;
+}
+
+int cgx_solver_run(cgx_solver *s, int maxit, double tol, int *iters) {
+  if (!s || !s->have_matrix || !s->have_rhs || maxit < 0) {
+    cgx::set_error("run: need matrix + rhs and maxit >= 0");
+    return CGX_EINVAL;
+  }
+  if (s->dtype == CGX_F32 && s->mode == CGX_MODE_EXACT) {
+    cgx::set_error("exact mode is fp64 only");
+    return CGX_EINVAL;
+  }
+  CGX_HIP(hipSetDevice(s->device));
+  if (s->n == 0) {  // empty system: nothing to iterate, x is empty
+    s->last_iters = maxit + 1;
+    if (iters) *iters = s->last_iters;
+    return 0;
+  }
+  return s->dtype == CGX_F32 ? run_t<float>(s, maxit, tol, iters)
+                             : run_t<double>(s, maxit, tol, iters);
+}
+
+int cgx_solver_get_x(cgx_solver *s, double *x) {
+  if (!s || !s->have_matrix || s->dtype != CGX_F64 || (s->n && !x))
+    return CGX_EINVAL;
+  CGX_HIP(hipSetDevice(s->device));
+  CGX_HIP(hipMemcpy(x, s->d_x, (size_t)s->n * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int cgx_solver_get_x_f32(cgx_solver *s, float *x) {
+  if (!s || !s->have_matrix || s->dtype != CGX_F32 || (s->n && !x))
+    return CGX_EINVAL;
+  CGX_HIP(hipSetDevice(s->device));
+  CGX_HIP(hipMemcpy(x, s->d_x, (size_t)s->n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int cgx_solver_get_history(cgx_solver *s, double *rr, int cap) {
+  if (!s || !rr || cap < 0) return CGX_EINVAL;
+  const int m = std::min(cap, std::min(s->last_iters, s->hist_alloc));
+  if (m <= 0) return 0;
+  CGX_HIP(hipSetDevice(s->device));
+  CGX_HIP(hipMemcpy(rr, s->d_hist, (size_t)m * 8, hipMemcpyDeviceToHost));
+  return m;
+}
+
+int cgx_solver_spmv(cgx_solver *s, const double *x, double *y) {
+  return s ? spmv_t<double>(s, x, y) : CGX_EINVAL;
+}
+
+int cgx_solver_spmv_f32(cgx_solver *s, const float *x, float *y) {
+  return s ? spmv_t<float>(s, x, y) : CGX_EINVAL;
+}
+
+int cgx_solver_info(cgx_solver *s, cgx_info *info) {
+  if (!s || !info) return CGX_EINVAL;
+  const double sv = (double)tsize(s->dtype);
+  info->n = s->n;
+  info->nnz = s->nnz;
+  info->dtype = s->dtype;
+  info->mode = s->mode;
+  info->alg = s->alg;
+  info->n_rowblocks = s->nblk;
+  info->spmv_grid = s->spmv_grid;
+  info->vec_grid = s->vec_grid;
+  // B_spmv = nnz*(s_v+4) + 4*(n+1) + 2*n*s_v; B_iter = B_spmv + 9*n*s_v
+  info->spmv_bytes = (double)s->nnz * (sv + 4) + 4.0 * (s->n + 1) + 2.0 * s->n * sv;
+  info->iter_bytes = info->spmv_bytes + 9.0 * s->n * sv;
+  info->device_bytes = s->dev_bytes;
+  return 0;
+}
+
+int cgx_solver_bench_prepare(cgx_solver *s, int warmup) {
+  if (!s || !s->have_matrix || !s->have_rhs || s->n == 0 || warmup < 0) {
+    cgx::set_error("bench_prepare: need a non-empty system and warmup >= 0");
+    return CGX_EINVAL;
+  }
+  if (s->mode == CGX_MODE_EXACT && s->dtype == CGX_F32) return CGX_EINVAL;
+  CGX_HIP(hipSetDevice(s->device));
+  return s->dtype == CGX_F32 ? bench_prepare_t<float>(s, warmup)
+                             : bench_prepare_t<double>(s, warmup);
+}
+
+int cgx_solver_bench_run(cgx_solver *s, int iters, int flags, double *total_ms,
+                         double *spmv_ms) {
+  if (!s || !s->bench_ready || iters < 1 || !total_ms || !spmv_ms) {
+    cgx::set_error("bench_run: call cgx_solver_bench_prepare first; iters >= 1");
+    return CGX_EINVAL;
+  }
+  CGX_HIP(hipSetDevice(s->device));
+  return s->dtype == CGX_F32
+             ? bench_run_t<float>(s, iters, flags, total_ms, spmv_ms)
+             : bench_run_t<double>(s, iters, flags, total_ms, spmv_ms);
+}
+
+int cgx_solver_bench(cgx_solver *s, int warmup, int iters, int flags,
+                     double *total_ms, double *spmv_ms) {
+  int rc = cgx_solver_bench_prepare(s, warmup);
+  if (rc) return rc;
+  return cgx_solver_bench_run(s, iters, flags, total_ms, spmv_ms);
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+/* cgx.h -- C ABI of libcgx.so, the MI355X-native (gfx950) Conjugate-Gradient
+ * solver that drops in for rnelias/Conjugate-Gradient's hot path
+ * (cg.c:88-141 conj_grad + mv_ops.c:117-259).
+ *
+ * Plain C types only (pointers + sizes); every pointer argument is a HOST
+ * pointer unless the name says otherwise.  All int-returning calls return
+ * >= 0 on success and < 0 on failure; cgx_last_error() describes the last
+ * failure of the calling thread.  There is no CPU fallback: without a usable
+ * gfx950 device every compute call fails with CGX_ENODEV.
+ */
+#ifndef CGX_H
+#define CGX_H
+
+#include <stddef.h>
+#include "mv_ops.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGX_EINVAL  (-1) /* NULL argument or size mismatch (reference convention) */
+#define CGX_ENODEV  (-2) /* no GPU / HIP failure                                  */
+#define CGX_ENOMEM  (-3) /* device or host allocation failed                       */
+#define CGX_ECOMM   (-4) /* RCCL failure                                          */
+
+/* ------------------------------------------------------------------------
+ * 1. Reference-compatible solver entry points
+ * ------------------------------------------------------------------------ */
+
+/* Replaces cg.c:88-141 (declared only at cg.c:24 in the reference).
+ * Hestenes-Stiefel CG from x0 = 0, exactly max_iter+1 SpMVs, no tolerance;
+ * *vec_x receives a freshly allocated host vector (any previous *vec_x is
+ * ignored, as in the reference, cg.c:104,138).  Returns 0 (the reference
+ * always returns 0) or < 0 on a device/argument failure.
+ * Environment: CGX_MODE=exact selects the reference's sequential dot-product
+ * order (bit-identical x on chained matrices); default is the parallel
+ * reduction order (x within fp64 rounding of the reference).
+ * CGX_DEVICE=<ordinal> picks the GPU (default 0). */
+int conj_grad(int max_iter, struct __mv_sparse *mat_A,
+              struct __mv_sparse *vec_b, struct __mv_sparse **vec_x);
+
+/* The north-star entry point (BASELINE.json): a superset of conj_grad.
+ * Same recurrences; stops after the r-update (the cg.c:125 position) when
+ * k == maxit or r.r <= tol*tol*b.b.  tol <= 0 is exactly conj_grad(maxit).
+ * Returns the number of x-updates performed (k+1 SpMVs), or < 0. */
+int solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
+          struct __mv_sparse **x, double tol, int maxit);
+
+/* Frees a struct and its arrays (the reference's free_mv_struct frees only
+ * the shell, mv_ops.c:39-42, which libcgx keeps for drop-in safety). */
+void cgx_free_mv_deep(struct __mv_sparse *m);
+
+const char *cgx_last_error(void);
+int cgx_device_count(void);
+
+/* ------------------------------------------------------------------------
+ * 2. Solver object: device-resident CSR, repeated solves, benchmarking
+ * ------------------------------------------------------------------------ */
+
+typedef struct cgx_solver cgx_solver;
+
+enum { CGX_MODE_FAST = 0,    /* two-stage parallel reductions (default)      */
+       CGX_MODE_EXACT = 1 }; /* sequential dots: reference bit order          */
+enum { CGX_ALG_HS = 0,       /* Hestenes-Stiefel, the reference recurrence    */
+       CGX_ALG_CG1 = 1 };    /* Chronopoulos-Gear, one fused reduction/iter   */
+enum { CGX_F64 = 0, CGX_F32 = 1 };
+
+typedef struct {
+  int n, nnz, dtype, mode, alg;
+  int n_rowblocks;      /* LDS-staged row blocks of the SpMV plan            */
+  int spmv_grid;        /* workgroups of the persistent SpMV launch          */
+  int vec_grid;         /* workgroups of the vector-update launches          */
+  double spmv_bytes;    /* algorithmic HBM bytes per SpMV     */
+  double iter_bytes;    /* algorithmic HBM bytes per CG iteration            */
+  size_t device_bytes;  /* device memory held by the solver                  */
+} cgx_info;
+
+int  cgx_solver_create(int device, cgx_solver **out);
+void cgx_solver_destroy(cgx_solver *s);
+int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
+/* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.
+ * Columns must be ascending within each row for bit-exact SpMV order. */
+int  cgx_solver_set_matrix(cgx_solver *s, int n, int nnz, const int *row_ptr,
+                           const int *col, const double *val);
+int  cgx_solver_set_matrix_f32(cgx_solver *s, int n, int nnz,
+                               const int *row_ptr, const int *col,
+                               const float *val);
+/* Right-hand side, length n, in the matrix's dtype. */
+int  cgx_solver_set_rhs(cgx_solver *s, const double *b);
+int  cgx_solver_set_rhs_f32(cgx_solver *s, const float *b);
+/* x0 = 0; stop rule as solve().  *iters = x-updates performed. */
+int  cgx_solver_run(cgx_solver *s, int maxit, double tol, int *iters);
+int  cgx_solver_get_x(cgx_solver *s, double *x);
+int  cgx_solver_get_x_f32(cgx_solver *s, float *x);
+/* r.r after each x-update of the last run (length >= iters). */
+int  cgx_solver_get_history(cgx_solver *s, double *rr, int cap);
+/* One y = A x with the loaded matrix (op-level parity). */
+int  cgx_solver_spmv(cgx_solver *s, const double *x, double *y);
+int  cgx_solver_spmv_f32(cgx_solver *s, const float *x, float *y);
+int  cgx_solver_info(cgx_solver *s, cgx_info *info);
+
+/* Benchmark hooks.  cgx_solver_bench_prepare: x0 = 0 prologue plus `warmup`
+ * untimed CG iterations (tol = 0, no iteration limit), then a device sync.
+ * cgx_solver_bench_run: `iters` further iterations of the same recurrence,
+ * timed with HIP events on the solver's stream; returns after they finished.
+ * flags & CGX_BENCH_GRAPH: replay the iteration loop as hipGraphs.
+ * flags & CGX_BENCH_SPMV_EVENTS: also bracket every SpMV launch with events
+ *   and report its average duration in *spmv_ms (else *spmv_ms = -1).
+ * cgx_solver_bench = prepare + run. */
+#define CGX_BENCH_GRAPH        1
+#define CGX_BENCH_SPMV_EVENTS  2
+int  cgx_solver_bench_prepare(cgx_solver *s, int warmup);
+int  cgx_solver_bench_run(cgx_solver *s, int iters, int flags, double *total_ms,
+                          double *spmv_ms);
+int  cgx_solver_bench(cgx_solver *s, int warmup, int iters, int flags,
+                      double *total_ms, double *spmv_ms);
+
+/* ------------------------------------------------------------------------
+ * 3. Synthetic SPD generators (host, row range [row_begin, row_end))
+ *    Two-pass: call with row_ptr == NULL to get the nnz of the range, then
+ *    with arrays of that size.  row_ptr is local (starts at 0); columns are
+ *    global indices.  Return nnz or < 0.
+ * ------------------------------------------------------------------------ */
+long long cgx_gen_laplacian2d(int nx, int ny, int row_begin, int row_end,
+                              int *row_ptr, int *col, double *val);
+long long cgx_gen_laplacian3d(int nx, int ny, int nz, int row_begin,
+                              int row_end, int *row_ptr, int *col, double *val);
+/* Random SPD: tridiagonal band + `partners` random partner columns per row
+ * from a splitmix64 stream (seed), symmetrised, off-diagonals -U(0,1],
+ * diagonal = sum|offdiag| + 1.  Values written as f32 when val32 != NULL. */
+long long cgx_gen_random_spd(int n, int partners, unsigned long long seed,
+                             int row_begin, int row_end, int *row_ptr,
+                             int *col, double *val, float *val32);
+/* 1 if the CSR is "chained" (ascending cols, no empty row,
+ * first_col(r+1) <= last_col(r)): the class on which the reference's
+ * dense-row mv_mult equals CSR SpMV. */
+int cgx_csr_is_chained(int n, const int *row_ptr, const int *col);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CGX_H */
