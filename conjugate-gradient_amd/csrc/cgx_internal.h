@@ -47,9 +47,14 @@ struct CgState {
 static_assert(sizeof(CgState) == 96, "CgState layout");
 
 // -------------------------------------------------------------- geometry
-constexpr int kSpmvBS = 256;          // rows per LDS row block (one per lane)
-constexpr int kSpmvCapF64 = 2048;     // LDS product slots per row block (16 KiB)
-constexpr int kSpmvCapF32 = 4096;     // (16 KiB)
+// SpMV row block: bs (256 or 512) rows, one per lane, and at most
+// spmv_cap(bs) products staged in LDS (16 KiB per 256 lanes).
+inline int spmv_cap(int bs, bool f64) { return bs * (f64 ? 8 : 16); }
+// Workgroups of one SpMV launch (= fused-dot partials it writes).
+inline int spmv_launch_grid(int bs, int wpb, int rbw, int nblk, int grid) {
+  if (bs == 64) return (nblk + wpb * rbw - 1) / (wpb * rbw);
+  return grid < 1 ? 1 : (grid > nblk ? nblk : grid);
+}
 constexpr int kVecBS = 256;
 constexpr int kFinBS = 1024;
 constexpr int kPad = 8;               // val/col padded to a multiple of this
@@ -72,15 +77,23 @@ struct SpmvArgs {
   const T *x;
   T *y;
   const int *blk_row;  // row-block boundaries, nblk_total+1 entries
+  const int *blk_k;    // rp[blk_row[i]]: nonzero offset of each row block
   const int *blk_list; // optional subset of row blocks (nullptr: 0..nblk-1)
   int nblk;            // row blocks processed by this launch
   double *part;        // per-workgroup partial of x[row]*y[row] (nullptr: none)
   const int *done;     // early-exit flag (nullptr: never)
+  int xcd;             // XCD-aware chunk mapping (speed only)
+  int nt;              // non-temporal val/col stream loads
+  int bs;              // rows per row block: 256 | 512 (workgroup-wide block),
+                       // 64 (one row block per wave, k_spmv_wave)
+  int wpb;             // k_spmv_wave: waves per workgroup (4 | 8)
+  int rbw;             // k_spmv_wave: row blocks per wave
+  int pipe;            // k_spmv_wave: prefetch the next row block's stream
 };
 
-// Row-block plan: consecutive rows, at most kSpmvBS rows and `cap` nonzeros
+// Row-block plan: consecutive rows, at most `rows` rows and `cap` nonzeros
 // per block; a row longer than `cap` gets a block of its own (chunked path).
-std::vector<int> plan_rowblocks(int n, const int *rp, int cap);
+std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap);
 
 // ------------------------------------------------------------- launchers
 // All launchers are graph-capturable (no sync, no allocation).

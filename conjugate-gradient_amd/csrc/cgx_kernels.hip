@@ -63,60 +63,109 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
 // coalesced VEC-wide loads of val/col; the products val[k]*x[col[k]] land in
 // LDS; then lane t sums row t's products sequentially in column order from
 // 0.0 -- the reference's per-row order (mv_ops.c:190-194), so y is
-// bit-identical to it on chained matrices.  The grid is persistent: workgroup
-// g owns a contiguous chunk of row blocks (x-gather locality in L1/L2) and
-// accumulates the fused x.y epilogue over its chunk in a fixed order.
-template <typename T, int BS, int CAP, int VEC, bool EPI>
+// bit-identical to it on chained matrices.
+//
+// Latency structure (one row block): every val/col load of the block is
+// issued before the first wait (NIT x VEC elements per lane in registers),
+// then every x gather, then the products -- two memory round trips per row
+// block instead of two per element.  The grid is persistent: workgroup g owns
+// a contiguous chunk of row blocks and accumulates the fused x.y epilogue
+// over its chunk in a fixed order.  With XCD = true the chunk index is
+// remapped so the workgroups that share an XCD (blockIdx % 8, the observed
+// round-robin dispatch; speed only, never correctness) own one contiguous
+// 1/8 of the rows, keeping the +-plane x re-reads inside that XCD's L2.
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p, bool nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+
+template <typename T, int BS, int CAP, int VEC, bool EPI, bool NT>
 __global__ __launch_bounds__(BS) void k_spmv(SpmvArgs<T> a) {
-  __shared__ T prod[CAP];
-  __shared__ int srp[BS + 1];
+  constexpr int NIT = CAP / (BS * VEC);  // load iterations per row block
+  static_assert(NIT * BS * VEC == CAP, "CAP must be a multiple of BS*VEC");
+  typedef T tv __attribute__((ext_vector_type(VEC)));
+  typedef int iv __attribute__((ext_vector_type(VEC)));
+  __shared__ __attribute__((aligned(16))) T prod[CAP];
   __shared__ double red[BS / kWave];
   if (a.done && *a.done) return;
 
   const int tid = threadIdx.x;
   const int G = gridDim.x;
-  const int lo = (int)(((long long)a.nblk * blockIdx.x) / G);
-  const int hi = (int)(((long long)a.nblk * (blockIdx.x + 1)) / G);
+  int g = blockIdx.x;
+  if (a.xcd && (G & 7) == 0) g = (g & 7) * (G >> 3) + (g >> 3);
+  const int lo = (int)(((long long)a.nblk * g) / G);
+  const int hi = (int)(((long long)a.nblk * (g + 1)) / G);
   double dot = 0.0;
 
   for (int i = lo; i < hi; ++i) {
     const int rb = a.blk_list ? a.blk_list[i] : i;
+    // Row-block descriptor: rows [r0, r0+nr), nonzeros [k0, k1) -- wave-
+    // uniform scalar loads, so the stream loads below issue without waiting
+    // on row_ptr.
     const int r0 = a.blk_row[rb];
     const int nr = a.blk_row[rb + 1] - r0;
-    for (int t = tid; t <= nr; t += BS) srp[t] = a.rp[r0 + t];
-    __syncthreads();
-    const int k0 = srp[0], k1 = srp[nr];
+    const int k0 = a.blk_k[rb], k1 = a.blk_k[rb + 1];
+    const int kb = k0 & ~(VEC - 1);
+    // Per-row bounds for the reduce phase and the epilogue operand: issued
+    // together with the stream, consumed after the barrier.
+    int j0 = 0, j1 = 0;
+    T xrow = T(0);
+    if (tid < nr) {
+      j0 = a.rp[r0 + tid];
+      j1 = a.rp[r0 + tid + 1];
+      if (EPI) xrow = a.x[r0 + tid];
+    }
 
-    if (k1 - k0 <= CAP) {
-      if (VEC == 1) {
-        for (int k = k0 + tid; k < k1; k += BS)
-          prod[k - k0] = a.val[k] * a.x[a.col[k]];
-      } else {
-        // VEC-aligned vector loads; val/col are padded to a multiple of
-        // kPad, so the aligned window never leaves the allocation.
-        typedef T tv __attribute__((ext_vector_type(VEC)));
-        typedef int iv __attribute__((ext_vector_type(VEC)));
-        const int kb = k0 & ~(VEC - 1);
-        for (int kk = kb + tid * VEC; kk < k1; kk += BS * VEC) {
-          const tv v = *reinterpret_cast<const tv *>(a.val + kk);
-          const iv c = *reinterpret_cast<const iv *>(a.col + kk);
+    if (k1 - kb <= CAP) {  // always true for multi-row blocks (planner cap)
+      tv v[NIT];
+      iv c[NIT];
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        int kk = kb + (it * BS + tid) * VEC;
+        kk = kk < k1 ? kk : kb;  // out-of-block lanes re-read a valid window
+        v[it] = ld_stream(reinterpret_cast<const tv *>(a.val + kk), NT);
+        c[it] = ld_stream(reinterpret_cast<const iv *>(a.col + kk), NT);
+      }
+      T xv[NIT][VEC];
+#pragma unroll
+      for (int it = 0; it < NIT; ++it)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const int k = kb + (it * BS + tid) * VEC + j;
+          const bool ok = k >= k0 && k < k1;
+          xv[it][j] = a.x[ok ? c[it][j] : 0];
+        }
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int kk = kb + (it * BS + tid) * VEC;
+        if (kk >= k0 && kk + VEC <= k1) {
+          tv pv;
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) pv[j] = v[it][j] * xv[it][j];
+          *reinterpret_cast<tv *>(prod + (kk - k0)) = pv;
+        } else {
 #pragma unroll
           for (int j = 0; j < VEC; ++j) {
             const int k = kk + j;
-            if (k >= k0 && k < k1) prod[k - k0] = v[j] * a.x[c[j]];
+            if (k >= k0 && k < k1) prod[k - k0] = v[it][j] * xv[it][j];
           }
         }
       }
       __syncthreads();
       if (tid < nr) {
-        const int j0 = srp[tid] - k0, j1 = srp[tid + 1] - k0;
+        int j = j0 - k0;
+        const int je = j1 - k0;
         T acc = T(0);
-        for (int j = j0; j < j1; ++j) acc = acc + prod[j];
-        a.y[r0 + tid] = acc;
-        if (EPI) {
-          const double xv = (double)a.x[r0 + tid];
-          dot = dot + xv * (double)acc;
+        for (; j + 4 <= je; j += 4) {  // 4 LDS reads in flight, adds in order
+          const T p0 = prod[j], p1 = prod[j + 1], p2 = prod[j + 2], p3 = prod[j + 3];
+          acc = acc + p0;
+          acc = acc + p1;
+          acc = acc + p2;
+          acc = acc + p3;
         }
+        for (; j < je; ++j) acc = acc + prod[j];
+        a.y[r0 + tid] = acc;
+        if (EPI) dot = dot + (double)xrow * (double)acc;
       }
     } else {
       // One row longer than CAP (planner guarantees nr == 1): stream it in
@@ -133,14 +182,187 @@ __global__ __launch_bounds__(BS) void k_spmv(SpmvArgs<T> a) {
       }
       if (tid == 0) {
         a.y[r0] = acc;
-        if (EPI) dot = dot + (double)a.x[r0] * (double)acc;
+        if (EPI) dot = dot + (double)xrow * (double)acc;
       }
     }
-    __syncthreads();  // srp/prod are reused by the next row block
+    if (i + 1 < hi) __syncthreads();  // prod is reused by the next row block
   }
   if (EPI) {
     const double s = block_sum<BS>(dot, red);
     if (tid == 0) a.part[blockIdx.x] = s;
+  }
+}
+
+// Wave-independent CSR-stream: the same algorithm with 64-row row blocks per
+// WAVE (CAPW products in the wave's own LDS slice), so a wave never waits on
+// a workgroup barrier in the main path and the 32 waves of a CU stream and
+// gather independently.  Each wave walks RBW consecutive row blocks; with
+// PIPE the stream loads (val/col) of block i+1 are issued before block i's
+// gathers are consumed, keeping two blocks of stream in flight per wave.  The
+// workgroup meets once, at the end, to combine the fused x.y epilogue.
+template <typename T, int CAPW, int VEC>
+struct WaveBlock {
+  static constexpr int NIT = CAPW / (kWave * VEC);
+  typedef T tv __attribute__((ext_vector_type(VEC)));
+  typedef int iv __attribute__((ext_vector_type(VEC)));
+  int r0, nr, k0, k1, kb;
+  tv v[NIT];
+  iv c[NIT];
+
+  __device__ __forceinline__ void describe(const SpmvArgs<T> &a, int wb) {
+    const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : wb);
+    r0 = __builtin_amdgcn_readfirstlane(a.blk_row[rb]);
+    nr = __builtin_amdgcn_readfirstlane(a.blk_row[rb + 1]) - r0;
+    k0 = __builtin_amdgcn_readfirstlane(a.blk_k[rb]);
+    k1 = __builtin_amdgcn_readfirstlane(a.blk_k[rb + 1]);
+    kb = k0 & ~(VEC - 1);
+  }
+  template <bool NT>
+  __device__ __forceinline__ void stream(const SpmvArgs<T> &a, int lane) {
+    if (k1 - kb > CAPW) return;  // long row: chunked path loads itself
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      int kk = kb + (it * kWave + lane) * VEC;
+      kk = kk < k1 ? kk : kb;  // out-of-block lanes re-read a valid window
+      v[it] = ld_stream(reinterpret_cast<const tv *>(a.val + kk), NT);
+      c[it] = ld_stream(reinterpret_cast<const iv *>(a.col + kk), NT);
+    }
+  }
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave complete in order; the fences keep the compiler from
+  // moving reads of other lanes' slots above the writes.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T, int CAPW, int VEC, bool EPI>
+__device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
+                                                    WaveBlock<T, CAPW, VEC> &B,
+                                                    T *prod, int lane) {
+  typedef WaveBlock<T, CAPW, VEC> WB;
+  const int r0 = B.r0, nr = B.nr, k0 = B.k0, k1 = B.k1, kb = B.kb;
+  int j0 = 0, j1 = 0;
+  T xrow = T(0);
+  if (lane < nr) {
+    j0 = a.rp[r0 + lane];
+    j1 = a.rp[r0 + lane + 1];
+    if (EPI) xrow = a.x[r0 + lane];
+  }
+  T acc = T(0);
+  if (k1 - kb <= CAPW) {
+    T xv[WB::NIT][VEC];
+#pragma unroll
+    for (int it = 0; it < WB::NIT; ++it)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const int k = kb + (it * kWave + lane) * VEC + j;
+        const bool ok = k >= k0 && k < k1;
+        xv[it][j] = a.x[ok ? B.c[it][j] : 0];
+      }
+#pragma unroll
+    for (int it = 0; it < WB::NIT; ++it) {
+      const int kk = kb + (it * kWave + lane) * VEC;
+      if (kk >= k0 && kk + VEC <= k1) {
+        typename WB::tv pv;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) pv[j] = B.v[it][j] * xv[it][j];
+        *reinterpret_cast<typename WB::tv *>(prod + (kk - k0)) = pv;
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const int k = kk + j;
+          if (k >= k0 && k < k1) prod[k - k0] = B.v[it][j] * xv[it][j];
+        }
+      }
+    }
+    wave_lds_sync();
+    if (lane < nr) {
+      int j = j0 - k0;
+      const int je = j1 - k0;
+      for (; j + 4 <= je; j += 4) {  // 4 LDS reads in flight, adds in order
+        const T p0 = prod[j], p1 = prod[j + 1], p2 = prod[j + 2], p3 = prod[j + 3];
+        acc = acc + p0;
+        acc = acc + p1;
+        acc = acc + p2;
+        acc = acc + p3;
+      }
+      for (; j < je; ++j) acc = acc + prod[j];
+    }
+    wave_lds_sync();  // the slot is rewritten by the next row block
+  } else {
+    // a single row longer than the wave's slice (nr == 1): chunked, lane 0
+    // keeps the sequential sum
+    for (int c0 = k0; c0 < k1; c0 += CAPW) {
+      const int m = min(CAPW, k1 - c0);
+      for (int t = lane; t < m; t += kWave)
+        prod[t] = a.val[c0 + t] * a.x[a.col[c0 + t]];
+      wave_lds_sync();
+      if (lane == 0)
+        for (int j = 0; j < m; ++j) acc = acc + prod[j];
+      wave_lds_sync();
+    }
+  }
+  double d = 0.0;
+  if (lane < nr) {
+    a.y[r0 + lane] = acc;
+    if (EPI) d = (double)xrow * (double)acc;
+  }
+  return d;
+}
+
+template <typename T, int WPB, int CAPW, int VEC, bool EPI, bool NT, bool PIPE>
+__global__ __launch_bounds__(WPB * kWave, PIPE ? 4 : 8) void k_spmv_wave(SpmvArgs<T> a) {
+  __shared__ __attribute__((aligned(16))) T lds[WPB * CAPW];
+  __shared__ double red[WPB];
+  if (a.done && *a.done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  T *prod = lds + wid * CAPW;
+  const int RBW = a.rbw;
+  const int first = (blockIdx.x * WPB + wid) * RBW;
+  const int last = min(first + RBW, a.nblk);
+  double dot = 0.0;
+  if (PIPE) {
+    WaveBlock<T, CAPW, VEC> B[2];
+    if (first < last) {
+      B[0].describe(a, first);
+      B[0].template stream<NT>(a, lane);
+    }
+    for (int i = first; i < last; i += 2) {
+      if (i + 1 < last) {
+        B[1].describe(a, i + 1);
+        B[1].template stream<NT>(a, lane);
+      }
+      dot = dot + wave_block_finish<T, CAPW, VEC, EPI>(a, B[0], prod, lane);
+      if (i + 1 < last) {
+        if (i + 2 < last) {
+          B[0].describe(a, i + 2);
+          B[0].template stream<NT>(a, lane);
+        }
+        dot = dot + wave_block_finish<T, CAPW, VEC, EPI>(a, B[1], prod, lane);
+      }
+    }
+  } else {
+    for (int i = first; i < last; ++i) {
+      WaveBlock<T, CAPW, VEC> B;
+      B.describe(a, i);
+      B.template stream<NT>(a, lane);
+      dot = dot + wave_block_finish<T, CAPW, VEC, EPI>(a, B, prod, lane);
+    }
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) s = s + red[w];
+      a.part[blockIdx.x] = s;
+    }
   }
 }
 
@@ -403,11 +625,23 @@ __global__ __launch_bounds__(BS) void k_dot_part(int n, const T *__restrict__ a,
 template <int BS>
 __device__ __forceinline__ double sum_parts(const double *pa, int na,
                                             double *red) {
+  // Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order; loads are
+  // issued 16 at a time (coalesced across the workgroup) before their adds.
+  constexpr int U = 16;
   double acc = 0.0;
-  if ((int)threadIdx.x < na) {
-    acc = pa[threadIdx.x];
-    for (int i = threadIdx.x + BS; i < na; i += BS) acc = acc + pa[i];
+  int i = threadIdx.x;
+  if (i < na) {
+    acc = pa[i];
+    i += BS;
   }
+  for (; i + (U - 1) * BS < na; i += U * BS) {
+    double v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = pa[i + j * BS];
+#pragma unroll
+    for (int j = 0; j < U; ++j) acc = acc + v[j];
+  }
+  for (; i < na; i += BS) acc = acc + pa[i];
   const double s = block_sum<BS>(acc, red);
   __syncthreads();
   return s;
@@ -509,23 +743,69 @@ __global__ __launch_bounds__(256) void k_gather(int m, const int *__restrict__ i
 
 // ------------------------------------------------------------- launchers
 
+template <typename T, int BS>
+static void launch_spmv_bs(const SpmvArgs<T> &a, int grid, int vec,
+                           hipStream_t st) {
+  constexpr int CAP = BS * (sizeof(T) == 8 ? 8 : 16);  // 16 KiB LDS per 256 lanes
+  const bool epi = a.part != nullptr;
+#define CGX_SPMV(V, E, N)                                                      \
+  hipLaunchKernelGGL((k_spmv<T, BS, CAP, V, E, N>), dim3(grid), dim3(BS), 0,  \
+                     st, a)
+#define CGX_SPMV_V(V)                                                          \
+  do {                                                                         \
+    if (a.nt) {                                                                \
+      if (epi) CGX_SPMV(V, true, true); else CGX_SPMV(V, false, true);        \
+    } else {                                                                   \
+      if (epi) CGX_SPMV(V, true, false); else CGX_SPMV(V, false, false);      \
+    }                                                                          \
+  } while (0)
+  if (vec == 4) CGX_SPMV_V(4);
+  else if (vec == 2) CGX_SPMV_V(2);
+  else CGX_SPMV_V(1);
+#undef CGX_SPMV_V
+#undef CGX_SPMV
+}
+
+template <typename T, int WPB>
+static void launch_spmv_wave(const SpmvArgs<T> &a, int vec, hipStream_t st) {
+  constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;  // 4 KiB LDS per wave
+  const int per = WPB * (a.rbw < 1 ? 1 : a.rbw);
+  const int grid = (a.nblk + per - 1) / per;
+  const bool epi = a.part != nullptr;
+#define CGX_SPMVW(V, E, N, P)                                                  \
+  hipLaunchKernelGGL((k_spmv_wave<T, WPB, CAPW, V, E, N, P>), dim3(grid),     \
+                     dim3(WPB * kWave), 0, st, a)
+#define CGX_SPMVW_P(V, N)                                                      \
+  do {                                                                         \
+    if (a.pipe) {                                                              \
+      if (epi) CGX_SPMVW(V, true, N, true); else CGX_SPMVW(V, false, N, true); \
+    } else {                                                                   \
+      if (epi) CGX_SPMVW(V, true, N, false); else CGX_SPMVW(V, false, N, false); \
+    }                                                                          \
+  } while (0)
+#define CGX_SPMVW_V(V)                                                         \
+  do {                                                                         \
+    if (a.nt) CGX_SPMVW_P(V, true); else CGX_SPMVW_P(V, false);               \
+  } while (0)
+  if (vec == 4) CGX_SPMVW_V(4);
+  else if (vec == 2) CGX_SPMVW_V(2);
+  else CGX_SPMVW_V(1);
+#undef CGX_SPMVW_V
+#undef CGX_SPMVW_P
+#undef CGX_SPMVW
+}
+
 template <typename T>
 hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) {
-  constexpr int CAP = sizeof(T) == 8 ? kSpmvCapF64 : kSpmvCapF32;
   if (a.nblk <= 0) return hipSuccess;
-  grid = grid < 1 ? 1 : (grid > a.nblk ? a.nblk : grid);
-  const bool epi = a.part != nullptr;
-#define CGX_SPMV(V, E)                                                         \
-  hipLaunchKernelGGL((k_spmv<T, kSpmvBS, CAP, V, E>), dim3(grid), dim3(kSpmvBS), \
-                     0, st, a)
-  if (vec == 4) {
-    if (epi) CGX_SPMV(4, true); else CGX_SPMV(4, false);
-  } else if (vec == 2) {
-    if (epi) CGX_SPMV(2, true); else CGX_SPMV(2, false);
-  } else {
-    if (epi) CGX_SPMV(1, true); else CGX_SPMV(1, false);
+  if (a.bs == 64) {
+    if (a.wpb == 8) launch_spmv_wave<T, 8>(a, vec, st);
+    else launch_spmv_wave<T, 4>(a, vec, st);
+    return hipGetLastError();
   }
-#undef CGX_SPMV
+  grid = grid < 1 ? 1 : (grid > a.nblk ? a.nblk : grid);
+  if (a.bs == 512) launch_spmv_bs<T, 512>(a, grid, vec, st);
+  else launch_spmv_bs<T, 256>(a, grid, vec, st);
   return hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ void set_error(const char *fmt, ...) {
   va_end(ap);
 }
 
-std::vector<int> plan_rowblocks(int n, const int *rp, int cap) {
+std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap) {
   std::vector<int> blk;
   blk.reserve((size_t)n / 128 + 2);
   blk.push_back(0);
@@ -43,7 +43,7 @@ std::vector<int> plan_rowblocks(int n, const int *rp, int cap) {
       blk.push_back(++r);
       continue;
     }
-    while (r < n && r - start < kSpmvBS && rp[r + 1] - k0 <= cap) ++r;
+    while (r < n && r - start < rows && rp[r + 1] - k0 <= cap) ++r;
     blk.push_back(r);
   }
   return blk;
@@ -74,10 +74,12 @@ struct cgx_solver {
   int n = 0, nnz = 0, dtype = CGX_F64;
   int mode = CGX_MODE_FAST, alg = CGX_ALG_HS;
   int vec = 2;
+  int spmv_xcd = 0, spmv_nt = 0, spmv_bs = 64, spmv_wpb = 4, spmv_rbw = 1,
+      spmv_pipe = 0;
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
   int graph_batch = 16;
-  int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr;
+  int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   void *d_val = nullptr;
   void *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr,
        *d_s = nullptr, *d_w = nullptr;
@@ -128,6 +130,7 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_rp);
   dfree((void **)&s->d_col);
   dfree((void **)&s->d_blk);
+  dfree((void **)&s->d_blkk);
   dfree(&s->d_val);
   dfree(&s->d_b);
   dfree(&s->d_x);
@@ -182,9 +185,9 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   s->dtype = sizeof(T) == 4 ? CGX_F32 : CGX_F64;
   s->n = n;
   s->nnz = nnz;
-  const int cap = sizeof(T) == 8 ? kSpmvCapF64 : kSpmvCapF32;
+  const int cap = spmv_cap(s->spmv_bs, sizeof(T) == 8);
   std::vector<int> blk;
-  if (n > 0) blk = plan_rowblocks(n, rp, cap);
+  if (n > 0) blk = plan_rowblocks(n, rp, s->spmv_bs, cap - kPad);  // room for VEC alignment
   else blk.push_back(0);
   s->nblk = (int)blk.size() - 1;
   const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kPad;
@@ -194,6 +197,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       (rc = dalloc(s, (void **)&s->d_col, nnz_pad * 4)) ||
       (rc = dalloc(s, &s->d_val, nnz_pad * sizeof(T))) ||
       (rc = dalloc(s, (void **)&s->d_blk, blk.size() * 4)) ||
+      (rc = dalloc(s, (void **)&s->d_blkk, blk.size() * 4)) ||
       (rc = dalloc(s, &s->d_b, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_x, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_r, nv * sizeof(T))) ||
@@ -203,8 +207,11 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
     free_matrix(s);
     return rc;
   }
-  s->spmv_grid = std::min(s->nblk, env_int("CGX_SPMV_GRID", s->cus * 8));
+  s->spmv_grid = std::min(s->nblk, env_int("CGX_SPMV_GRID", INT_MAX));
+  if (s->spmv_grid >= 64 && s->spmv_grid < s->nblk)
+    s->spmv_grid &= ~7;  // XCD-aware mapping needs G % 8 == 0
   if (s->spmv_grid < 1) s->spmv_grid = 1;
+  s->spmv_grid = spmv_launch_grid(s->spmv_bs, s->spmv_wpb, s->spmv_rbw, s->nblk, s->spmv_grid);
   s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
   s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
   if ((rc = dalloc(s, (void **)&s->d_pa, (size_t)s->part_cap * 8)) ||
@@ -224,7 +231,11 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
                              hipMemcpyHostToDevice, s->stream));
     }
   }
+  std::vector<int> blkk(blk.size());
+  for (size_t i = 0; i < blk.size(); ++i) blkk[i] = n > 0 ? rp[blk[i]] : 0;
   CGX_HIP(hipMemcpyAsync(s->d_blk, blk.data(), blk.size() * 4,
+                         hipMemcpyHostToDevice, s->stream));
+  CGX_HIP(hipMemcpyAsync(s->d_blkk, blkk.data(), blkk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
   s->have_matrix = true;
@@ -259,10 +270,17 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.x = (const T *)x;
   a.y = (T *)y;
   a.blk_row = s->d_blk;
+  a.blk_k = s->d_blkk;
   a.blk_list = nullptr;
   a.nblk = s->nblk;
   a.part = part;
   a.done = with_done ? &s->d_st->done : nullptr;
+  a.xcd = s->spmv_xcd;
+  a.nt = s->spmv_nt;
+  a.bs = s->spmv_bs;
+  a.wpb = s->spmv_wpb;
+  a.rbw = s->spmv_rbw;
+  a.pipe = s->spmv_pipe;
   return a;
 }
 
@@ -288,8 +306,7 @@ int enqueue_init(cgx_solver *s) {
     CGX_HIP(launch_spmv<T>(spmv_args<T>(s, r, s->d_w, s->d_pb, false),
                            s->spmv_grid, s->vec, st));
     CGX_HIP(launch_finalize(FIN_INIT_CG1, s->d_pa, s->vec_grid, s->d_pb,
-                            std::min(s->spmv_grid, std::max(s->nblk, 1)),
-                            s->d_st, s->d_hist, nullptr, st));
+                            s->spmv_grid, s->d_st, s->d_hist, nullptr, st));
   }
   return 0;
 }
@@ -300,7 +317,7 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   hipStream_t st = s->stream;
   T *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p, *sv = (T *)s->d_s,
     *w = (T *)s->d_w;
-  const int sg = std::min(s->spmv_grid, std::max(s->nblk, 1));
+  const int sg = s->spmv_grid;
   if (s->alg == CGX_ALG_HS) {
     const bool exact = s->mode == CGX_MODE_EXACT;
     if (ev0) CGX_HIP(hipEventRecord(ev0, st));
@@ -532,8 +549,17 @@ int cgx_solver_create(int device, cgx_solver **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess)
     s->cus = prop.multiProcessorCount;
-  s->vec = cgx::env_int("CGX_SPMV_VEC", 2);
-  if (s->vec != 1 && s->vec != 2 && s->vec != 4) s->vec = 2;
+  s->vec = cgx::env_int("CGX_SPMV_VEC", 4);
+  s->spmv_wpb = cgx::env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
+  s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", 1));
+  s->spmv_pipe = cgx::env_int("CGX_SPMV_PIPE", 0);
+  s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
+  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", 0);
+  {
+    const int bs = cgx::env_int("CGX_SPMV_BS", 64);
+    s->spmv_bs = (bs == 512 || bs == 64) ? bs : 256;
+  }
+  if (s->vec != 1 && s->vec != 2 && s->vec != 4) s->vec = 4;
   s->use_graph = cgx::env_int("CGX_GRAPH", 1) != 0;
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||

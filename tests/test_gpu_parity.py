@@ -65,13 +65,50 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
+@pytest.mark.parametrize("bs", ["64", "256", "512"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
-def test_spmv_vector_widths_bit_exact(vec, monkeypatch):
+def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
+    """Every SpMV variant (wave / workgroup row blocks, load widths) keeps the
+    sequential per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
+    monkeypatch.setenv("CGX_SPMV_BS", bs)
     rp, col, val, b = H.random_spd(4000, 9, seed=3)
+    g = H.load_golden("dense128")
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
+        s.set_matrix(g["row_ptr"], g["col"], g["val"])
+        assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"])
+        rp32, col32, v32 = cgx.random_spd(5000, 40, 9, f32=True)
+        x32 = np.random.default_rng(2).standard_normal(5000).astype(np.float32)
+        s.set_matrix(rp32, col32, v32)
+        assert np.array_equal(s.spmv(x32).view(np.uint32),
+                              H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
+        # a CG run through the fused-epilogue path
+        g = H.load_golden("lap3d_12")
+        s.set_matrix(g["row_ptr"], g["col"], g["val"])
+        s.set_rhs(g["b"])
+        s.run(20)
+        x_ref, _ = H.o_conj_grad(20, g["row_ptr"], g["col"], g["val"], g["b"])
+        assert rel(s.x(), x_ref) <= FAST_RTOL
+
+
+@pytest.mark.parametrize("bs", ["64", "256"])
+def test_spmv_long_rows_variants(bs, monkeypatch):
+    monkeypatch.setenv("CGX_SPMV_BS", bs)
+    n = 3000
+    rng = np.random.default_rng(8)
+    rows = [np.arange(n) if i in (0, 7, n - 1) else
+            np.unique(np.concatenate([[max(i - 1, 0), i, min(i + 1, n - 1)], rng.integers(0, n, 3)]))
+            for i in range(n)]
+    rp = np.zeros(n + 1, np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.standard_normal(len(col))
+    x = rng.standard_normal(n)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
 def test_spmv_long_rows_bit_exact(solver):

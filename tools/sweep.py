@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of SpMV/solver knobs in ONE process (methodology rule 24).
+
+  python tools/sweep.py --workload c3 --rounds 3 --iters 30 \
+      --variant base: --variant vec4:CGX_SPMV_VEC=4 --variant nt:CGX_SPMV_NT=1
+
+Each variant is a solver created with its CGX_* environment; the matrix is
+uploaded once per variant.  Prints per-variant median/min SpMV time and
+iteration time over the rounds."""
+import argparse
+import os
+import statistics
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "conjugate-gradient_amd"))
+sys.path.insert(0, str(REPO / "tests"))
+
+import bench  # noqa: E402
+import cgx  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="c3")
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--iters", type=int, default=30)
+ap.add_argument("--alg", default="hs")
+ap.add_argument("--variant", action="append", default=[])
+a = ap.parse_args()
+variants = a.variant or ["base:"]
+
+sysm = bench.make_system(bench.WORKLOADS[a.workload])
+solvers = []
+for v in variants:
+    name, _, envs = v.partition(":")
+    saved = {}
+    for kv in filter(None, envs.split(",")):
+        k, _, val = kv.partition("=")
+        saved[k] = os.environ.get(k)
+        os.environ[k] = val
+    s = cgx.Solver(0, alg=cgx.CGX_ALG_CG1 if a.alg == "cg1" else cgx.CGX_ALG_HS)
+    s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+    s.set_rhs(sysm["b"])
+    s.bench_prepare(3)
+    for k, old in saved.items():
+        if old is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = old
+    solvers.append((name, s))
+info = solvers[0][1].info()
+res = {n: {"spmv": [], "iter": []} for n, _ in solvers}
+for r in range(a.rounds):
+    for name, s in solvers:
+        tot, sp = s.bench_run(a.iters, graph=False, spmv_events=True)
+        res[name]["spmv"].append(sp * 1e3)
+        tot, _ = s.bench_run(a.iters, graph=True)
+        res[name]["iter"].append(tot / a.iters * 1e3)
+print(f"workload {a.workload}: n={info['n']} nnz={info['nnz']} spmv_bytes={info['spmv_bytes']:.0f} "
+      f"iter_bytes={info['iter_bytes']:.0f} grid={info['spmv_grid']} rowblocks={info['n_rowblocks']}")
+for name, d in res.items():
+    sm, si = statistics.median(d["spmv"]), statistics.median(d["iter"])
+    print(f"{name:>14}: spmv med {sm:8.2f} us min {min(d['spmv']):8.2f}  "
+          f"({info['spmv_bytes'] / sm / 1e3:7.1f} GB/s)   iter med {si:8.2f} us "
+          f"({1e6 / si:7.1f} it/s, {info['iter_bytes'] / si / 1e3:7.1f} GB/s)")
