@@ -111,7 +111,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--alg", default=None, choices=["hs", "cg1"])
+    ap.add_argument("--alg", default=None, choices=["hs", "cg1", "cg1-dist"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -134,23 +134,33 @@ def main():
             dist.barrier()
 
     wl = WORKLOADS[args.workload]
-    alg = args.alg or ("cg1" if world > 1 else "hs")
+    alg = args.alg or ("cg1-dist" if world > 1 else "hs")
     sysm = make_system(wl, rank, world)
 
-    if world > 1:
-        raise SystemExit("bench.py: multi-GPU path not available in this build")
-
-    s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
-    s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
-    s.set_rhs(sysm["b"])
-    info = s.info()
+    use_dist = world > 1 or alg == "cg1-dist"
+    if use_dist:
+        # one rank per GPU; RCCL communicator from an id rank 0 broadcasts
+        uid = [cgx.dist_unique_id() if (rank == 0 and world > 1) else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        s = cgx.DistSolver(local_rank, world, rank, uid[0])
+        s.set_matrix(sysm["n_global"], sysm["rp"], sysm["col"], sysm["val"])
+        s.set_rhs(sysm["b"])
+        dinfo = s.info()
+        info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"])
+    else:
+        s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
+        s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+        s.set_rhs(sysm["b"])
+        info = s.info()
+        dinfo = None
 
     # ---- timed region: exactly K steps, barrier + sync on both sides
     s.bench_prepare(args.warmup)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dev_ms, _ = s.bench_run(args.steps, graph=True)
+    dev_ms = s.bench_run(args.steps)[0] if use_dist else s.bench_run(args.steps, graph=True)[0]
     torch.cuda.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -162,7 +172,10 @@ def main():
 
     # ---- roofline of the dominant kernel (SpMV): HIP events around every
     # SpMV launch on the solver's stream over K more iterations.
-    tot2, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
+    if use_dist:
+        _, spmv_ms = s.bench_run(args.steps, spmv_events=True)
+    else:
+        _, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
     achieved = info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload, alg)
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
@@ -182,7 +195,8 @@ def main():
         higher_is_better=True, scaling="weak", vs_baseline=None,
         dtype=wl["dtype"], data="synthetic",
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz_local=int(len(sysm["col"])),
-                    alg=alg, graph=True, parallelism=f"row-partition x{world}"),
+                    alg=alg, graph=not use_dist, parallelism=f"row-partition x{world}",
+                    halo_bytes_per_iter=(dinfo or {}).get("halo_bytes")),
         device_ms_per_step=round(dev_ms / args.steps, 4),
         iter_bytes=int(info["iter_bytes"]),
         iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),

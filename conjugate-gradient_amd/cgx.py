@@ -47,6 +47,15 @@ class CgxInfo(ctypes.Structure):
                 ("iter_bytes", ctypes.c_double), ("device_bytes", ctypes.c_size_t)]
 
 
+class CgxDistStats(ctypes.Structure):
+    _fields_ = [("n_global", ctypes.c_longlong), ("row_begin", ctypes.c_int),
+                ("n_loc", ctypes.c_int), ("n_ghost", ctypes.c_int), ("n_send", ctypes.c_int),
+                ("nnz", ctypes.c_int), ("interior_blocks", ctypes.c_int),
+                ("boundary_blocks", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
+                ("iter_bytes", ctypes.c_double), ("halo_bytes", ctypes.c_double),
+                ("device_bytes", ctypes.c_size_t)]
+
+
 _MVP = ctypes.POINTER(MvSparse)
 _MVPP = ctypes.POINTER(_MVP)
 
@@ -103,6 +112,37 @@ _SIGS = {
                                                ctypes.c_int, _i32p, _i32p, _f64p,
                                                _f32p]),
     "cgx_csr_is_chained": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p]),
+    # partition layer
+    "cgx_partition_rows": (None, [ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "cgx_partition_owner": (ctypes.c_int, [ctypes.c_longlong, ctypes.c_int, ctypes.c_longlong]),
+    "cgx_part_create": (ctypes.c_int, [ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                       ctypes.POINTER(_vp)]),
+    "cgx_part_destroy": (None, [_vp]),
+    "cgx_part_info": (ctypes.c_int, [_vp] + [ctypes.POINTER(ctypes.c_int)] * 4),
+    "cgx_part_local_cols": (ctypes.c_int, [_vp, _i32p]),
+    "cgx_part_ghosts": (ctypes.c_int, [_vp, _i32p]),
+    "cgx_part_recv_counts": (ctypes.c_int, [_vp, _i32p]),
+    "cgx_part_set_requests": (ctypes.c_int, [_vp, _i32p, _i32p]),
+    "cgx_part_send_counts": (ctypes.c_int, [_vp, _i32p]),
+    "cgx_part_send_local": (ctypes.c_int, [_vp, _i32p]),
+    # distributed solver
+    "cgx_dist_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "cgx_dist_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "cgx_dist_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "cgx_dist_destroy": (None, [_vp]),
+    "cgx_dist_set_matrix": (ctypes.c_int, [_vp, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                           _i32p, _i32p, _f64p]),
+    "cgx_dist_set_rhs": (ctypes.c_int, [_vp, _f64p]),
+    "cgx_dist_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
+                                    ctypes.POINTER(ctypes.c_int)]),
+    "cgx_dist_get_x": (ctypes.c_int, [_vp, _f64p]),
+    "cgx_dist_get_history": (ctypes.c_int, [_vp, _f64p, ctypes.c_int]),
+    "cgx_dist_bench_prepare": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_bench_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _f64p, _f64p]),
+    "cgx_dist_info": (ctypes.c_int, [_vp, ctypes.POINTER(CgxDistStats)]),
 }
 
 _lib = None
@@ -345,3 +385,153 @@ def solve(A: Mv, b: Mv, tol, maxit):
     x = mv_values(out)
     lib().cgx_free_mv_deep(out)
     return x, its
+
+
+# ------------------------------------------------------------ partitioning
+
+def partition_rows(n, nranks, rank):
+    rb, re_ = ctypes.c_int(0), ctypes.c_int(0)
+    lib().cgx_partition_rows(n, nranks, rank, ctypes.byref(rb), ctypes.byref(re_))
+    return rb.value, re_.value
+
+
+class Partition:
+    """cgx_part: ghost discovery, local renumbering and halo send lists of
+    one rank's rows (host only)."""
+
+    def __init__(self, n_global, nranks, rank, rp, col_global):
+        self.rp = np.ascontiguousarray(rp, np.int32)
+        self.col = np.ascontiguousarray(col_global, np.int32)
+        self.nranks, self.rank = nranks, rank
+        self._h = _vp()
+        check(lib().cgx_part_create(n_global, nranks, rank, len(self.rp) - 1, len(self.col),
+                                    _p(self.rp, _i32p), _p(self.col, _i32p),
+                                    ctypes.byref(self._h)), "cgx_part_create")
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().cgx_part_destroy(self._h)
+        except Exception:
+            pass
+
+    def info(self):
+        v = [ctypes.c_int(0) for _ in range(4)]
+        check(lib().cgx_part_info(self._h, *[ctypes.byref(x) for x in v]), "part_info")
+        return dict(n_loc=v[0].value, n_ghost=v[1].value, row_begin=v[2].value,
+                    n_send=v[3].value)
+
+    def local_cols(self):
+        out = np.empty(max(len(self.col), 1), np.int32)
+        check(lib().cgx_part_local_cols(self._h, _p(out, _i32p)), "local_cols")
+        return out[:len(self.col)]
+
+    def ghosts(self):
+        n = self.info()["n_ghost"]
+        out = np.empty(max(n, 1), np.int32)
+        check(lib().cgx_part_ghosts(self._h, _p(out, _i32p)), "ghosts")
+        return out[:n]
+
+    def recv_counts(self):
+        out = np.empty(self.nranks, np.int32)
+        check(lib().cgx_part_recv_counts(self._h, _p(out, _i32p)), "recv_counts")
+        return out
+
+    def set_requests(self, counts, globals_):
+        counts = np.ascontiguousarray(counts, np.int32)
+        g = np.ascontiguousarray(globals_, np.int32)
+        if len(g) == 0:
+            g = np.zeros(1, np.int32)
+        check(lib().cgx_part_set_requests(self._h, _p(counts, _i32p), _p(g, _i32p)),
+              "set_requests")
+
+    def send_counts(self):
+        out = np.empty(self.nranks, np.int32)
+        check(lib().cgx_part_send_counts(self._h, _p(out, _i32p)), "send_counts")
+        return out
+
+    def send_local(self):
+        n = self.info()["n_send"]
+        out = np.empty(max(n, 1), np.int32)
+        check(lib().cgx_part_send_local(self._h, _p(out, _i32p)), "send_local")
+        return out[:n]
+
+
+# ---------------------------------------------------------- multi-GPU solver
+
+def dist_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    check(lib().cgx_dist_unique_id(buf), "cgx_dist_unique_id")
+    return buf.raw
+
+
+class DistSolver:
+    """One rank of the multi-GPU CG solver (cgx_dist_*)."""
+
+    def __init__(self, device=0, nranks=1, rank=0, uid=None, _handle=None):
+        self._keep = []
+        if _handle is not None:
+            self._h = _handle
+            self._owner = False
+            return
+        self._h = _vp()
+        self._owner = True
+        check(lib().cgx_dist_create(device, nranks, rank, uid, ctypes.byref(self._h)),
+              "cgx_dist_create")
+
+    @staticmethod
+    def local_group(device, nparts):
+        arr = (_vp * nparts)()
+        check(lib().cgx_dist_create_local(device, nparts, arr), "cgx_dist_create_local")
+        parts = [DistSolver(_handle=_vp(arr[i])) for i in range(nparts)]
+        parts[0]._owner = True
+        return parts
+
+    def close(self):
+        if self._h and self._owner:
+            lib().cgx_dist_destroy(self._h)
+        self._h = _vp()
+
+    def set_matrix(self, n_global, rp, col_global, val):
+        rp = np.ascontiguousarray(rp, np.int32)
+        col = np.ascontiguousarray(col_global, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        check(lib().cgx_dist_set_matrix(self._h, n_global, len(rp) - 1, len(col),
+                                        _p(rp, _i32p), _p(col, _i32p), _p(val, _f64p)),
+              "dist_set_matrix")
+        self.n_loc = len(rp) - 1
+
+    def set_rhs(self, b):
+        b = np.ascontiguousarray(b, np.float64)
+        check(lib().cgx_dist_set_rhs(self._h, _p(b, _f64p)), "dist_set_rhs")
+
+    def run(self, maxit, tol=0.0):
+        it = ctypes.c_int(0)
+        check(lib().cgx_dist_run(self._h, maxit, tol, ctypes.byref(it)), "dist_run")
+        return it.value
+
+    def x(self):
+        out = np.empty(self.n_loc, np.float64)
+        check(lib().cgx_dist_get_x(self._h, _p(out, _f64p)), "dist_get_x")
+        return out
+
+    def history(self, cap):
+        out = np.zeros(cap, np.float64)
+        m = check(lib().cgx_dist_get_history(self._h, _p(out, _f64p), cap), "dist_history")
+        return out[:m]
+
+    def bench_prepare(self, warmup):
+        check(lib().cgx_dist_bench_prepare(self._h, warmup), "dist_bench_prepare")
+
+    def bench_run(self, iters, spmv_events=False):
+        """Returns (device ms for all iters, average SpMV ms or -1)."""
+        ms, sp = ctypes.c_double(0), ctypes.c_double(0)
+        check(lib().cgx_dist_bench_run(self._h, iters,
+                                       CGX_BENCH_SPMV_EVENTS if spmv_events else 0,
+                                       ctypes.byref(ms), ctypes.byref(sp)), "dist_bench_run")
+        return ms.value, sp.value
+
+    def info(self):
+        st = CgxDistStats()
+        check(lib().cgx_dist_info(self._h, ctypes.byref(st)), "dist_info")
+        return {k: getattr(st, k) for k, _ in CgxDistStats._fields_}

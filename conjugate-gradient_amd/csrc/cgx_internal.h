@@ -67,6 +67,7 @@ enum FinOp {
   FIN_INIT_CG1 = 3, // gamma = bb = sum(a), delta = sum(b), alpha = gamma/delta
   FIN_CG1 = 4,      // gamma' = sum(a), delta = sum(b); stop test; alpha, beta
   FIN_SUM = 5,      // out[0] = sum(a) (op-level dot)
+  FIN_SUM2 = 6,     // out[0] = sum(a), out[1] = sum(b) (local sums to all-reduce)
 };
 
 template <typename T>
@@ -137,6 +138,14 @@ template <typename T>
 hipError_t launch_gather(int m, const int *idx, const T *x, T *buf,
                          hipStream_t st);
 
+hipError_t launch_group_sum(const double *const *srcs, int P, int count,
+                            double *dst, hipStream_t st);
+
 int vec_grid_for(int n, int cus);
+int env_int(const char *name, int dflt);
+
+// Partition helpers (cgx_partition.cpp)
+long long part_begin(long long n, int G, int g);
+int part_owner(long long n, int G, long long c);
 
 }  // namespace cgx

@@ -653,7 +653,8 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
                                                  CgState *st, double *hist,
                                                  double *out) {
   __shared__ double red[BS / kWave];
-  if (op != FIN_SUM && op != FIN_INIT_HS && op != FIN_INIT_CG1 && st->done)
+  if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_INIT_HS &&
+      op != FIN_INIT_CG1 && st->done)
     return;
   const double sa = sum_parts<BS>(pa, na, red);
   const double sb = pb ? sum_parts<BS>(pb, nb, red) : 0.0;
@@ -661,6 +662,10 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
   switch (op) {
     case FIN_SUM:
       out[0] = sa;
+      break;
+    case FIN_SUM2:
+      out[0] = sa;
+      out[1] = sb;
       break;
     case FIN_INIT_HS:
       st->bb = sa;
@@ -729,6 +734,17 @@ __global__ __launch_bounds__(BS) void k_axpby(int op, int n, double sc,
     else v = a[i] - b[i];               // vec_sub, mv_ops.c:258
     r[i] = v;
   }
+}
+
+// In-process all-reduce of the multi-partition transport: every partition
+// adds the partitions' local sums in the same fixed order (0..P-1).
+__global__ void k_group_sum(const double *const *srcs, int P, int count,
+                            double *dst) {
+  const int c = threadIdx.x;
+  if (c >= count) return;
+  double acc = srcs[0][c];
+  for (int q = 1; q < P; ++q) acc = acc + srcs[q][c];
+  dst[c] = acc;
 }
 
 template <typename T>
@@ -880,6 +896,12 @@ hipError_t launch_axpby(int op, int n, double s, const T *a, const T *b, T *r,
                         int grid, hipStream_t st) {
   hipLaunchKernelGGL((k_axpby<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, op,
                      n, s, a, b, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_sum(const double *const *srcs, int P, int count,
+                            double *dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, st, srcs, P, count, dst);
   return hipGetLastError();
 }
 

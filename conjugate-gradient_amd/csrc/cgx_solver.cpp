@@ -58,7 +58,7 @@ int vec_grid_for(int n, int cus) {
   return (int)g;
 }
 
-static int env_int(const char *name, int dflt) {
+int env_int(const char *name, int dflt) {
   const char *v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }

@@ -136,6 +136,73 @@ long long cgx_gen_random_spd(int n, int partners, unsigned long long seed,
  * dense-row mv_mult equals CSR SpMV. */
 int cgx_csr_is_chained(int n, const int *row_ptr, const int *col);
 
+/* ------------------------------------------------------------------------
+ * 4. Row partition layer (host only, no GPU)
+ *    rank g of G owns rows [floor(g*n/G), floor((g+1)*n/G)); its local
+ *    columns are owned rows -> [0, n_loc) and ghosts -> n_loc + position in
+ *    the ghost list (sorted by global index, hence grouped by owner rank).
+ * ------------------------------------------------------------------------ */
+void cgx_partition_rows(long long n, int nranks, int rank, int *row_begin,
+                        int *row_end);
+int  cgx_partition_owner(long long n, int nranks, long long col);
+
+typedef struct cgx_part cgx_part;
+/* row_ptr (n_loc+1, local) and col_global (nnz) describe this rank's rows. */
+int  cgx_part_create(long long n_global, int nranks, int rank, int n_loc,
+                     int nnz, const int *row_ptr, const int *col_global,
+                     cgx_part **out);
+void cgx_part_destroy(cgx_part *p);
+int  cgx_part_info(const cgx_part *p, int *n_loc, int *n_ghost,
+                   int *row_begin, int *n_send);
+int  cgx_part_local_cols(const cgx_part *p, int *col_local);   /* nnz     */
+int  cgx_part_ghosts(const cgx_part *p, int *ghost_global);    /* n_ghost */
+int  cgx_part_recv_counts(const cgx_part *p, int *counts);     /* nranks  */
+/* Requests received from every rank (counts[nranks]; global row indices
+ * concatenated by rank) -> this rank's halo send lists. */
+int  cgx_part_set_requests(cgx_part *p, const int *req_counts,
+                           const int *req_global);
+int  cgx_part_send_counts(const cgx_part *p, int *counts);     /* nranks  */
+int  cgx_part_send_local(const cgx_part *p, int *send_local);  /* n_send  */
+
+/* ------------------------------------------------------------------------
+ * 5. Multi-GPU solver: one rank per GPU, halo exchange + ONE fused
+ *    all-reduce per iteration (Chronopoulos-Gear CG) over RCCL.
+ *    Stop rule as solve(); x0 = 0; every rank passes its own rows.
+ * ------------------------------------------------------------------------ */
+typedef struct cgx_dist cgx_dist;
+typedef struct {
+  long long n_global;
+  int row_begin, n_loc, n_ghost, n_send, nnz;
+  int interior_blocks, boundary_blocks;  /* 64-row SpMV blocks            */
+  double spmv_bytes, iter_bytes;         /* algorithmic, this rank        */
+  double halo_bytes;                     /* sent + received per iteration */
+  size_t device_bytes;
+} cgx_dist_stats;
+
+/* Rank 0 creates the id and distributes it (e.g. torch.distributed). */
+int  cgx_dist_unique_id(unsigned char id[128]);
+/* nranks == 1 needs no id and no communication. */
+int  cgx_dist_create(int device, int nranks, int rank,
+                     const unsigned char id[128], cgx_dist **out);
+/* In-process transport: nparts partitions on one device driven by one host
+ * thread (device copies for the halo, fixed-order sum for the all-reduce).
+ * Run/bench through parts[0]; destroy through parts[0]. */
+int  cgx_dist_create_local(int device, int nparts, cgx_dist **parts);
+void cgx_dist_destroy(cgx_dist *d);
+int  cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
+                         const int *row_ptr, const int *col_global,
+                         const double *val);
+int  cgx_dist_set_rhs(cgx_dist *d, const double *b_local);
+int  cgx_dist_run(cgx_dist *d, int maxit, double tol, int *iters);
+int  cgx_dist_get_x(cgx_dist *d, double *x_local);
+int  cgx_dist_get_history(cgx_dist *d, double *rr, int cap);
+int  cgx_dist_bench_prepare(cgx_dist *d, int warmup);
+/* flags: CGX_BENCH_SPMV_EVENTS brackets the interior and boundary SpMV
+ * launches of partition 0 with events; *spmv_ms = their average sum. */
+int  cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms,
+                        double *spmv_ms);
+int  cgx_dist_info(cgx_dist *d, cgx_dist_stats *s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,111 @@
+"""GPU: the partitioned solver (cgx_dist).  On one MI355X the in-process
+transport runs P = 1..8 partitions with the exact phase code of the RCCL
+path (halo copies + fixed-order all-reduce); RCCL itself is exercised at
+world size 1 here and at N = 2/4/8 by bench.py on a full node.
+
+Bar: x within 1e-9 (relative) of the serial oracle's Chronopoulos-Gear
+solve, iteration count within 1, true residual below the tolerance."""
+import numpy as np
+import pytest
+
+import cgx
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def system(kind):
+    if kind == "lap3d":
+        rp, col, val = cgx.laplacian3d(24, 20, 30)
+        b = np.ones(len(rp) - 1)
+    elif kind == "lap2d":
+        rp, col, val = cgx.laplacian2d(90, 70)
+        b = np.random.default_rng(4).standard_normal(len(rp) - 1)
+    else:
+        rp, col, val = cgx.random_spd(20000, 8, 21)
+        b = np.random.default_rng(5).standard_normal(20000)
+    return rp, col, val, b
+
+
+def solve_local(rp, col, val, b, P, maxit, tol):
+    n = len(rp) - 1
+    parts = cgx.DistSolver.local_group(0, P)
+    try:
+        for g, d in enumerate(parts):
+            rb, re_ = cgx.partition_rows(n, P, g)
+            d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]],
+                         val[rp[rb]:rp[re_]])
+            d.set_rhs(b[rb:re_])
+        its = parts[0].run(maxit, tol)
+        x = np.concatenate([d.x() for d in parts])
+        hist = parts[0].history(its)
+        stats = [d.info() for d in parts]
+    finally:
+        parts[0].close()
+    return x, its, hist, stats
+
+
+@pytest.mark.parametrize("kind", ["lap3d", "lap2d", "rand"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_local_partitions_match_oracle(kind, P):
+    rp, col, val, b = system(kind)
+    x, its, hist, stats = solve_local(rp, col, val, b, P, 2000, 1e-10)
+    x_ref, its_ref, hist_ref = H.o_solve(2000, 1e-10, rp, col, val, b, cg1=True)
+    assert abs(its - its_ref) <= 1
+    assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
+    m = min(len(hist), len(hist_ref)) - 2
+    assert np.allclose(hist[:m], hist_ref[:m], rtol=1e-6, atol=0)
+    res = b - H.o_spmv(rp, col, val, x)
+    assert np.linalg.norm(res) <= 2e-10 * np.linalg.norm(b)
+    if P > 1:
+        assert all(s["n_ghost"] > 0 for s in stats)
+        assert sum(s["n_send"] for s in stats) == sum(s["n_ghost"] for s in stats)
+
+
+def test_fixed_iterations_agree_across_partition_counts():
+    """tol = 0: exactly maxit+1 x-updates whatever P; P only changes the
+    reduction order, so x agrees to rounding."""
+    rp, col, val, b = system("lap3d")
+    xs = [solve_local(rp, col, val, b, P, 60, 0.0) for P in (1, 2, 4, 8)]
+    assert all(x[1] == 61 for x in xs)
+    for x in xs[1:]:
+        assert np.linalg.norm(x[0] - xs[0][0]) <= 1e-11 * np.linalg.norm(xs[0][0])
+
+
+def test_rccl_world1():
+    rp, col, val, b = system("rand")
+    d = cgx.DistSolver(0, 1, 0, None)
+    try:
+        d.set_matrix(len(rp) - 1, rp, col, val)
+        d.set_rhs(b)
+        its = d.run(1000, 1e-10)
+        x = d.x()
+        d.bench_prepare(3)
+        ms, sp = d.bench_run(5, spmv_events=True)
+        assert ms > 0 and 0 < sp < ms
+    finally:
+        d.close()
+    x_ref, its_ref, _ = H.o_solve(1000, 1e-10, rp, col, val, b, cg1=True)
+    assert abs(its - its_ref) <= 1
+    assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
+
+
+def test_local_group_bench_and_interior_split():
+    rp, col, val = cgx.laplacian3d(32, 32, 64)
+    n = len(rp) - 1
+    parts = cgx.DistSolver.local_group(0, 4)
+    try:
+        for g, d in enumerate(parts):
+            rb, re_ = cgx.partition_rows(n, 4, g)
+            d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+            d.set_rhs(np.ones(re_ - rb))
+        parts[0].bench_prepare(2)
+        assert parts[0].bench_run(5)[0] > 0
+        st = [d.info() for d in parts]
+    finally:
+        parts[0].close()
+    # z-slabs of 16 planes: one ghost plane per neighbour, boundary blocks
+    # are the first and last plane's 64-row blocks
+    assert [s["n_ghost"] for s in st] == [1024, 2048, 2048, 1024]
+    assert all(s["boundary_blocks"] <= 2 * 1024 // 64 + 2 for s in st)
+    assert all(s["interior_blocks"] > 0 for s in st)
