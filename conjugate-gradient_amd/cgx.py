@@ -112,6 +112,7 @@ _SIGS = {
                                                ctypes.c_int, _i32p, _i32p, _f64p,
                                                _f32p]),
     "cgx_csr_is_chained": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p]),
+    "cgx_read_input_file": (ctypes.c_int, [ctypes.c_char_p, _MVP, _MVP]),
     # partition layer
     "cgx_partition_rows": (None, [ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),

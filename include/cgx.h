@@ -131,6 +131,13 @@ long long cgx_gen_laplacian3d(int nx, int ny, int nz, int row_begin,
 long long cgx_gen_random_spd(int n, int partners, unsigned long long seed,
                              int row_begin, int row_end, int *row_ptr,
                              int *col, double *val, float *val32);
+/* Reader for the reference's 4-line input format (replaces read_input_file,
+ * cg.c:23,146-218): col_indices / row_ptr / values / b, comma separated.
+ * Fills *A (CSR) and *b (vector) with freshly allocated host arrays.
+ * Re-entrant, bounds-safe, accepts a missing final newline.  0 or -1. */
+int cgx_read_input_file(const char *path, struct __mv_sparse *A,
+                        struct __mv_sparse *b);
+
 /* 1 if the CSR is "chained" (ascending cols, no empty row,
  * first_col(r+1) <= last_col(r)): the class on which the reference's
  * dense-row mv_mult equals CSR SpMV. */

@@ -1,0 +1,79 @@
+"""Next rows of SURVEY.md 8f: the reader for the reference's 4-line input
+format (cg.c:146-218) and the drop-in `cg` CLI (cg.c:42-85)."""
+import ctypes
+import gzip
+import subprocess
+
+import numpy as np
+import pytest
+
+import cgx
+import helpers as H
+
+CLI = H.REPO / "conjugate-gradient_amd" / "bin" / "cg"
+
+
+def read(path):
+    A, b = cgx.lib().new_mv_struct(), cgx.lib().new_mv_struct()
+    rc = cgx.lib().cgx_read_input_file(str(path).encode(), A, b)
+    if rc != 0:
+        return None
+    a, bb = A.contents, b.contents
+    rp = np.ctypeslib.as_array(a.row_ptr, shape=(a.size + 1,)).copy()
+    col = np.ctypeslib.as_array(a.col_indices, shape=(max(rp[-1], 1),))[:rp[-1]].copy()
+    val = np.ctypeslib.as_array(a.values, shape=(max(a.nnz, 1),))[:a.nnz].copy()
+    bv = np.ctypeslib.as_array(bb.values, shape=(max(bb.size, 1),))[:bb.size].copy()
+    out = dict(n=a.size, nnz=a.nnz, rp=rp, col=col, val=val, b=bv, bsize=bb.size, bnnz=bb.nnz)
+    cgx.lib().cgx_free_mv_deep(A)
+    cgx.lib().cgx_free_mv_deep(b)
+    return out
+
+
+@pytest.mark.parametrize("name", H.golden_names())
+def test_reader_matches_fixture(name, tmp_path):
+    src = tmp_path / f"{name}.txt"
+    src.write_bytes(gzip.open(H.GOLDEN / f"{name}.txt.gz").read())
+    g = H.load_golden(name)
+    for _ in range(2):  # re-entrant: the reference's reader works once per process
+        r = read(src)
+        assert r["n"] == g["n"] and r["nnz"] == g["nnz"]
+        assert r["bsize"] == r["bnnz"] == len(g["b"])
+        assert np.array_equal(r["rp"], g["row_ptr"]) and np.array_equal(r["col"], g["col"])
+        assert H.same_bits_or_both_nan(r["val"], g["val"])
+        assert H.same_bits_or_both_nan(r["b"], g["b"])
+
+
+def test_reader_edge_cases(tmp_path):
+    p = tmp_path / "eof.txt"
+    p.write_text("0,1\n0,1,2\n2.5,-1e-3\n1,2")  # no final newline
+    r = read(p)
+    assert r["n"] == 2 and list(r["b"]) == [1.0, 2.0] and list(r["val"]) == [2.5, -1e-3]
+    p.write_text("0,,1\n0,2,3\n1,2,3\n4,5\n")  # empty token parses as 0 (cg.c:350)
+    r = read(p)
+    assert list(r["col"]) == [0, 0, 1]
+    assert read(tmp_path / "missing.txt") is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,it", [("kat_tridiag10", 4), ("lap2d_32", 25), ("dense128", 11)])
+def test_cli_output_matches_reference(name, it, tmp_path):
+    """Same stdout as the reference CLI: 'CG took approx %d seconds' then
+    print_sparse(x) with %f values (mv_ops.c:77-95)."""
+    src = tmp_path / f"{name}.txt"
+    src.write_bytes(gzip.open(H.GOLDEN / f"{name}.txt.gz").read())
+    out = subprocess.run([str(CLI), str(src), str(it)], capture_output=True, text=True,
+                         check=True, env={**__import__("os").environ, "CGX_MODE": "exact"}).stdout
+    lines = out.splitlines()
+    want = H.load_golden(name)["iters"][it]
+    assert lines[0].startswith("CG took approx ") and lines[0].endswith(" seconds")
+    assert lines[1] == "Sparse Object:"
+    assert lines[2] == f"\tSize: {len(want)}" and lines[3] == f"\tNNZ: {len(want)}"
+    assert lines[4].startswith("\tValues: ")
+    assert lines[5:] == ["\t%f" % v for v in want]
+
+
+def test_cli_usage_and_missing_input():
+    r = subprocess.run([str(CLI)], capture_output=True, text=True)
+    assert r.returncode != 0 and "Usage:" in r.stderr
+    r = subprocess.run([str(CLI), "/nonexistent/input.txt", "3"], capture_output=True, text=True)
+    assert r.returncode != 0 and "Failed to open input file" in r.stderr
