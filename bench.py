@@ -147,7 +147,8 @@ def main():
         s.set_matrix(sysm["n_global"], sysm["rp"], sysm["col"], sysm["val"])
         s.set_rhs(sysm["b"])
         dinfo = s.info()
-        info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"])
+        info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"],
+                    spmv_iter_bytes=dinfo["spmv_bytes"])
     else:
         s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
@@ -176,13 +177,13 @@ def main():
         _, spmv_ms = s.bench_run(args.steps, spmv_events=True)
     else:
         _, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
-    achieved = info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9
+    achieved = info["spmv_iter_bytes"] / (spmv_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload, alg)
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                     traffic=traffic, kernel="k_spmv (CSR-stream, LDS-staged)",
                     spmv_us=round(spmv_ms * 1e3, 2),
-                    algorithmic_bytes_per_launch=int(info["spmv_bytes"]))
+                    algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

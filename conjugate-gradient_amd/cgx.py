@@ -44,7 +44,8 @@ class CgxInfo(ctypes.Structure):
                 ("mode", ctypes.c_int), ("alg", ctypes.c_int),
                 ("n_rowblocks", ctypes.c_int), ("spmv_grid", ctypes.c_int),
                 ("vec_grid", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
-                ("iter_bytes", ctypes.c_double), ("device_bytes", ctypes.c_size_t)]
+                ("iter_bytes", ctypes.c_double), ("spmv_iter_bytes", ctypes.c_double),
+                ("device_bytes", ctypes.c_size_t)]
 
 
 class CgxDistStats(ctypes.Structure):

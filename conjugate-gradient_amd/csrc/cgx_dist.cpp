@@ -393,6 +393,9 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.bs = 64;
   a.wpb = d->wpb;
   a.rbw = 1;
+  a.st = d->d_st;
+  a.tg = env_int("CGX_SPMV_TG", 1);
+  a.tk = TicketArgs{};
   return a;
 }
 

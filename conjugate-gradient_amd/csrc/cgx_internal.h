@@ -70,6 +70,19 @@ enum FinOp {
   FIN_SUM2 = 6,     // out[0] = sum(a), out[1] = sum(b) (local sums to all-reduce)
 };
 
+// In-kernel two-level ticket reduction (see ticket_finish in
+// cgx_kernels.hip): replaces a k_finalize launch.  cnt1 == nullptr: off.
+constexpr int kTicketGroup = 64;
+struct TicketArgs {
+  double *part1;    // >= grid partials
+  double *part2;    // >= ceil(grid / kTicketGroup)
+  unsigned *cnt1;   // >= ceil(grid / kTicketGroup), zero-initialised
+  unsigned *cnt2;   // 1, zero-initialised
+  int op;           // FinOp applied by the final workgroup
+  CgState *st;
+  double *hist;
+};
+
 template <typename T>
 struct SpmvArgs {
   const int *rp;       // row_ptr (local rows)
@@ -89,7 +102,14 @@ struct SpmvArgs {
                        // 64 (one row block per wave, k_spmv_wave)
   int wpb;             // k_spmv_wave: waves per workgroup (4 | 8)
   int rbw;             // k_spmv_wave: row blocks per wave
-  int pipe;            // k_spmv_wave: prefetch the next row block's stream
+  // fused p-update (k_spmv_wave only): x2 = p_old (nullptr: off); the gathered
+  // operand is x + beta*x2 with beta = st->beta, and xout receives it for the
+  // owned rows (p_new; must not alias x or x2).
+  const T *x2;
+  T *xout;
+  const CgState *st;
+  int tg;              // k_spmv_wave: transposed (row-per-lane) gather
+  TicketArgs tk;       // k_spmv_wave + EPI: in-kernel finalize (cnt1 != 0)
 };
 
 // Row-block plan: consecutive rows, at most `rows` rows and `cap` nonzeros
@@ -103,14 +123,15 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st);
 
 template <typename T>
 hipError_t launch_init_hs(int n, const T *b, T *x, T *r, T *p, double *part,
-                          int grid, hipStream_t st);
+                          int grid, hipStream_t st, bool p_zero = false,
+                          const TicketArgs *tk = nullptr);
 template <typename T>
 hipError_t launch_init_cg1(int n, const T *b, T *x, T *r, T *p, T *s,
                            double *part, int grid, hipStream_t st);
 template <typename T>
 hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
                             const CgState *stt, double *part, int grid,
-                            hipStream_t st);
+                            hipStream_t st, const TicketArgs *tk = nullptr);
 template <typename T>
 hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
                        hipStream_t st);

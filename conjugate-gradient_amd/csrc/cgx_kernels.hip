@@ -58,6 +58,129 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
   return s;
 }
 
+// The scalar lines of the recurrence (cg.c:113, 125-129; CG1 analogues) on
+// the reduced sums sa, sb -- run by ONE thread (k_finalize, or the last
+// workgroup of a ticket reduction).
+__device__ void apply_fin(int op, double sa, double sb, CgState *st,
+                          double *hist, double *out) {
+  switch (op) {
+    case FIN_SUM:
+      out[0] = sa;
+      break;
+    case FIN_SUM2:
+      out[0] = sa;
+      out[1] = sb;
+      break;
+    case FIN_INIT_HS:
+      st->bb = sa;
+      st->rr = sa;  // r = b (cg.c:107), so r.r == b.b bit for bit
+      st->tol2bb = st->tol * st->tol * sa;
+      st->k = 0;
+      st->done = 0;
+      break;
+    case FIN_HS_ALPHA:
+      st->ps = sa;
+      st->alpha = st->rr / sa;  // cg.c:113
+      break;
+    case FIN_HS_BETA: {
+      const double rr_new = sa;
+      const int k = st->k;
+      if (k < st->hist_cap) hist[k] = rr_new;
+      if (k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb)) {
+        st->done = 1;  // cg.c:125 break position
+      } else {
+        st->beta = rr_new / st->rr;  // cg.c:129
+        st->rr = rr_new;
+        st->k = k + 1;
+      }
+      break;
+    }
+    case FIN_INIT_CG1:
+      st->bb = sa;
+      st->rr = sa;
+      st->delta = sb;
+      st->tol2bb = st->tol * st->tol * sa;
+      st->alpha = sa / sb;
+      st->beta = 0.0;
+      st->k = 0;
+      st->done = 0;
+      break;
+    case FIN_CG1: {
+      const double g = sa, d = sb;
+      const int k = st->k;
+      if (k < st->hist_cap) hist[k] = g;
+      if (k >= st->max_iter || (st->use_tol && g <= st->tol2bb)) {
+        st->done = 1;
+      } else {
+        const double beta = g / st->rr;
+        st->delta = d;
+        st->alpha = g / (d - beta * g / st->alpha);
+        st->beta = beta;
+        st->rr = g;
+        st->k = k + 1;
+      }
+      break;
+    }
+  }
+}
+
+// In-kernel deterministic two-level reduction ("last arriver" tickets),
+// replacing a separate k_finalize launch.  Every workgroup publishes its
+// partial (agent-scope sc1 store, drained before its ticket), then takes a
+// ticket on its group's counter (kTicketGroup consecutive workgroups); the
+// group's last arriver (told by the returned ticket) sums the group's
+// partials in fixed order and takes a ticket on the global counter; the
+// last of those sums the group sums in fixed order and runs the scalar
+// step.  The sums never depend on arrival order, so results are
+// bit-reproducible.  Counters are reset by their last arriver, so they are
+// zero again when the kernel ends (placement-independent protocol of
+// cdna_hip_programming.md Guideline 16: sc1 payload + drained vmcnt +
+// agent-scope atomic; the consumer adds an agent acquire and sc1 loads).
+__device__ __forceinline__ bool take_ticket(unsigned *cnt, unsigned n,
+                                            double *slot, double v) {
+  __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned t =
+      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != n - 1) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+__device__ __forceinline__ double ld_published(const double *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// v: this workgroup's partial, valid in thread 0.  All threads must call it.
+template <int BS>
+__device__ void ticket_finish(double v, const TicketArgs &t, double *red) {
+  __shared__ int s_last;
+  const int b = blockIdx.x, G = gridDim.x;
+  const int ng = (G + kTicketGroup - 1) / kTicketGroup, grp = b / kTicketGroup;
+  const int gsz = min(kTicketGroup, G - grp * kTicketGroup);
+  if (threadIdx.x == 0) s_last = take_ticket(t.cnt1 + grp, gsz, t.part1 + b, v);
+  __syncthreads();
+  if (!s_last) return;
+  double g = 0.0;
+  if (threadIdx.x < kWave) {
+    const int i = threadIdx.x;
+    g = wave_sum(i < gsz ? ld_published(t.part1 + grp * kTicketGroup + i) : 0.0);
+  }
+  if (ng > 1) {
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = take_ticket(t.cnt2, ng, t.part2 + grp, g);
+    __syncthreads();
+    if (!s_last) return;
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < ng; i += BS)
+      acc = (i == (int)threadIdx.x) ? ld_published(t.part2 + i)
+                                    : acc + ld_published(t.part2 + i);
+    g = block_sum<BS>(acc, red);
+  }
+  if (threadIdx.x == 0) apply_fin(t.op, g, 0.0, t.st, t.hist, nullptr);
+}
+
 // ---------------------------------------------------------------- SpMV
 // CSR-stream: each row block (<= BS rows, <= CAP nonzeros) is streamed with
 // coalesced VEC-wide loads of val/col; the products val[k]*x[col[k]] land in
@@ -196,10 +319,11 @@ __global__ __launch_bounds__(BS) void k_spmv(SpmvArgs<T> a) {
 // Wave-independent CSR-stream: the same algorithm with 64-row row blocks per
 // WAVE (CAPW products in the wave's own LDS slice), so a wave never waits on
 // a workgroup barrier in the main path and the 32 waves of a CU stream and
-// gather independently.  Each wave walks RBW consecutive row blocks; with
-// PIPE the stream loads (val/col) of block i+1 are issued before block i's
-// gathers are consumed, keeping two blocks of stream in flight per wave.  The
-// workgroup meets once, at the end, to combine the fused x.y epilogue.
+// gather independently.  Each wave walks RBW consecutive row blocks (1 by
+// default: a wave per row block measured fastest).  The workgroup meets once,
+// at the end, to combine the fused x.y epilogue.  With XPAY the gathered
+// operand is p = r + beta*p_old, computed on the fly, and the owned rows' p is
+// written out: the separate p-update pass of cg.c:131-132 disappears.
 template <typename T, int CAPW, int VEC>
 struct WaveBlock {
   static constexpr int NIT = CAPW / (kWave * VEC);
@@ -230,6 +354,19 @@ struct WaveBlock {
   }
 };
 
+// XCD-contiguous block order (speed only, never correctness): workgroups are
+// dealt round-robin over the 8 XCDs, so blocks b, b+8, b+16, ... share one
+// XCD's L2.  Give XCD x the contiguous range of logical blocks
+// [x*q + min(x, rem), ...) (bijective for any grid size), so each L2 sees
+// consecutive rows and the stencil's x re-reads (rows +-1, +-nx, +-nx*ny)
+// come from its own L2 instead of the Infinity Cache.
+__device__ __forceinline__ int xcd_block(int on) {
+  const int b = blockIdx.x, G = gridDim.x;
+  if (!on || G < 16) return b;
+  const int x = b & 7, i = b >> 3, q = G >> 3, rem = G & 7;
+  return x * q + min(x, rem) + i;
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   // LDS ops of one wave complete in order; the fences keep the compiler from
   // moving reads of other lanes' slots above the writes.
@@ -238,10 +375,19 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <typename T, int CAPW, int VEC, bool EPI>
+// Gathered operand: x[c], or with XPAY the fused search direction
+// p[c] = r[c] + beta*p_old[c] (cg.c:131-132, two roundings as the reference).
+template <typename T, bool XPAY>
+__device__ __forceinline__ T operand(const SpmvArgs<T> &a, T beta, int c) {
+  if (!XPAY) return a.x[c];
+  const T bp = beta * a.x2[c];
+  return a.x[c] + bp;
+}
+
+template <typename T, int CAPW, int VEC, bool EPI, bool XPAY>
 __device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
                                                     WaveBlock<T, CAPW, VEC> &B,
-                                                    T *prod, int lane) {
+                                                    T *prod, int lane, T beta) {
   typedef WaveBlock<T, CAPW, VEC> WB;
   const int r0 = B.r0, nr = B.nr, k0 = B.k0, k1 = B.k1, kb = B.kb;
   int j0 = 0, j1 = 0;
@@ -249,7 +395,8 @@ __device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
   if (lane < nr) {
     j0 = a.rp[r0 + lane];
     j1 = a.rp[r0 + lane + 1];
-    if (EPI) xrow = a.x[r0 + lane];
+    if (EPI || XPAY) xrow = operand<T, XPAY>(a, beta, r0 + lane);
+    if (XPAY) a.xout[r0 + lane] = xrow;  // p_new for the owned row
   }
   T acc = T(0);
   if (k1 - kb <= CAPW) {
@@ -260,7 +407,7 @@ __device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
       for (int j = 0; j < VEC; ++j) {
         const int k = kb + (it * kWave + lane) * VEC + j;
         const bool ok = k >= k0 && k < k1;
-        xv[it][j] = a.x[ok ? B.c[it][j] : 0];
+        xv[it][j] = operand<T, XPAY>(a, beta, ok ? B.c[it][j] : 0);
       }
 #pragma unroll
     for (int it = 0; it < WB::NIT; ++it) {
@@ -298,7 +445,7 @@ __device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
     for (int c0 = k0; c0 < k1; c0 += CAPW) {
       const int m = min(CAPW, k1 - c0);
       for (int t = lane; t < m; t += kWave)
-        prod[t] = a.val[c0 + t] * a.x[a.col[c0 + t]];
+        prod[t] = a.val[c0 + t] * operand<T, XPAY>(a, beta, a.col[c0 + t]);
       wave_lds_sync();
       if (lane == 0)
         for (int j = 0; j < m; ++j) acc = acc + prod[j];
@@ -313,54 +460,117 @@ __device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
   return d;
 }
 
-template <typename T, int WPB, int CAPW, int VEC, bool EPI, bool NT, bool PIPE>
-__global__ __launch_bounds__(WPB * kWave, PIPE ? 4 : 8) void k_spmv_wave(SpmvArgs<T> a) {
+// Transposed-gather finish (TG): the block's val/col window is staged in the
+// wave's LDS slice in element order, then lane t walks ROW t's nonzeros
+// itself -- for the j-th nonzero the 64 lanes read x at 64 consecutive rows'
+// columns (for banded/stencil matrices: a few contiguous runs instead of ~20
+// scattered lines per instruction).  Products are rounded separately and
+// added in column order from 0.0: the reference's per-row order.
+template <typename T, int CAPW, int VEC, bool EPI, bool XPAY>
+__device__ __forceinline__ double wave_block_finish_t(const SpmvArgs<T> &a,
+                                                      WaveBlock<T, CAPW, VEC> &B,
+                                                      T *lval, int *lcol,
+                                                      int lane, T beta) {
+  typedef WaveBlock<T, CAPW, VEC> WB;
+  const int r0 = B.r0, nr = B.nr, k0 = B.k0, k1 = B.k1, kb = B.kb;
+  int j0 = 0, j1 = 0;
+  T xrow = T(0);
+  if (lane < nr) {
+    j0 = a.rp[r0 + lane];
+    j1 = a.rp[r0 + lane + 1];
+    if (EPI || XPAY) xrow = operand<T, XPAY>(a, beta, r0 + lane);
+    if (XPAY) a.xout[r0 + lane] = xrow;
+  }
+  T acc = T(0);
+  if (k1 - kb <= CAPW) {
+#pragma unroll
+    for (int it = 0; it < WB::NIT; ++it) {
+      const int off = (it * kWave + lane) * VEC;  // window-relative slot
+      *reinterpret_cast<typename WB::tv *>(lval + off) = B.v[it];
+      *reinterpret_cast<typename WB::iv *>(lcol + off) = B.c[it];
+    }
+    wave_lds_sync();
+    if (lane < nr) {
+      constexpr int U = 4;
+      for (int j = j0 - kb; j < j1 - kb; j += U) {
+        const int cnt = min(U, j1 - kb - j);
+        int cc[U];
+        T vv[U], xx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cc[u] = u < cnt ? lcol[j + u] : 0;
+          vv[u] = u < cnt ? lval[j + u] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xx[u] = operand<T, XPAY>(a, beta, cc[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (u < cnt) {
+            const T prod = vv[u] * xx[u];
+            acc = acc + prod;
+          }
+      }
+    }
+    wave_lds_sync();  // the slice is rewritten by the next row block
+  } else {
+    T *prod = lval;
+    for (int c0 = k0; c0 < k1; c0 += CAPW) {
+      const int m = min(CAPW, k1 - c0);
+      for (int t = lane; t < m; t += kWave)
+        prod[t] = a.val[c0 + t] * operand<T, XPAY>(a, beta, a.col[c0 + t]);
+      wave_lds_sync();
+      if (lane == 0)
+        for (int j = 0; j < m; ++j) acc = acc + prod[j];
+      wave_lds_sync();
+    }
+  }
+  double d = 0.0;
+  if (lane < nr) {
+    a.y[r0 + lane] = acc;
+    if (EPI) d = (double)xrow * (double)acc;
+  }
+  return d;
+}
+
+template <typename T, int WPB, int CAPW, int VEC, bool EPI, bool NT, bool XPAY,
+          bool TG>
+__global__ __launch_bounds__(WPB * kWave, TG ? 6 : 8) void k_spmv_wave(SpmvArgs<T> a) {
   __shared__ __attribute__((aligned(16))) T lds[WPB * CAPW];
+  __shared__ __attribute__((aligned(16))) int ldsc[TG ? WPB * CAPW : 1];
   __shared__ double red[WPB];
   if (a.done && *a.done) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   T *prod = lds + wid * CAPW;
+  const T beta = XPAY ? (T)a.st->beta : T(0);
   const int RBW = a.rbw;
-  const int first = (blockIdx.x * WPB + wid) * RBW;
+  const int first = (xcd_block(a.xcd) * WPB + wid) * RBW;
   const int last = min(first + RBW, a.nblk);
   double dot = 0.0;
-  if (PIPE) {
-    WaveBlock<T, CAPW, VEC> B[2];
-    if (first < last) {
-      B[0].describe(a, first);
-      B[0].template stream<NT>(a, lane);
-    }
-    for (int i = first; i < last; i += 2) {
-      if (i + 1 < last) {
-        B[1].describe(a, i + 1);
-        B[1].template stream<NT>(a, lane);
-      }
-      dot = dot + wave_block_finish<T, CAPW, VEC, EPI>(a, B[0], prod, lane);
-      if (i + 1 < last) {
-        if (i + 2 < last) {
-          B[0].describe(a, i + 2);
-          B[0].template stream<NT>(a, lane);
-        }
-        dot = dot + wave_block_finish<T, CAPW, VEC, EPI>(a, B[1], prod, lane);
-      }
-    }
-  } else {
-    for (int i = first; i < last; ++i) {
-      WaveBlock<T, CAPW, VEC> B;
-      B.describe(a, i);
-      B.template stream<NT>(a, lane);
-      dot = dot + wave_block_finish<T, CAPW, VEC, EPI>(a, B, prod, lane);
-    }
+  for (int i = first; i < last; ++i) {
+    WaveBlock<T, CAPW, VEC> B;
+    B.describe(a, i);
+    B.template stream<NT>(a, lane);
+    if (TG)
+      dot = dot + wave_block_finish_t<T, CAPW, VEC, EPI, XPAY>(
+                      a, B, prod, ldsc + wid * CAPW, lane, beta);
+    else
+      dot = dot + wave_block_finish<T, CAPW, VEC, EPI, XPAY>(a, B, prod, lane, beta);
   }
   if (EPI) {
     dot = wave_sum(dot);
     if (lane == 0) red[wid] = dot;
     __syncthreads();
+    double s = 0.0;
     if (threadIdx.x == 0) {
-      double s = red[0];
+      s = red[0];
 #pragma unroll
       for (int w = 1; w < WPB; ++w) s = s + red[w];
+    }
+    if (a.tk.cnt1) {
+      __syncthreads();
+      ticket_finish<WPB * kWave>(s, a.tk, red);
+    } else if (threadIdx.x == 0) {
       a.part[blockIdx.x] = s;
     }
   }
@@ -371,13 +581,16 @@ __global__ __launch_bounds__(WPB * kWave, PIPE ? 4 : 8) void k_spmv_wave(SpmvArg
 // by global thread 0.  Reductions: per-thread fixed-order sums, then
 // block_sum -> part[blockIdx.x]; finalize adds the partials in index order.
 
-// x = 0, r = b, p = b; part = b.b partials (HS prologue, cg.c:104-108)
+// x = 0, r = b, p = b; part = b.b partials (HS prologue, cg.c:104-108).
+// With p_zero the p written is 0 instead: the fused SpMV then forms
+// p_0 = r + 0*0 = r on the fly (beta is 0 before the first update).
 template <typename T, int BS>
 __global__ __launch_bounds__(BS) void k_init_hs(int n, const T *__restrict__ b,
                                                 T *__restrict__ x,
                                                 T *__restrict__ r,
                                                 T *__restrict__ p,
-                                                double *__restrict__ part) {
+                                                double *__restrict__ part,
+                                                int p_zero, TicketArgs tk) {
   __shared__ double red[BS / kWave];
   typedef typename Vec16<T>::type V;
   constexpr int W = Vec16<T>::W;
@@ -388,18 +601,23 @@ __global__ __launch_bounds__(BS) void k_init_hs(int n, const T *__restrict__ b,
     const V bv = reinterpret_cast<const V *>(b)[i];
     reinterpret_cast<V *>(x)[i] = V(T(0));
     reinterpret_cast<V *>(r)[i] = bv;
-    reinterpret_cast<V *>(p)[i] = bv;
+    reinterpret_cast<V *>(p)[i] = p_zero ? V(T(0)) : bv;
 #pragma unroll
     for (int j = 0; j < W; ++j) acc = acc + (double)bv[j] * (double)bv[j];
   }
   if (gid == 0)
     for (int i = nv * W; i < n; ++i) {
       const T bv = b[i];
-      x[i] = T(0); r[i] = bv; p[i] = bv;
+      x[i] = T(0); r[i] = bv; p[i] = p_zero ? T(0) : bv;
       acc = acc + (double)bv * (double)bv;
     }
   const double s = block_sum<BS>(acc, red);
-  if (threadIdx.x == 0 && part) part[blockIdx.x] = s;
+  if (tk.cnt1) {
+    __syncthreads();
+    ticket_finish<BS>(s, tk, red);
+  } else if (threadIdx.x == 0 && part) {
+    part[blockIdx.x] = s;
+  }
 }
 
 // x = 0, r = b, p = s = 0; part = b.b partials (CG1 prologue)
@@ -442,7 +660,8 @@ __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
                                                   T *__restrict__ r,
                                                   const T *__restrict__ s,
                                                   const CgState *__restrict__ st,
-                                                  double *__restrict__ part) {
+                                                  double *__restrict__ part,
+                                                  TicketArgs tk) {
   __shared__ double red[BS / kWave];
   if (st->done) return;
   typedef typename Vec16<T>::type V;
@@ -476,9 +695,14 @@ __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
       r[i] = ri;
       acc = acc + (double)ri * (double)ri;
     }
-  if (part) {
+  if (part || tk.cnt1) {
     const double sum = block_sum<BS>(acc, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = sum;
+    if (tk.cnt1) {
+      __syncthreads();
+      ticket_finish<BS>(sum, tk, red);
+    } else if (threadIdx.x == 0) {
+      part[blockIdx.x] = sum;
+    }
   }
 }
 
@@ -659,65 +883,7 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
   const double sa = sum_parts<BS>(pa, na, red);
   const double sb = pb ? sum_parts<BS>(pb, nb, red) : 0.0;
   if (threadIdx.x != 0) return;
-  switch (op) {
-    case FIN_SUM:
-      out[0] = sa;
-      break;
-    case FIN_SUM2:
-      out[0] = sa;
-      out[1] = sb;
-      break;
-    case FIN_INIT_HS:
-      st->bb = sa;
-      st->rr = sa;  // r = b (cg.c:107), so r.r == b.b bit for bit
-      st->tol2bb = st->tol * st->tol * sa;
-      st->k = 0;
-      st->done = 0;
-      break;
-    case FIN_HS_ALPHA:
-      st->ps = sa;
-      st->alpha = st->rr / sa;  // cg.c:113
-      break;
-    case FIN_HS_BETA: {
-      const double rr_new = sa;
-      const int k = st->k;
-      if (k < st->hist_cap) hist[k] = rr_new;
-      if (k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb)) {
-        st->done = 1;  // cg.c:125 break position
-      } else {
-        st->beta = rr_new / st->rr;  // cg.c:129
-        st->rr = rr_new;
-        st->k = k + 1;
-      }
-      break;
-    }
-    case FIN_INIT_CG1:
-      st->bb = sa;
-      st->rr = sa;
-      st->delta = sb;
-      st->tol2bb = st->tol * st->tol * sa;
-      st->alpha = sa / sb;
-      st->beta = 0.0;
-      st->k = 0;
-      st->done = 0;
-      break;
-    case FIN_CG1: {
-      const double g = sa, d = sb;
-      const int k = st->k;
-      if (k < st->hist_cap) hist[k] = g;
-      if (k >= st->max_iter || (st->use_tol && g <= st->tol2bb)) {
-        st->done = 1;
-      } else {
-        const double beta = g / st->rr;
-        st->delta = d;
-        st->alpha = g / (d - beta * g / st->alpha);
-        st->beta = beta;
-        st->rr = g;
-        st->k = k + 1;
-      }
-      break;
-    }
-  }
+  apply_fin(op, sa, sb, st, hist, out);
 }
 
 template <typename T, int BS>
@@ -788,26 +954,32 @@ static void launch_spmv_wave(const SpmvArgs<T> &a, int vec, hipStream_t st) {
   const int per = WPB * (a.rbw < 1 ? 1 : a.rbw);
   const int grid = (a.nblk + per - 1) / per;
   const bool epi = a.part != nullptr;
-#define CGX_SPMVW(V, E, N, P)                                                  \
-  hipLaunchKernelGGL((k_spmv_wave<T, WPB, CAPW, V, E, N, P>), dim3(grid),     \
+  const bool xpay = a.x2 != nullptr;
+#define CGX_SPMVW(V, E, N, X, G)                                               \
+  hipLaunchKernelGGL((k_spmv_wave<T, WPB, CAPW, V, E, N, X, G>), dim3(grid),     \
                      dim3(WPB * kWave), 0, st, a)
-#define CGX_SPMVW_P(V, N)                                                      \
+#define CGX_SPMVW_G(V, N, X)                                                     \
+  do {                                                                           \
+    if (a.tg) {                                                                  \
+      if (epi) CGX_SPMVW(V, true, N, X, true); else CGX_SPMVW(V, false, N, X, true); \
+    } else {                                                                     \
+      if (epi) CGX_SPMVW(V, true, N, X, false); else CGX_SPMVW(V, false, N, X, false); \
+    }                                                                            \
+  } while (0)
+#define CGX_SPMVW_X(V, N)                                                      \
   do {                                                                         \
-    if (a.pipe) {                                                              \
-      if (epi) CGX_SPMVW(V, true, N, true); else CGX_SPMVW(V, false, N, true); \
-    } else {                                                                   \
-      if (epi) CGX_SPMVW(V, true, N, false); else CGX_SPMVW(V, false, N, false); \
-    }                                                                          \
+    if (xpay) CGX_SPMVW_G(V, N, true); else CGX_SPMVW_G(V, N, false);         \
   } while (0)
 #define CGX_SPMVW_V(V)                                                         \
   do {                                                                         \
-    if (a.nt) CGX_SPMVW_P(V, true); else CGX_SPMVW_P(V, false);               \
+    if (a.nt) CGX_SPMVW_X(V, true); else CGX_SPMVW_X(V, false);               \
   } while (0)
   if (vec == 4) CGX_SPMVW_V(4);
   else if (vec == 2) CGX_SPMVW_V(2);
   else CGX_SPMVW_V(1);
 #undef CGX_SPMVW_V
-#undef CGX_SPMVW_P
+#undef CGX_SPMVW_X
+#undef CGX_SPMVW_G
 #undef CGX_SPMVW
 }
 
@@ -819,6 +991,7 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     else launch_spmv_wave<T, 4>(a, vec, st);
     return hipGetLastError();
   }
+  if (a.x2) return hipErrorInvalidValue;  // fused xpay: wave kernel only
   grid = grid < 1 ? 1 : (grid > a.nblk ? a.nblk : grid);
   if (a.bs == 512) launch_spmv_bs<T, 512>(a, grid, vec, st);
   else launch_spmv_bs<T, 256>(a, grid, vec, st);
@@ -827,9 +1000,11 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
 
 template <typename T>
 hipError_t launch_init_hs(int n, const T *b, T *x, T *r, T *p, double *part,
-                          int grid, hipStream_t st) {
+                          int grid, hipStream_t st, bool p_zero,
+                          const TicketArgs *tk) {
+  TicketArgs t = tk ? *tk : TicketArgs{};
   hipLaunchKernelGGL((k_init_hs<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n,
-                     b, x, r, p, part);
+                     b, x, r, p, part, p_zero ? 1 : 0, t);
   return hipGetLastError();
 }
 
@@ -844,9 +1019,10 @@ hipError_t launch_init_cg1(int n, const T *b, T *x, T *r, T *p, T *s,
 template <typename T>
 hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
                             const CgState *stt, double *part, int grid,
-                            hipStream_t st) {
+                            hipStream_t st, const TicketArgs *tk) {
+  TicketArgs t = tk ? *tk : TicketArgs{};
   hipLaunchKernelGGL((k_update_xr<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
-                     n, x, p, r, s, stt, part);
+                     n, x, p, r, s, stt, part, t);
   return hipGetLastError();
 }
 
@@ -918,12 +1094,14 @@ hipError_t launch_gather(int m, const int *idx, const T *x, T *buf,
   template hipError_t launch_spmv<T>(const SpmvArgs<T> &, int, int,           \
                                      hipStream_t);                             \
   template hipError_t launch_init_hs<T>(int, const T *, T *, T *, T *,        \
-                                        double *, int, hipStream_t);           \
+                                        double *, int, hipStream_t, bool,      \
+                                        const TicketArgs *);                   \
   template hipError_t launch_init_cg1<T>(int, const T *, T *, T *, T *, T *,  \
                                          double *, int, hipStream_t);          \
   template hipError_t launch_update_xr<T>(int, T *, const T *, T *,           \
                                           const T *, const CgState *,         \
-                                          double *, int, hipStream_t);         \
+                                          double *, int, hipStream_t,         \
+                                          const TicketArgs *);                 \
   template hipError_t launch_xpay<T>(int, T *, const T *, const CgState *,    \
                                      int, hipStream_t);                        \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *,           \

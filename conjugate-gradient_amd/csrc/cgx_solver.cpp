@@ -75,24 +75,33 @@ struct cgx_solver {
   int mode = CGX_MODE_FAST, alg = CGX_ALG_HS;
   int vec = 2;
   int spmv_xcd = 0, spmv_nt = 0, spmv_bs = 64, spmv_wpb = 4, spmv_rbw = 1,
-      spmv_pipe = 0;
+      spmv_tg = 1;
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   void *d_val = nullptr;
   void *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr,
-       *d_s = nullptr, *d_w = nullptr;
+       *d_s = nullptr, *d_w = nullptr, *d_p2 = nullptr;
+  // HS with the fused p-update: p alternates between d_p and d_p2; `par`
+  // says which one holds the previous direction (the SpMV's p_old)
+  bool fuse_xpay = true;
+  int par = 0;
   double *d_pa = nullptr, *d_pb = nullptr;
   int part_cap = 0;
+  // in-kernel ticket reduction (replaces the k_finalize launches of HS)
+  bool ticket = true;
+  int ngmax = 0;
+  double *d_tpart2 = nullptr;
+  unsigned *d_tcnt = nullptr;  // [ngroups_max] level-1 counters + [1] level-2
   CgState *d_st = nullptr, *h_st = nullptr;
   double *d_hist = nullptr;
   int hist_alloc = 0;
   size_t dev_bytes = 0;
   bool have_matrix = false, have_rhs = false, bench_ready = false;
   int last_iters = 0;
-  hipGraphExec_t gexec = nullptr;
-  int gexec_key = -1;
+  hipGraphExec_t gexec[2] = {nullptr, nullptr};  // by starting parity
+  int gexec_key[2] = {-1, -1};
   std::vector<hipEvent_t> events;
 };
 
@@ -120,9 +129,11 @@ void dfree(void **p) {
 }
 
 void drop_graph(cgx_solver *s) {
-  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-  s->gexec = nullptr;
-  s->gexec_key = -1;
+  for (int i = 0; i < 2; ++i) {
+    if (s->gexec[i]) (void)hipGraphExecDestroy(s->gexec[i]);
+    s->gexec[i] = nullptr;
+    s->gexec_key[i] = -1;
+  }
 }
 
 void free_matrix(cgx_solver *s) {
@@ -138,8 +149,11 @@ void free_matrix(cgx_solver *s) {
   dfree(&s->d_p);
   dfree(&s->d_s);
   dfree(&s->d_w);
+  dfree(&s->d_p2);
   dfree((void **)&s->d_pa);
   dfree((void **)&s->d_pb);
+  dfree((void **)&s->d_tpart2);
+  dfree((void **)&s->d_tcnt);
   dfree((void **)&s->d_hist);
   s->hist_alloc = 0;
   s->dev_bytes = 0;
@@ -203,7 +217,8 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       (rc = dalloc(s, &s->d_r, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_p, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_s, nv * sizeof(T))) ||
-      (rc = dalloc(s, &s->d_w, nv * sizeof(T)))) {
+      (rc = dalloc(s, &s->d_w, nv * sizeof(T))) ||
+      (rc = dalloc(s, &s->d_p2, nv * sizeof(T)))) {
     free_matrix(s);
     return rc;
   }
@@ -214,11 +229,16 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   s->spmv_grid = spmv_launch_grid(s->spmv_bs, s->spmv_wpb, s->spmv_rbw, s->nblk, s->spmv_grid);
   s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
   s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
+  const size_t ngmax = (size_t)s->part_cap / kTicketGroup + 2;
   if ((rc = dalloc(s, (void **)&s->d_pa, (size_t)s->part_cap * 8)) ||
-      (rc = dalloc(s, (void **)&s->d_pb, (size_t)s->part_cap * 8))) {
+      (rc = dalloc(s, (void **)&s->d_pb, (size_t)s->part_cap * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_tpart2, ngmax * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_tcnt, (ngmax + 1) * 4))) {
     free_matrix(s);
     return rc;
   }
+  CGX_HIP(hipMemsetAsync(s->d_tcnt, 0, (ngmax + 1) * 4, s->stream));
+  s->ngmax = (int)ngmax;
   CGX_HIP(hipMemsetAsync(s->d_col, 0, nnz_pad * 4, s->stream));
   CGX_HIP(hipMemsetAsync(s->d_val, 0, nnz_pad * sizeof(T), s->stream));
   if (n > 0) {
@@ -280,8 +300,33 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.bs = s->spmv_bs;
   a.wpb = s->spmv_wpb;
   a.rbw = s->spmv_rbw;
-  a.pipe = s->spmv_pipe;
+  a.x2 = nullptr;
+  a.xout = nullptr;
+  a.st = s->d_st;
+  a.tg = s->spmv_tg;
+  a.tk = TicketArgs{};
   return a;
+}
+
+TicketArgs ticket_args(cgx_solver *s, int op) {
+  TicketArgs t;
+  t.part1 = s->d_pa;
+  t.part2 = s->d_tpart2;
+  t.cnt1 = s->d_tcnt;
+  t.cnt2 = s->d_tcnt + s->ngmax;
+  t.op = op;
+  t.st = s->d_st;
+  t.hist = s->d_hist;
+  return t;
+}
+
+bool use_ticket(const cgx_solver *s) {
+  return s->ticket && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST &&
+         s->spmv_bs == 64;
+}
+
+bool fused(const cgx_solver *s) {
+  return s->fuse_xpay && s->alg == CGX_ALG_HS && s->spmv_bs == 64;
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -289,14 +334,20 @@ template <typename T>
 int enqueue_init(cgx_solver *s) {
   hipStream_t st = s->stream;
   T *b = (T *)s->d_b, *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p;
+  s->par = 0;
   if (s->alg == CGX_ALG_HS) {
+    const bool pz = fused(s);
     if (s->mode == CGX_MODE_EXACT) {
-      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, nullptr, s->vec_grid, st));
+      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, nullptr, s->vec_grid, st, pz));
       CGX_HIP(launch_dot_seq<T>(s->n, b, b, s->d_pa, nullptr, st));
       CGX_HIP(launch_finalize(FIN_INIT_HS, s->d_pa, 1, nullptr, 0, s->d_st,
                               s->d_hist, nullptr, st));
+    } else if (use_ticket(s)) {
+      const TicketArgs tk = ticket_args(s, FIN_INIT_HS);
+      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, s->d_pa, s->vec_grid, st, pz,
+                                &tk));
     } else {
-      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, s->d_pa, s->vec_grid, st));
+      CGX_HIP(launch_init_hs<T>(s->n, b, x, r, p, s->d_pa, s->vec_grid, st, pz));
       CGX_HIP(launch_finalize(FIN_INIT_HS, s->d_pa, s->vec_grid, nullptr, 0,
                               s->d_st, s->d_hist, nullptr, st));
     }
@@ -320,11 +371,23 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   const int sg = s->spmv_grid;
   if (s->alg == CGX_ALG_HS) {
     const bool exact = s->mode == CGX_MODE_EXACT;
+    const bool fx = fused(s);
+    // with the fused p-update the SpMV reads p_old, writes p = r + beta p_old
+    T *pold = fx ? (T *)(s->par ? s->d_p2 : s->d_p) : p;
+    if (fx) p = (T *)(s->par ? s->d_p : s->d_p2);
+    SpmvArgs<T> sa = spmv_args<T>(s, fx ? (void *)r : (void *)p, sv,
+                                  exact ? nullptr : s->d_pa, true);
+    if (fx) {
+      sa.x2 = pold;
+      sa.xout = p;
+    }
+    // Tickets only where workgroups live long (k_update_xr): a short-lived
+    // SpMV workgroup waiting on its ticket's round trip cost 20% (r01 A/B).
+    const bool tkt = use_ticket(s);
     if (ev0) CGX_HIP(hipEventRecord(ev0, st));
-    CGX_HIP(launch_spmv<T>(spmv_args<T>(s, p, sv, exact ? nullptr : s->d_pa,
-                                        true),
-                           s->spmv_grid, s->vec, st));           // cg.c:111
+    CGX_HIP(launch_spmv<T>(sa, s->spmv_grid, s->vec, st));       // cg.c:111 (+131-132)
     if (ev1) CGX_HIP(hipEventRecord(ev1, st));
+    if (fx) s->par ^= 1;
     if (exact) {
       CGX_HIP(launch_dot_seq<T>(s->n, p, sv, s->d_pa, &s->d_st->done, st));
       CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, 1, nullptr, 0, s->d_st,
@@ -334,6 +397,12 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
       CGX_HIP(launch_dot_seq<T>(s->n, r, r, s->d_pa, &s->d_st->done, st));
       CGX_HIP(launch_finalize(FIN_HS_BETA, s->d_pa, 1, nullptr, 0, s->d_st,
                               s->d_hist, nullptr, st));           // cg.c:125-129
+    } else if (tkt) {  // the beta step runs in k_update_xr's last workgroup
+      CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, sg, nullptr, 0, s->d_st,
+                              s->d_hist, nullptr, st));
+      const TicketArgs tk = ticket_args(s, FIN_HS_BETA);
+      CGX_HIP(launch_update_xr<T>(s->n, x, p, r, sv, s->d_st, s->d_pa,
+                                  s->vec_grid, st, &tk));
     } else {
       CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, sg, nullptr, 0, s->d_st,
                               s->d_hist, nullptr, st));
@@ -342,7 +411,8 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
       CGX_HIP(launch_finalize(FIN_HS_BETA, s->d_pa, s->vec_grid, nullptr, 0,
                               s->d_st, s->d_hist, nullptr, st));
     }
-    CGX_HIP(launch_xpay<T>(s->n, p, r, s->d_st, s->vec_grid, st));  // cg.c:131-132
+    if (!fx)
+      CGX_HIP(launch_xpay<T>(s->n, p, r, s->d_st, s->vec_grid, st));  // cg.c:131-132
   } else {
     CGX_HIP(launch_cg1_update<T>(s->n, x, p, r, sv, w, s->d_st, s->d_pa,
                                  s->vec_grid, st));
@@ -358,29 +428,33 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
 
 template <typename T>
 int enqueue_iters(cgx_solver *s, long long count) {
-  const int B = s->graph_batch;
+  int B = s->graph_batch;
+  if (B & 1) ++B;  // even: the fused p buffers return to the same parity
   const int key = s->alg * 2 + s->mode;
   if (s->use_graph && count >= B) {
-    if (!s->gexec || s->gexec_key != key) {
-      drop_graph(s);
+    const int par = s->par;
+    if (!s->gexec[par] || s->gexec_key[par] != key) {
+      if (s->gexec[par]) (void)hipGraphExecDestroy(s->gexec[par]);
+      s->gexec[par] = nullptr;
       hipGraph_t g = nullptr;
       CGX_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
       int rc = 0;
       for (int i = 0; i < B && rc == 0; ++i)
         rc = enqueue_iter<T>(s, nullptr, nullptr);
       hipError_t e = hipStreamEndCapture(s->stream, &g);
+      s->par = par;  // capture only recorded the iterations
       if (rc) {
         if (g) (void)hipGraphDestroy(g);
         return rc;
       }
       CGX_HIP(e);
-      e = hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0);
+      e = hipGraphInstantiate(&s->gexec[par], g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
       CGX_HIP(e);
-      s->gexec_key = key;
+      s->gexec_key[par] = key;
     }
     while (count >= B) {
-      CGX_HIP(hipGraphLaunch(s->gexec, s->stream));
+      CGX_HIP(hipGraphLaunch(s->gexec[par], s->stream));
       count -= B;
     }
   }
@@ -552,7 +626,6 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->vec = cgx::env_int("CGX_SPMV_VEC", 4);
   s->spmv_wpb = cgx::env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
   s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", 1));
-  s->spmv_pipe = cgx::env_int("CGX_SPMV_PIPE", 0);
   s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
   s->spmv_nt = cgx::env_int("CGX_SPMV_NT", 0);
   {
@@ -562,6 +635,9 @@ int cgx_solver_create(int device, cgx_solver **out) {
   if (s->vec != 1 && s->vec != 2 && s->vec != 4) s->vec = 4;
   s->use_graph = cgx::env_int("CGX_GRAPH", 1) != 0;
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
+  s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
+  s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
+  s->ticket = cgx::env_int("CGX_TICKET", 0) != 0;
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
       hipHostMalloc((void **)&s->h_st, sizeof(CgState), hipHostMallocDefault) !=
@@ -689,6 +765,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   // B_spmv = nnz*(s_v+4) + 4*(n+1) + 2*n*s_v; B_iter = B_spmv + 9*n*s_v
   info->spmv_bytes = (double)s->nnz * (sv + 4) + 4.0 * (s->n + 1) + 2.0 * s->n * sv;
   info->iter_bytes = info->spmv_bytes + 9.0 * s->n * sv;
+  info->spmv_iter_bytes = info->spmv_bytes + (fused(s) ? 2.0 * s->n * sv : 0.0);
   info->device_bytes = s->dev_bytes;
   return 0;
 }

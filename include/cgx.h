@@ -71,7 +71,10 @@ typedef struct {
   int spmv_grid;        /* workgroups of the persistent SpMV launch          */
   int vec_grid;         /* workgroups of the vector-update launches          */
   double spmv_bytes;    /* algorithmic HBM bytes per SpMV     */
-  double iter_bytes;    /* algorithmic HBM bytes per CG iteration            */
+  double iter_bytes;    /* algorithmic HBM bytes per CG iteration (8d)       */
+  double spmv_iter_bytes; /* algorithmic bytes of the SpMV launch as it runs
+                             inside the iteration (HS fuses p = r + beta p:
+                             + r and p_old gathered, p_new written)         */
   size_t device_bytes;  /* device memory held by the solver                  */
 } cgx_info;
 

@@ -349,3 +349,51 @@ def test_empty_system():
     assert L.conj_grad(3, A.ptr, b.ptr, ctypes.byref(out)) == 0
     assert out.contents.size == 0
     L.cgx_free_mv_deep(out)
+
+
+@pytest.mark.parametrize("ticket", ["0", "1"])
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_reduction_paths_match_oracle_and_reproduce(ticket, fuse, monkeypatch):
+    """Finalize kernels vs the in-kernel ticket reduction, with and without
+    the fused p-update: all within FAST_RTOL of the reference order, and each
+    bit-reproducible run to run (deterministic reductions, no fp64 atomics)."""
+    monkeypatch.setenv("CGX_TICKET", ticket)
+    monkeypatch.setenv("CGX_FUSE_XPAY", fuse)
+    rp, col, val, b = H.random_spd(30000, 9, seed=12)
+    x_ref, _ = H.o_conj_grad(60, rp, col, val, b)
+    xs, hs = [], []
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        for _ in range(2):
+            s.set_rhs(b)
+            assert s.run(60) == 61
+            xs.append(s.x())
+            hs.append(s.history(61))
+        its = s.run(1000, 1e-9)
+        x_tol = s.x()
+    assert rel(xs[0], x_ref) <= FAST_RTOL
+    assert H.same_bits_or_both_nan(xs[0], xs[1]) and H.same_bits_or_both_nan(hs[0], hs[1])
+    _, its_o, _ = H.o_solve(1000, 1e-9, rp, col, val, b)
+    assert abs(its - its_o) <= 1
+    r = b - H.o_spmv(rp, col, val, x_tol)
+    assert np.linalg.norm(r) <= 1.01e-9 * np.linalg.norm(b)
+
+
+def test_ticket_large_grid_and_tiny():
+    """Ticket reduction across > kTicketGroup^2 workgroups (two full levels)
+    and with a single workgroup."""
+    rp, col, val = cgx.laplacian3d(160, 160, 160)   # 4.1 M rows, 64 K SpMV workgroups
+    b = np.random.default_rng(3).standard_normal(len(rp) - 1)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        s.run(5)
+        x = s.x()
+    x_ref, _ = H.o_conj_grad(5, rp, col, val, b)
+    assert rel(x, x_ref) <= FAST_RTOL
+    g = H.load_golden("kat_tridiag10")
+    with cgx.Solver(0) as s:
+        s.set_matrix(g["row_ptr"], g["col"], g["val"])
+        s.set_rhs(g["b"])
+        s.run(3)
+        assert rel(s.x(), g["iters"][3]) <= FAST_RTOL

@@ -1,0 +1,7 @@
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 600 python tools/sweep.py --workload c3 --rounds 3 --iters 30 \
+  --variant fused:CGX_FUSE_XPAY=1 --variant unfused:CGX_FUSE_XPAY=0 --variant fused_nt:CGX_FUSE_XPAY=1,CGX_SPMV_NT=1 \
+  > gpurun_out/sweep6.log 2>&1; rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep6.log | grep -v amdgpu.ids

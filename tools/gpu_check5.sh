@@ -1,0 +1,8 @@
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 600 python tools/sweep.py --workload c3 --rounds 3 --iters 30 \
+  --variant ticket:CGX_TICKET=1 --variant noticket:CGX_TICKET=0 --variant ticket_nt:CGX_TICKET=1,CGX_SPMV_NT=1 \
+  --variant ticket_fused:CGX_TICKET=1,CGX_FUSE_XPAY=1 \
+  > gpurun_out/sweep9.log 2>&1; rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep9.log | grep -v amdgpu.ids

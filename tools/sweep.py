@@ -50,6 +50,7 @@ for v in variants:
             os.environ[k] = old
     solvers.append((name, s))
 info = solvers[0][1].info()
+infos = {n: s.info() for n, s in solvers}
 res = {n: {"spmv": [], "iter": []} for n, _ in solvers}
 for r in range(a.rounds):
     for name, s in solvers:
@@ -61,6 +62,7 @@ print(f"workload {a.workload}: n={info['n']} nnz={info['nnz']} spmv_bytes={info[
       f"iter_bytes={info['iter_bytes']:.0f} grid={info['spmv_grid']} rowblocks={info['n_rowblocks']}")
 for name, d in res.items():
     sm, si = statistics.median(d["spmv"]), statistics.median(d["iter"])
+    sb = infos[name]["spmv_iter_bytes"]
     print(f"{name:>14}: spmv med {sm:8.2f} us min {min(d['spmv']):8.2f}  "
-          f"({info['spmv_bytes'] / sm / 1e3:7.1f} GB/s)   iter med {si:8.2f} us "
+          f"({sb / sm / 1e3:7.1f} GB/s)   iter med {si:8.2f} us "
           f"({1e6 / si:7.1f} it/s, {info['iter_bytes'] / si / 1e3:7.1f} GB/s)")
