@@ -110,7 +110,15 @@ struct SpmvArgs {
   const CgState *st;
   int tg;              // k_spmv_wave: transposed (row-per-lane) gather
   TicketArgs tk;       // k_spmv_wave + EPI: in-kernel finalize (cnt1 != 0)
+  // SELL-64 layout (k_spmv_sell) when s_off != nullptr: val/col hold the
+  // sliced arrays, s_off[i] = slice i's first element / 64, s_len[i] = width
+  const int *s_off;
+  const int *s_len;
+  int nslices;
+  int n;
 };
+
+inline int spmv_sell_grid(int nslices) { return (nslices + 3) / 4; }
 
 // Row-block plan: consecutive rows, at most `rows` rows and `cap` nonzeros
 // per block; a row longer than `cap` gets a block of its own (chunked path).

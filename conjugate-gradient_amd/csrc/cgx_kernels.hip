@@ -576,6 +576,71 @@ __global__ __launch_bounds__(WPB * kWave, TG ? 6 : 8) void k_spmv_wave(SpmvArgs<
   }
 }
 
+// SELL-64 (sliced ELLPACK, one 64-row slice per wave, column-major inside the
+// slice): lane t owns row t of its slice and walks the row's nonzeros in
+// column order, so every load is a coalesced wave-wide line (val 512 B, col
+// 256 B per instruction), the x gathers of step j hit 64 consecutive rows'
+// j-th columns, no row_ptr is streamed and nothing is staged in LDS.  Padding
+// (val 0, col = the row itself) sits after the row's real entries, so the
+// sequential sum is the reference's order (mv_ops.c:190-194): +-0 products
+// never change a sum.  Internal layout only; the C ABI still takes CSR.
+template <typename T, int WPB, bool EPI, bool XPAY>
+__global__ __launch_bounds__(WPB * kWave) void k_spmv_sell(SpmvArgs<T> a) {
+  __shared__ double red[WPB];
+  if (a.done && *a.done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int slice = blockIdx.x * WPB + wid;
+  const T beta = XPAY ? (T)a.st->beta : T(0);
+  double dot = 0.0;
+  if (slice < a.nslices) {
+    const long long off = (long long)__builtin_amdgcn_readfirstlane(a.s_off[slice]) * kWave;
+    const int len = __builtin_amdgcn_readfirstlane(a.s_len[slice]);
+    const int row = slice * kWave + lane;
+    const T *vs = a.val + off + lane;
+    const int *cs = a.col + off + lane;
+    T acc = T(0);
+    constexpr int U = 8;
+    for (int j0 = 0; j0 < len; j0 += U) {
+      T v[U];
+      int c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = j0 + u < len;  // wave-uniform
+        v[u] = ok ? vs[(j0 + u) * kWave] : T(0);
+        c[u] = ok ? cs[(j0 + u) * kWave] : 0;
+      }
+      T xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xv[u] = operand<T, XPAY>(a, beta, c[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j0 + u < len) {
+          const T prod = v[u] * xv[u];
+          acc = acc + prod;
+        }
+    }
+    if (row < a.n) {
+      T xrow = T(0);
+      if (EPI || XPAY) xrow = operand<T, XPAY>(a, beta, row);
+      if (XPAY) a.xout[row] = xrow;
+      a.y[row] = acc;
+      if (EPI) dot = (double)xrow * (double)acc;
+    }
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) s = s + red[w];
+      a.part[blockIdx.x] = s;
+    }
+  }
+}
+
 // ------------------------------------------------------- vector kernels
 // All grid-stride over 16-byte vectors; the scalar tail (n % W) is handled
 // by global thread 0.  Reductions: per-thread fixed-order sums, then
@@ -985,6 +1050,17 @@ static void launch_spmv_wave(const SpmvArgs<T> &a, int vec, hipStream_t st) {
 
 template <typename T>
 hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) {
+  if (a.s_off) {  // SELL-64 layout
+    if (a.nslices <= 0) return hipSuccess;
+    constexpr int WPB = 4;
+    const int g = (a.nslices + WPB - 1) / WPB;
+    const bool epi = a.part != nullptr, xp = a.x2 != nullptr;
+    if (epi && xp) hipLaunchKernelGGL((k_spmv_sell<T, WPB, true, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi) hipLaunchKernelGGL((k_spmv_sell<T, WPB, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (xp) hipLaunchKernelGGL((k_spmv_sell<T, WPB, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_sell<T, WPB, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.nblk <= 0) return hipSuccess;
   if (a.bs == 64) {
     if (a.wpb == 8) launch_spmv_wave<T, 8>(a, vec, st);

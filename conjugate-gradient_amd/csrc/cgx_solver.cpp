@@ -49,6 +49,51 @@ std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap) {
   return blk;
 }
 
+// SELL-64: slice i = rows [64i, 64i+64), width = its longest row, element
+// (j, lane) at 64*(s_off[i] + j) + lane.  Padding (val 0, col = the row)
+// follows each row's entries.  Returns false (use CSR) when the padded size
+// exceeds max_pad * nnz, i.e. for irregular row lengths.
+template <typename T>
+bool csr_to_sell64(int n, const int *rp, const int *col, const T *val,
+                   double max_pad, std::vector<int> &s_off,
+                   std::vector<int> &s_len, std::vector<T> &sval,
+                   std::vector<int> &scol) {
+  const int nsl = (n + 63) / 64;
+  s_off.assign((size_t)nsl + 1, 0);
+  s_len.assign((size_t)nsl, 0);
+  long long tot = 0;  // in units of 64 elements
+  for (int i = 0; i < nsl; ++i) {
+    int w = 0;
+    for (int r = 64 * i; r < std::min(n, 64 * i + 64); ++r)
+      w = std::max(w, rp[r + 1] - rp[r]);
+    s_len[i] = w;
+    s_off[i] = (int)tot;
+    tot += w;
+    if (tot > INT32_MAX) return false;
+  }
+  s_off[nsl] = (int)tot;
+  const long long nnz = n > 0 ? rp[n] : 0;
+  if ((double)tot * 64 > max_pad * (double)std::max<long long>(nnz, 1) + 64.0 * nsl)
+    return false;
+  sval.assign((size_t)tot * 64, T(0));
+  scol.assign((size_t)tot * 64, 0);
+  for (int i = 0; i < nsl; ++i)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int r = 64 * i + lane;
+      const int len = r < n ? rp[r + 1] - rp[r] : 0;
+      for (int j = 0; j < s_len[i]; ++j) {
+        const size_t e = ((size_t)s_off[i] + j) * 64 + lane;
+        if (j < len) {
+          sval[e] = val[rp[r] + j];
+          scol[e] = col[rp[r] + j];
+        } else {
+          scol[e] = r < n ? r : 0;
+        }
+      }
+    }
+  return true;
+}
+
 int vec_grid_for(int n, int cus) {
   const long long vecs = (n + 1) / 2;
   long long g = (vecs + kVecBS - 1) / kVecBS;
@@ -80,6 +125,11 @@ struct cgx_solver {
   bool use_graph = true;
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
+  // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
+  bool want_sell = false, sell = false;
+  int *d_soff = nullptr, *d_slen = nullptr;
+  int nslices = 0;
+  long long sell_elems = 0;
   void *d_val = nullptr;
   void *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr,
        *d_s = nullptr, *d_w = nullptr, *d_p2 = nullptr;
@@ -142,6 +192,11 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_col);
   dfree((void **)&s->d_blk);
   dfree((void **)&s->d_blkk);
+  dfree((void **)&s->d_soff);
+  dfree((void **)&s->d_slen);
+  s->sell = false;
+  s->nslices = 0;
+  s->sell_elems = 0;
   dfree(&s->d_val);
   dfree(&s->d_b);
   dfree(&s->d_x);
@@ -258,6 +313,35 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   CGX_HIP(hipMemcpyAsync(s->d_blkk, blkk.data(), blkk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
+  if (s->want_sell && n > 0) {
+    std::vector<int> soff, slen, scol;
+    std::vector<T> sval;
+    if (csr_to_sell64<T>(n, rp, col, val, 1.25, soff, slen, sval, scol)) {
+      dfree((void **)&s->d_col);
+      dfree(&s->d_val);
+      const size_t ne = sval.size() + kPad;
+      if ((rc = dalloc(s, (void **)&s->d_col, ne * 4)) ||
+          (rc = dalloc(s, &s->d_val, ne * sizeof(T))) ||
+          (rc = dalloc(s, (void **)&s->d_soff, soff.size() * 4)) ||
+          (rc = dalloc(s, (void **)&s->d_slen, slen.size() * 4 + 4))) {
+        free_matrix(s);
+        return rc;
+      }
+      CGX_HIP(hipMemcpy(s->d_col, scol.data(), scol.size() * 4, hipMemcpyHostToDevice));
+      CGX_HIP(hipMemcpy(s->d_val, sval.data(), sval.size() * sizeof(T), hipMemcpyHostToDevice));
+      CGX_HIP(hipMemcpy(s->d_soff, soff.data(), soff.size() * 4, hipMemcpyHostToDevice));
+      CGX_HIP(hipMemcpy(s->d_slen, slen.data(), slen.size() * 4, hipMemcpyHostToDevice));
+      s->sell = true;
+      s->nslices = (int)slen.size();
+      s->sell_elems = (long long)sval.size();
+      s->spmv_grid = spmv_sell_grid(s->nslices);
+      if (s->spmv_grid + 1 > s->part_cap) {
+        set_error("internal: SELL grid exceeds partial buffer");
+        free_matrix(s);
+        return CGX_ENOMEM;
+      }
+    }
+  }
   s->have_matrix = true;
   return 0;
 }
@@ -305,6 +389,10 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.st = s->d_st;
   a.tg = s->spmv_tg;
   a.tk = TicketArgs{};
+  a.s_off = s->sell ? s->d_soff : nullptr;
+  a.s_len = s->sell ? s->d_slen : nullptr;
+  a.nslices = s->nslices;
+  a.n = s->n;
   return a;
 }
 
@@ -322,11 +410,11 @@ TicketArgs ticket_args(cgx_solver *s, int op) {
 
 bool use_ticket(const cgx_solver *s) {
   return s->ticket && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST &&
-         s->spmv_bs == 64;
+         (s->spmv_bs == 64 || s->sell);
 }
 
 bool fused(const cgx_solver *s) {
-  return s->fuse_xpay && s->alg == CGX_ALG_HS && s->spmv_bs == 64;
+  return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell);
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -638,6 +726,10 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0;
+  {
+    const char *l = getenv("CGX_LAYOUT");
+    s->want_sell = l && strcmp(l, "sell") == 0;
+  }
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
       hipHostMalloc((void **)&s->h_st, sizeof(CgState), hipHostMallocDefault) !=
@@ -765,7 +857,12 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   // B_spmv = nnz*(s_v+4) + 4*(n+1) + 2*n*s_v; B_iter = B_spmv + 9*n*s_v
   info->spmv_bytes = (double)s->nnz * (sv + 4) + 4.0 * (s->n + 1) + 2.0 * s->n * sv;
   info->iter_bytes = info->spmv_bytes + 9.0 * s->n * sv;
-  info->spmv_iter_bytes = info->spmv_bytes + (fused(s) ? 2.0 * s->n * sv : 0.0);
+  if (s->sell)  // the SELL kernel's own algorithmic bytes: padded slices, no row_ptr
+    info->spmv_iter_bytes = (double)s->sell_elems * (sv + 4) + 8.0 * s->nslices +
+                            2.0 * s->n * sv;
+  else
+    info->spmv_iter_bytes = info->spmv_bytes;
+  if (fused(s)) info->spmv_iter_bytes += 2.0 * s->n * sv;
   info->device_bytes = s->dev_bytes;
   return 0;
 }

@@ -397,3 +397,30 @@ def test_ticket_large_grid_and_tiny():
         s.set_rhs(g["b"])
         s.run(3)
         assert rel(s.x(), g["iters"][3]) <= FAST_RTOL
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_sell_layout_bit_exact(fuse, monkeypatch):
+    """SELL-64 internal layout: SpMV bit-exact (padding after each row's
+    entries), CG within tolerance; irregular matrices fall back to CSR."""
+    monkeypatch.setenv("CGX_LAYOUT", "sell")
+    monkeypatch.setenv("CGX_FUSE_XPAY", fuse)
+    with cgx.Solver(0) as s:
+        for name in ["lap3d_12", "lap2d_32", "dense128", "rand_spd_2000", "kat_tridiag10"]:
+            g = H.load_golden(name)
+            s.set_matrix(g["row_ptr"], g["col"], g["val"])
+            assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"]), name
+            s.set_rhs(g["b"])
+            it = max(k for k in g["iters"] if not np.any(np.isnan(g["iters"][k])))
+            s.run(it)
+            assert rel(s.x(), g["iters"][it]) <= FAST_RTOL, name
+        rp, col, val = cgx.laplacian3d(70, 60, 50)
+        x = np.random.default_rng(6).standard_normal(len(rp) - 1)
+        s.set_matrix(rp, col, val)
+        assert s.info()["spmv_iter_bytes"] < s.info()["spmv_bytes"] + 4 * len(x) * 8
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        rp32, col32, v32 = cgx.random_spd(5000, 40, 9, f32=True)
+        x32 = np.random.default_rng(2).standard_normal(5000).astype(np.float32)
+        s.set_matrix(rp32, col32, v32)
+        assert np.array_equal(s.spmv(x32).view(np.uint32),
+                              H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
