@@ -15,7 +15,7 @@ from pathlib import Path
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "lib" / "libcgx.so"
+LIB_PATH = Path(os.environ["CGX_LIB"]) if os.environ.get("CGX_LIB") else HERE / "lib" / "libcgx.so"
 
 CGX_EINVAL, CGX_ENODEV, CGX_ENOMEM, CGX_ECOMM = -1, -2, -3, -4
 CGX_MODE_FAST, CGX_MODE_EXACT = 0, 1

@@ -68,6 +68,11 @@ struct cgx_dist {
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   int *d_list_int = nullptr, *d_list_bnd = nullptr;
   int n_int = 0, n_bnd = 0, g_int = 0, g_bnd = 0;
+  // interior / boundary row blocks as contiguous runs {first, count} when
+  // there are few of them (slab partitions: 1 interior + 2 boundary runs);
+  // otherwise the index lists above are used (one launch each)
+  std::vector<std::pair<int, int>> runs_int, runs_bnd;
+  bool use_runs = false;
   double *d_val = nullptr;
   double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr,
          *d_s = nullptr, *d_w = nullptr;
@@ -88,11 +93,17 @@ struct cgx_dist {
   std::vector<hipEvent_t> spmv_ev;
   bool rec_spmv = false;
   size_t ev_i = 0;
+  // single rank, no transport: the iteration is [update, SpMV, finalize] on
+  // one stream, replayed as hipGraphs of graph_batch iterations
+  hipGraphExec_t gexec = nullptr;
+  int graph_batch = 16;
 };
 
 namespace {
 
 using namespace cgx;
+
+bool solo(const cgx_dist *d) { return d->nranks == 1 && !d->local; }
 
 #define CGX_NCCL(call)                                                       \
   do {                                                                       \
@@ -124,6 +135,8 @@ void dfree(P **p) {
 }
 
 void free_system(cgx_dist *d) {
+  if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
+  d->gexec = nullptr;
   dfree(&d->d_rp); dfree(&d->d_col); dfree(&d->d_blk); dfree(&d->d_blkk);
   dfree(&d->d_list_int); dfree(&d->d_list_bnd); dfree(&d->d_val);
   dfree(&d->d_b); dfree(&d->d_x); dfree(&d->d_r); dfree(&d->d_p);
@@ -159,6 +172,7 @@ int init_common(cgx_dist *d, int device) {
   d->vec = env_int("CGX_SPMV_VEC", 4);
   if (d->vec != 1 && d->vec != 2 && d->vec != 4) d->vec = 4;
   d->wpb = env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
+  d->graph_batch = env_int("CGX_GRAPH", 1) ? std::max(1, env_int("CGX_GRAPH_BATCH", 16)) : 0;
   CGX_HIP(hipSetDevice(device));
   CGX_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
   CGX_HIP(hipStreamCreateWithFlags(&d->st_comm, hipStreamNonBlocking));
@@ -209,11 +223,29 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
   }
   d->n_int = (int)lint.size();
   d->n_bnd = (int)lbnd.size();
-  d->g_int = spmv_launch_grid(64, d->wpb, 1, d->n_int, 0);
-  d->g_bnd = spmv_launch_grid(64, d->wpb, 1, d->n_bnd, 0);
+  auto runs = [](const std::vector<int> &l) {
+    std::vector<std::pair<int, int>> r;
+    for (int b : l) {
+      if (!r.empty() && r.back().first + r.back().second == b) r.back().second++;
+      else r.push_back({b, 1});
+    }
+    return r;
+  };
+  d->runs_int = runs(lint);
+  d->runs_bnd = runs(lbnd);
+  d->use_runs = d->runs_int.size() <= 4 && d->runs_bnd.size() <= 4 &&
+                env_int("CGX_DIST_RUNS", 1) != 0;
+  if (d->use_runs) {
+    d->g_int = d->g_bnd = 0;
+    for (auto &r : d->runs_int) d->g_int += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
+    for (auto &r : d->runs_bnd) d->g_bnd += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
+  } else {
+    d->g_int = spmv_launch_grid(64, d->wpb, 1, d->n_int, 0);
+    d->g_bnd = spmv_launch_grid(64, d->wpb, 1, d->n_bnd, 0);
+  }
   d->vec_grid = vec_grid_for(n_loc, d->cus);
 
-  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kPad;
+  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
   const size_t nv = (size_t)n_loc + kPad;
   if ((rc = dalloc(d, &d->d_rp, ((size_t)n_loc + 1) * 4)) ||
       (rc = dalloc(d, &d->d_col, nnz_pad * 4)) ||
@@ -387,6 +419,7 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.blk_row = d->d_blk;
   a.blk_k = d->d_blkk;
   a.blk_list = boundary ? d->d_list_bnd : d->d_list_int;
+  a.blk_first = 0;
   a.nblk = boundary ? d->n_bnd : d->n_int;
   a.part = boundary ? d->d_pb + d->g_int : d->d_pb;
   a.done = &d->d_st->done;
@@ -409,6 +442,7 @@ int phase_update(cgx_dist *d, bool init) {
     CGX_HIP(launch_cg1_update<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_s,
                                       d->d_w, d->d_st, d->d_pa, d->vec_grid,
                                       d->st));
+  if (solo(d)) return 0;
   CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, d->d_r, d->d_sendbuf,
                                 d->st));
   CGX_HIP(hipEventRecord(d->ev_packed, d->st));
@@ -417,6 +451,7 @@ int phase_update(cgx_dist *d, bool init) {
 
 // phase B: halo exchange on the communication stream
 int phase_halo(cgx_dist *d) {
+  if (solo(d)) return 0;
   CGX_HIP(hipSetDevice(d->device));
   CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_packed, 0));
   double *ghost = d->d_r + d->n_loc;
@@ -447,19 +482,41 @@ int phase_halo(cgx_dist *d) {
 }
 
 // phase C: SpMV (interior overlapping the halo, then boundary) + local sums
+// SpMV over one set of row blocks (interior or boundary): one launch per
+// contiguous run, partials packed after each other from d_pb + part_off.
+int spmv_set(cgx_dist *d, bool boundary) {
+  SpmvArgs<double> a = spmv_args(d, boundary);
+  if (!d->use_runs) {
+    CGX_HIP(launch_spmv<double>(a, boundary ? d->g_bnd : d->g_int, d->vec, d->st));
+    return 0;
+  }
+  a.blk_list = nullptr;
+  double *part = boundary ? d->d_pb + d->g_int : d->d_pb;
+  for (const auto &r : boundary ? d->runs_bnd : d->runs_int) {
+    a.blk_first = r.first;
+    a.nblk = r.second;
+    a.part = part;
+    CGX_HIP(launch_spmv<double>(a, 0, d->vec, d->st));
+    part += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
+  }
+  return 0;
+}
+
 int phase_spmv(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
+  int rc;
   if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i], d->st));
-  CGX_HIP(launch_spmv<double>(spmv_args(d, false), d->g_int, d->vec, d->st));
+  if ((rc = spmv_set(d, false))) return rc;
   if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 1], d->st));
-  CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
+  if (!solo(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
   if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 2], d->st));
-  CGX_HIP(launch_spmv<double>(spmv_args(d, true), d->g_bnd, d->vec, d->st));
+  if ((rc = spmv_set(d, true))) return rc;
   if (rec) {
     CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 3], d->st));
     d->ev_i += 4;
   }
+  if (solo(d)) return 0;  // phase_reduce finalizes straight from the partials
   CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, d->vec_grid, d->d_pb,
                           d->g_int + d->g_bnd, d->d_st, d->d_hist, d->d_sums,
                           d->st));
@@ -470,6 +527,12 @@ int phase_spmv(cgx_dist *d) {
 // phase D: the one all-reduce of the iteration (gamma, delta), then scalars
 int phase_reduce(cgx_dist *d, bool init) {
   CGX_HIP(hipSetDevice(d->device));
+  if (solo(d)) {
+    CGX_HIP(launch_finalize(init ? FIN_INIT_CG1 : FIN_CG1, d->d_pa, d->vec_grid,
+                            d->d_pb, d->g_int + d->g_bnd, d->d_st, d->d_hist,
+                            nullptr, d->st));
+    return 0;
+  }
   const double *g = d->d_gsums;
   if (d->local) {
     for (cgx_dist *o : d->group->parts)
@@ -487,7 +550,36 @@ int phase_reduce(cgx_dist *d, bool init) {
   return 0;
 }
 
+int run_phases_eager(Group *g, bool init, long long iters);
+
 int run_phases(Group *g, bool init, long long iters) {
+  cgx_dist *d = g->parts[0];
+  const int B = d->graph_batch;
+  if (!init && solo(d) && B > 0 && iters >= B && !d->rec_spmv) {
+    if (!d->gexec) {
+      hipGraph_t gr = nullptr;
+      CGX_HIP(hipSetDevice(d->device));
+      CGX_HIP(hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal));
+      int rc = run_phases_eager(g, false, B);
+      hipError_t e = hipStreamEndCapture(d->st, &gr);
+      if (rc) {
+        if (gr) (void)hipGraphDestroy(gr);
+        return rc;
+      }
+      CGX_HIP(e);
+      e = hipGraphInstantiate(&d->gexec, gr, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(gr);
+      CGX_HIP(e);
+    }
+    while (iters >= B) {
+      CGX_HIP(hipGraphLaunch(d->gexec, d->st));
+      iters -= B;
+    }
+  }
+  return run_phases_eager(g, init, iters);
+}
+
+int run_phases_eager(Group *g, bool init, long long iters) {
   auto &P = g->parts;
   for (long long it = 0; it < (init ? 1 : iters); ++it) {
     int rc;

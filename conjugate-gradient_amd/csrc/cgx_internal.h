@@ -51,13 +51,17 @@ static_assert(sizeof(CgState) == 96, "CgState layout");
 // spmv_cap(bs) products staged in LDS (16 KiB per 256 lanes).
 inline int spmv_cap(int bs, bool f64) { return bs * (f64 ? 8 : 16); }
 // Workgroups of one SpMV launch (= fused-dot partials it writes).
-inline int spmv_launch_grid(int bs, int wpb, int rbw, int nblk, int grid) {
+inline int spmv_launch_grid(int bs, int wpb, int rbw, int nblk, int grid,
+                            int dma = 0) {
+  if (bs == 64 && dma == 2) return (nblk + 2 * rbw - 1) / (2 * rbw);
+  if (bs == 64 && dma) return (nblk + 3) / 4;
   if (bs == 64) return (nblk + wpb * rbw - 1) / (wpb * rbw);
   return grid < 1 ? 1 : (grid > nblk ? nblk : grid);
 }
 constexpr int kVecBS = 256;
 constexpr int kFinBS = 1024;
 constexpr int kPad = 8;               // val/col padded to a multiple of this
+constexpr int kWindowPad = 1024;      // + one SpMV window (LDS-DMA reads whole windows)
 
 // Finalize ops (single-workgroup scalar steps of the recurrence).
 enum FinOp {
@@ -92,7 +96,9 @@ struct SpmvArgs {
   T *y;
   const int *blk_row;  // row-block boundaries, nblk_total+1 entries
   const int *blk_k;    // rp[blk_row[i]]: nonzero offset of each row block
-  const int *blk_list; // optional subset of row blocks (nullptr: 0..nblk-1)
+  const int *blk_list; // optional subset of row blocks (nullptr: a contiguous
+                       // run blk_first .. blk_first+nblk-1)
+  int blk_first;
   int nblk;            // row blocks processed by this launch
   double *part;        // per-workgroup partial of x[row]*y[row] (nullptr: none)
   const int *done;     // early-exit flag (nullptr: never)
@@ -116,6 +122,9 @@ struct SpmvArgs {
   const int *s_len;
   int nslices;
   int n;
+  int dma;             // 1: k_spmv_dma (LDS-DMA stream, one block per wave)
+                       // 2: k_spmv_pipe (persistent waves, rbw blocks each,
+                       //    next block's stream prefetched by LDS-DMA)
 };
 
 inline int spmv_sell_grid(int nslices) { return (nslices + 3) / 4; }

@@ -14,6 +14,7 @@
 // fuses multiply-add (Makefile:2 builds -O0), and x + alpha*p must round
 // twice to stay bit-identical.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include "cgx_internal.h"
 
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(BS) void k_spmv(SpmvArgs<T> a) {
   double dot = 0.0;
 
   for (int i = lo; i < hi; ++i) {
-    const int rb = a.blk_list ? a.blk_list[i] : i;
+    const int rb = a.blk_list ? a.blk_list[i] : a.blk_first + i;
     // Row-block descriptor: rows [r0, r0+nr), nonzeros [k0, k1) -- wave-
     // uniform scalar loads, so the stream loads below issue without waiting
     // on row_ptr.
@@ -334,7 +335,7 @@ struct WaveBlock {
   iv c[NIT];
 
   __device__ __forceinline__ void describe(const SpmvArgs<T> &a, int wb) {
-    const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : wb);
+    const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : a.blk_first + wb);
     r0 = __builtin_amdgcn_readfirstlane(a.blk_row[rb]);
     nr = __builtin_amdgcn_readfirstlane(a.blk_row[rb + 1]) - r0;
     k0 = __builtin_amdgcn_readfirstlane(a.blk_k[rb]);
@@ -571,6 +572,333 @@ __global__ __launch_bounds__(WPB * kWave, TG ? 6 : 8) void k_spmv_wave(SpmvArgs<
       __syncthreads();
       ticket_finish<WPB * kWave>(s, a.tk, red);
     } else if (threadIdx.x == 0) {
+      a.part[blockIdx.x] = s;
+    }
+  }
+}
+
+// LDS-DMA CSR-stream: the wave's val/col window goes straight from memory
+// into its LDS slice with global_load_lds_dwordx4 (1 KiB per wave-instruction,
+// no VGPRs), then lane t walks row t from LDS as in the transposed-gather
+// finish (sequential per-row sums: bit-exact).  val/col are padded by one
+// window past nnz, so the window load never leaves the allocation.
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename T, int WPB, int CAPW, bool EPI, bool XPAY>
+__global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
+  static_assert((CAPW * sizeof(T)) % 1024 == 0 && (CAPW * 4) % 1024 == 0, "window");
+  __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
+  __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
+  __shared__ double red[WPB];
+  if (a.done && *a.done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  T *lval = lval_all + wid * CAPW;
+  int *lcol = lcol_all + wid * CAPW;
+  const T beta = XPAY ? (T)a.st->beta : T(0);
+  const int wb = blockIdx.x * WPB + wid;
+  double dot = 0.0;
+  if (wb < a.nblk) {
+    const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : a.blk_first + wb);
+    const int r0 = __builtin_amdgcn_readfirstlane(a.blk_row[rb]);
+    const int nr = __builtin_amdgcn_readfirstlane(a.blk_row[rb + 1]) - r0;
+    const int k0 = __builtin_amdgcn_readfirstlane(a.blk_k[rb]);
+    const int k1 = __builtin_amdgcn_readfirstlane(a.blk_k[rb + 1]);
+    const int kb = k0 & ~3;  // 16-B aligned for both val (T) and col (int)
+    const bool fits = k1 - kb <= CAPW;
+    if (fits) {
+      constexpr int EV = 16 / sizeof(T);  // elements of T per lane per DMA
+#pragma unroll
+      for (int i = 0; i < (int)(CAPW * sizeof(T) / 1024); ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(a.val + kb + i * kWave * EV + lane * EV),
+            (lds_void *)(lval + i * kWave * EV), 16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < CAPW * 4 / 1024; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(a.col + kb + i * kWave * 4 + lane * 4),
+            (lds_void *)(lcol + i * kWave * 4), 16, 0, 0);
+    }
+    int j0 = 0, j1 = 0;
+    T xrow = T(0);
+    if (lane < nr) {
+      j0 = a.rp[r0 + lane];
+      j1 = a.rp[r0 + lane + 1];
+      if (EPI || XPAY) xrow = operand<T, XPAY>(a, beta, r0 + lane);
+      if (XPAY) a.xout[r0 + lane] = xrow;
+    }
+    T acc = T(0);
+    if (fits) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wave_lds_sync();
+      if (lane < nr) {
+        constexpr int U = 4;
+        for (int j = j0 - kb; j < j1 - kb; j += U) {
+          const int cnt = min(U, j1 - kb - j);
+          int cc[U];
+          T vv[U], xx[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            cc[u] = u < cnt ? lcol[j + u] : 0;
+            vv[u] = u < cnt ? lval[j + u] : T(0);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) xx[u] = operand<T, XPAY>(a, beta, cc[u]);
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (u < cnt) {
+              const T prod = vv[u] * xx[u];
+              acc = acc + prod;
+            }
+        }
+      }
+    } else {
+      for (int c0 = k0; c0 < k1; c0 += CAPW) {
+        const int m = min(CAPW, k1 - c0);
+        for (int t = lane; t < m; t += kWave)
+          lval[t] = a.val[c0 + t] * operand<T, XPAY>(a, beta, a.col[c0 + t]);
+        wave_lds_sync();
+        if (lane == 0)
+          for (int j = 0; j < m; ++j) acc = acc + lval[j];
+        wave_lds_sync();
+      }
+    }
+    if (lane < nr) {
+      a.y[r0 + lane] = acc;
+      if (EPI) dot = (double)xrow * (double)acc;
+    }
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) s = s + red[w];
+      a.part[blockIdx.x] = s;
+    }
+  }
+}
+
+// Pipelined LDS-DMA CSR-stream.  The per-block chain (descriptor -> row_ptr
+// -> stream -> gather -> store) is ~70 us of pure latency on C3 when every
+// wave does one block (r01 diagnostics: the val/col stream alone is ~135 us
+// at 6.2 TB/s and the two ADD instead of overlapping).  Here a persistent
+// wave walks RBW consecutive row blocks with a two-slot LDS ring: while block
+// i's x gathers and row sums run, block i+1's val/col window (LDS-DMA, no
+// VGPRs), row bounds and epilogue operand are already in flight.  Wait
+// discipline (vmcnt counts in issue order): gathers(i) are issued BEFORE the
+// prefetch of i+1, so waiting on them leaves the prefetch in flight; the
+// top-of-iteration vmcnt(0) then only waits for the prefetch issued one
+// block of work earlier.  Row sums stay sequential: bit-exact.
+// gathers + next window's LDS-DMA as ONE asm block ending in a partial
+// vmcnt.  LLVM's waitcnt pass treats an in-flight global_load_lds as a
+// different event type and answers any later VGPR-load use with vmcnt(0),
+// which would drain the prefetch; inside the block the order is explicit:
+// 8 gathers, then the DMA ops, then vmcnt(#DMA) = gathers complete.
+// The DMA addresses are per-op register pairs (an instruction offset would
+// also move the LDS address); M0 holds the LDS base, s_nop 0 after each write.
+__device__ __forceinline__ void gather8_dma(double (&xv)[8], const double *const (&g)[8],
+                                            const void *const (&d)[6], unsigned lv,
+                                            unsigned lc) {
+  asm volatile(
+      "global_load_dwordx2 %0, %8, off\n\t"
+      "global_load_dwordx2 %1, %9, off\n\t"
+      "global_load_dwordx2 %2, %10, off\n\t"
+      "global_load_dwordx2 %3, %11, off\n\t"
+      "global_load_dwordx2 %4, %12, off\n\t"
+      "global_load_dwordx2 %5, %13, off\n\t"
+      "global_load_dwordx2 %6, %14, off\n\t"
+      "global_load_dwordx2 %7, %15, off\n\t"
+      "s_mov_b32 m0, %22\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %16, off\n\t"
+      "s_add_u32 m0, %22, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %17, off\n\t"
+      "s_add_u32 m0, %22, 0x800\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %18, off\n\t"
+      "s_add_u32 m0, %22, 0xc00\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %19, off\n\t"
+      "s_mov_b32 m0, %23\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %20, off\n\t"
+      "s_add_u32 m0, %23, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %21, off\n\t"
+      "s_waitcnt vmcnt(6)"
+      : "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2]), "=&v"(xv[3]), "=&v"(xv[4]),
+        "=&v"(xv[5]), "=&v"(xv[6]), "=&v"(xv[7])
+      : "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]),
+        "v"(g[7]), "v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]), "v"(d[4]), "v"(d[5]),
+        "s"(lv), "s"(lc)
+      : "memory", "m0", "scc");
+}
+
+__device__ __forceinline__ void gather8_dma(float (&xv)[8], const float *const (&g)[8],
+                                            const void *const (&d)[8], unsigned lv,
+                                            unsigned lc) {
+  asm volatile(
+      "global_load_dword %0, %8, off\n\t"
+      "global_load_dword %1, %9, off\n\t"
+      "global_load_dword %2, %10, off\n\t"
+      "global_load_dword %3, %11, off\n\t"
+      "global_load_dword %4, %12, off\n\t"
+      "global_load_dword %5, %13, off\n\t"
+      "global_load_dword %6, %14, off\n\t"
+      "global_load_dword %7, %15, off\n\t"
+      "s_mov_b32 m0, %24\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %16, off\n\t"
+      "s_add_u32 m0, %24, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %17, off\n\t"
+      "s_add_u32 m0, %24, 0x800\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %18, off\n\t"
+      "s_add_u32 m0, %24, 0xc00\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %19, off\n\t"
+      "s_mov_b32 m0, %25\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %20, off\n\t"
+      "s_add_u32 m0, %25, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %21, off\n\t"
+      "s_add_u32 m0, %25, 0x800\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %22, off\n\t"
+      "s_add_u32 m0, %25, 0xc00\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %23, off\n\t"
+      "s_waitcnt vmcnt(8)"
+      : "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2]), "=&v"(xv[3]), "=&v"(xv[4]),
+        "=&v"(xv[5]), "=&v"(xv[6]), "=&v"(xv[7])
+      : "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]),
+        "v"(g[7]), "v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]), "v"(d[4]), "v"(d[5]),
+        "v"(d[6]), "v"(d[7]), "s"(lv), "s"(lc)
+      : "memory", "m0", "scc");
+}
+
+template <typename T, int WPB, int CAPW, bool EPI>
+__global__ __launch_bounds__(WPB * kWave) void k_spmv_pipe(SpmvArgs<T> a) {
+  // Branch-free prefetch: descriptors are preloaded into lanes (readlane),
+  // row bounds use clamped indices, windows are always DMA'd (nnz is padded
+  // by kWindowPad >= CAPW) and the last block of a wave is peeled.
+  static_assert(CAPW * sizeof(T) == 4096 && CAPW * 4 == (sizeof(T) == 8 ? 2048 : 4096),
+                "window layout is baked into gather8_dma");
+  constexpr int EV = 16 / (int)sizeof(T);
+  constexpr int NDMA = (int)(CAPW * sizeof(T) / 1024) + CAPW * 4 / 1024;
+  constexpr int U = 8;  // entries per row gathered before the prefetch
+  __shared__ __attribute__((aligned(16))) T lval_all[WPB * 2 * CAPW];
+  __shared__ __attribute__((aligned(16))) int lcol_all[WPB * 2 * CAPW];
+  __shared__ double red[WPB];
+  if (a.done && *a.done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  T *lv = lval_all + wid * 2 * CAPW;
+  int *lc = lcol_all + wid * 2 * CAPW;
+  const int first = (blockIdx.x * WPB + wid) * a.rbw;
+  const int last = min(first + a.rbw, a.nblk);  // rbw <= 63 (host clamps)
+  double dot = 0.0;
+
+  int drow = 0, dk = 0;  // lane l: descriptor of block first + l
+  if (first < last && lane <= last - first) {
+    drow = a.blk_row[a.blk_first + first + lane];
+    dk = a.blk_k[a.blk_first + first + lane];
+  }
+
+  int r0n = 0, nrn = 0, k0n = 0, k1n = 0, j0n = 0, j1n = 0;
+  T xrn = T(0);
+  auto load_desc = [&](int blk) {  // scalar descriptor + row bounds (tracked)
+    const int l = blk - first;
+    r0n = __builtin_amdgcn_readlane(drow, l);
+    nrn = __builtin_amdgcn_readlane(drow, l + 1) - r0n;
+    k0n = __builtin_amdgcn_readlane(dk, l);
+    k1n = __builtin_amdgcn_readlane(dk, l + 1);
+  };
+  auto load_rows = [&]() {
+    const int rr = lane < nrn ? r0n + lane : r0n;
+    j0n = a.rp[rr];
+    j1n = a.rp[rr + 1];
+    if (EPI) xrn = a.x[rr];
+  };
+  auto lds_addr = [](const void *p) {
+    return (unsigned)(uintptr_t)(lds_void *)p;
+  };
+
+  auto body = [&](int i, auto pf) {
+    constexpr bool PF = decltype(pf)::value;
+    const int slot = (i - first) & 1;
+    // vmcnt(0) as an intrinsic (0x0F70: expcnt/lgkmcnt at max) so the waitcnt
+    // pass also knows nothing is pending
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    wave_lds_sync();
+    const int r0 = r0n, nr = nrn, k0 = k0n, k1 = k1n, kb = k0n & ~3;
+    const int j0 = j0n, j1 = j1n;
+    const T xrow = xrn;
+    const bool fit = k1 - kb <= CAPW;
+    const T *cv = lv + slot * CAPW;
+    const int *cc = lc + slot * CAPW;
+    T acc = T(0);
+    if (!fit) {
+      // a single long row: chunked through the slot, lane 0 sums in order
+      T *pr = lv + slot * CAPW;
+      for (int c0 = k0; c0 < k1; c0 += CAPW) {
+        const int m = min(CAPW, k1 - c0);
+        for (int t = lane; t < m; t += kWave) pr[t] = a.val[c0 + t] * a.x[a.col[c0 + t]];
+        wave_lds_sync();
+        if (lane == 0)
+          for (int j = 0; j < m; ++j) acc = acc + pr[j];
+        wave_lds_sync();
+      }
+    }
+    const int cnt = (fit && lane < nr) ? min(U, j1 - j0) : 0;
+    const T *gp[U];
+    T v[U], xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = u < cnt ? j0 - kb + u : 0;
+      const int c = cc[idx];
+      gp[u] = a.x + (u < cnt ? c : 0);
+      v[u] = cv[idx];
+    }
+    if constexpr (PF) {
+      load_desc(i + 1);
+      const int kbn = k0n & ~3;
+      const void *d[NDMA];
+#pragma unroll
+      for (int q = 0; q < (int)(CAPW * sizeof(T) / 1024); ++q)
+        d[q] = (const void *)(a.val + kbn + q * kWave * EV + lane * EV);
+#pragma unroll
+      for (int q = 0; q < CAPW * 4 / 1024; ++q)
+        d[(int)(CAPW * sizeof(T) / 1024) + q] = (const void *)(a.col + kbn + q * kWave * 4 + lane * 4);
+      gather8_dma(xv, gp, d, lds_addr(lv + (slot ^ 1) * CAPW), lds_addr(lc + (slot ^ 1) * CAPW));
+      load_rows();
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) xv[u] = *gp[u];
+    }
+    // unconditional: acc + (+0) == acc exactly, so padding terms are inert
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const T prod = v[u] * xv[u];
+      acc = acc + (u < cnt ? prod : T(0));
+    }
+    if (fit && lane < nr)
+      for (int j = j0 + U; j < j1; ++j) {  // rows longer than U, in order
+        const T prod = cv[j - kb] * a.x[cc[j - kb]];
+        acc = acc + prod;
+      }
+    if (lane < nr) {
+      a.y[r0 + lane] = acc;
+      if (EPI) dot = dot + (double)xrow * (double)acc;
+    }
+  };
+
+  if (first < last) {
+    load_desc(first);
+    {
+      const int kb = k0n & ~3;
+#pragma unroll
+      for (int q = 0; q < (int)(CAPW * sizeof(T) / 1024); ++q)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(a.val + kb + q * kWave * EV + lane * EV),
+            (lds_void *)(lv + q * kWave * EV), 16, 0, 0);
+#pragma unroll
+      for (int q = 0; q < CAPW * 4 / 1024; ++q)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(a.col + kb + q * kWave * 4 + lane * 4),
+            (lds_void *)(lc + q * kWave * 4), 16, 0, 0);
+    }
+    load_rows();
+    int i = first;
+    for (; i + 1 < last; ++i) body(i, std::true_type{});
+    body(i, std::false_type{});
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) s = s + red[w];
       a.part[blockIdx.x] = s;
     }
   }
@@ -1062,6 +1390,26 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     return hipGetLastError();
   }
   if (a.nblk <= 0) return hipSuccess;
+  if (a.bs == 64 && a.dma == 2 && !a.blk_list && !a.x2) {  // pipelined LDS-DMA
+    constexpr int WPB = 2;
+    constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;
+    const int per = WPB * (a.rbw < 1 ? 1 : a.rbw);
+    const int g = (a.nblk + per - 1) / per;
+    if (a.part) hipLaunchKernelGGL((k_spmv_pipe<T, WPB, CAPW, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_pipe<T, WPB, CAPW, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    return hipGetLastError();
+  }
+  if (a.bs == 64 && a.dma) {
+    constexpr int WPB = 4;
+    constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;
+    const int g = (a.nblk + WPB - 1) / WPB;
+    const bool epi = a.part != nullptr, xp = a.x2 != nullptr;
+    if (epi && xp) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (xp) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.bs == 64) {
     if (a.wpb == 8) launch_spmv_wave<T, 8>(a, vec, st);
     else launch_spmv_wave<T, 4>(a, vec, st);

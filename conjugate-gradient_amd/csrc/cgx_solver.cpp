@@ -120,7 +120,7 @@ struct cgx_solver {
   int mode = CGX_MODE_FAST, alg = CGX_ALG_HS;
   int vec = 2;
   int spmv_xcd = 0, spmv_nt = 0, spmv_bs = 64, spmv_wpb = 4, spmv_rbw = 1,
-      spmv_tg = 1;
+      spmv_tg = 1, spmv_dma = 0;
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
   int graph_batch = 16;
@@ -259,7 +259,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   if (n > 0) blk = plan_rowblocks(n, rp, s->spmv_bs, cap - kPad);  // room for VEC alignment
   else blk.push_back(0);
   s->nblk = (int)blk.size() - 1;
-  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kPad;
+  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
   const size_t nv = (size_t)n + kPad;
   int rc;
   if ((rc = dalloc(s, (void **)&s->d_rp, ((size_t)n + 1) * 4)) ||
@@ -281,7 +281,8 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   if (s->spmv_grid >= 64 && s->spmv_grid < s->nblk)
     s->spmv_grid &= ~7;  // XCD-aware mapping needs G % 8 == 0
   if (s->spmv_grid < 1) s->spmv_grid = 1;
-  s->spmv_grid = spmv_launch_grid(s->spmv_bs, s->spmv_wpb, s->spmv_rbw, s->nblk, s->spmv_grid);
+  s->spmv_grid = spmv_launch_grid(s->spmv_bs, s->spmv_wpb, s->spmv_rbw, s->nblk,
+                                  s->spmv_grid, s->spmv_dma);
   s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
   s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
   const size_t ngmax = (size_t)s->part_cap / kTicketGroup + 2;
@@ -376,6 +377,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.blk_row = s->d_blk;
   a.blk_k = s->d_blkk;
   a.blk_list = nullptr;
+  a.blk_first = 0;
   a.nblk = s->nblk;
   a.part = part;
   a.done = with_done ? &s->d_st->done : nullptr;
@@ -393,6 +395,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.s_len = s->sell ? s->d_slen : nullptr;
   a.nslices = s->nslices;
   a.n = s->n;
+  a.dma = s->spmv_dma;
   return a;
 }
 
@@ -414,7 +417,8 @@ bool use_ticket(const cgx_solver *s) {
 }
 
 bool fused(const cgx_solver *s) {
-  return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell);
+  return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
+         s->spmv_dma != 2;
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -713,7 +717,9 @@ int cgx_solver_create(int device, cgx_solver **out) {
     s->cus = prop.multiProcessorCount;
   s->vec = cgx::env_int("CGX_SPMV_VEC", 4);
   s->spmv_wpb = cgx::env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
-  s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", 1));
+  s->spmv_dma = cgx::env_int("CGX_SPMV_DMA", 0);
+  s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", s->spmv_dma == 2 ? 8 : 1));
+  if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
   s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
   s->spmv_nt = cgx::env_int("CGX_SPMV_NT", 0);
   {
@@ -725,7 +731,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
   s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
-  s->ticket = cgx::env_int("CGX_TICKET", 0) != 0;
+  s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma != 2;  // pipe: partials only
   {
     const char *l = getenv("CGX_LAYOUT");
     s->want_sell = l && strcmp(l, "sell") == 0;

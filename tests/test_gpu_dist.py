@@ -45,9 +45,11 @@ def solve_local(rp, col, val, b, P, maxit, tol):
     return x, its, hist, stats
 
 
+@pytest.mark.parametrize("runs", ["1", "0"])
 @pytest.mark.parametrize("kind", ["lap3d", "lap2d", "rand"])
 @pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
-def test_local_partitions_match_oracle(kind, P):
+def test_local_partitions_match_oracle(kind, P, runs, monkeypatch):
+    monkeypatch.setenv("CGX_DIST_RUNS", runs)
     rp, col, val, b = system(kind)
     x, its, hist, stats = solve_local(rp, col, val, b, P, 2000, 1e-10)
     x_ref, its_ref, hist_ref = H.o_solve(2000, 1e-10, rp, col, val, b, cg1=True)

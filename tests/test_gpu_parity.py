@@ -65,13 +65,23 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
-    """Every SpMV variant (wave / workgroup row blocks, load widths) keeps the
-    sequential per-row order, fp64 and fp32, including long rows."""
+    """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
+    pipelined persistent waves with 1/8/63 blocks each) keeps the sequential
+    per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
-    monkeypatch.setenv("CGX_SPMV_BS", bs)
+    if bs == "dma":
+        monkeypatch.setenv("CGX_SPMV_DMA", "1")
+    elif bs.startswith("pipe"):
+        monkeypatch.setenv("CGX_SPMV_DMA", "2")
+        if bs != "pipe":
+            monkeypatch.setenv("CGX_SPMV_RBW", bs[4:])
+    elif bs == "notg":
+        monkeypatch.setenv("CGX_SPMV_TG", "0")
+    else:
+        monkeypatch.setenv("CGX_SPMV_BS", bs)
     rp, col, val, b = H.random_spd(4000, 9, seed=3)
     g = H.load_golden("dense128")
     with cgx.Solver(0) as s:
@@ -93,9 +103,14 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
         assert rel(s.x(), x_ref) <= FAST_RTOL
 
 
-@pytest.mark.parametrize("bs", ["64", "256"])
+@pytest.mark.parametrize("bs", ["64", "256", "dma", "pipe"])
 def test_spmv_long_rows_variants(bs, monkeypatch):
-    monkeypatch.setenv("CGX_SPMV_BS", bs)
+    if bs == "dma":
+        monkeypatch.setenv("CGX_SPMV_DMA", "1")
+    elif bs == "pipe":
+        monkeypatch.setenv("CGX_SPMV_DMA", "2")
+    else:
+        monkeypatch.setenv("CGX_SPMV_BS", bs)
     n = 3000
     rng = np.random.default_rng(8)
     rows = [np.arange(n) if i in (0, 7, n - 1) else
@@ -150,13 +165,16 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-def test_spmv_c3_full_size_bit_exact(solver):
+@pytest.mark.parametrize("dma", ["0", "2"])
+def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
-    bit-exact against the oracle at full size."""
+    bit-exact against the oracle at full size (default and pipelined kernels)."""
+    monkeypatch.setenv("CGX_SPMV_DMA", dma)
     rp, col, val = cgx.laplacian3d(216, 216, 216)
     x = np.random.default_rng(2).standard_normal(len(rp) - 1)
-    solver.set_matrix(rp, col, val)
-    assert H.same_bits_or_both_nan(solver.spmv(x), H.o_spmv(rp, col, val, x))
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
 # -------------------------------------------------------- mv_ops.h op list
