@@ -428,6 +428,7 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.rbw = 1;
   a.st = d->d_st;
   a.tg = env_int("CGX_SPMV_TG", 1);
+  a.nt = env_int("CGX_SPMV_NT", 0);  // as the single-GPU solver
   a.tk = TicketArgs{};
   return a;
 }

@@ -584,8 +584,11 @@ __global__ __launch_bounds__(WPB * kWave, TG ? 6 : 8) void k_spmv_wave(SpmvArgs<
 // window past nnz, so the window load never leaves the allocation.
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <typename T, int WPB, int CAPW, bool EPI, bool XPAY>
+template <typename T, int WPB, int CAPW, bool EPI, bool XPAY, bool NT = false>
 __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
+  // NT: the once-per-iteration matrix stream is loaded non-temporal (aux = 2)
+  // so it does not displace the CG vectors from the Infinity Cache.
+  constexpr int AUX = NT ? 2 : 0;
   static_assert((CAPW * sizeof(T)) % 1024 == 0 && (CAPW * 4) % 1024 == 0, "window");
   __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
@@ -612,12 +615,12 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
       for (int i = 0; i < (int)(CAPW * sizeof(T) / 1024); ++i)
         __builtin_amdgcn_global_load_lds(
             (const void *)(a.val + kb + i * kWave * EV + lane * EV),
-            (lds_void *)(lval + i * kWave * EV), 16, 0, 0);
+            (lds_void *)(lval + i * kWave * EV), 16, 0, AUX);
 #pragma unroll
       for (int i = 0; i < CAPW * 4 / 1024; ++i)
         __builtin_amdgcn_global_load_lds(
             (const void *)(a.col + kb + i * kWave * 4 + lane * 4),
-            (lds_void *)(lcol + i * kWave * 4), 16, 0, 0);
+            (lds_void *)(lcol + i * kWave * 4), 16, 0, AUX);
     }
     int j0 = 0, j1 = 0;
     T xrow = T(0);
@@ -1047,7 +1050,7 @@ __global__ __launch_bounds__(BS) void k_init_cg1(int n, const T *__restrict__ b,
 }
 
 // x += alpha*p (cg.c:115-118); r -= alpha*s (cg.c:122-123); part = r.r
-template <typename T, int BS>
+template <typename T, int BS, bool XNT = false>
 __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
                                                   const T *__restrict__ p,
                                                   T *__restrict__ r,
@@ -1064,7 +1067,10 @@ __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
   const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
   double acc = 0.0;
   for (int i = gid; i < nv; i += stride) {
-    V xv = reinterpret_cast<const V *>(x)[i];
+    // XNT: x is touched only here -- keep it out of the Infinity Cache so
+    // p, r and Ap (read again within the iteration) stay resident
+    V xv = XNT ? __builtin_nontemporal_load(reinterpret_cast<const V *>(x) + i)
+               : reinterpret_cast<const V *>(x)[i];
     const V pv = reinterpret_cast<const V *>(p)[i];
     V rv = reinterpret_cast<const V *>(r)[i];
     const V sv = reinterpret_cast<const V *>(s)[i];
@@ -1076,7 +1082,8 @@ __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
       rv[j] = rv[j] - as;
       acc = acc + (double)rv[j] * (double)rv[j];
     }
-    reinterpret_cast<V *>(x)[i] = xv;
+    if (XNT) __builtin_nontemporal_store(xv, reinterpret_cast<V *>(x) + i);
+    else reinterpret_cast<V *>(x)[i] = xv;
     reinterpret_cast<V *>(r)[i] = rv;
   }
   if (gid == 0)
@@ -1242,23 +1249,24 @@ __global__ __launch_bounds__(BS) void k_dot_part(int n, const T *__restrict__ a,
 template <int BS>
 __device__ __forceinline__ double sum_parts(const double *pa, int na,
                                             double *red) {
-  // Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order; loads are
-  // issued 16 at a time (coalesced across the workgroup) before their adds.
-  constexpr int U = 16;
+  // Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order.  All of a
+  // thread's loads (up to U) are issued before the first add, so a 40K-entry
+  // partial array costs one memory round trip, not one per 16 entries.
+  constexpr int U = 48;
   double acc = 0.0;
   int i = threadIdx.x;
-  if (i < na) {
-    acc = pa[i];
-    i += BS;
-  }
-  for (; i + (U - 1) * BS < na; i += U * BS) {
+  bool first = true;
+  for (; i < na; i += U * BS) {
     double v[U];
 #pragma unroll
-    for (int j = 0; j < U; ++j) v[j] = pa[i + j * BS];
+    for (int j = 0; j < U; ++j) v[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
 #pragma unroll
-    for (int j = 0; j < U; ++j) acc = acc + v[j];
+    for (int j = 0; j < U; ++j)
+      if (i + j * BS < na) {
+        acc = first ? v[j] : acc + v[j];
+        first = false;
+      }
   }
-  for (; i < na; i += BS) acc = acc + pa[i];
   const double s = block_sum<BS>(acc, red);
   __syncthreads();
   return s;
@@ -1270,12 +1278,13 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
                                                  CgState *st, double *hist,
                                                  double *out) {
   __shared__ double red[BS / kWave];
-  if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_INIT_HS &&
-      op != FIN_INIT_CG1 && st->done)
-    return;
+  // partial loads go out before the done-flag round trip
   const double sa = sum_parts<BS>(pa, na, red);
   const double sb = pb ? sum_parts<BS>(pb, nb, red) : 0.0;
   if (threadIdx.x != 0) return;
+  if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_INIT_HS &&
+      op != FIN_INIT_CG1 && st->done)
+    return;
   apply_fin(op, sa, sb, st, hist, out);
 }
 
@@ -1405,7 +1414,9 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     const int g = (a.nblk + WPB - 1) / WPB;
     const bool epi = a.part != nullptr, xp = a.x2 != nullptr;
     if (epi && xp) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (!xp && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (xp) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     return hipGetLastError();
@@ -1445,8 +1456,13 @@ hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
                             const CgState *stt, double *part, int grid,
                             hipStream_t st, const TicketArgs *tk) {
   TicketArgs t = tk ? *tk : TicketArgs{};
-  hipLaunchKernelGGL((k_update_xr<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
-                     n, x, p, r, s, stt, part, t);
+  static const bool xnt = env_int("CGX_VEC_XNT", 0) != 0;
+  if (xnt)
+    hipLaunchKernelGGL((k_update_xr<T, kVecBS, true>), dim3(grid), dim3(kVecBS), 0, st,
+                       n, x, p, r, s, stt, part, t);
+  else
+    hipLaunchKernelGGL((k_update_xr<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st,
+                       n, x, p, r, s, stt, part, t);
   return hipGetLastError();
 }
 

@@ -721,7 +721,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", s->spmv_dma == 2 ? 8 : 1));
   if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
   s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
-  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", 0);
+  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", 0);  // order-rotated A/B (sweep15): nt +4% on the wave kernel
   {
     const int bs = cgx::env_int("CGX_SPMV_BS", 64);
     s->spmv_bs = (bs == 512 || bs == 64) ? bs : 256;

@@ -27,8 +27,13 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--alg", default="hs")
 ap.add_argument("--variant", action="append", default=[])
+ap.add_argument("--control", action="store_true",
+                help="append a second copy of the first variant (placement/order control)")
 a = ap.parse_args()
 variants = a.variant or ["base:"]
+if a.control:
+    n0, _, e0 = variants[0].partition(":")
+    variants = variants + [f"{n0}_ctl:{e0}"]
 
 sysm = bench.make_system(bench.WORKLOADS[a.workload])
 solvers = []
@@ -53,7 +58,8 @@ info = solvers[0][1].info()
 infos = {n: s.info() for n, s in solvers}
 res = {n: {"spmv": [], "iter": []} for n, _ in solvers}
 for r in range(a.rounds):
-    for name, s in solvers:
+    k = r % len(solvers)  # rotate the order so no variant always runs first
+    for name, s in solvers[k:] + solvers[:k]:
         tot, sp = s.bench_run(a.iters, graph=False, spmv_events=True)
         res[name]["spmv"].append(sp * 1e3)
         tot, _ = s.bench_run(a.iters, graph=True)
