@@ -82,6 +82,19 @@ def load_traffic(workload, alg):
         return None
 
 
+def spmv_kernel_label():
+    """The SpMV kernel the solver selects (cgx_solver.cpp defaults, CGX_* knobs)."""
+    if os.environ.get("CGX_LAYOUT") == "sell":
+        return "k_spmv_sell (SELL-64)"
+    dma = os.environ.get("CGX_SPMV_DMA", "1")
+    nt = os.environ.get("CGX_SPMV_NT", "1" if dma == "1" else "0") == "1"
+    name = {"0": "k_spmv_wave (register-staged CSR-stream, LDS row sums)",
+            "1": "k_spmv_dma (LDS-DMA CSR-stream, LDS row sums)",
+            "2": "k_spmv_pipe (persistent waves, LDS-DMA prefetch)",
+            "8": "k_spmv_dma (LDS-DMA CSR-stream, 8 gathers per chunk)"}.get(dma, f"dma={dma}")
+    return name + (", nt stream" if nt else "")
+
+
 def cpu_baseline(sysm, budget_s):
     """The oracle's CSR-sequential HS-CG (bit-exact to the reference on chained
     matrices) on ONE host core, on the same matrix, for as many iterations as
@@ -181,7 +194,7 @@ def main():
     traffic = load_traffic(args.workload, alg)
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                    traffic=traffic, kernel="k_spmv (CSR-stream, LDS-staged)",
+                    traffic=traffic, kernel=spmv_kernel_label(),
                     spmv_us=round(spmv_ms * 1e3, 2),
                     algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]))
 

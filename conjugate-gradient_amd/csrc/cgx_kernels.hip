@@ -467,6 +467,35 @@ __device__ __forceinline__ double wave_block_finish(const SpmvArgs<T> &a,
 // columns (for banded/stencil matrices: a few contiguous runs instead of ~20
 // scattered lines per instruction).  Products are rounded separately and
 // added in column order from 0.0: the reference's per-row order.
+// One row's sequential sum over its LDS-staged entries [jb, je), U entries
+// per chunk.  Branch-free: clamped LDS index (all 2U LDS reads go out
+// together), every gather issued before the first add, padding terms
+// selected to +0 (acc + 0 == acc, so the row order and bits are unchanged).
+template <typename T, int U, bool XPAY>
+__device__ __forceinline__ T row_sum_lds(const SpmvArgs<T> &a, T beta, const T *lval,
+                                         const int *lcol, int jb, int je, T acc) {
+  for (int j = jb; j < je; j += U) {
+    const int cnt = min(U, je - j);
+    int cc[U];
+    T vv[U], xx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = u < cnt ? j + u : j;
+      const int c = lcol[idx];
+      cc[u] = u < cnt ? c : 0;
+      vv[u] = lval[idx];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) xx[u] = operand<T, XPAY>(a, beta, cc[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const T prod = vv[u] * xx[u];
+      acc = acc + (u < cnt ? prod : T(0));
+    }
+  }
+  return acc;
+}
+
 template <typename T, int CAPW, int VEC, bool EPI, bool XPAY>
 __device__ __forceinline__ double wave_block_finish_t(const SpmvArgs<T> &a,
                                                       WaveBlock<T, CAPW, VEC> &B,
@@ -491,27 +520,7 @@ __device__ __forceinline__ double wave_block_finish_t(const SpmvArgs<T> &a,
       *reinterpret_cast<typename WB::iv *>(lcol + off) = B.c[it];
     }
     wave_lds_sync();
-    if (lane < nr) {
-      constexpr int U = 4;
-      for (int j = j0 - kb; j < j1 - kb; j += U) {
-        const int cnt = min(U, j1 - kb - j);
-        int cc[U];
-        T vv[U], xx[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          cc[u] = u < cnt ? lcol[j + u] : 0;
-          vv[u] = u < cnt ? lval[j + u] : T(0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) xx[u] = operand<T, XPAY>(a, beta, cc[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (u < cnt) {
-            const T prod = vv[u] * xx[u];
-            acc = acc + prod;
-          }
-      }
-    }
+    if (lane < nr) acc = row_sum_lds<T, 4, XPAY>(a, beta, lval, lcol, j0 - kb, j1 - kb, acc);
     wave_lds_sync();  // the slice is rewritten by the next row block
   } else {
     T *prod = lval;
@@ -584,7 +593,8 @@ __global__ __launch_bounds__(WPB * kWave, TG ? 6 : 8) void k_spmv_wave(SpmvArgs<
 // window past nnz, so the window load never leaves the allocation.
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <typename T, int WPB, int CAPW, bool EPI, bool XPAY, bool NT = false>
+template <typename T, int WPB, int CAPW, bool EPI, bool XPAY, bool NT = false, int U = 4,
+          bool EXACT = true>
 __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
   // NT: the once-per-iteration matrix stream is loaded non-temporal (aux = 2)
   // so it does not displace the CG vectors from the Infinity Cache.
@@ -610,17 +620,23 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
     const int kb = k0 & ~3;  // 16-B aligned for both val (T) and col (int)
     const bool fits = k1 - kb <= CAPW;
     if (fits) {
+      // only the 16-B pieces this block needs: the window tail belongs to the
+      // next block, and with nt loads the Infinity Cache would not absorb
+      // the second read
       constexpr int EV = 16 / sizeof(T);  // elements of T per lane per DMA
+      const int m = k1 - kb;
 #pragma unroll
       for (int i = 0; i < (int)(CAPW * sizeof(T) / 1024); ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(a.val + kb + i * kWave * EV + lane * EV),
-            (lds_void *)(lval + i * kWave * EV), 16, 0, AUX);
+        if (!EXACT || (i * kWave * EV < m && (i * kWave + lane) * EV < m))
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(a.val + kb + i * kWave * EV + lane * EV),
+              (lds_void *)(lval + i * kWave * EV), 16, 0, AUX);
 #pragma unroll
       for (int i = 0; i < CAPW * 4 / 1024; ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(a.col + kb + i * kWave * 4 + lane * 4),
-            (lds_void *)(lcol + i * kWave * 4), 16, 0, AUX);
+        if (!EXACT || (i * kWave * 4 < m && (i * kWave + lane) * 4 < m))
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(a.col + kb + i * kWave * 4 + lane * 4),
+              (lds_void *)(lcol + i * kWave * 4), 16, 0, AUX);
     }
     int j0 = 0, j1 = 0;
     T xrow = T(0);
@@ -635,25 +651,8 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       wave_lds_sync();
       if (lane < nr) {
-        constexpr int U = 4;
-        for (int j = j0 - kb; j < j1 - kb; j += U) {
-          const int cnt = min(U, j1 - kb - j);
-          int cc[U];
-          T vv[U], xx[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            cc[u] = u < cnt ? lcol[j + u] : 0;
-            vv[u] = u < cnt ? lval[j + u] : T(0);
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u) xx[u] = operand<T, XPAY>(a, beta, cc[u]);
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (u < cnt) {
-              const T prod = vv[u] * xx[u];
-              acc = acc + prod;
-            }
-        }
+        // U gathers in flight per row chunk (U = 8: a 7-point row is one round trip)
+        acc = row_sum_lds<T, U, XPAY>(a, beta, lval, lcol, j0 - kb, j1 - kb, acc);
       }
     } else {
       for (int c0 = k0; c0 < k1; c0 += CAPW) {
@@ -1414,6 +1413,9 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     const int g = (a.nblk + WPB - 1) / WPB;
     const bool epi = a.part != nullptr, xp = a.x2 != nullptr;
     if (epi && xp) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi && a.dma == 3 && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true, 4, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi && a.dma == 8 && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true, 8>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi && a.dma == 8) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, false, 8>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (!xp && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);

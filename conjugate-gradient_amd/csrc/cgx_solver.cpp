@@ -717,11 +717,14 @@ int cgx_solver_create(int device, cgx_solver **out) {
     s->cus = prop.multiProcessorCount;
   s->vec = cgx::env_int("CGX_SPMV_VEC", 4);
   s->spmv_wpb = cgx::env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
-  s->spmv_dma = cgx::env_int("CGX_SPMV_DMA", 0);
+  // LDS-DMA stream + nt: best or tied-best in three order-rotated A/Bs (r01
+  // sweeps 14-16: 192-201 us vs 201-210 us for the register-staged kernel)
+  s->spmv_dma = cgx::env_int("CGX_SPMV_DMA", 1);
   s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", s->spmv_dma == 2 ? 8 : 1));
   if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
   s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
-  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", 0);  // order-rotated A/B (sweep15): nt +4% on the wave kernel
+  // nt helps the LDS-DMA stream, hurts the register-staged one (sweep15)
+  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 ? 1 : 0);
   {
     const int bs = cgx::env_int("CGX_SPMV_BS", 64);
     s->spmv_bs = (bs == 512 || bs == 64) ? bs : 256;
@@ -731,7 +734,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
   s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
-  s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma != 2;  // pipe: partials only
+  s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {
     const char *l = getenv("CGX_LAYOUT");
     s->want_sell = l && strcmp(l, "sell") == 0;

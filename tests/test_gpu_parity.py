@@ -65,15 +65,16 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
     pipelined persistent waves with 1/8/63 blocks each) keeps the sequential
     per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
-    if bs == "dma":
-        monkeypatch.setenv("CGX_SPMV_DMA", "1")
+    monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
+    if bs in ("dma", "dma8"):
+        monkeypatch.setenv("CGX_SPMV_DMA", "1" if bs == "dma" else "8")
     elif bs.startswith("pipe"):
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
         if bs != "pipe":
@@ -103,10 +104,11 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
         assert rel(s.x(), x_ref) <= FAST_RTOL
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "dma", "pipe"])
+@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "pipe"])
 def test_spmv_long_rows_variants(bs, monkeypatch):
-    if bs == "dma":
-        monkeypatch.setenv("CGX_SPMV_DMA", "1")
+    monkeypatch.setenv("CGX_SPMV_DMA", "0")
+    if bs in ("dma", "dma8"):
+        monkeypatch.setenv("CGX_SPMV_DMA", "1" if bs == "dma" else "8")
     elif bs == "pipe":
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
     else:
@@ -165,7 +167,7 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "2"])
+@pytest.mark.parametrize("dma", ["0", "2", "8"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
@@ -371,12 +373,17 @@ def test_empty_system():
 
 @pytest.mark.parametrize("ticket", ["0", "1"])
 @pytest.mark.parametrize("fuse", ["0", "1"])
-def test_reduction_paths_match_oracle_and_reproduce(ticket, fuse, monkeypatch):
-    """Finalize kernels vs the in-kernel ticket reduction, with and without
-    the fused p-update: all within FAST_RTOL of the reference order, and each
-    bit-reproducible run to run (deterministic reductions, no fp64 atomics)."""
+@pytest.mark.parametrize("dma", ["0", "1"])
+def test_reduction_paths_match_oracle_and_reproduce(ticket, fuse, dma, monkeypatch):
+    """Finalize kernels vs the in-kernel ticket reduction (register-staged
+    SpMV only), with and without the fused p-update, on both SpMV kernels:
+    all within FAST_RTOL of the reference order, and each bit-reproducible
+    run to run (deterministic reductions, no fp64 atomics)."""
+    if ticket == "1" and dma == "1":
+        pytest.skip("the LDS-DMA SpMV has no ticket epilogue (solver ignores CGX_TICKET)")
     monkeypatch.setenv("CGX_TICKET", ticket)
     monkeypatch.setenv("CGX_FUSE_XPAY", fuse)
+    monkeypatch.setenv("CGX_SPMV_DMA", dma)
     rp, col, val, b = H.random_spd(30000, 9, seed=12)
     x_ref, _ = H.o_conj_grad(60, rp, col, val, b)
     xs, hs = [], []
@@ -397,9 +404,11 @@ def test_reduction_paths_match_oracle_and_reproduce(ticket, fuse, monkeypatch):
     assert np.linalg.norm(r) <= 1.01e-9 * np.linalg.norm(b)
 
 
-def test_ticket_large_grid_and_tiny():
+def test_ticket_large_grid_and_tiny(monkeypatch):
     """Ticket reduction across > kTicketGroup^2 workgroups (two full levels)
     and with a single workgroup."""
+    monkeypatch.setenv("CGX_TICKET", "1")
+    monkeypatch.setenv("CGX_SPMV_DMA", "0")
     rp, col, val = cgx.laplacian3d(160, 160, 160)   # 4.1 M rows, 64 K SpMV workgroups
     b = np.random.default_rng(3).standard_normal(len(rp) - 1)
     with cgx.Solver(0) as s:

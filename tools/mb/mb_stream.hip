@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void k_mb(Args a) {
   for (; b < a.nblk; b += (MODE == 6 ? nwaves : a.nblk)) {
     const int k0 = a.blk_k[b], k1 = a.blk_k[b + 1];
     const int kb = k0 & ~3;
-    if (MODE == 1 || MODE == 2 || MODE == 6) {
+    if (MODE == 1 || MODE == 2 || MODE == 6 || MODE >= 9) {
       const double4 *vv = (const double4 *)(a.val + kb);  // 32 B/lane x 2 = 4 KB
       const int4 *cc = (const int4 *)(a.col + kb);
       double2 v0 = ((const double2 *)(a.val + kb))[lane];
@@ -63,6 +63,21 @@ __global__ __launch_bounds__(256) void k_mb(Args a) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
       acc += ((double *)L)[lane * 7 % 512] + ((int *)(L + 4096))[lane];
     }
+    if (MODE == 9) {  // y store only
+      const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
+      if (lane < nr) a.y[r0 + lane] = acc;
+    }
+    if (MODE == 10) {  // row_ptr only
+      const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
+      if (lane < nr) acc += (double)(a.rp[r0 + lane + 1] - a.rp[r0 + lane]);
+    }
+    if (MODE == 11) {  // row_ptr + nt y store
+      const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
+      if (lane < nr) {
+        const int j0 = a.rp[r0 + lane], j1 = a.rp[r0 + lane + 1];
+        __builtin_nontemporal_store(acc + (double)(j1 - j0), a.y + r0 + lane);
+      }
+    }
     if (MODE == 2 || MODE == 4 || MODE == 5 || MODE == 6) {
       const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
       if (lane < nr) {
@@ -71,7 +86,7 @@ __global__ __launch_bounds__(256) void k_mb(Args a) {
       }
     }
   }
-  if (MODE == 1 || MODE == 3) if (acc == 12345.678) a.sink[0] = acc;
+  if (MODE == 1 || MODE == 3 || MODE == 10) if (acc == 12345.678) a.sink[0] = acc;
 }
 
 __global__ void k_copy(const double2 *__restrict__ s, double2 *__restrict__ d, size_t n) {
@@ -128,7 +143,12 @@ int main() {
   run("3 dma window", [&] { hipLaunchKernelGGL(k_mb<3>, dim3(g1), dim3(256), 0, 0, a); }, stream);
   run("4 dma window + rp + y", [&] { hipLaunchKernelGGL(k_mb<4>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
   run("5 exact pieces + rp + y", [&] { hipLaunchKernelGGL(k_mb<5>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
-  for (int m : {2, 4, 8, 16})
+  run("9 vgpr window + y", [&] { hipLaunchKernelGGL(k_mb<9>, dim3(g1), dim3(256), 0, 0, a); }, stream + (double)n * 8);
+  run("10 vgpr window + rp", [&] { hipLaunchKernelGGL(k_mb<10>, dim3(g1), dim3(256), 0, 0, a); }, stream + (double)n * 4);
+  run("11 vgpr window + rp + nt y", [&] { hipLaunchKernelGGL(k_mb<11>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
+  run("1 vgpr window (again)", [&] { hipLaunchKernelGGL(k_mb<1>, dim3(g1), dim3(256), 0, 0, a); }, stream);
+  run("2 vgpr window + rp + y (again)", [&] { hipLaunchKernelGGL(k_mb<2>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
+  for (int m : {4})
   { char nm[64]; snprintf(nm, 64, "6 persistent x%d + rp + y", m);
     run(nm, [&] { hipLaunchKernelGGL(k_mb<6>, dim3(cus * m), dim3(256), 0, 0, a); }, stream + ry); }
   const size_t n2 = (size_t)nnz / 2;
