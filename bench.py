@@ -82,12 +82,14 @@ def load_traffic(workload, alg):
         return None
 
 
-def spmv_kernel_label():
-    """The SpMV kernel the solver selects (cgx_solver.cpp defaults, CGX_* knobs)."""
+def spmv_kernel_label(stream_bytes):
+    """The SpMV kernel the solver selects (cgx_solver.cpp defaults, CGX_* knobs;
+    nt by default only above kNtStreamBytes = 160 MiB of val+col)."""
     if os.environ.get("CGX_LAYOUT") == "sell":
         return "k_spmv_sell (SELL-64)"
     dma = os.environ.get("CGX_SPMV_DMA", "1")
-    nt = os.environ.get("CGX_SPMV_NT", "1" if dma == "1" else "0") == "1"
+    nt_env = os.environ.get("CGX_SPMV_NT")
+    nt = (nt_env == "1") if nt_env is not None else (dma in ("1", "3") and stream_bytes > 160 * 2**20)
     name = {"0": "k_spmv_wave (register-staged CSR-stream, LDS row sums)",
             "1": "k_spmv_dma (LDS-DMA CSR-stream, LDS row sums)",
             "2": "k_spmv_pipe (persistent waves, LDS-DMA prefetch)",
@@ -151,6 +153,8 @@ def main():
     sysm = make_system(wl, rank, world)
 
     use_dist = world > 1 or alg == "cg1-dist"
+    torch.cuda.synchronize()
+    t_up = time.perf_counter()  # host -> HBM upload + row-block plan (outside `value`)
     if use_dist:
         # one rank per GPU; RCCL communicator from an id rank 0 broadcasts
         uid = [cgx.dist_unique_id() if (rank == 0 and world > 1) else None]
@@ -168,6 +172,9 @@ def main():
         s.set_rhs(sysm["b"])
         info = s.info()
         dinfo = None
+
+    torch.cuda.synchronize()
+    upload_ms = 1e3 * (time.perf_counter() - t_up)
 
     # ---- timed region: exactly K steps, barrier + sync on both sides
     s.bench_prepare(args.warmup)
@@ -194,7 +201,8 @@ def main():
     traffic = load_traffic(args.workload, alg)
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                    traffic=traffic, kernel=spmv_kernel_label(),
+                    traffic=traffic,
+                    kernel=spmv_kernel_label(len(sysm["col"]) * (4 + sysm["val"].itemsize)),
                     spmv_us=round(spmv_ms * 1e3, 2),
                     algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]))
 
@@ -212,6 +220,8 @@ def main():
                     alg=alg, graph=not use_dist, parallelism=f"row-partition x{world}",
                     halo_bytes_per_iter=(dinfo or {}).get("halo_bytes")),
         device_ms_per_step=round(dev_ms / args.steps, 4),
+        # the C boundary takes host CSR buffers: one-time upload + plan, not in `value`
+        upload_ms=round(upload_ms, 1),
         iter_bytes=int(info["iter_bytes"]),
         iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),
         roofline=roofline, cpu_baseline=cpu,

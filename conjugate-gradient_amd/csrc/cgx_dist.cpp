@@ -430,7 +430,8 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.tg = env_int("CGX_SPMV_TG", 1);
   a.dma = d->wpb == 4 ? env_int("CGX_SPMV_DMA", 1) : 0;  // as the single-GPU solver
   if (a.dma != 1) a.dma = 0;  // grids below assume one block per wave, 4 waves per WG
-  a.nt = env_int("CGX_SPMV_NT", a.dma ? 1 : 0);
+  a.nt = env_int("CGX_SPMV_NT", -1);
+  if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes;
   a.tk = TicketArgs{};
   return a;
 }

@@ -62,6 +62,10 @@ constexpr int kVecBS = 256;
 constexpr int kFinBS = 1024;
 constexpr int kPad = 8;               // val/col padded to a multiple of this
 constexpr int kWindowPad = 1024;      // + one SpMV window (LDS-DMA reads whole windows)
+// Non-temporal matrix stream only when the matrix cannot stay resident in the
+// 256 MiB Infinity Cache anyway (C3: 843 MB -> nt helps the vectors stay; C2:
+// 60 MB -> nt would evict a matrix that otherwise never leaves the cache).
+constexpr double kNtStreamBytes = 160.0 * 1024 * 1024;
 
 // Finalize ops (single-workgroup scalar steps of the recurrence).
 enum FinOp {

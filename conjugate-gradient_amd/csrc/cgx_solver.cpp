@@ -119,7 +119,7 @@ struct cgx_solver {
   int n = 0, nnz = 0, dtype = CGX_F64;
   int mode = CGX_MODE_FAST, alg = CGX_ALG_HS;
   int vec = 2;
-  int spmv_xcd = 0, spmv_nt = 0, spmv_bs = 64, spmv_wpb = 4, spmv_rbw = 1,
+  int spmv_xcd = 0, spmv_nt = -1, spmv_bs = 64, spmv_wpb = 4, spmv_rbw = 1,
       spmv_tg = 1, spmv_dma = 0;
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
@@ -382,7 +382,9 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.part = part;
   a.done = with_done ? &s->d_st->done : nullptr;
   a.xcd = s->spmv_xcd;
-  a.nt = s->spmv_nt;
+  a.nt = s->spmv_nt < 0
+             ? (double)s->nnz * (double)(sizeof(T) + 4) > cgx::kNtStreamBytes
+             : s->spmv_nt;
   a.bs = s->spmv_bs;
   a.wpb = s->spmv_wpb;
   a.rbw = s->spmv_rbw;
@@ -724,7 +726,9 @@ int cgx_solver_create(int device, cgx_solver **out) {
   if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
   s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
   // nt helps the LDS-DMA stream, hurts the register-staged one (sweep15)
-  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 ? 1 : 0);
+  // -1 = by size at set_matrix (kNtStreamBytes; nt helps the LDS-DMA stream
+  // only, it hurts the register-staged one: sweep15)
+  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 ? -1 : 0);
   {
     const int bs = cgx::env_int("CGX_SPMV_BS", 64);
     s->spmv_bs = (bs == 512 || bs == 64) ? bs : 256;
