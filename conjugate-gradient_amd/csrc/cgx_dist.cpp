@@ -599,6 +599,11 @@ int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
   for (cgx_dist *d : g->parts) {
     CGX_HIP(hipSetDevice(d->device));
     if (hist_cap > d->hist_alloc) {
+      if (d->gexec) {  // the captured graph holds the old history pointer
+        CGX_HIP(hipStreamSynchronize(d->st));
+        (void)hipGraphExecDestroy(d->gexec);
+        d->gexec = nullptr;
+      }
       dfree(&d->d_hist);
       int rc = dalloc(d, &d->d_hist, (size_t)hist_cap * 8);
       if (rc) return rc;

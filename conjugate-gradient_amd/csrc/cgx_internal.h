@@ -71,6 +71,8 @@ constexpr double kNtStreamBytes = 160.0 * 1024 * 1024;
 enum FinOp {
   FIN_INIT_HS = 0,  // bb = rr = sum(a)
   FIN_HS_ALPHA = 1, // alpha = rr / sum(a)            (cg.c:113)
+  FIN_HS_ALPHA_X = 7, // as FIN_HS_ALPHA; deferred-x mode: a stop flag of 1
+                      // (x update of the stop iteration pending) becomes 2
   FIN_HS_BETA = 2,  // rr_new = sum(a); stop test; beta = rr_new/rr (cg.c:125-129)
   FIN_INIT_CG1 = 3, // gamma = bb = sum(a), delta = sum(b), alpha = gamma/delta
   FIN_CG1 = 4,      // gamma' = sum(a), delta = sum(b); stop test; alpha, beta
@@ -153,6 +155,12 @@ template <typename T>
 hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
                             const CgState *stt, double *part, int grid,
                             hipStream_t st, const TicketArgs *tk = nullptr);
+template <typename T>
+hipError_t launch_update_r(int n, T *r, const T *s, const CgState *stt,
+                           double *part, int grid, hipStream_t st);
+template <typename T>
+hipError_t launch_xpay_x(int n, T *x, T *p, const T *r, const CgState *stt,
+                         int grid, hipStream_t st);
 template <typename T>
 hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
                        hipStream_t st);

@@ -1106,6 +1106,89 @@ __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
 }
 
 // p = r + beta*p (cg.c:131-132)
+// Deferred-x HS (CGX_XDEFER): x += alpha p moves from the r-update into the
+// p-update, which reads p_old anyway -- one 8n-byte read of p less per
+// iteration.  Same per-element roundings as k_update_xr / k_xpay.
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_update_r(int n, T *__restrict__ r,
+                                                 const T *__restrict__ s,
+                                                 const CgState *__restrict__ st,
+                                                 double *__restrict__ part) {
+  __shared__ double red[BS / kWave];
+  if (st->done) return;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T alpha = (T)st->alpha;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    V rv = reinterpret_cast<const V *>(r)[i];
+    const V sv = reinterpret_cast<const V *>(s)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T as = alpha * sv[j];
+      rv[j] = rv[j] - as;
+      acc = acc + (double)rv[j] * (double)rv[j];
+    }
+    reinterpret_cast<V *>(r)[i] = rv;
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T as = alpha * s[i];
+      const T ri = r[i] - as;
+      r[i] = ri;
+      acc = acc + (double)ri * (double)ri;
+    }
+  const double sum = block_sum<BS>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = sum;
+}
+
+// stop flag 0: x += alpha p_old, p = r + beta p_old; 1 (stopped in this
+// iteration, cg.c:125 breaks after the x update): x only; 2: nothing.
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_xpay_x(int n, T *__restrict__ x,
+                                               T *__restrict__ p,
+                                               const T *__restrict__ r,
+                                               const CgState *__restrict__ st) {
+  const int done = st->done;
+  if (done > 1) return;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T alpha = (T)st->alpha, beta = (T)st->beta;
+  const int nv = n / W;
+  const int gid = blockIdx.x * BS + threadIdx.x, stride = gridDim.x * BS;
+  for (int i = gid; i < nv; i += stride) {
+    V pv = reinterpret_cast<const V *>(p)[i];
+    V xv = reinterpret_cast<const V *>(x)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T ap = alpha * pv[j];
+      xv[j] = xv[j] + ap;
+    }
+    reinterpret_cast<V *>(x)[i] = xv;
+    if (done == 0) {
+      const V rv = reinterpret_cast<const V *>(r)[i];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T bp = beta * pv[j];
+        pv[j] = rv[j] + bp;
+      }
+      reinterpret_cast<V *>(p)[i] = pv;
+    }
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T pi = p[i];
+      const T ap = alpha * pi;
+      x[i] = x[i] + ap;
+      if (done == 0) {
+        const T bp = beta * pi;
+        p[i] = r[i] + bp;
+      }
+    }
+}
+
 template <typename T, int BS>
 __global__ __launch_bounds__(BS) void k_xpay(int n, T *__restrict__ p,
                                              const T *__restrict__ r,
@@ -1281,6 +1364,15 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
   const double sa = sum_parts<BS>(pa, na, red);
   const double sb = pb ? sum_parts<BS>(pb, nb, red) : 0.0;
   if (threadIdx.x != 0) return;
+  if (op == FIN_HS_ALPHA_X) {
+    // one thread, so the 1 -> 2 step cannot race: k_xpay_x of the stop
+    // iteration (flag 1) has applied the last x update, later ones must not
+    if (st->done) {
+      if (st->done == 1) st->done = 2;
+      return;
+    }
+    op = FIN_HS_ALPHA;
+  }
   if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_INIT_HS &&
       op != FIN_INIT_CG1 && st->done)
     return;
@@ -1407,6 +1499,18 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     else hipLaunchKernelGGL((k_spmv_pipe<T, WPB, CAPW, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     return hipGetLastError();
   }
+  if (a.bs == 64 && a.dma == 4) {  // 32-row blocks, 3 KiB windows: 2x the waves per CU
+    constexpr int WPB = 4;
+    constexpr int CAPW = sizeof(T) == 8 ? 256 : 512;
+    const int g = (a.nblk + WPB - 1) / WPB;
+    const bool epi = a.part != nullptr;
+    if (a.x2) return hipErrorInvalidValue;  // no fused p-update in this variant
+    if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.bs == 64 && a.dma) {
     constexpr int WPB = 4;
     constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;
@@ -1473,6 +1577,22 @@ hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
                        hipStream_t st) {
   hipLaunchKernelGGL((k_xpay<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n, p,
                      r, stt);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_update_r(int n, T *r, const T *s, const CgState *stt,
+                           double *part, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_update_r<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n, r,
+                     s, stt, part);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_xpay_x(int n, T *x, T *p, const T *r, const CgState *stt,
+                         int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_xpay_x<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n, x,
+                     p, r, stt);
   return hipGetLastError();
 }
 
@@ -1546,6 +1666,10 @@ hipError_t launch_gather(int m, const int *idx, const T *x, T *buf,
                                           const TicketArgs *);                 \
   template hipError_t launch_xpay<T>(int, T *, const T *, const CgState *,    \
                                      int, hipStream_t);                        \
+  template hipError_t launch_update_r<T>(int, T *, const T *, const CgState *,\
+                                         double *, int, hipStream_t);          \
+  template hipError_t launch_xpay_x<T>(int, T *, T *, const T *,              \
+                                       const CgState *, int, hipStream_t);     \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *,           \
                                            const T *, const CgState *,        \
                                            double *, int, hipStream_t);        \

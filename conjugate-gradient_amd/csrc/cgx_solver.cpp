@@ -123,6 +123,7 @@ struct cgx_solver {
       spmv_tg = 1, spmv_dma = 0;
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
+  bool xdefer = false;  // CGX_XDEFER: x update folded into the p-update
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
@@ -254,9 +255,10 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   s->dtype = sizeof(T) == 4 ? CGX_F32 : CGX_F64;
   s->n = n;
   s->nnz = nnz;
-  const int cap = spmv_cap(s->spmv_bs, sizeof(T) == 8);
+  const bool half = s->spmv_dma == 4 && s->spmv_bs == 64;  // 32-row blocks
+  const int cap = half ? spmv_cap(32, sizeof(T) == 8) : spmv_cap(s->spmv_bs, sizeof(T) == 8);
   std::vector<int> blk;
-  if (n > 0) blk = plan_rowblocks(n, rp, s->spmv_bs, cap - kPad);  // room for VEC alignment
+  if (n > 0) blk = plan_rowblocks(n, rp, half ? 32 : s->spmv_bs, cap - kPad);  // room for VEC alignment
   else blk.push_back(0);
   s->nblk = (int)blk.size() - 1;
   const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
@@ -420,7 +422,7 @@ bool use_ticket(const cgx_solver *s) {
 
 bool fused(const cgx_solver *s) {
   return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
-         s->spmv_dma != 2;
+         s->spmv_dma != 2 && s->spmv_dma != 4;
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -497,6 +499,17 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
       const TicketArgs tk = ticket_args(s, FIN_HS_BETA);
       CGX_HIP(launch_update_xr<T>(s->n, x, p, r, sv, s->d_st, s->d_pa,
                                   s->vec_grid, st, &tk));
+    } else if (s->xdefer && !fx) {
+      // deferred x: r-update alone, x += alpha p_old folded into the p-update
+      CGX_HIP(launch_finalize(FIN_HS_ALPHA_X, s->d_pa, sg, nullptr, 0, s->d_st,
+                              s->d_hist, nullptr, st));           // cg.c:113
+      CGX_HIP(launch_update_r<T>(s->n, r, sv, s->d_st, s->d_pa, s->vec_grid,
+                                 st));                            // cg.c:118-123
+      CGX_HIP(launch_finalize(FIN_HS_BETA, s->d_pa, s->vec_grid, nullptr, 0,
+                              s->d_st, s->d_hist, nullptr, st));  // cg.c:125-129
+      CGX_HIP(launch_xpay_x<T>(s->n, x, p, r, s->d_st, s->vec_grid,
+                               st));                              // cg.c:115-116, 131-132
+      return 0;
     } else {
       CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, sg, nullptr, 0, s->d_st,
                               s->d_hist, nullptr, st));
@@ -561,6 +574,8 @@ int enqueue_iters(cgx_solver *s, long long count) {
 
 int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
   if (hist_cap > s->hist_alloc) {
+    drop_graph(s);  // captured graphs hold the old history pointer
+    CGX_HIP(hipStreamSynchronize(s->stream));
     dfree((void **)&s->d_hist);
     int rc = dalloc(s, (void **)&s->d_hist, (size_t)hist_cap * 8);
     if (rc) return rc;
@@ -728,7 +743,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   // nt helps the LDS-DMA stream, hurts the register-staged one (sweep15)
   // -1 = by size at set_matrix (kNtStreamBytes; nt helps the LDS-DMA stream
   // only, it hurts the register-staged one: sweep15)
-  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 ? -1 : 0);
+  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 || s->spmv_dma == 4 ? -1 : 0);
   {
     const int bs = cgx::env_int("CGX_SPMV_BS", 64);
     s->spmv_bs = (bs == 512 || bs == 64) ? bs : 256;
@@ -737,6 +752,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->use_graph = cgx::env_int("CGX_GRAPH", 1) != 0;
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
   s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
+  s->xdefer = cgx::env_int("CGX_XDEFER", 1) != 0;  // -4.4% per C3 iteration (sweep20), bit-identical
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {

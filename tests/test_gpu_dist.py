@@ -111,3 +111,32 @@ def test_local_group_bench_and_interior_split():
     assert [s["n_ghost"] for s in st] == [1024, 2048, 2048, 1024]
     assert all(s["boundary_blocks"] <= 2 * 1024 // 64 + 2 for s in st)
     assert all(s["interior_blocks"] > 0 for s in st)
+
+
+def test_history_after_buffer_growth():
+    """A replayed graph must not keep the old history pointer when a later,
+    longer run reallocates the history buffer (regression: r01)."""
+    rp, col, val, b = system("lap3d")
+    n = len(rp) - 1
+
+    def fresh():
+        d = cgx.DistSolver.local_group(0, 1)[0]
+        d.set_matrix(n, rp, col, val)
+        d.set_rhs(b)
+        return d
+
+    d = fresh()
+    try:
+        d.run(40)                    # captures the replay graph (short history)
+        its = d.run(5000, 1e-10)     # longer history: buffer reallocated
+        h = d.history(its)
+    finally:
+        d.close()
+    d = fresh()
+    try:
+        its2 = d.run(5000, 1e-10)
+        h2 = d.history(its2)
+    finally:
+        d.close()
+    assert its == its2
+    assert H.same_bits_or_both_nan(h, h2)

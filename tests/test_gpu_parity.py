@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -73,8 +73,8 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
     monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
-    if bs in ("dma", "dma8"):
-        monkeypatch.setenv("CGX_SPMV_DMA", "1" if bs == "dma" else "8")
+    if bs in ("dma", "dma8", "dma32"):
+        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4"}[bs])
     elif bs.startswith("pipe"):
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
         if bs != "pipe":
@@ -104,11 +104,11 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
         assert rel(s.x(), x_ref) <= FAST_RTOL
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "pipe"])
+@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "dma32", "pipe"])
 def test_spmv_long_rows_variants(bs, monkeypatch):
     monkeypatch.setenv("CGX_SPMV_DMA", "0")
-    if bs in ("dma", "dma8"):
-        monkeypatch.setenv("CGX_SPMV_DMA", "1" if bs == "dma" else "8")
+    if bs in ("dma", "dma8", "dma32"):
+        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4"}[bs])
     elif bs == "pipe":
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
     else:
@@ -167,7 +167,7 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "2", "8"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "8"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
@@ -451,3 +451,57 @@ def test_sell_layout_bit_exact(fuse, monkeypatch):
         s.set_matrix(rp32, col32, v32)
         assert np.array_equal(s.spmv(x32).view(np.uint32),
                               H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
+
+
+@pytest.mark.parametrize("dma", ["0", "1"])
+def test_deferred_x_bit_identical(dma, monkeypatch):
+    """CGX_XDEFER folds x += alpha p into the p-update (one read of p less per
+    iteration).  Same per-element roundings and reductions, so x, the r.r
+    history and the stop iteration are bit-identical to the standard HS path,
+    for fixed iteration counts (max_iter stop) and for tolerance stops that
+    land inside a replayed batch (the stop iteration's x update must still
+    happen, later ones must not)."""
+    monkeypatch.setenv("CGX_SPMV_DMA", dma)
+    cases = [H.random_spd(30000, 9, seed=21), None]
+    g = H.load_golden("lap3d_12")
+    cases[1] = (g["row_ptr"], g["col"], g["val"], g["b"])
+    for rp, col, val, b in cases:
+        out = {}
+        for xd in ("0", "1"):
+            monkeypatch.setenv("CGX_XDEFER", xd)
+            with cgx.Solver(0) as s:
+                s.set_matrix(rp, col, val)
+                res = []
+                for maxit, tol in [(0, 0.0), (1, 0.0), (37, 0.0), (2000, 1e-9), (2000, 1e-6)]:
+                    s.set_rhs(b)
+                    its = s.run(maxit, tol)
+                    res.append((its, s.x(), s.history(its)))
+                out[xd] = res
+        for (i0, x0, h0), (i1, x1, h1) in zip(out["0"], out["1"]):
+            assert i0 == i1
+            assert H.same_bits_or_both_nan(x0, x1)
+            assert H.same_bits_or_both_nan(h0, h1)
+    x_ref, _ = H.o_conj_grad(37, g["row_ptr"], g["col"], g["val"], g["b"])
+    assert rel(out["1"][2][1], x_ref) <= FAST_RTOL
+
+
+@pytest.mark.parametrize("xd", ["0", "1"])
+def test_history_after_buffer_growth(xd, monkeypatch):
+    """Cached hipGraphs are dropped when a longer run reallocates the r.r
+    history buffer (regression: r01, the graph kept the freed pointer)."""
+    monkeypatch.setenv("CGX_XDEFER", xd)
+    rp, col, val, b = H.random_spd(30000, 9, seed=21)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        s.run(37)
+        s.set_rhs(b)
+        its = s.run(2000, 1e-9)
+        h = s.history(its)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        its2 = s.run(2000, 1e-9)
+        h2 = s.history(its2)
+    assert its == its2
+    assert H.same_bits_or_both_nan(h, h2)
