@@ -38,6 +38,9 @@ WORKLOADS = {
     "c2": dict(desc="C2: 5-point 2-D Laplacian 1000^2 (1,000,000 rows), fp64, b = 1 "
                     "(working set fits the 256 MiB Infinity Cache)",
                kind="lap2d", dims=(1000, 1000), dtype="f64"),
+    "c4": dict(desc="C4: 7-point 3-D Laplacian 400^3 (64,000,000 rows), fp64, b = 1, "
+                    "row-partitioned over the ranks (strong scaling)",
+               kind="lap3d", dims=(400, 400, 400), dtype="f64", strong=True),
     "c5": dict(desc="C5: random SPD 5,000,000 rows, 32 partners/row symmetrised "
                     "(~64 nnz/row), splitmix64 seed 42, fp32",
                kind="rand", n=5_000_000, partners=32, seed=42, dtype="f32"),
@@ -49,7 +52,7 @@ def make_system(wl, rank=0, world=1):
     import cgx
     if wl["kind"] == "lap3d":
         nx, ny, nz = wl["dims"]
-        nz_g = nz * world
+        nz_g = nz if wl.get("strong") else nz * world
         n_g = nx * ny * nz_g
         rb, re_ = n_g * rank // world, n_g * (rank + 1) // world
         rp, col, val = cgx.laplacian3d(nx, ny, nz_g, rb, re_)
@@ -95,6 +98,39 @@ def spmv_kernel_label(stream_bytes):
             "2": "k_spmv_pipe (persistent waves, LDS-DMA prefetch)",
             "8": "k_spmv_dma (LDS-DMA CSR-stream, 8 gathers per chunk)"}.get(dma, f"dma={dma}")
     return name + (", nt stream" if nt else "")
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_mt(sysm, budget_s):
+    """SURVEY.md 8d leg (c): the same CSR-sequential HS-CG with its row loops
+    split over all host cores this job may use (oracle_solve_mt, pthreads;
+    OMP_NUM_THREADS on the GPU box = the box's CPU share)."""
+    import numpy as np
+    import helpers as H
+    rp, col, val, b = sysm["rp"], sysm["col"], sysm["val"], sysm["b"]
+    if val.dtype != np.float64:
+        val = val.astype(np.float64)
+        b = b.astype(np.float64)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    H.o_solve_mt(0, 0.0, rp, col, val, b, threads)
+    t1 = time.perf_counter() - t0
+    its = max(1, min(2000, int(budget_s / max(t1, 1e-6))))
+    t0 = time.perf_counter()
+    _, done = H.o_solve_mt(its - 1, 0.0, rp, col, val, b, threads)
+    dt = time.perf_counter() - t0
+    return dict(value=done / dt, unit="it/s", cores=threads, kind="port",
+                sample=f"{done} HS-CG iterations, row loops on {threads} threads "
+                       f"(oracle_solve_mt), {dt:.1f} s")
 
 
 def cpu_baseline(sysm, budget_s):
@@ -206,9 +242,21 @@ def main():
                     spmv_us=round(spmv_ms * 1e3, 2),
                     algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]))
 
+    # on-box HBM ceilings: STREAM triad (1/3 writes) and a
+    # read-only stream, 512 MiB arrays.  The SpMV is 92% reads (its only
+    # write is y), so the read ceiling is the one it is compared with.
+    triad = cgx.stream_bench(local_rank, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)
+    rd = cgx.stream_bench(local_rank, 64 * 2**20, 10, cgx.CGX_STREAM_READ)
+    roofline["stream_triad_gbs"] = round(triad, 1)
+    roofline["stream_read_gbs"] = round(rd, 1)
+    roofline["frac_of_stream_read"] = round(achieved / rd, 4)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(sysm, args.cpu_seconds)
+        cpu["cpu_model"] = cpu_model()
+        cpu["nproc"] = os.cpu_count()
+        cpu["all_cores"] = cpu_baseline_mt(sysm, args.cpu_seconds / 2)
 
     value = (args.steps / wall) * world  # weak scaling: slab-iterations/s
     out = dict(

@@ -80,6 +80,8 @@ _SIGS = {
     "cgx_free_mv_deep": (None, [_MVP]),
     "cgx_last_error": (ctypes.c_char_p, []),
     "cgx_device_count": (ctypes.c_int, []),
+    "cgx_stream_bench": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
+                                        ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "cgx_solver_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "cgx_solver_destroy": (None, [_vp]),
     "cgx_solver_set_mode": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
@@ -206,6 +208,18 @@ def _gen(fn, args, m, want_f32=False):
 def laplacian2d(nx, ny, row_begin=0, row_end=None):
     row_end = nx * ny if row_end is None else row_end
     return _gen("cgx_gen_laplacian2d", (nx, ny, row_begin, row_end), row_end - row_begin)
+
+
+CGX_STREAM_TRIAD, CGX_STREAM_READ = 0, 1
+
+
+def stream_bench(device, n, reps=10, kind=CGX_STREAM_TRIAD):
+    """On-box HBM ceiling (cgx_stream_bench): best-of-reps GB/s over fp64
+    arrays of n elements; kind CGX_STREAM_TRIAD (a = b + s c, 24 n bytes) or
+    CGX_STREAM_READ (read-only sum, 8 n bytes)."""
+    g = ctypes.c_double(0.0)
+    check(lib().cgx_stream_bench(device, kind, n, reps, ctypes.byref(g)), "stream_bench")
+    return g.value
 
 
 def laplacian3d(nx, ny, nz, row_begin=0, row_end=None):

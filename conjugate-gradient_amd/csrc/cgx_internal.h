@@ -155,6 +155,10 @@ template <typename T>
 hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s,
                             const CgState *stt, double *part, int grid,
                             hipStream_t st, const TicketArgs *tk = nullptr);
+hipError_t launch_triad(long long n2, double *a, const double *b, const double *c,
+                        int grid, hipStream_t st);
+hipError_t launch_stream_read(long long n2, const double *b, double *sink, int grid,
+                              hipStream_t st);
 template <typename T>
 hipError_t launch_update_r(int n, T *r, const T *s, const CgState *stt,
                            double *part, int grid, hipStream_t st);

@@ -721,6 +721,52 @@ int cgx_device_count(void) {
   return cnt;
 }
 
+int cgx_stream_bench(int device, int kind, long long n, int reps, double *gbs) {
+  if (!gbs || n < 2 || reps < 1 || (kind != CGX_STREAM_TRIAD && kind != CGX_STREAM_READ))
+    return CGX_EINVAL;
+  int rc = check_device(device);
+  if (rc) return rc;
+  CGX_HIP(hipSetDevice(device));
+  const long long n2 = n / 2;
+  double *buf = nullptr;
+  if (hipMalloc((void **)&buf, (size_t)n2 * 16 * 3) != hipSuccess) {
+    set_error("stream_bench: out of device memory");
+    return CGX_ENOMEM;
+  }
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+  double *a = buf, *b = buf + 2 * n2, *c = buf + 4 * n2;
+  float best = 1e30f;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  if (e == hipSuccess) e = hipMemsetAsync(buf, 0, (size_t)n2 * 48, st);
+  for (int r = -2; r < reps && e == hipSuccess; ++r) {  // two untimed warm-ups
+    e = hipEventRecord(e0, st);
+    if (e == hipSuccess)
+      e = kind == CGX_STREAM_TRIAD ? launch_triad(n2, a, b, c, cus * 16, st)
+                                   : launch_stream_read(n2, b, a, cus * 16, st);
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess && r >= 0) best = std::min(best, ms);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  (void)hipFree(buf);
+  if (e != hipSuccess) {
+    set_error("stream_bench: %s", hipGetErrorString(e));
+    return CGX_ENODEV;
+  }
+  *gbs = (kind == CGX_STREAM_TRIAD ? 48.0 : 16.0) * (double)n2 / (best * 1e-3) / 1e9;
+  return 0;
+}
+
 int cgx_solver_create(int device, cgx_solver **out) {
   if (!out) return CGX_EINVAL;
   *out = nullptr;

@@ -53,6 +53,15 @@ void cgx_free_mv_deep(struct __mv_sparse *m);
 const char *cgx_last_error(void);
 int cgx_device_count(void);
 
+/* On-box HBM ceilings (SURVEY.md 8d "STREAM-triad ceiling"), fp64 arrays of
+ * n elements on `device`, best of `reps` timed launches, 16 B per lane:
+ *   CGX_STREAM_TRIAD  a[i] = b[i] + s*c[i]      *gbs = 24 n B / time
+ *   CGX_STREAM_READ   sum of a[i] (read only)   *gbs =  8 n B / time
+ * Measurement only (bench.py's roofline context). */
+#define CGX_STREAM_TRIAD 0
+#define CGX_STREAM_READ 1
+int cgx_stream_bench(int device, int kind, long long n, int reps, double *gbs);
+
 /* ------------------------------------------------------------------------
  * 2. Solver object: device-resident CSR, repeated solves, benchmarking
  * ------------------------------------------------------------------------ */

@@ -108,6 +108,8 @@ def test_no_cpu_fallback():
     assert L.conj_grad(3, A.ptr, b.ptr, ctypes.byref(out)) == cgx.CGX_ENODEV
     assert not out
     assert L.dot_product(b.ptr, b.ptr) == -1.0
+    gbs = ctypes.c_double(0.0)
+    assert L.cgx_stream_bench(0, 0, 1 << 20, 1, ctypes.byref(gbs)) == cgx.CGX_ENODEV
 
 
 @pytest.mark.parametrize("shape", [(1, 1), (5, 3), (32, 32), (17, 9)])

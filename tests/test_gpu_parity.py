@@ -505,3 +505,11 @@ def test_history_after_buffer_growth(xd, monkeypatch):
         h2 = s.history(its2)
     assert its == its2
     assert H.same_bits_or_both_nan(h, h2)
+
+
+def test_stream_ceilings():
+    """The on-box ceilings bench.py reports beside the SpMV roofline: sane
+    fractions of the 8 TB/s spec, reads faster than the triad's mix."""
+    t = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_TRIAD)
+    r = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_READ)
+    assert 2000.0 < t < 8000.0 and 2000.0 < r < 8000.0
