@@ -128,6 +128,11 @@ struct SpmvArgs {
   const int *s_len;
   int nslices;
   int n;
+  // column panels (k_spmv_dma): running row sums of the previous panels,
+  // the row's sum starts from yacc[row] instead of 0 (nullptr: from 0).  The
+  // entries of a row are ascending in column, so summing panel after panel
+  // is the reference's sequential order.  May alias y.
+  const T *yacc;
   int dma;             // 1: k_spmv_dma (LDS-DMA stream, one block per wave)
                        // 2: k_spmv_pipe (persistent waves, rbw blocks each,
                        //    next block's stream prefetched by LDS-DMA)

@@ -640,13 +640,14 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
     }
     int j0 = 0, j1 = 0;
     T xrow = T(0);
+    T acc = T(0);
     if (lane < nr) {
       j0 = a.rp[r0 + lane];
       j1 = a.rp[r0 + lane + 1];
       if (EPI || XPAY) xrow = operand<T, XPAY>(a, beta, r0 + lane);
       if (XPAY) a.xout[r0 + lane] = xrow;
+      if (a.yacc) acc = a.yacc[r0 + lane];  // column panels: continue the row sum
     }
-    T acc = T(0);
     if (fits) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       wave_lds_sync();
@@ -1354,15 +1355,51 @@ __device__ __forceinline__ double sum_parts(const double *pa, int na,
   return s;
 }
 
+// Two partial arrays summed with all loads of both in flight at once; each
+// sum keeps sum_parts' order (thread t: index order, then the block tree).
+template <int BS>
+__device__ __forceinline__ void sum_parts2(const double *pa, int na, const double *pb,
+                                           int nb, double *red, double &sa, double &sb) {
+  constexpr int U = 24;
+  double acc_a = 0.0, acc_b = 0.0;
+  bool fa = true, fb = true;
+  const int nmax = na > nb ? na : nb;
+  for (int i = threadIdx.x; i < nmax; i += U * BS) {
+    double va[U], vb[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      va[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
+      vb[j] = i + j * BS < nb ? pb[i + j * BS] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (i + j * BS < na) {
+        acc_a = fa ? va[j] : acc_a + va[j];
+        fa = false;
+      }
+      if (i + j * BS < nb) {
+        acc_b = fb ? vb[j] : acc_b + vb[j];
+        fb = false;
+      }
+    }
+  }
+  sa = block_sum<BS>(acc_a, red);
+  __syncthreads();
+  sb = block_sum<BS>(acc_b, red);
+  __syncthreads();
+}
+
 template <int BS>
 __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int na,
                                                  const double *pb, int nb,
                                                  CgState *st, double *hist,
                                                  double *out) {
   __shared__ double red[BS / kWave];
-  // partial loads go out before the done-flag round trip
-  const double sa = sum_parts<BS>(pa, na, red);
-  const double sb = pb ? sum_parts<BS>(pb, nb, red) : 0.0;
+  // partial loads go out before the done-flag round trip; with two partial
+  // arrays, both arrays' loads are in flight together (one round trip)
+  double sa, sb = 0.0;
+  if (pb) sum_parts2<BS>(pa, na, pb, nb, red, sa, sb);
+  else sa = sum_parts<BS>(pa, na, red);
   if (threadIdx.x != 0) return;
   if (op == FIN_HS_ALPHA_X) {
     // one thread, so the 1 -> 2 step cannot race: k_xpay_x of the stop

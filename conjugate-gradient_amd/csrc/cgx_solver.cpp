@@ -49,6 +49,69 @@ std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap) {
   return blk;
 }
 
+// Column panels for matrices whose gathers have no locality (SURVEY.md C5:
+// random SPD).  x is read through per-XCD L2s of 4 MiB; when x is larger and
+// most entries lie far from the diagonal, every gather is a line fetched from
+// the Infinity Cache.  Splitting the columns into panels whose x slice fits
+// an L2 and running one SpMV pass per panel keeps the gathers L2-resident,
+// for P row_ptr reads and P-1 y round trips more.  Auto-selected when x >
+// 8 MiB and >= 30 % of (sampled) entries are more than a panel width from the
+// diagonal; CGX_LAYOUT=panel forces, CGX_LAYOUT=csr disables;
+// CGX_PANEL_KB sets the x bytes per panel (default 2048).
+int choose_panels(int n, const int *rp, const int *col, size_t tsize) {
+  const char *l = getenv("CGX_LAYOUT");
+  if (n <= 0 || (l && strcmp(l, "panel") != 0)) return 1;  // csr / sell
+  const long long pcols =
+      std::max<long long>(1024, (long long)env_int("CGX_PANEL_KB", 2048) * 1024 / (long long)tsize);
+  if (n <= pcols) return 1;
+  if (!l) {
+    if ((double)n * (double)tsize <= 8.0 * 1024 * 1024) return 1;
+    long long far = 0, tot = 0;
+    for (int i = 0; i < n; i += 61)
+      for (int k = rp[i]; k < rp[i + 1]; ++k) {
+        ++tot;
+        far += std::llabs((long long)col[k] - i) > pcols;
+      }
+    if (far * 10 < tot * 3) return 1;
+  }
+  return (int)std::min<long long>(64, (n + pcols - 1) / pcols);
+}
+
+// Panel-major CSR: panel q holds, for every row, the row's entries with
+// column in [q*pc, (q+1)*pc), in the row's order; prp[q*(n+1) + i] are
+// offsets into the concatenated col/val (panel q's block starts at base q).
+template <typename T>
+void build_panels(int n, const int *rp, const int *col, const T *val, int P,
+                  std::vector<int> &prp, std::vector<int> &pcol, std::vector<T> &pval) {
+  const int nnz = rp[n];
+  const long long pc = ((long long)n + P - 1) / P;
+  std::vector<long long> base((size_t)P + 1, 0);
+  for (int k = 0; k < nnz; ++k) base[(size_t)(col[k] / pc) + 1]++;
+  for (int q = 0; q < P; ++q) base[q + 1] += base[q];
+  prp.assign((size_t)P * ((size_t)n + 1), 0);
+  std::vector<int> cnt((size_t)P);
+  for (int q = 0; q < P; ++q) prp[(size_t)q * (n + 1)] = (int)base[q];
+  for (int i = 0; i < n; ++i) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int k = rp[i]; k < rp[i + 1]; ++k) cnt[(size_t)(col[k] / pc)]++;
+    for (int q = 0; q < P; ++q) {
+      const size_t o = (size_t)q * (n + 1) + i;
+      prp[o + 1] = prp[o] + cnt[q];
+    }
+  }
+  pcol.resize((size_t)nnz);
+  pval.resize((size_t)nnz);
+  std::vector<int> cur((size_t)P);
+  for (int i = 0; i < n; ++i) {
+    for (int q = 0; q < P; ++q) cur[q] = prp[(size_t)q * (n + 1) + i];
+    for (int k = rp[i]; k < rp[i + 1]; ++k) {
+      const int q = (int)(col[k] / pc);
+      pcol[(size_t)cur[q]] = col[k];
+      pval[(size_t)cur[q]++] = val[k];
+    }
+  }
+}
+
 // SELL-64: slice i = rows [64i, 64i+64), width = its longest row, element
 // (j, lane) at 64*(s_off[i] + j) + lane.  Padding (val 0, col = the row)
 // follows each row's entries.  Returns false (use CSR) when the padded size
@@ -124,6 +187,10 @@ struct cgx_solver {
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
   bool xdefer = false;  // CGX_XDEFER: x update folded into the p-update
+  // column panels (irregular matrices): npanel SpMV passes, panel q's rows in
+  // d_rp + q (n+1), its row blocks at blk index panel_off[q] (panel_nblk[q])
+  int npanel = 1;
+  std::vector<int> panel_off, panel_nblk, panel_grid;
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
@@ -257,14 +324,42 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   s->nnz = nnz;
   const bool half = s->spmv_dma == 4 && s->spmv_bs == 64;  // 32-row blocks
   const int cap = half ? spmv_cap(32, sizeof(T) == 8) : spmv_cap(s->spmv_bs, sizeof(T) == 8);
-  std::vector<int> blk;
-  if (n > 0) blk = plan_rowblocks(n, rp, half ? 32 : s->spmv_bs, cap - kPad);  // room for VEC alignment
-  else blk.push_back(0);
-  s->nblk = (int)blk.size() - 1;
+  std::vector<int> blk, blkk;
+  std::vector<int> prp, pcol;
+  std::vector<T> pval;
+  s->npanel = choose_panels(n, rp, col, sizeof(T));
+  s->panel_off.clear();
+  s->panel_nblk.clear();
+  s->panel_grid.clear();
+  if (s->npanel > 1) {
+    // k_spmv_dma over each panel's row blocks; the panel arrays replace the CSR
+    build_panels<T>(n, rp, col, val, s->npanel, prp, pcol, pval);
+    for (int q = 0; q < s->npanel; ++q) {
+      const int *rq = prp.data() + (size_t)q * (n + 1);
+      std::vector<int> b = plan_rowblocks(n, rq, 64, spmv_cap(64, sizeof(T) == 8) - kPad);
+      s->panel_off.push_back((int)blk.size());
+      s->panel_nblk.push_back((int)b.size() - 1);
+      s->panel_grid.push_back(spmv_launch_grid(64, 4, 1, (int)b.size() - 1, 0, 1));
+      for (int r : b) {
+        blk.push_back(r);
+        blkk.push_back(rq[r]);
+      }
+    }
+    rp = prp.data();
+    col = pcol.data();
+    val = pval.data();
+  } else {
+    if (n > 0) blk = plan_rowblocks(n, rp, half ? 32 : s->spmv_bs, cap - kPad);  // room for VEC alignment
+    else blk.push_back(0);
+    blkk.resize(blk.size());
+    for (size_t i = 0; i < blk.size(); ++i) blkk[i] = n > 0 ? rp[blk[i]] : 0;
+  }
+  const size_t rp_len = (size_t)s->npanel * ((size_t)n + 1);
+  s->nblk = s->npanel > 1 ? (int)blk.size() - s->npanel : (int)blk.size() - 1;
   const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
   const size_t nv = (size_t)n + kPad;
   int rc;
-  if ((rc = dalloc(s, (void **)&s->d_rp, ((size_t)n + 1) * 4)) ||
+  if ((rc = dalloc(s, (void **)&s->d_rp, rp_len * 4)) ||
       (rc = dalloc(s, (void **)&s->d_col, nnz_pad * 4)) ||
       (rc = dalloc(s, &s->d_val, nnz_pad * sizeof(T))) ||
       (rc = dalloc(s, (void **)&s->d_blk, blk.size() * 4)) ||
@@ -285,8 +380,11 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   if (s->spmv_grid < 1) s->spmv_grid = 1;
   s->spmv_grid = spmv_launch_grid(s->spmv_bs, s->spmv_wpb, s->spmv_rbw, s->nblk,
                                   s->spmv_grid, s->spmv_dma);
+  if (s->npanel > 1)  // the last panel's launch writes the epilogue partials
+    s->spmv_grid = s->panel_grid.back();
   s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
   s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
+  for (int g : s->panel_grid) s->part_cap = std::max(s->part_cap, g + 1);
   const size_t ngmax = (size_t)s->part_cap / kTicketGroup + 2;
   if ((rc = dalloc(s, (void **)&s->d_pa, (size_t)s->part_cap * 8)) ||
       (rc = dalloc(s, (void **)&s->d_pb, (size_t)s->part_cap * 8)) ||
@@ -300,8 +398,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   CGX_HIP(hipMemsetAsync(s->d_col, 0, nnz_pad * 4, s->stream));
   CGX_HIP(hipMemsetAsync(s->d_val, 0, nnz_pad * sizeof(T), s->stream));
   if (n > 0) {
-    CGX_HIP(hipMemcpyAsync(s->d_rp, rp, ((size_t)n + 1) * 4,
-                           hipMemcpyHostToDevice, s->stream));
+    CGX_HIP(hipMemcpyAsync(s->d_rp, rp, rp_len * 4, hipMemcpyHostToDevice, s->stream));
     if (nnz > 0) {
       CGX_HIP(hipMemcpyAsync(s->d_col, col, (size_t)nnz * 4,
                              hipMemcpyHostToDevice, s->stream));
@@ -309,14 +406,12 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
                              hipMemcpyHostToDevice, s->stream));
     }
   }
-  std::vector<int> blkk(blk.size());
-  for (size_t i = 0; i < blk.size(); ++i) blkk[i] = n > 0 ? rp[blk[i]] : 0;
   CGX_HIP(hipMemcpyAsync(s->d_blk, blk.data(), blk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipMemcpyAsync(s->d_blkk, blkk.data(), blkk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
-  if (s->want_sell && n > 0) {
+  if (s->want_sell && n > 0 && s->npanel == 1) {
     std::vector<int> soff, slen, scol;
     std::vector<T> sval;
     if (csr_to_sell64<T>(n, rp, col, val, 1.25, soff, slen, sval, scol)) {
@@ -400,7 +495,29 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.nslices = s->nslices;
   a.n = s->n;
   a.dma = s->spmv_dma;
+  a.yacc = nullptr;
   return a;
+}
+
+// One SpMV of the solver's matrix: a single launch, or one per column panel
+// (rows continue their sums from y; the epilogue partials on the last panel).
+template <typename T>
+hipError_t launch_spmv_s(cgx_solver *s, SpmvArgs<T> a, hipStream_t st) {
+  if (s->npanel <= 1) return launch_spmv<T>(a, s->spmv_grid, s->vec, st);
+  double *part = a.part;
+  for (int q = 0; q < s->npanel; ++q) {
+    SpmvArgs<T> b = a;
+    b.rp = s->d_rp + (size_t)q * ((size_t)s->n + 1);
+    b.blk_first = s->panel_off[q];
+    b.nblk = s->panel_nblk[q];
+    b.yacc = q ? a.y : nullptr;
+    b.part = q + 1 == s->npanel ? part : nullptr;
+    b.dma = 1;
+    b.bs = 64;
+    const hipError_t e = launch_spmv<T>(b, s->panel_grid[q], s->vec, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 TicketArgs ticket_args(cgx_solver *s, int op) {
@@ -417,12 +534,12 @@ TicketArgs ticket_args(cgx_solver *s, int op) {
 
 bool use_ticket(const cgx_solver *s) {
   return s->ticket && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST &&
-         (s->spmv_bs == 64 || s->sell);
+         (s->spmv_bs == 64 || s->sell) && s->npanel == 1;
 }
 
 bool fused(const cgx_solver *s) {
   return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
-         s->spmv_dma != 2 && s->spmv_dma != 4;
+         s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1;
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -450,8 +567,7 @@ int enqueue_init(cgx_solver *s) {
   } else {
     CGX_HIP(launch_init_cg1<T>(s->n, b, x, r, p, (T *)s->d_s, s->d_pa,
                                s->vec_grid, st));
-    CGX_HIP(launch_spmv<T>(spmv_args<T>(s, r, s->d_w, s->d_pb, false),
-                           s->spmv_grid, s->vec, st));
+    CGX_HIP(launch_spmv_s<T>(s, spmv_args<T>(s, r, s->d_w, s->d_pb, false), st));
     CGX_HIP(launch_finalize(FIN_INIT_CG1, s->d_pa, s->vec_grid, s->d_pb,
                             s->spmv_grid, s->d_st, s->d_hist, nullptr, st));
   }
@@ -481,7 +597,7 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     // SpMV workgroup waiting on its ticket's round trip cost 20% (r01 A/B).
     const bool tkt = use_ticket(s);
     if (ev0) CGX_HIP(hipEventRecord(ev0, st));
-    CGX_HIP(launch_spmv<T>(sa, s->spmv_grid, s->vec, st));       // cg.c:111 (+131-132)
+    CGX_HIP(launch_spmv_s<T>(s, sa, st));                         // cg.c:111 (+131-132)
     if (ev1) CGX_HIP(hipEventRecord(ev1, st));
     if (fx) s->par ^= 1;
     if (exact) {
@@ -524,8 +640,7 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     CGX_HIP(launch_cg1_update<T>(s->n, x, p, r, sv, w, s->d_st, s->d_pa,
                                  s->vec_grid, st));
     if (ev0) CGX_HIP(hipEventRecord(ev0, st));
-    CGX_HIP(launch_spmv<T>(spmv_args<T>(s, r, w, s->d_pb, true), s->spmv_grid,
-                           s->vec, st));
+    CGX_HIP(launch_spmv_s<T>(s, spmv_args<T>(s, r, w, s->d_pb, true), st));
     if (ev1) CGX_HIP(hipEventRecord(ev1, st));
     CGX_HIP(launch_finalize(FIN_CG1, s->d_pa, s->vec_grid, s->d_pb, sg,
                             s->d_st, s->d_hist, nullptr, st));
@@ -699,8 +814,8 @@ int spmv_t(cgx_solver *s, const T *x, T *y) {
   CGX_HIP(hipSetDevice(s->device));
   CGX_HIP(hipMemcpyAsync(s->d_p, x, (size_t)s->n * sizeof(T),
                          hipMemcpyHostToDevice, s->stream));
-  CGX_HIP(launch_spmv<T>(spmv_args<T>(s, s->d_p, s->d_s, nullptr, false),
-                         s->spmv_grid, s->vec, s->stream));
+  CGX_HIP(launch_spmv_s<T>(s, spmv_args<T>(s, s->d_p, s->d_s, nullptr, false),
+                           s->stream));
   CGX_HIP(hipMemcpyAsync(y, s->d_s, (size_t)s->n * sizeof(T),
                          hipMemcpyDeviceToHost, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
@@ -937,8 +1052,12 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                             2.0 * s->n * sv;
   else
     info->spmv_iter_bytes = info->spmv_bytes;
+  if (s->npanel > 1)  // the panel passes' own bytes: P row_ptrs, y written P x, read P-1 x
+    info->spmv_iter_bytes = (double)s->nnz * (sv + 4) + 4.0 * s->npanel * (s->n + 1.0) +
+                            (double)s->n * sv * (1.0 + 2.0 * s->npanel - 1.0);
   if (fused(s)) info->spmv_iter_bytes += 2.0 * s->n * sv;
   info->device_bytes = s->dev_bytes;
+  info->n_panels = s->npanel;
   return 0;
 }
 

@@ -81,10 +81,12 @@ typedef struct {
   int vec_grid;         /* workgroups of the vector-update launches          */
   double spmv_bytes;    /* algorithmic HBM bytes per SpMV     */
   double iter_bytes;    /* algorithmic HBM bytes per CG iteration (8d)       */
-  double spmv_iter_bytes; /* algorithmic bytes of the SpMV launch as it runs
-                             inside the iteration (HS fuses p = r + beta p:
-                             + r and p_old gathered, p_new written)         */
+  double spmv_iter_bytes; /* algorithmic bytes of the SpMV as it runs inside
+                             the iteration, in the layout it runs on (fused
+                             p-update: + r, p_old gathered, p_new written;
+                             column panels: + P row_ptrs, y round trips)    */
   size_t device_bytes;  /* device memory held by the solver                  */
+  int n_panels;         /* column panels of the SpMV (1: plain CSR)          */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);

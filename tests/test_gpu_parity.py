@@ -513,3 +513,62 @@ def test_stream_ceilings():
     t = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_TRIAD)
     r = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_READ)
     assert 2000.0 < t < 8000.0 and 2000.0 < r < 8000.0
+
+
+@pytest.mark.parametrize("kb", ["8", "64"])
+def test_column_panels_bit_exact(kb, monkeypatch):
+    """Column-panel layout (CGX_LAYOUT=panel): rows continue their sequential
+    sums panel after panel, so SpMV stays bit-exact in fp64 and fp32, rows
+    longer than a window (dense rows crossing every panel) and rows with no
+    entry in a panel included; CG matches the oracle."""
+    monkeypatch.setenv("CGX_LAYOUT", "panel")
+    monkeypatch.setenv("CGX_PANEL_KB", kb)
+    rp, col, val, b = H.random_spd(30000, 9, seed=31)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_panels"] > 1
+        assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
+        s.set_rhs(b)
+        s.run(40)
+        x_ref, _ = H.o_conj_grad(40, rp, col, val, b)
+        assert rel(s.x(), x_ref) <= FAST_RTOL
+        s.set_rhs(b)
+        its = s.run(2000, 1e-9)
+        _, its_o, _ = H.o_solve(2000, 1e-9, rp, col, val, b)
+        assert abs(its - its_o) <= 1
+        # dense rows (long-row path) crossing all panels
+        n = 6000
+        rng = np.random.default_rng(9)
+        rows = [np.arange(n) if i in (0, 17, n - 1) else
+                np.unique(np.concatenate([[max(i - 1, 0), i, min(i + 1, n - 1)],
+                                          rng.integers(0, n, 4)])) for i in range(n)]
+        rp2 = np.zeros(n + 1, np.int32)
+        rp2[1:] = np.cumsum([len(c) for c in rows])
+        col2 = np.concatenate(rows).astype(np.int32)
+        val2 = rng.standard_normal(len(col2))
+        x2 = rng.standard_normal(n)
+        s.set_matrix(rp2, col2, val2)
+        assert H.same_bits_or_both_nan(s.spmv(x2), H.o_spmv(rp2, col2, val2, x2))
+        rp32, col32, v32 = cgx.random_spd(20000, 40, 9, f32=True)
+        x32 = np.random.default_rng(2).standard_normal(20000).astype(np.float32)
+        s.set_matrix(rp32, col32, v32)
+        assert s.info()["n_panels"] > 1
+        assert np.array_equal(s.spmv(x32).view(np.uint32),
+                              H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
+
+
+def test_column_panels_auto_c5():
+    """C5 (random SPD, 5 M rows, fp32) selects column panels by itself and is
+    bit-exact at full size; a large Laplacian keeps plain CSR."""
+    rp, col, val = cgx.random_spd(5_000_000, 32, 42, f32=True)
+    x = np.random.default_rng(3).standard_normal(len(rp) - 1).astype(np.float32)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_panels"] == 10
+        assert np.array_equal(s.spmv(x).view(np.uint32),
+                              H.o_spmv_f32(rp, col, val, x).view(np.uint32))
+    del rp, col, val
+    rp, col, val = cgx.laplacian3d(128, 128, 128)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_panels"] == 1
