@@ -191,6 +191,7 @@ struct cgx_solver {
   // d_rp + q (n+1), its row blocks at blk index panel_off[q] (panel_nblk[q])
   int npanel = 1;
   std::vector<int> panel_off, panel_nblk, panel_grid;
+  bool panel_win512 = false;  // fp32 panels: 512-entry LDS windows
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
@@ -328,6 +329,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   std::vector<int> prp, pcol;
   std::vector<T> pval;
   s->npanel = choose_panels(n, rp, col, sizeof(T));
+  s->panel_win512 = sizeof(T) == 4 && env_int("CGX_PANEL_WIN512", 0) != 0;
   s->panel_off.clear();
   s->panel_nblk.clear();
   s->panel_grid.clear();
@@ -336,7 +338,10 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
     build_panels<T>(n, rp, col, val, s->npanel, prp, pcol, pval);
     for (int q = 0; q < s->npanel; ++q) {
       const int *rq = prp.data() + (size_t)q * (n + 1);
-      std::vector<int> b = plan_rowblocks(n, rq, 64, spmv_cap(64, sizeof(T) == 8) - kPad);
+      // fp32: 512-entry windows (4 KiB of LDS per wave, 2x the waves of the
+      // 1024-entry default) when CGX_PANEL_WIN512 (k_spmv_dma, dma == 4 branch)
+      std::vector<int> b = plan_rowblocks(
+          n, rq, 64, (s->panel_win512 ? 512 : spmv_cap(64, sizeof(T) == 8)) - kPad);
       s->panel_off.push_back((int)blk.size());
       s->panel_nblk.push_back((int)b.size() - 1);
       s->panel_grid.push_back(spmv_launch_grid(64, 4, 1, (int)b.size() - 1, 0, 1));
@@ -512,7 +517,7 @@ hipError_t launch_spmv_s(cgx_solver *s, SpmvArgs<T> a, hipStream_t st) {
     b.nblk = s->panel_nblk[q];
     b.yacc = q ? a.y : nullptr;
     b.part = q + 1 == s->npanel ? part : nullptr;
-    b.dma = 1;
+    b.dma = s->panel_win512 ? 4 : 1;  // dma 4: fp32 CAPW 512
     b.bs = 64;
     const hipError_t e = launch_spmv<T>(b, s->panel_grid[q], s->vec, st);
     if (e != hipSuccess) return e;

@@ -515,14 +515,16 @@ def test_stream_ceilings():
     assert 2000.0 < t < 8000.0 and 2000.0 < r < 8000.0
 
 
-@pytest.mark.parametrize("kb", ["8", "64"])
+@pytest.mark.parametrize("kb", ["8", "64", "64w"])
 def test_column_panels_bit_exact(kb, monkeypatch):
     """Column-panel layout (CGX_LAYOUT=panel): rows continue their sequential
     sums panel after panel, so SpMV stays bit-exact in fp64 and fp32, rows
     longer than a window (dense rows crossing every panel) and rows with no
     entry in a panel included; CG matches the oracle."""
     monkeypatch.setenv("CGX_LAYOUT", "panel")
-    monkeypatch.setenv("CGX_PANEL_KB", kb)
+    monkeypatch.setenv("CGX_PANEL_KB", kb.rstrip("w"))
+    if kb.endswith("w"):
+        monkeypatch.setenv("CGX_PANEL_WIN512", "1")
     rp, col, val, b = H.random_spd(30000, 9, seed=31)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
