@@ -42,9 +42,16 @@ struct CgState {
   int done;       // set by the finalize step; every kernel early-exits on it
   int use_tol;
   int hist_cap;
-  int pad[3];
+  // folded HS (CGX_FOLD): the scalar steps run inside the vector kernels, so
+  // each kernel reads only what the previous one wrote: k_update_rf writes
+  // rr_u / k_u (+ alpha), k_xpay_xf writes rr_x / k_x (+ rr, k, beta, done)
+  int k_u;
+  int k_x;
+  int pad;
+  double rr_u;
+  double rr_x;
 };
-static_assert(sizeof(CgState) == 96, "CgState layout");
+static_assert(sizeof(CgState) == 112, "CgState layout");
 
 // -------------------------------------------------------------- geometry
 // SpMV row block: bs (256 or 512) rows, one per lane, and at most
@@ -164,6 +171,13 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
                         int grid, hipStream_t st);
 hipError_t launch_stream_read(long long n2, const double *b, double *sink, int grid,
                               hipStream_t st);
+template <typename T>
+hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
+                            int nps, double *rr_part, int grid, hipStream_t st);
+template <typename T>
+hipError_t launch_xpay_xf(int n, T *x, T *p, const T *r, CgState *stt,
+                          const double *rr_part, int nrr, double *hist, int grid,
+                          hipStream_t st);
 template <typename T>
 hipError_t launch_update_r(int n, T *r, const T *s, const CgState *stt,
                            double *part, int grid, hipStream_t st);

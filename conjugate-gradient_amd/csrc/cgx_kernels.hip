@@ -75,8 +75,10 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st,
     case FIN_INIT_HS:
       st->bb = sa;
       st->rr = sa;  // r = b (cg.c:107), so r.r == b.b bit for bit
+      st->rr_x = sa;
       st->tol2bb = st->tol * st->tol * sa;
       st->k = 0;
+      st->k_x = 0;
       st->done = 0;
       break;
     case FIN_HS_ALPHA:
@@ -1107,6 +1109,214 @@ __global__ __launch_bounds__(BS) void k_update_xr(int n, T *__restrict__ x,
 }
 
 // p = r + beta*p (cg.c:131-132)
+template <int BS>
+__device__ __forceinline__ double sum_parts(const double *pa, int na,
+                                            double *red) {
+  // Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order.  All of a
+  // thread's loads (up to U) are issued before the first add, so a 40K-entry
+  // partial array costs one memory round trip, not one per 16 entries.
+  constexpr int U = 48;
+  double acc = 0.0;
+  int i = threadIdx.x;
+  bool first = true;
+  for (; i < na; i += U * BS) {
+    double v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (i + j * BS < na) {
+        acc = first ? v[j] : acc + v[j];
+        first = false;
+      }
+  }
+  const double s = block_sum<BS>(acc, red);
+  __syncthreads();
+  return s;
+}
+
+// Two partial arrays summed with all loads of both in flight at once; each
+// sum keeps sum_parts' order (thread t: index order, then the block tree).
+template <int BS>
+__device__ __forceinline__ void sum_parts2(const double *pa, int na, const double *pb,
+                                           int nb, double *red, double &sa, double &sb) {
+  constexpr int U = 24;
+  double acc_a = 0.0, acc_b = 0.0;
+  bool fa = true, fb = true;
+  const int nmax = na > nb ? na : nb;
+  for (int i = threadIdx.x; i < nmax; i += U * BS) {
+    double va[U], vb[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      va[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
+      vb[j] = i + j * BS < nb ? pb[i + j * BS] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (i + j * BS < na) {
+        acc_a = fa ? va[j] : acc_a + va[j];
+        fa = false;
+      }
+      if (i + j * BS < nb) {
+        acc_b = fb ? vb[j] : acc_b + vb[j];
+        fb = false;
+      }
+    }
+  }
+  sa = block_sum<BS>(acc_a, red);
+  __syncthreads();
+  sb = block_sum<BS>(acc_b, red);
+  __syncthreads();
+}
+
+// Folded HS (CGX_FOLD): no finalize kernels.  Every workgroup of the vector
+// kernels sums the previous kernel's partials itself -- the same
+// sum_parts<1024> order as k_finalize<1024>, so alpha, beta and the stop test
+// are bit-identical to the finalize path -- and workgroup 0 publishes the
+// state for later kernels.  A kernel never writes a field its own workgroups
+// read: k_update_rf reads rr_x / k_x and writes rr_u / k_u / alpha;
+// k_xpay_xf reads rr_u / k_u / alpha and writes rr_x / k_x / rr / k / beta /
+// done.  The stop flag: k_xpay_xf sets 1 after the stop iteration's x update,
+// the next k_update_rf turns it into 2; only 2 stops k_xpay_xf (a 1 seen
+// there was written by its own workgroup 0 during this launch).
+constexpr int kFoldBS = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
+                                                       const T *__restrict__ s,
+                                                       CgState *__restrict__ st,
+                                                       const double *__restrict__ ps_part,
+                                                       int nps, double *__restrict__ rr_part) {
+  __shared__ double red[kFoldBS / kWave];
+  __shared__ double bcast;
+  const int done = st->done;
+  if (done) {
+    if (done == 1 && blockIdx.x == 0 && threadIdx.x == 0) st->done = 2;
+    return;
+  }
+  const double ps = sum_parts<kFoldBS>(ps_part, nps, red);
+  if (threadIdx.x == 0) {
+    const double rr = st->rr_x;
+    const double alpha = rr / ps;  // cg.c:113
+    bcast = alpha;
+    if (blockIdx.x == 0) {
+      st->ps = ps;
+      st->alpha = alpha;
+      st->rr_u = rr;
+      st->k_u = st->k_x;
+    }
+  }
+  __syncthreads();
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T alpha = (T)bcast;
+  const int nv = n / W;
+  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    V rv = reinterpret_cast<const V *>(r)[i];
+    const V sv = reinterpret_cast<const V *>(s)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T as = alpha * sv[j];
+      rv[j] = rv[j] - as;
+      acc = acc + (double)rv[j] * (double)rv[j];
+    }
+    reinterpret_cast<V *>(r)[i] = rv;
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T as = alpha * s[i];
+      const T ri = r[i] - as;
+      r[i] = ri;
+      acc = acc + (double)ri * (double)ri;
+    }
+  // one partial per 256-thread quarter, reduced exactly as block_sum<256>:
+  // the same terms per partial and the same order as k_update_r<T, 256>, so
+  // r.r (and beta) match the finalize path bit for bit
+  acc = wave_sum(acc);
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) red[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x < kFoldBS / 256) {
+    constexpr int WQ = 256 / kWave;
+    double q = red[threadIdx.x * WQ];
+#pragma unroll
+    for (int w = 1; w < WQ; ++w) q = q + red[threadIdx.x * WQ + w];
+    rr_part[blockIdx.x * (kFoldBS / 256) + threadIdx.x] = q;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x,
+                                                     T *__restrict__ p,
+                                                     const T *__restrict__ r,
+                                                     CgState *__restrict__ st,
+                                                     const double *__restrict__ rr_part,
+                                                     int nrr, double *__restrict__ hist) {
+  __shared__ double red[kFoldBS / kWave];
+  __shared__ double bcast;
+  __shared__ int bstop;
+  if (st->done > 1) return;
+  const double rr_new = sum_parts<kFoldBS>(rr_part, nrr, red);
+  if (threadIdx.x == 0) {
+    const int k = st->k_u;
+    const bool stop = k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb);
+    const double beta = rr_new / st->rr_u;  // cg.c:129
+    bcast = beta;
+    bstop = stop;
+    if (blockIdx.x == 0) {  // cg.c:125-129
+      if (k < st->hist_cap) hist[k] = rr_new;
+      if (stop) {
+        st->k = k;
+        st->done = 1;
+      } else {
+        st->beta = beta;
+        st->rr = rr_new;
+        st->rr_x = rr_new;
+        st->k = k + 1;
+        st->k_x = k + 1;
+      }
+    }
+  }
+  __syncthreads();
+  const bool stop = bstop != 0;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const T alpha = (T)st->alpha, beta = (T)bcast;
+  const int nv = n / W;
+  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+  for (int i = gid; i < nv; i += stride) {
+    V pv = reinterpret_cast<const V *>(p)[i];
+    V xv = reinterpret_cast<const V *>(x)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T ap = alpha * pv[j];
+      xv[j] = xv[j] + ap;
+    }
+    reinterpret_cast<V *>(x)[i] = xv;
+    if (!stop) {
+      const V rv = reinterpret_cast<const V *>(r)[i];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T bp = beta * pv[j];
+        pv[j] = rv[j] + bp;
+      }
+      reinterpret_cast<V *>(p)[i] = pv;
+    }
+  }
+  if (gid == 0)
+    for (int i = nv * W; i < n; ++i) {
+      const T pi = p[i];
+      const T ap = alpha * pi;
+      x[i] = x[i] + ap;
+      if (!stop) {
+        const T bp = beta * pi;
+        p[i] = r[i] + bp;
+      }
+    }
+}
+
 // Deferred-x HS (CGX_XDEFER): x += alpha p moves from the r-update into the
 // p-update, which reads p_old anyway -- one 8n-byte read of p less per
 // iteration.  Same per-element roundings as k_update_xr / k_xpay.
@@ -1329,65 +1539,6 @@ __global__ __launch_bounds__(BS) void k_dot_part(int n, const T *__restrict__ a,
 // Fixed-order sum of na partials by one workgroup (thread t adds
 // pa[t], pa[t+BS], ... in order; then the block tree).  Starts from the first
 // partial, so a single partial (exact mode) passes through unchanged.
-template <int BS>
-__device__ __forceinline__ double sum_parts(const double *pa, int na,
-                                            double *red) {
-  // Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order.  All of a
-  // thread's loads (up to U) are issued before the first add, so a 40K-entry
-  // partial array costs one memory round trip, not one per 16 entries.
-  constexpr int U = 48;
-  double acc = 0.0;
-  int i = threadIdx.x;
-  bool first = true;
-  for (; i < na; i += U * BS) {
-    double v[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) v[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (i + j * BS < na) {
-        acc = first ? v[j] : acc + v[j];
-        first = false;
-      }
-  }
-  const double s = block_sum<BS>(acc, red);
-  __syncthreads();
-  return s;
-}
-
-// Two partial arrays summed with all loads of both in flight at once; each
-// sum keeps sum_parts' order (thread t: index order, then the block tree).
-template <int BS>
-__device__ __forceinline__ void sum_parts2(const double *pa, int na, const double *pb,
-                                           int nb, double *red, double &sa, double &sb) {
-  constexpr int U = 24;
-  double acc_a = 0.0, acc_b = 0.0;
-  bool fa = true, fb = true;
-  const int nmax = na > nb ? na : nb;
-  for (int i = threadIdx.x; i < nmax; i += U * BS) {
-    double va[U], vb[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      va[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
-      vb[j] = i + j * BS < nb ? pb[i + j * BS] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (i + j * BS < na) {
-        acc_a = fa ? va[j] : acc_a + va[j];
-        fa = false;
-      }
-      if (i + j * BS < nb) {
-        acc_b = fb ? vb[j] : acc_b + vb[j];
-        fb = false;
-      }
-    }
-  }
-  sa = block_sum<BS>(acc_a, red);
-  __syncthreads();
-  sb = block_sum<BS>(acc_b, red);
-  __syncthreads();
-}
 
 template <int BS>
 __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int na,
@@ -1634,6 +1785,23 @@ hipError_t launch_xpay_x(int n, T *x, T *p, const T *r, const CgState *stt,
 }
 
 template <typename T>
+hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
+                            int nps, double *rr_part, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_update_rf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt,
+                     ps_part, nps, rr_part);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_xpay_xf(int n, T *x, T *p, const T *r, CgState *stt,
+                          const double *rr_part, int nrr, double *hist, int grid,
+                          hipStream_t st) {
+  hipLaunchKernelGGL((k_xpay_xf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, r, stt,
+                     rr_part, nrr, hist);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w,
                              const CgState *stt, double *part, int grid,
                              hipStream_t st) {
@@ -1745,6 +1913,12 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
                                          double *, int, hipStream_t);          \
   template hipError_t launch_xpay_x<T>(int, T *, T *, const T *,              \
                                        const CgState *, int, hipStream_t);     \
+  template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *,     \
+                                          const double *, int, double *, int,  \
+                                          hipStream_t);                        \
+  template hipError_t launch_xpay_xf<T>(int, T *, T *, const T *, CgState *,  \
+                                        const double *, int, double *, int,    \
+                                        hipStream_t);                          \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *,           \
                                            const T *, const CgState *,        \
                                            double *, int, hipStream_t);        \

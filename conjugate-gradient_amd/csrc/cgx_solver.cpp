@@ -187,6 +187,7 @@ struct cgx_solver {
   int nblk = 0, spmv_grid = 0, vec_grid = 0;
   bool use_graph = true;
   bool xdefer = false;  // CGX_XDEFER: x update folded into the p-update
+  bool fold = false;    // CGX_FOLD: alpha/beta steps inside the vector kernels
   // column panels (irregular matrices): npanel SpMV passes, panel q's rows in
   // d_rp + q (n+1), its row blocks at blk index panel_off[q] (panel_nblk[q])
   int npanel = 1;
@@ -388,6 +389,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   if (s->npanel > 1)  // the last panel's launch writes the epilogue partials
     s->spmv_grid = s->panel_grid.back();
   s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
+  s->vec_grid = (std::max(s->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
   s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
   for (int g : s->panel_grid) s->part_cap = std::max(s->part_cap, g + 1);
   const size_t ngmax = (size_t)s->part_cap / kTicketGroup + 2;
@@ -620,6 +622,15 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
       const TicketArgs tk = ticket_args(s, FIN_HS_BETA);
       CGX_HIP(launch_update_xr<T>(s->n, x, p, r, sv, s->d_st, s->d_pa,
                                   s->vec_grid, st, &tk));
+    } else if (s->xdefer && s->fold && !fx) {
+      // folded: alpha inside k_update_rf, beta + stop test inside k_xpay_xf
+      // (no finalize launches; bit-identical scalars, see k_update_rf)
+      const int gf = s->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
+      CGX_HIP(launch_update_rf<T>(s->n, r, sv, s->d_st, s->d_pa, sg, s->d_pb, gf,
+                                  st));                           // cg.c:113, 118-123
+      CGX_HIP(launch_xpay_xf<T>(s->n, x, p, r, s->d_st, s->d_pb, 4 * gf, s->d_hist,
+                                gf, st));                         // cg.c:115-116, 125-132
+      return 0;
     } else if (s->xdefer && !fx) {
       // deferred x: r-update alone, x += alpha p_old folded into the p-update
       CGX_HIP(launch_finalize(FIN_HS_ALPHA_X, s->d_pa, sg, nullptr, 0, s->d_st,
@@ -918,7 +929,8 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->use_graph = cgx::env_int("CGX_GRAPH", 1) != 0;
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
   s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
-  s->xdefer = cgx::env_int("CGX_XDEFER", 1) != 0;  // -4.4% per C3 iteration (sweep20), bit-identical
+  s->xdefer = cgx::env_int("CGX_XDEFER", 1) != 0;
+  s->fold = cgx::env_int("CGX_FOLD", 1) != 0;  // C3 -1%, C2 -8% (sweep22), bit-identical  // -4.4% per C3 iteration (sweep20), bit-identical
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {

@@ -467,8 +467,11 @@ def test_deferred_x_bit_identical(dma, monkeypatch):
     cases[1] = (g["row_ptr"], g["col"], g["val"], g["b"])
     for rp, col, val, b in cases:
         out = {}
-        for xd in ("0", "1"):
-            monkeypatch.setenv("CGX_XDEFER", xd)
+        for xd in ("0", "1", "fold"):
+            # "fold": CGX_FOLD, the alpha/beta/stop steps inside the vector
+            # kernels (no finalize launches) -- same scalars bit for bit
+            monkeypatch.setenv("CGX_XDEFER", "0" if xd == "0" else "1")
+            monkeypatch.setenv("CGX_FOLD", "1" if xd == "fold" else "0")
             with cgx.Solver(0) as s:
                 s.set_matrix(rp, col, val)
                 res = []
@@ -477,19 +480,21 @@ def test_deferred_x_bit_identical(dma, monkeypatch):
                     its = s.run(maxit, tol)
                     res.append((its, s.x(), s.history(its)))
                 out[xd] = res
-        for (i0, x0, h0), (i1, x1, h1) in zip(out["0"], out["1"]):
-            assert i0 == i1
-            assert H.same_bits_or_both_nan(x0, x1)
-            assert H.same_bits_or_both_nan(h0, h1)
+        for other in ("1", "fold"):
+            for (i0, x0, h0), (i1, x1, h1) in zip(out["0"], out[other]):
+                assert i0 == i1, other
+                assert H.same_bits_or_both_nan(x0, x1), other
+                assert H.same_bits_or_both_nan(h0, h1), other
     x_ref, _ = H.o_conj_grad(37, g["row_ptr"], g["col"], g["val"], g["b"])
     assert rel(out["1"][2][1], x_ref) <= FAST_RTOL
 
 
-@pytest.mark.parametrize("xd", ["0", "1"])
+@pytest.mark.parametrize("xd", ["0", "1", "fold"])
 def test_history_after_buffer_growth(xd, monkeypatch):
     """Cached hipGraphs are dropped when a longer run reallocates the r.r
     history buffer (regression: r01, the graph kept the freed pointer)."""
-    monkeypatch.setenv("CGX_XDEFER", xd)
+    monkeypatch.setenv("CGX_XDEFER", "0" if xd == "0" else "1")
+    monkeypatch.setenv("CGX_FOLD", "1" if xd == "fold" else "0")
     rp, col, val, b = H.random_spd(30000, 9, seed=21)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
