@@ -61,6 +61,7 @@ inline int spmv_cap(int bs, bool f64) { return bs * (f64 ? 8 : 16); }
 inline int spmv_launch_grid(int bs, int wpb, int rbw, int nblk, int grid,
                             int dma = 0) {
   if (bs == 64 && dma == 2) return (nblk + 2 * rbw - 1) / (2 * rbw);
+  if (bs == 64 && dma == 1 && wpb == 8) return (nblk + 7) / 8;
   if (bs == 64 && dma) return (nblk + 3) / 4;
   if (bs == 64) return (nblk + wpb * rbw - 1) / (wpb * rbw);
   return grid < 1 ? 1 : (grid > nblk ? nblk : grid);

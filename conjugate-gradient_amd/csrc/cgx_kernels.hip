@@ -1699,6 +1699,17 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     return hipGetLastError();
   }
+  if (a.bs == 64 && a.dma == 1 && a.wpb == 8 && !a.x2) {  // 8 waves: half the partials
+    constexpr int WPB = 8;
+    constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;
+    const int g = (a.nblk + WPB - 1) / WPB;
+    const bool epi = a.part != nullptr;
+    if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.bs == 64 && a.dma) {
     constexpr int WPB = 4;
     constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;

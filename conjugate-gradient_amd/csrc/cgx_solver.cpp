@@ -345,7 +345,9 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
           n, rq, 64, (s->panel_win512 ? 512 : spmv_cap(64, sizeof(T) == 8)) - kPad);
       s->panel_off.push_back((int)blk.size());
       s->panel_nblk.push_back((int)b.size() - 1);
-      s->panel_grid.push_back(spmv_launch_grid(64, 4, 1, (int)b.size() - 1, 0, 1));
+      s->panel_grid.push_back(spmv_launch_grid(64, s->panel_win512 ? 4 : s->spmv_wpb, 1,
+                                               (int)b.size() - 1, 0,
+                                               s->panel_win512 ? 4 : 1));
       for (int r : b) {
         blk.push_back(r);
         blkk.push_back(rq[r]);
@@ -546,7 +548,8 @@ bool use_ticket(const cgx_solver *s) {
 
 bool fused(const cgx_solver *s) {
   return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
-         s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1;
+         s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1 &&
+         !(s->spmv_dma == 1 && s->spmv_wpb == 8);  // no fused variant at 8 waves
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.

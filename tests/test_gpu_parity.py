@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -73,8 +73,10 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
     monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
-    if bs in ("dma", "dma8", "dma32"):
-        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4"}[bs])
+    if bs in ("dma", "dma8", "dma32", "dmaw8"):
+        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4", "dmaw8": "1"}[bs])
+        if bs == "dmaw8":
+            monkeypatch.setenv("CGX_SPMV_WPB", "8")
     elif bs.startswith("pipe"):
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
         if bs != "pipe":
