@@ -611,7 +611,11 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
   T *lval = lval_all + wid * CAPW;
   int *lcol = lcol_all + wid * CAPW;
   const T beta = XPAY ? (T)a.st->beta : T(0);
-  const int wb = blockIdx.x * WPB + wid;
+  // a.xcd: XCD-contiguous row ranges (workgroups are dealt round-robin to the
+  // 8 XCDs; remapped so each XCD walks one contiguous eighth of the blocks and
+  // the x lines a row block shares with its +-1 / +-nx / +-nx*ny neighbours
+  // hit that XCD's L2 instead of being re-fetched over the fabric)
+  const int wb = xcd_block(a.xcd) * WPB + wid;
   double dot = 0.0;
   if (wb < a.nblk) {
     const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : a.blk_first + wb);

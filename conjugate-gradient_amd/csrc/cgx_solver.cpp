@@ -919,7 +919,10 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_dma = cgx::env_int("CGX_SPMV_DMA", 1);
   s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", s->spmv_dma == 2 ? 8 : 1));
   if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
-  s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", 0);
+  // XCD-contiguous block order for the LDS-DMA kernel: time-neutral, but the
+  // x lines shared by neighbouring row blocks stay in one XCD's L2 (EA reads
+  // 1265 -> 976 MB per C3 SpMV = the algorithmic 965 MB; sweep25)
+  s->spmv_xcd = cgx::env_int("CGX_SPMV_XCD", s->spmv_dma == 1 ? 1 : 0);
   // nt helps the LDS-DMA stream, hurts the register-staged one (sweep15)
   // -1 = by size at set_matrix (kNtStreamBytes; nt helps the LDS-DMA stream
   // only, it hurts the register-staged one: sweep15)

@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -73,10 +73,13 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
     monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
-    if bs in ("dma", "dma8", "dma32", "dmaw8"):
-        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4", "dmaw8": "1"}[bs])
+    if bs in ("dma", "dma8", "dma32", "dmaw8", "dmaxcd"):
+        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4", "dmaw8": "1",
+                                            "dmaxcd": "1"}[bs])
         if bs == "dmaw8":
             monkeypatch.setenv("CGX_SPMV_WPB", "8")
+        if bs == "dmaxcd":
+            monkeypatch.setenv("CGX_SPMV_XCD", "1")
     elif bs.startswith("pipe"):
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
         if bs != "pipe":
@@ -169,11 +172,13 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "8"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "8", "1x"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
-    monkeypatch.setenv("CGX_SPMV_DMA", dma)
+    monkeypatch.setenv("CGX_SPMV_DMA", dma.rstrip("x"))
+    if dma.endswith("x"):
+        monkeypatch.setenv("CGX_SPMV_XCD", "1")
     rp, col, val = cgx.laplacian3d(216, 216, 216)
     x = np.random.default_rng(2).standard_normal(len(rp) - 1)
     with cgx.Solver(0) as s:

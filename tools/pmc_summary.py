@@ -1,16 +1,19 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh collection into profiles/ (committed):
   profiles/<round>_<tag>_kernel_stats.csv   rocprofv3 --stats output, verbatim
-  profiles/<round>_<tag>.md                 per-kernel time + HBM bytes table
+  profiles/<round>_<tag>.md                 per-kernel time + memory-side bytes
   profiles/pmc_<workload>.json              read by bench.py (roofline.traffic)
 
-HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE
-and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
-16-B-per-lane streaming read, so reads are doubled.  The calibration was
-checked on this code's own streaming kernels (k_update_xr / k_xpay read
-exactly 2 x FETCH_SIZE = the algorithmic bytes).  The SpMV's x gathers and
-row_ptr loads are narrower accesses (uncalibrated); doubling them makes the
-SpMV figure an upper bound.
+Two byte estimates per launch, both from separate single-counter --pmc passes:
+* EA bytes (used for `traffic`): the size-resolved L2->fabric requests,
+  128 RDREQ_128B + 64 RDREQ_64B + 32 RDREQ_32B reads and 64 WRREQ_64B +
+  32 (WRREQ - WRREQ_64B) writes.  Calibrated on the bench's k_stream_read,
+  which reads exactly 512 MiB: 4,194,304 RDREQ_128B.
+* the guide's rule (/opt/skills/guides/MI355X_MICROARCH.md, HBM section):
+  2 x FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE reports half of a 16-B/lane
+  stream on gfx950).  Agrees with the EA bytes on the streaming kernels.
+Both count L2 misses, including those the Infinity Cache serves: an upper
+bound of DRAM traffic.
 
   python tools/pmc_summary.py <tag> <round> <workload> [algorithmic_spmv_bytes]
 """
@@ -28,46 +31,67 @@ src = REPO / "gpurun_out" / f"prof_{tag}"
 dst = REPO / "profiles"
 dst.mkdir(exist_ok=True)
 
+COUNTERS = ["FETCH_SIZE", "WRITE_SIZE", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+            "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"]
+
 
 def short(name):
-    name = name.replace("cgx::(anonymous namespace)::", "")
+    name = name.replace("cgx::(anonymous namespace)::", "").replace("cgx::", "")
     return name.split("(")[0] if "(" in name and "<" not in name.split("(")[0][-1:] else name[:90]
 
 
 stats = list(csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")))
 shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / f"{rnd}_{tag}_kernel_stats.csv")
-pmc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in ("fetch", "write"):
-    for r in csv.DictReader(open(src / f / "run_counter_collection.csv")):
-        pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+pmc = collections.defaultdict(dict)
+for c in COUNTERS:
+    f = src / f"pmc_{c}" / "run_counter_collection.csv"
+    if not f.exists():
+        continue
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    for k, v in acc.items():
+        pmc[k][c] = sum(v) / len(v)
 
-rows, spmv = [], None
+rows, spmv, calib = [], None, None
 for s in stats:
     name = s["Name"]
     c = pmc.get(name, {})
-    fetch = sum(c.get("FETCH_SIZE", [0])) / max(len(c.get("FETCH_SIZE", [1])), 1) * 1024
-    write = sum(c.get("WRITE_SIZE", [0])) / max(len(c.get("WRITE_SIZE", [1])), 1) * 1024
+    g = lambda k: c.get(k, 0.0)  # noqa: E731
+    guide = 2 * g("FETCH_SIZE") * 1024 + g("WRITE_SIZE") * 1024
+    ea_rd = 128 * g("TCC_EA0_RDREQ_128B_sum") + 64 * g("TCC_EA0_RDREQ_64B_sum") + \
+        32 * g("TCC_EA0_RDREQ_32B_sum")
+    ea_wr = 64 * g("TCC_EA0_WRREQ_64B_sum") + 32 * (g("TCC_EA0_WRREQ_sum") - g("TCC_EA0_WRREQ_64B_sum"))
     avg_ns = float(s["AverageNs"])
-    hbm = 2 * fetch + write
+    ea = ea_rd + ea_wr
     rows.append((short(name), int(s["Calls"]), avg_ns / 1e3, float(s["Percentage"]),
-                 fetch / 1e6, write / 1e6, hbm / 1e6, hbm / avg_ns if avg_ns else 0))
+                 ea_rd / 1e6, ea_wr / 1e6, guide / 1e6, ea / avg_ns if avg_ns else 0))
+    if "k_stream_read" in name:
+        calib = ea_rd
     if "k_spmv" in name and (spmv is None or int(s["Calls"]) > spmv["calls"]):
         spmv = dict(kernel=short(name), calls=int(s["Calls"]), avg_us=avg_ns / 1e3,
-                    fetch_size_bytes_raw=fetch, write_size_bytes=write,
-                    spmv_hbm_bytes_per_launch=hbm)
-md = [f"# {rnd} {tag}: rocprofv3 --kernel-trace --stats + --pmc FETCH_SIZE / WRITE_SIZE",
-      "", "| kernel | calls | avg us | % time | FETCH raw MB | WRITE MB | HBM MB (2F+W) | GB/s |",
+                    ea_read_bytes=ea_rd, ea_write_bytes=ea_wr,
+                    guide_bytes_2fetch_plus_write=guide,
+                    spmv_hbm_bytes_per_launch=ea)
+md = [f"# {rnd} {tag}: rocprofv3 --kernel-trace --stats + single-counter --pmc passes",
+      "", "EA = L2->fabric requests by size (see tools/pmc_summary.py); guide = 2 x FETCH_SIZE "
+      "+ WRITE_SIZE.  Both include Infinity-Cache hits.", "",
+      "| kernel | calls | avg us | % time | EA read MB | EA write MB | guide MB | EA GB/s |",
       "|---|---|---|---|---|---|---|---|"]
 for r in rows:
     md.append(f"| `{r[0]}` | {r[1]} | {r[2]:.2f} | {r[3]:.1f} | {r[4]:.1f} | {r[5]:.1f} | "
               f"{r[6]:.1f} | {r[7]:.0f} |")
+if calib:
+    md += ["", f"Calibration: k_stream_read reads 536.9 MB by construction; EA read = "
+           f"{calib / 1e6:.1f} MB."]
 if spmv and alg_bytes:
-    md += ["", f"SpMV algorithmic bytes per launch: {alg_bytes:.0f}; measured HBM (upper "
-           f"bound, see tools/pmc_summary.py): {spmv['spmv_hbm_bytes_per_launch']:.0f} "
-           f"({spmv['spmv_hbm_bytes_per_launch'] / alg_bytes:.2f}x)"]
+    md += ["", f"SpMV algorithmic bytes per launch: {alg_bytes:.0f}; EA bytes: "
+           f"{spmv['spmv_hbm_bytes_per_launch']:.0f} "
+           f"({spmv['spmv_hbm_bytes_per_launch'] / alg_bytes:.3f}x)."]
 (dst / f"{rnd}_{tag}.md").write_text("\n".join(md) + "\n")
 if spmv:
     spmv["algorithmic_bytes_per_launch"] = alg_bytes
-    spmv["source"] = f"profiles/{rnd}_{tag}_kernel_stats.csv + PMC passes ({rnd})"
+    spmv["calibration_stream_read_bytes"] = calib
+    spmv["source"] = f"profiles/{rnd}_{tag}_kernel_stats.csv + single-counter PMC passes ({rnd})"
     (dst / f"pmc_{workload}.json").write_text(json.dumps(spmv, indent=1) + "\n")
 print("\n".join(md))
