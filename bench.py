@@ -251,6 +251,23 @@ def main():
     roofline["stream_read_gbs"] = round(rd, 1)
     roofline["frac_of_stream_read"] = round(achieved / rd, 4)
 
+    # matrix-free upper bound for the Laplacian runs -- the same
+    # operator as a stencil (bit-identical SpMV), only x and y move
+    mf = None
+    if world == 1 and wl["kind"] in ("lap3d", "lap2d"):
+        with cgx.Solver(local_rank) as ms:
+            dims = wl["dims"]
+            ms.set_stencil(3 if wl["kind"] == "lap3d" else 2, dims[0], dims[1],
+                           dims[2] if len(dims) > 2 else 1)
+            ms.set_rhs(sysm["b"])
+            ms.bench_prepare(args.warmup)
+            mf_ms = ms.bench_run(args.steps, graph=True)[0]
+            _, mf_spmv = ms.bench_run(min(args.steps, 50), graph=False, spmv_events=True)
+        mf = dict(value=round(args.steps / (mf_ms * 1e-3), 2), unit="it/s",
+                  spmv_us=round(mf_spmv * 1e3, 2),
+                  note="matrix-free 7/5-point stencil SpMV (cgx_solver_set_stencil): "
+                       "not the CSR path, an upper bound for it")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(sysm, args.cpu_seconds)
@@ -272,7 +289,7 @@ def main():
         upload_ms=round(upload_ms, 1),
         iter_bytes=int(info["iter_bytes"]),
         iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),
-        roofline=roofline, cpu_baseline=cpu,
+        roofline=roofline, cpu_baseline=cpu, matrix_free_upper_bound=mf,
     )
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -89,6 +89,14 @@ _SIGS = {
                                              _i32p, _i32p, _f64p]),
     "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                                  _i32p, _i32p, _f32p]),
+    "cgx_solver_gen_laplacian": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int]),
+    "cgx_solver_set_stencil": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int]),
+    "cgx_solver_get_matrix": (ctypes.c_int, [_vp, _i32p, _i32p, _f64p]),
+    "cgx_laplacian_row_ptr": (ctypes.c_longlong, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  _i32p]),
     "cgx_solver_set_rhs": (ctypes.c_int, [_vp, _f64p]),
     "cgx_solver_set_rhs_f32": (ctypes.c_int, [_vp, _f32p]),
     "cgx_solver_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
@@ -222,6 +230,17 @@ def stream_bench(device, n, reps=10, kind=CGX_STREAM_TRIAD):
     return g.value
 
 
+def laplacian_row_ptr(dim, nx, ny, nz=1, row_begin=0, row_end=None):
+    """Closed-form row_ptr of Laplacian rows [row_begin, row_end) (host)."""
+    n = nx * ny * (nz if dim == 3 else 1)
+    row_end = n if row_end is None else row_end
+    rp = np.empty(row_end - row_begin + 1, np.int32)
+    nnz = lib().cgx_laplacian_row_ptr(dim, nx, ny, nz, row_begin, row_end, _p(rp, _i32p))
+    if nnz < 0:
+        raise CgxError(f"laplacian_row_ptr failed ({nnz})")
+    return rp
+
+
 def laplacian3d(nx, ny, nz, row_begin=0, row_end=None):
     row_end = nx * ny * nz if row_end is None else row_end
     return _gen("cgx_gen_laplacian3d", (nx, ny, nz, row_begin, row_end),
@@ -272,6 +291,29 @@ class Solver:
 
     def set_mode(self, mode, alg=CGX_ALG_HS):
         check(lib().cgx_solver_set_mode(self._h, mode, alg), "set_mode")
+
+    def gen_laplacian(self, dim, nx, ny, nz=1):
+        """Laplacian CSR generated in device memory (cgx_solver_gen_laplacian)."""
+        check(lib().cgx_solver_gen_laplacian(self._h, dim, nx, ny, nz), "gen_laplacian")
+        self.f32 = False
+        self.n = nx * ny * (nz if dim == 3 else 1)
+
+    def set_stencil(self, dim, nx, ny, nz=1):
+        """Matrix-free Laplacian operator (cgx_solver_set_stencil)."""
+        check(lib().cgx_solver_set_stencil(self._h, dim, nx, ny, nz), "set_stencil")
+        self.f32 = False
+        self.n = nx * ny * (nz if dim == 3 else 1)
+
+    def matrix(self):
+        """The device CSR as numpy arrays (row_ptr, col, val); fp64 plain CSR."""
+        i = self.info()
+        n, nnz = i["n"], i["nnz"]
+        rp = np.empty(n + 1, np.int32)
+        col = np.empty(max(nnz, 1), np.int32)
+        val = np.empty(max(nnz, 1), np.float64)
+        check(lib().cgx_solver_get_matrix(self._h, _p(rp, _i32p), _p(col, _i32p),
+                                          _p(val, _f64p)), "get_matrix")
+        return rp, col[:nnz], val[:nnz]
 
     def set_matrix(self, rp, col, val):
         rp = np.ascontiguousarray(rp, np.int32)

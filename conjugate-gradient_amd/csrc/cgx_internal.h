@@ -172,6 +172,39 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
                         int grid, hipStream_t st);
 hipError_t launch_stream_read(long long n2, const double *b, double *sink, int grid,
                               hipStream_t st);
+// ---------------------------------------------------- Laplacian operators
+// The 5-point 2-D (dim 2, nz = 1, diagonal 4) and 7-point 3-D (dim 3,
+// diagonal 6) Laplacians of cgx_gen.cpp, natural ordering, -1 off-diagonals.
+struct LapSpec {
+  int dim, nx, ny, nz;
+};
+
+// Entries in rows [0, i): (2 dim + 1) i minus the missing neighbours of the
+// boundary rows, counted per face in closed form (O(1), host and device).
+__host__ __device__ inline long long lap_rp(long long i, const LapSpec &g) {
+  const long long nx = g.nx, ny = g.ny, pl = nx * ny;
+  long long miss = (i + nx - 1) / nx + i / nx;  // x == 0, x == nx-1
+  if (g.dim == 3) {
+    const long long f = i / pl, rem = i % pl;
+    miss += f * nx + (rem < nx ? rem : nx);                        // y == 0
+    miss += f * nx + (rem > (ny - 1) * nx ? rem - (ny - 1) * nx : 0);  // y == ny-1
+    miss += i < pl ? i : pl;                                       // z == 0
+    const long long top = ((long long)g.nz - 1) * pl;
+    miss += i > top ? i - top : 0;                                 // z == nz-1
+  } else {
+    miss += i < nx ? i : nx;                                       // y == 0
+    const long long top = (ny - 1) * nx;
+    miss += i > top ? i - top : 0;                                 // y == ny-1
+  }
+  return (2LL * g.dim + 1) * i - miss;
+}
+
+hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
+                                hipStream_t st);
+template <typename T>
+hipError_t launch_stencil(const LapSpec &g, int n, const T *x, T *y, double *part,
+                          const int *done, int grid, hipStream_t st);
+
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st);

@@ -15,6 +15,7 @@
 // twice to stay bit-identical.
 #include <hip/hip_runtime.h>
 #include <type_traits>
+#include <algorithm>
 
 #include "cgx_internal.h"
 
@@ -1910,6 +1911,86 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
   return hipGetLastError();
 }
 
+// ------------------------------------------- on-device Laplacian
+// CSR of the whole grid written straight into HBM: row r's entries at
+// lap_rp(r), columns ascending -- cgx_gen_laplacian2d/3d bit for bit.
+__global__ __launch_bounds__(256) void k_gen_laplacian(LapSpec g, int n, int *__restrict__ col,
+                                                       double *__restrict__ val) {
+  const int nx = g.nx, ny = g.ny, pl = g.nx * g.ny;
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < n; r += gridDim.x * 256) {
+    long long k = lap_rp(r, g);
+    const int i = r % nx, j = (r / nx) % ny, l = r / pl;
+    auto put = [&](int c, double v) {
+      col[k] = c;
+      val[k] = v;
+      ++k;
+    };
+    if (g.dim == 3 && l > 0) put(r - pl, -1.0);
+    if (j > 0) put(r - nx, -1.0);
+    if (i > 0) put(r - 1, -1.0);
+    put(r, g.dim == 3 ? 6.0 : 4.0);
+    if (i < nx - 1) put(r + 1, -1.0);
+    if (j < ny - 1) put(r + nx, -1.0);
+    if (g.dim == 3 && l < g.nz - 1) put(r + pl, -1.0);
+  }
+}
+
+hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
+                                hipStream_t st) {
+  const int grid = std::max(1, std::min((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_gen_laplacian, dim3(grid), dim3(256), 0, st, g, n, col, val);
+  return hipGetLastError();
+}
+
+// Matrix-free SpMV of the same operator: row r sums its products in the CSR
+// row's column order from 0 with the same values (-1 products are exact), so
+// y is bit-identical to the CSR SpMV.  Only x (once, coalesced along rows)
+// and y move: the upper bound SURVEY.md 8f asks for beside the CSR runs.
+template <typename T, bool EPI>
+__global__ __launch_bounds__(256) void k_stencil(LapSpec g, int n, const T *__restrict__ x,
+                                                 T *__restrict__ y, double *__restrict__ part,
+                                                 const int *done) {
+  __shared__ double red[256 / kWave];
+  if (done && *done) return;
+  const int nx = g.nx, ny = g.ny, pl = g.nx * g.ny;
+  const T m1 = T(-1), dg = T(g.dim == 3 ? 6 : 4);
+  double dot = 0.0;
+  // one row per thread: XCD-contiguous workgroup order, so each XCD sweeps a
+  // contiguous slab and the +-plane x lines stay in its L2
+  const bool once = (long long)gridDim.x * 256 >= n;
+  const int b0 = once ? xcd_block(1) : blockIdx.x;
+  for (int r = b0 * 256 + threadIdx.x; r < n; r += gridDim.x * 256) {
+    const int i = r % nx, j = (r / nx) % ny, l = r / pl;
+    T acc = T(0);
+    if (g.dim == 3 && l > 0) acc = acc + m1 * x[r - pl];
+    if (j > 0) acc = acc + m1 * x[r - nx];
+    if (i > 0) acc = acc + m1 * x[r - 1];
+    const T xr = x[r];
+    acc = acc + dg * xr;
+    if (i < nx - 1) acc = acc + m1 * x[r + 1];
+    if (j < ny - 1) acc = acc + m1 * x[r + nx];
+    if (g.dim == 3 && l < g.nz - 1) acc = acc + m1 * x[r + pl];
+    y[r] = acc;
+    if (EPI) dot = dot + (double)xr * (double)acc;
+  }
+  if (EPI) {
+    const double sum = block_sum<256>(dot, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = sum;
+  }
+}
+
+template <typename T>
+hipError_t launch_stencil(const LapSpec &g, int n, const T *x, T *y, double *part,
+                          const int *done, int grid, hipStream_t st) {
+  if (part)
+    hipLaunchKernelGGL((k_stencil<T, true>), dim3(grid), dim3(256), 0, st, g, n, x, y, part,
+                       done);
+  else
+    hipLaunchKernelGGL((k_stencil<T, false>), dim3(grid), dim3(256), 0, st, g, n, x, y,
+                       part, done);
+  return hipGetLastError();
+}
+
 #define CGX_INSTANTIATE(T)                                                     \
   template hipError_t launch_spmv<T>(const SpmvArgs<T> &, int, int,           \
                                      hipStream_t);                             \
@@ -1928,6 +2009,9 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
                                          double *, int, hipStream_t);          \
   template hipError_t launch_xpay_x<T>(int, T *, T *, const T *,              \
                                        const CgState *, int, hipStream_t);     \
+  template hipError_t launch_stencil<T>(const LapSpec &, int, const T *, T *, \
+                                        double *, const int *, int,            \
+                                        hipStream_t);                          \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *,     \
                                           const double *, int, double *, int,  \
                                           hipStream_t);                        \

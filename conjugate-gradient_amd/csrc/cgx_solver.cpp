@@ -193,6 +193,9 @@ struct cgx_solver {
   int npanel = 1;
   std::vector<int> panel_off, panel_nblk, panel_grid;
   bool panel_win512 = false;  // fp32 panels: 512-entry LDS windows
+  // matrix-free Laplacian (cgx_solver_set_stencil): no CSR arrays at all
+  bool is_stencil = false;
+  cgx::LapSpec lap{};
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
@@ -283,6 +286,7 @@ void free_matrix(cgx_solver *s) {
   s->hist_alloc = 0;
   s->dev_bytes = 0;
   s->have_matrix = s->have_rhs = s->bench_ready = false;
+  s->is_stencil = false;
   s->n = s->nnz = s->nblk = 0;
 }
 
@@ -310,8 +314,10 @@ int check_device(int device) {
 
 template <typename T>
 int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
-                  const T *val) {
-  if (n < 0 || nnz < 0 || (n > 0 && (!rp || (nnz > 0 && (!col || !val))))) {
+                  const T *val, const LapSpec *gen = nullptr) {
+  // gen: col/val are generated on the device (cgx_solver_gen_laplacian);
+  // rp is the host closed form, used for the row-block plan and uploaded
+  if (n < 0 || nnz < 0 || (n > 0 && (!rp || (nnz > 0 && !gen && (!col || !val))))) {
     set_error("set_matrix: invalid arguments");
     return CGX_EINVAL;
   }
@@ -329,7 +335,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   std::vector<int> blk, blkk;
   std::vector<int> prp, pcol;
   std::vector<T> pval;
-  s->npanel = choose_panels(n, rp, col, sizeof(T));
+  s->npanel = gen ? 1 : choose_panels(n, rp, col, sizeof(T));
   s->panel_win512 = sizeof(T) == 4 && env_int("CGX_PANEL_WIN512", 0) != 0;
   s->panel_off.clear();
   s->panel_nblk.clear();
@@ -408,7 +414,9 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   CGX_HIP(hipMemsetAsync(s->d_val, 0, nnz_pad * sizeof(T), s->stream));
   if (n > 0) {
     CGX_HIP(hipMemcpyAsync(s->d_rp, rp, rp_len * 4, hipMemcpyHostToDevice, s->stream));
-    if (nnz > 0) {
+    if (nnz > 0 && gen) {
+      CGX_HIP(launch_gen_laplacian(*gen, n, s->d_col, (double *)s->d_val, s->stream));
+    } else if (nnz > 0) {
       CGX_HIP(hipMemcpyAsync(s->d_col, col, (size_t)nnz * 4,
                              hipMemcpyHostToDevice, s->stream));
       CGX_HIP(hipMemcpyAsync(s->d_val, val, (size_t)nnz * sizeof(T),
@@ -420,7 +428,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   CGX_HIP(hipMemcpyAsync(s->d_blkk, blkk.data(), blkk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
-  if (s->want_sell && n > 0 && s->npanel == 1) {
+  if (s->want_sell && n > 0 && s->npanel == 1 && !gen) {
     std::vector<int> soff, slen, scol;
     std::vector<T> sval;
     if (csr_to_sell64<T>(n, rp, col, val, 1.25, soff, slen, sval, scol)) {
@@ -449,6 +457,53 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       }
     }
   }
+  s->have_matrix = true;
+  return 0;
+}
+
+// Matrix-free Laplacian: vectors and partial buffers only.
+int set_stencil(cgx_solver *s, const LapSpec &g) {
+  const long long n = (long long)g.nx * g.ny * g.nz;
+  if ((g.dim != 2 && g.dim != 3) || g.nx < 1 || g.ny < 1 || g.nz < 1 ||
+      (g.dim == 2 && g.nz != 1) || n > INT32_MAX || lap_rp(n, g) > INT32_MAX) {
+    set_error("set_stencil: bad grid");
+    return CGX_EINVAL;
+  }
+  CGX_HIP(hipSetDevice(s->device));
+  free_matrix(s);
+  s->dtype = CGX_F64;
+  s->n = (int)n;
+  s->nnz = (int)lap_rp(n, g);
+  s->npanel = 1;
+  s->panel_off.clear();
+  s->panel_nblk.clear();
+  s->panel_grid.clear();
+  const size_t nv = (size_t)n + kPad;
+  // one row per thread: the stencil's 7 loads per row are latency-bound, so
+  // every row gets its own lane (grid-stride at cus*16 WGs ran at 2.3 TB/s)
+  s->spmv_grid = (int)std::max<long long>(
+      1, std::min<long long>((n + 255) / 256, env_int("CGX_STENCIL_GRID", INT_MAX)));
+  s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for((int)n, s->cus));
+  s->vec_grid = (std::max(s->vec_grid, 1) + 3) / 4 * 4;
+  s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
+  const size_t ngmax = (size_t)s->part_cap / kTicketGroup + 2;
+  int rc;
+  if ((rc = dalloc(s, &s->d_b, nv * 8)) || (rc = dalloc(s, &s->d_x, nv * 8)) ||
+      (rc = dalloc(s, &s->d_r, nv * 8)) || (rc = dalloc(s, &s->d_p, nv * 8)) ||
+      (rc = dalloc(s, &s->d_s, nv * 8)) || (rc = dalloc(s, &s->d_w, nv * 8)) ||
+      (rc = dalloc(s, &s->d_p2, nv * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_pa, (size_t)s->part_cap * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_pb, (size_t)s->part_cap * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_tpart2, ngmax * 8)) ||
+      (rc = dalloc(s, (void **)&s->d_tcnt, (ngmax + 1) * 4))) {
+    free_matrix(s);
+    return rc;
+  }
+  CGX_HIP(hipMemsetAsync(s->d_tcnt, 0, (ngmax + 1) * 4, s->stream));
+  CGX_HIP(hipStreamSynchronize(s->stream));
+  s->ngmax = (int)ngmax;
+  s->is_stencil = true;
+  s->lap = g;
   s->have_matrix = true;
   return 0;
 }
@@ -512,6 +567,8 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
 // (rows continue their sums from y; the epilogue partials on the last panel).
 template <typename T>
 hipError_t launch_spmv_s(cgx_solver *s, SpmvArgs<T> a, hipStream_t st) {
+  if (s->is_stencil)
+    return launch_stencil<T>(s->lap, s->n, a.x, a.y, a.part, a.done, s->spmv_grid, st);
   if (s->npanel <= 1) return launch_spmv<T>(a, s->spmv_grid, s->vec, st);
   double *part = a.part;
   for (int q = 0; q < s->npanel; ++q) {
@@ -543,13 +600,14 @@ TicketArgs ticket_args(cgx_solver *s, int op) {
 
 bool use_ticket(const cgx_solver *s) {
   return s->ticket && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST &&
-         (s->spmv_bs == 64 || s->sell) && s->npanel == 1;
+         (s->spmv_bs == 64 || s->sell) && s->npanel == 1 && !s->is_stencil;
 }
 
 bool fused(const cgx_solver *s) {
   return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
          s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1 &&
-         !(s->spmv_dma == 1 && s->spmv_wpb == 8);  // no fused variant at 8 waves
+         !(s->spmv_dma == 1 && s->spmv_wpb == 8) &&  // no fused variant at 8 waves
+         !s->is_stencil;
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -996,6 +1054,56 @@ int cgx_solver_set_matrix_f32(cgx_solver *s, int n, int nnz,
   return upload_matrix<float>(s, n, nnz, row_ptr, col, val);
 }
 
+long long cgx_laplacian_row_ptr(int dim, int nx, int ny, int nz, int row_begin,
+                                int row_end, int *row_ptr) {
+  const LapSpec g{dim, nx, ny, dim == 3 ? nz : 1};
+  const long long n = (long long)nx * ny * g.nz;
+  if ((dim != 2 && dim != 3) || nx < 1 || ny < 1 || g.nz < 1 || n > INT32_MAX ||
+      row_begin < 0 || row_end < row_begin || row_end > n)
+    return CGX_EINVAL;
+  const long long base = lap_rp(row_begin, g);
+  if (row_ptr)
+    for (long long i = row_begin; i <= row_end; ++i)
+      row_ptr[i - row_begin] = (int)(lap_rp(i, g) - base);
+  return lap_rp(row_end, g) - base;
+}
+
+int cgx_solver_gen_laplacian(cgx_solver *s, int dim, int nx, int ny, int nz) {
+  if (!s) return CGX_EINVAL;
+  const LapSpec g{dim, nx, ny, dim == 3 ? nz : 1};
+  const long long n = (long long)nx * ny * g.nz;
+  if ((dim != 2 && dim != 3) || nx < 1 || ny < 1 || g.nz < 1 || n > INT32_MAX ||
+      lap_rp(n, g) > INT32_MAX) {
+    set_error("gen_laplacian: bad grid");
+    return CGX_EINVAL;
+  }
+  std::vector<int> rp((size_t)n + 1);
+  for (long long i = 0; i <= n; ++i) rp[(size_t)i] = (int)lap_rp(i, g);
+  return upload_matrix<double>(s, (int)n, rp[(size_t)n], rp.data(), nullptr, nullptr, &g);
+}
+
+int cgx_solver_set_stencil(cgx_solver *s, int dim, int nx, int ny, int nz) {
+  if (!s) return CGX_EINVAL;
+  return set_stencil(s, LapSpec{dim, nx, ny, dim == 3 ? nz : 1});
+}
+
+int cgx_solver_get_matrix(cgx_solver *s, int *row_ptr, int *col, double *val) {
+  if (!s || !s->have_matrix || s->is_stencil || s->sell || s->npanel > 1 ||
+      s->dtype != CGX_F64 || (s->n > 0 && (!row_ptr || (s->nnz > 0 && (!col || !val))))) {
+    set_error("get_matrix: needs an fp64 plain-CSR matrix and output arrays");
+    return CGX_EINVAL;
+  }
+  CGX_HIP(hipSetDevice(s->device));
+  if (s->n > 0) {
+    CGX_HIP(hipMemcpy(row_ptr, s->d_rp, ((size_t)s->n + 1) * 4, hipMemcpyDeviceToHost));
+    if (s->nnz > 0) {
+      CGX_HIP(hipMemcpy(col, s->d_col, (size_t)s->nnz * 4, hipMemcpyDeviceToHost));
+      CGX_HIP(hipMemcpy(val, s->d_val, (size_t)s->nnz * 8, hipMemcpyDeviceToHost));
+    }
+  }
+  return 0;
+}
+
 int cgx_solver_set_rhs(cgx_solver *s, const double *b) {
   return s ? upload_rhs<double>(s, b) : CGX_EINVAL;
 }
@@ -1075,6 +1183,8 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                             2.0 * s->n * sv;
   else
     info->spmv_iter_bytes = info->spmv_bytes;
+  if (s->is_stencil)  // matrix-free: x read once, y written once
+    info->spmv_iter_bytes = 2.0 * s->n * sv;
   if (s->npanel > 1)  // the panel passes' own bytes: P row_ptrs, y written P x, read P-1 x
     info->spmv_iter_bytes = (double)s->nnz * (sv + 4) + 4.0 * s->npanel * (s->n + 1.0) +
                             (double)s->n * sv * (1.0 + 2.0 * s->npanel - 1.0);

@@ -99,6 +99,23 @@ int  cgx_solver_set_matrix(cgx_solver *s, int n, int nnz, const int *row_ptr,
 int  cgx_solver_set_matrix_f32(cgx_solver *s, int n, int nnz,
                                const int *row_ptr, const int *col,
                                const float *val);
+
+/* SURVEY.md 8f, on-device generators and the matrix-free stencil.  The
+ * 5-point 2-D (dim 2; nz ignored) / 7-point 3-D Laplacian of an nx*ny*nz
+ * grid, natural ordering -- the matrix of cgx_gen_laplacian2d/3d:
+ *   gen_laplacian  fp64 CSR written straight into device memory (no host
+ *                  arrays, no PCIe copy of col/val); row_ptr in closed form
+ *   set_stencil    matrix-free operator: same rows, same column order, same
+ *                  products, so the SpMV is bit-identical to the CSR one and
+ *                  its CG an upper bound for the CSR runs (x and y only)
+ *   get_matrix     the device CSR back to host arrays (plain fp64 CSR only)
+ *   cgx_laplacian_row_ptr  the closed-form row_ptr of rows [row_begin,
+ *                  row_end) (host; returns their nnz, or < 0) */
+int  cgx_solver_gen_laplacian(cgx_solver *s, int dim, int nx, int ny, int nz);
+int  cgx_solver_set_stencil(cgx_solver *s, int dim, int nx, int ny, int nz);
+int  cgx_solver_get_matrix(cgx_solver *s, int *row_ptr, int *col, double *val);
+long long cgx_laplacian_row_ptr(int dim, int nx, int ny, int nz, int row_begin,
+                                int row_end, int *row_ptr);
 /* Right-hand side, length n, in the matrix's dtype. */
 int  cgx_solver_set_rhs(cgx_solver *s, const double *b);
 int  cgx_solver_set_rhs_f32(cgx_solver *s, const float *b);

@@ -173,3 +173,29 @@ def test_gen_random_spd_properties():
 def test_chained_flag_matches_fixture(name):
     g = H.load_golden(name)
     assert cgx.is_chained(g["row_ptr"], g["col"]) == g["chained"]
+
+
+@pytest.mark.parametrize("dim,shape", [(3, (1, 1, 1)), (3, (4, 3, 2)), (3, (12, 12, 12)),
+                                       (3, (7, 5, 9)), (3, (1, 6, 4)), (3, (5, 1, 3)),
+                                       (2, (1, 1, 1)), (2, (5, 3, 1)), (2, (32, 32, 1)),
+                                       (2, (1, 9, 1)), (2, (17, 9, 1))])
+def test_laplacian_row_ptr_closed_form(dim, shape):
+    """The closed-form row_ptr the on-device generator and the stencil use
+    equals the host generator's, for whole grids and for row ranges."""
+    nx, ny, nz = shape
+    n = nx * ny * nz
+    if dim == 3:
+        rp, _, _ = cgx.laplacian3d(nx, ny, nz)
+    else:
+        rp, _, _ = cgx.laplacian2d(nx, ny)
+    assert np.array_equal(cgx.laplacian_row_ptr(dim, nx, ny, nz), rp)
+    for rb, re_ in [(0, n), (n // 3, n), (n // 5, (4 * n) // 5), (n, n)]:
+        sub = cgx.laplacian_row_ptr(dim, nx, ny, nz, rb, re_)
+        assert np.array_equal(sub, rp[rb:re_ + 1] - rp[rb])
+
+
+def test_laplacian_row_ptr_c4_total():
+    """C4 (400^3): the closed form's nnz is SURVEY.md's 447,040,000."""
+    nnz = cgx.lib().cgx_laplacian_row_ptr(3, 400, 400, 400, 0, 64_000_000, None)
+    assert nnz == 447_040_000
+    assert cgx.lib().cgx_laplacian_row_ptr(3, 216, 216, 216, 0, 216 ** 3, None) == 70_263_936

@@ -586,3 +586,52 @@ def test_column_panels_auto_c5():
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         assert s.info()["n_panels"] == 1
+
+
+@pytest.mark.parametrize("dim,shape", [(3, (12, 12, 12)), (3, (7, 5, 9)), (3, (1, 6, 4)),
+                                       (2, (32, 32, 1)), (2, (17, 9, 1)), (3, (216, 216, 216))])
+def test_device_generated_laplacian_bit_exact(dim, shape):
+    """the Laplacian generated in device memory is the host
+    generator's CSR bit for bit (C3 at full size included), and solves alike."""
+    nx, ny, nz = shape
+    host = cgx.laplacian3d(nx, ny, nz) if dim == 3 else cgx.laplacian2d(nx, ny)
+    with cgx.Solver(0) as s:
+        s.gen_laplacian(dim, nx, ny, nz)
+        rp, col, val = s.matrix()
+        assert np.array_equal(rp, host[0]) and np.array_equal(col, host[1])
+        assert H.same_bits_or_both_nan(val, host[2])
+        if len(rp) - 1 <= 2000:
+            b = np.random.default_rng(4).standard_normal(len(rp) - 1)
+            s.set_rhs(b)
+            s.run(25)
+            x_ref, _ = H.o_conj_grad(25, *host, b)
+            assert rel(s.x(), x_ref) <= FAST_RTOL
+
+
+@pytest.mark.parametrize("dim,shape", [(3, (12, 12, 12)), (3, (7, 5, 9)), (3, (1, 6, 4)),
+                                       (2, (32, 32, 1)), (2, (17, 9, 1)), (3, (216, 216, 216))])
+def test_matrix_free_stencil_bit_exact(dim, shape):
+    """the matrix-free stencil SpMV is bit-identical to the CSR
+    SpMV of the same Laplacian (same column order, same products), and its
+    CG matches the oracle within FAST_RTOL and stops at the same iteration."""
+    nx, ny, nz = shape
+    rp, col, val = cgx.laplacian3d(nx, ny, nz) if dim == 3 else cgx.laplacian2d(nx, ny)
+    n = len(rp) - 1
+    x = np.random.default_rng(5).standard_normal(n)
+    with cgx.Solver(0) as s:
+        s.set_stencil(dim, nx, ny, nz)
+        assert s.info()["nnz"] == len(col)
+        y = s.spmv(x)
+    assert H.same_bits_or_both_nan(y, H.o_spmv(rp, col, val, x))
+    if n <= 2000:
+        b = np.random.default_rng(6).standard_normal(n)
+        with cgx.Solver(0) as s:
+            s.set_stencil(dim, nx, ny, nz)
+            s.set_rhs(b)
+            s.run(25)
+            x_ref, _ = H.o_conj_grad(25, rp, col, val, b)
+            assert rel(s.x(), x_ref) <= FAST_RTOL
+            s.set_rhs(b)
+            its = s.run(3000, 1e-10)
+        _, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+        assert abs(its - its_o) <= 1
