@@ -133,6 +133,34 @@ def cpu_baseline_mt(sysm, budget_s):
                        f"(oracle_solve_mt), {dt:.1f} s")
 
 
+def reference_c1(budget_s=2.0):
+    """SURVEY.md 8d leg (a): the reference ITSELF (oracle/_ref/ref_harness =
+    the reference's cg.c + mv_ops.c at its Makefile flags, built by
+    `make -C oracle ref`) timing conj_grad on C1, the dense 128 SPD system --
+    the one configuration where its O(n^2) dense-row SpMV is feasible.
+    Returns None when the binary was not built (no /root/reference)."""
+    import subprocess
+    import tempfile
+    import helpers as H
+    exe = REPO / "oracle" / "_ref" / "ref_harness"
+    if not exe.exists():
+        return None
+    rp, col, val, b = H.dense_spd(128, seed=1)
+    maxit = 11  # ~tol 1e-10 on C1 (SURVEY.md 8d); conj_grad does maxit+1 SpMVs
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "c1.txt"
+        H.write_ref_format(f, rp, col, val, b)
+        probe = float(subprocess.run([str(exe), "time", str(f), str(maxit), "20"],
+                                     capture_output=True, text=True, timeout=60).stdout)
+        reps = max(20, int(budget_s / max(probe, 1e-6)))
+        sec = float(subprocess.run([str(exe), "time", str(f), str(maxit), str(reps)],
+                                   capture_output=True, text=True, timeout=120).stdout)
+    return dict(value=(maxit + 1) / sec, unit="it/s", cores=1, kind="reference",
+                sample=f"C1 dense 128 SPD, conj_grad({maxit}) x {reps} in one process: "
+                       f"{sec * 1e6:.1f} us per call, {maxit + 1} x-updates each "
+                       f"(oracle/_ref/ref_harness, the reference's own sources and flags)")
+
+
 def cpu_baseline(sysm, budget_s):
     """The oracle's CSR-sequential HS-CG (bit-exact to the reference on chained
     matrices) on ONE host core, on the same matrix, for as many iterations as
@@ -274,6 +302,7 @@ def main():
         cpu["cpu_model"] = cpu_model()
         cpu["nproc"] = os.cpu_count()
         cpu["all_cores"] = cpu_baseline_mt(sysm, args.cpu_seconds / 2)
+        cpu["reference_c1"] = reference_c1()
 
     value = (args.steps / wall) * world  # weak scaling: slab-iterations/s
     out = dict(
