@@ -602,7 +602,9 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
   // NT: the once-per-iteration matrix stream is loaded non-temporal (aux = 2)
   // so it does not displace the CG vectors from the Infinity Cache.
   constexpr int AUX = NT ? 2 : 0;
-  static_assert((CAPW * sizeof(T)) % 1024 == 0 && (CAPW * 4) % 1024 == 0, "window");
+  // CAPW entries per wave window; need not fill whole 1 KiB DMA rows (the
+  // lanes past it are masked), only keep every region 16-B aligned
+  static_assert(CAPW % 4 == 0, "window");
   __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
   __shared__ double red[WPB];
@@ -632,15 +634,16 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
       // the second read
       constexpr int EV = 16 / sizeof(T);  // elements of T per lane per DMA
       const int m = k1 - kb;
+      const int mm = EXACT ? m : CAPW;
 #pragma unroll
-      for (int i = 0; i < (int)(CAPW * sizeof(T) / 1024); ++i)
-        if (!EXACT || (i * kWave * EV < m && (i * kWave + lane) * EV < m))
+      for (int i = 0; i < (int)((CAPW * sizeof(T) + 1023) / 1024); ++i)
+        if (i * kWave * EV < mm && (i * kWave + lane) * EV < mm)
           __builtin_amdgcn_global_load_lds(
               (const void *)(a.val + kb + i * kWave * EV + lane * EV),
               (lds_void *)(lval + i * kWave * EV), 16, 0, AUX);
 #pragma unroll
-      for (int i = 0; i < CAPW * 4 / 1024; ++i)
-        if (!EXACT || (i * kWave * 4 < m && (i * kWave + lane) * 4 < m))
+      for (int i = 0; i < (CAPW * 4 + 1023) / 1024; ++i)
+        if (i * kWave * 4 < mm && (i * kWave + lane) * 4 < mm)
           __builtin_amdgcn_global_load_lds(
               (const void *)(a.col + kb + i * kWave * 4 + lane * 4),
               (lds_void *)(lcol + i * kWave * 4), 16, 0, AUX);
@@ -1707,6 +1710,18 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
   if (a.bs == 64 && a.dma == 1 && a.wpb == 8 && !a.x2) {  // 8 waves: half the partials
     constexpr int WPB = 8;
     constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;
+    const int g = (a.nblk + WPB - 1) / WPB;
+    const bool epi = a.part != nullptr;
+    if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    return hipGetLastError();
+  }
+  if (a.bs == 64 && a.dma == 1 && a.capw == 456 && sizeof(T) == 8 && !a.x2) {
+    // 456-entry windows (a 7-point block's 448 + alignment): 5.3 KiB of LDS
+    // per wave, 7 workgroups per CU instead of 6
+    constexpr int WPB = 4, CAPW = 456;
     const int g = (a.nblk + WPB - 1) / WPB;
     const bool epi = a.part != nullptr;
     if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);

@@ -193,6 +193,7 @@ struct cgx_solver {
   int npanel = 1;
   std::vector<int> panel_off, panel_nblk, panel_grid;
   bool panel_win512 = false;  // fp32 panels: 512-entry LDS windows
+  int spmv_capw = 0;           // CGX_SPMV_CAPW: fp64 LDS-DMA window (456 or 512)
   // matrix-free Laplacian (cgx_solver_set_stencil): no CSR arrays at all
   bool is_stencil = false;
   cgx::LapSpec lap{};
@@ -331,7 +332,13 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   s->n = n;
   s->nnz = nnz;
   const bool half = s->spmv_dma == 4 && s->spmv_bs == 64;  // 32-row blocks
-  const int cap = half ? spmv_cap(32, sizeof(T) == 8) : spmv_cap(s->spmv_bs, sizeof(T) == 8);
+  int cap = half ? spmv_cap(32, sizeof(T) == 8) : spmv_cap(s->spmv_bs, sizeof(T) == 8);
+  s->spmv_capw = 0;
+  if (sizeof(T) == 8 && s->spmv_dma == 1 && s->spmv_bs == 64 && s->spmv_wpb == 4 &&
+      env_int("CGX_SPMV_CAPW", 512) == 456) {
+    s->spmv_capw = 456;
+    cap = 456;
+  }
   std::vector<int> blk, blkk;
   std::vector<int> prp, pcol;
   std::vector<T> pval;
@@ -375,8 +382,11 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   int rc;
   if ((rc = dalloc(s, (void **)&s->d_rp, rp_len * 4)) ||
       (rc = dalloc(s, (void **)&s->d_col, nnz_pad * 4)) ||
-      (rc = dalloc(s, &s->d_val, nnz_pad * sizeof(T))) ||
-      (rc = dalloc(s, (void **)&s->d_blk, blk.size() * 4)) ||
+      (rc = dalloc(s, &s->d_val, nnz_pad * sizeof(T)))) {
+    free_matrix(s);
+    return rc;
+  }
+  if ((rc = dalloc(s, (void **)&s->d_blk, blk.size() * 4)) ||
       (rc = dalloc(s, (void **)&s->d_blkk, blk.size() * 4)) ||
       (rc = dalloc(s, &s->d_b, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_x, nv * sizeof(T))) ||
@@ -410,6 +420,9 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   }
   CGX_HIP(hipMemsetAsync(s->d_tcnt, 0, (ngmax + 1) * 4, s->stream));
   s->ngmax = (int)ngmax;
+  if (env_int("CGX_DEBUG_PTRS", 0))
+    fprintf(stderr, "cgx ptrs rp %p col %p val %p x(p) %p y(s) %p r %p\n", (void *)s->d_rp,
+            (void *)s->d_col, s->d_val, s->d_p, s->d_s, s->d_r);
   CGX_HIP(hipMemsetAsync(s->d_col, 0, nnz_pad * 4, s->stream));
   CGX_HIP(hipMemsetAsync(s->d_val, 0, nnz_pad * sizeof(T), s->stream));
   if (n > 0) {
@@ -560,6 +573,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.n = s->n;
   a.dma = s->spmv_dma;
   a.yacc = nullptr;
+  a.capw = s->spmv_capw;
   return a;
 }
 
@@ -579,6 +593,7 @@ hipError_t launch_spmv_s(cgx_solver *s, SpmvArgs<T> a, hipStream_t st) {
     b.yacc = q ? a.y : nullptr;
     b.part = q + 1 == s->npanel ? part : nullptr;
     b.dma = s->panel_win512 ? 4 : 1;  // dma 4: fp32 CAPW 512
+    b.capw = 0;                       // panel plans use the default windows
     b.bs = 64;
     const hipError_t e = launch_spmv<T>(b, s->panel_grid[q], s->vec, st);
     if (e != hipSuccess) return e;
@@ -607,6 +622,7 @@ bool fused(const cgx_solver *s) {
   return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
          s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1 &&
          !(s->spmv_dma == 1 && s->spmv_wpb == 8) &&  // no fused variant at 8 waves
+         s->spmv_capw != 456 &&
          !s->is_stencil;
 }
 

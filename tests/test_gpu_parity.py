@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -73,9 +73,11 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
     monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
-    if bs in ("dma", "dma8", "dma32", "dmaw8", "dmaxcd"):
+    if bs in ("dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456"):
         monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4", "dmaw8": "1",
-                                            "dmaxcd": "1"}[bs])
+                                            "dmaxcd": "1", "dma456": "1"}[bs])
+        if bs == "dma456":
+            monkeypatch.setenv("CGX_SPMV_CAPW", "456")
         if bs == "dmaw8":
             monkeypatch.setenv("CGX_SPMV_WPB", "8")
         if bs == "dmaxcd":
@@ -172,13 +174,15 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "8", "1x"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "8", "1x", "1w"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
-    monkeypatch.setenv("CGX_SPMV_DMA", dma.rstrip("x"))
+    monkeypatch.setenv("CGX_SPMV_DMA", dma.rstrip("xw"))
     if dma.endswith("x"):
         monkeypatch.setenv("CGX_SPMV_XCD", "1")
+    if dma.endswith("w"):
+        monkeypatch.setenv("CGX_SPMV_CAPW", "456")
     rp, col, val = cgx.laplacian3d(216, 216, 216)
     x = np.random.default_rng(2).standard_normal(len(rp) - 1)
     with cgx.Solver(0) as s:

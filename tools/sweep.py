@@ -27,6 +27,9 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--alg", default="hs")
 ap.add_argument("--variant", action="append", default=[])
+ap.add_argument("--instances", type=int, default=1,
+                help="solvers per variant (device placement varies by +-5%% between "
+                     "allocations; the report is the median over instances)")
 ap.add_argument("--control", action="store_true",
                 help="append a second copy of the first variant (placement/order control)")
 a = ap.parse_args()
@@ -44,31 +47,36 @@ for v in variants:
         k, _, val = kv.partition("=")
         saved[k] = os.environ.get(k)
         os.environ[k] = val
-    s = cgx.Solver(0, alg=cgx.CGX_ALG_CG1 if a.alg == "cg1" else cgx.CGX_ALG_HS)
-    s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
-    s.set_rhs(sysm["b"])
-    s.bench_prepare(3)
+    for inst in range(a.instances):
+        s = cgx.Solver(0, alg=cgx.CGX_ALG_CG1 if a.alg == "cg1" else cgx.CGX_ALG_HS)
+        s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+        s.set_rhs(sysm["b"])
+        s.bench_prepare(3)
+        solvers.append((name, inst, s))
     for k, old in saved.items():
         if old is None:
             os.environ.pop(k, None)
         else:
             os.environ[k] = old
-    solvers.append((name, s))
-info = solvers[0][1].info()
-infos = {n: s.info() for n, s in solvers}
-res = {n: {"spmv": [], "iter": []} for n, _ in solvers}
+info = solvers[0][2].info()
+infos = {n: s.info() for n, _, s in solvers}
+res = {(n, i): {"spmv": [], "iter": []} for n, i, _ in solvers}
 for r in range(a.rounds):
-    k = r % len(solvers)  # rotate the order so no variant always runs first
-    for name, s in solvers[k:] + solvers[:k]:
+    k = r % len(solvers)  # rotate the order so no solver always runs first
+    for name, inst, s in solvers[k:] + solvers[:k]:
         tot, sp = s.bench_run(a.iters, graph=False, spmv_events=True)
-        res[name]["spmv"].append(sp * 1e3)
+        res[(name, inst)]["spmv"].append(sp * 1e3)
         tot, _ = s.bench_run(a.iters, graph=True)
-        res[name]["iter"].append(tot / a.iters * 1e3)
+        res[(name, inst)]["iter"].append(tot / a.iters * 1e3)
 print(f"workload {a.workload}: n={info['n']} nnz={info['nnz']} spmv_bytes={info['spmv_bytes']:.0f} "
-      f"iter_bytes={info['iter_bytes']:.0f} grid={info['spmv_grid']} rowblocks={info['n_rowblocks']}")
-for name, d in res.items():
-    sm, si = statistics.median(d["spmv"]), statistics.median(d["iter"])
+      f"iter_bytes={info['iter_bytes']:.0f} grid={info['spmv_grid']} rowblocks={info['n_rowblocks']}"
+      f" instances={a.instances}")
+names = list(dict.fromkeys(n for n, _, _ in solvers))
+for name in names:
+    sp = [statistics.median(res[(name, i)]["spmv"]) for i in range(a.instances)]
+    it = [statistics.median(res[(name, i)]["iter"]) for i in range(a.instances)]
+    sm, si = statistics.median(sp), statistics.median(it)
     sb = infos[name]["spmv_iter_bytes"]
-    print(f"{name:>14}: spmv med {sm:8.2f} us min {min(d['spmv']):8.2f}  "
-          f"({sb / sm / 1e3:7.1f} GB/s)   iter med {si:8.2f} us "
-          f"({1e6 / si:7.1f} it/s, {info['iter_bytes'] / si / 1e3:7.1f} GB/s)")
+    spread = f" [{min(sp):.1f}-{max(sp):.1f}]" if a.instances > 1 else ""
+    print(f"{name:>14}: spmv med {sm:8.2f} us{spread} ({sb / sm / 1e3:7.1f} GB/s)   iter med "
+          f"{si:8.2f} us ({1e6 / si:7.1f} it/s, {info['iter_bytes'] / si / 1e3:7.1f} GB/s)")
