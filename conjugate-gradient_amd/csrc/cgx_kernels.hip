@@ -1501,18 +1501,29 @@ __global__ __launch_bounds__(kWave) void k_dot_seq(int n, const T *__restrict__ 
                                                    const T *__restrict__ b,
                                                    double *__restrict__ out,
                                                    const int *__restrict__ done) {
+  // The sum is one dependent add chain (the reference's order, mv_ops.c:
+  // 127-129); the products of the NEXT chunk are loaded while lane 0 adds the
+  // current one, so HBM latency hides behind the chain.
   constexpr int CH = 8 * kWave;
   __shared__ double buf[CH];
   if (done && *done) return;
   const int lane = threadIdx.x;
   double acc = 0.0;
-  for (int base = 0; base < n; base += CH) {
+  T va[8], vb[8];
+  auto load = [&](int base) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = base + j * kWave + lane;
-      buf[j * kWave + lane] = (i < n) ? (double)(a[i] * b[i]) : 0.0;
+      va[j] = i < n ? a[i] : T(0);
+      vb[j] = i < n ? b[i] : T(0);
     }
+  };
+  load(0);
+  for (int base = 0; base < n; base += CH) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) buf[j * kWave + lane] = (double)(va[j] * vb[j]);
     __syncthreads();
+    if (base + CH < n) load(base + CH);  // in flight during the adds below
     if (lane == 0) {
       const int m = min(CH, n - base);
       for (int t = 0; t < m; ++t) acc = acc + buf[t];
@@ -1739,6 +1750,8 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     else if (epi && a.dma == 3 && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true, 4, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi && a.dma == 8 && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true, 8>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi && a.dma == 8) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, false, 8>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (!xp && a.dma == 8 && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true, 8>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    else if (!xp && a.dma == 8) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, false, 8>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     else if (!xp && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);

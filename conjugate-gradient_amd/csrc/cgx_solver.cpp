@@ -592,7 +592,8 @@ hipError_t launch_spmv_s(cgx_solver *s, SpmvArgs<T> a, hipStream_t st) {
     b.nblk = s->panel_nblk[q];
     b.yacc = q ? a.y : nullptr;
     b.part = q + 1 == s->npanel ? part : nullptr;
-    b.dma = s->panel_win512 ? 4 : 1;  // dma 4: fp32 CAPW 512
+    // dma 4: fp32 CAPW 512; dma 8: 8 gathers per row chunk (CGX_PANEL_U8)
+    b.dma = s->panel_win512 ? 4 : (env_int("CGX_PANEL_U8", 0) ? 8 : 1);
     b.capw = 0;                       // panel plans use the default windows
     b.bs = 64;
     const hipError_t e = launch_spmv<T>(b, s->panel_grid[q], s->vec, st);
