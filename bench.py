@@ -213,6 +213,8 @@ def main():
             dist.barrier()
 
     wl = WORKLOADS[args.workload]
+    if world > 1 and wl["kind"] == "rand":
+        raise SystemExit("bench: C5 (random SPD) is a single-GPU configuration (BASELINE.json)")
     alg = args.alg or ("cg1-dist" if world > 1 else "hs")
     sysm = make_system(wl, rank, world)
 
@@ -304,14 +306,18 @@ def main():
         cpu["all_cores"] = cpu_baseline_mt(sysm, args.cpu_seconds / 2)
         cpu["reference_c1"] = reference_c1()
 
-    value = (args.steps / wall) * world  # weak scaling: slab-iterations/s
+    # weak scaling (default): every rank owns one slab, value = slab-iterations/s
+    # summed over ranks; strong (c4): one system over all ranks, value = its it/s
+    strong = bool(wl.get("strong"))
+    value = (args.steps / wall) * (1 if strong else world)
     out = dict(
         metric=METRIC, value=round(value, 2), unit="it/s", n_gpus=world,
         steps=args.steps, warmup=args.warmup, ms_per_step=round(ms_per_step, 4),
-        higher_is_better=True, scaling="weak", vs_baseline=None,
+        higher_is_better=True, scaling="strong" if strong else "weak", vs_baseline=None,
         dtype=wl["dtype"], data="synthetic",
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz_local=int(len(sysm["col"])),
-                    alg=alg, graph=not use_dist, parallelism=f"row-partition x{world}",
+                    alg=alg, graph=not use_dist or world == 1,
+                    parallelism=f"row-partition x{world}",
                     halo_bytes_per_iter=(dinfo or {}).get("halo_bytes")),
         device_ms_per_step=round(dev_ms / args.steps, 4),
         # the C boundary takes host CSR buffers: one-time upload + plan, not in `value`
