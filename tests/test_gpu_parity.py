@@ -639,3 +639,19 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
             its = s.run(3000, 1e-10)
         _, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
         assert abs(its - its_o) <= 1
+
+
+def test_c4_full_size_spmv_device_generated():
+    """C4 at full size (400^3: 64,000,000 rows, 447,040,000 nnz -- the largest
+    BASELINE config, int32 offsets up to 2^28.7): the device-generated CSR
+    SpMV equals the matrix-free stencil bit for bit (the stencil is pinned to
+    the oracle's CSR SpMV at small sizes by test_matrix_free_stencil_bit_exact)."""
+    x = np.random.default_rng(11).standard_normal(400 ** 3)
+    with cgx.Solver(0) as s:
+        s.gen_laplacian(3, 400, 400, 400)
+        assert s.info()["nnz"] == 447_040_000
+        y = s.spmv(x)
+    with cgx.Solver(0) as s:
+        s.set_stencil(3, 400, 400, 400)
+        y2 = s.spmv(x)
+    assert H.same_bits_or_both_nan(y, y2)
