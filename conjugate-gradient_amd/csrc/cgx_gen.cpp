@@ -161,4 +161,20 @@ int cgx_csr_is_chained(int n, const int *row_ptr, const int *col) {
   return 1;
 }
 
+// Closed-form row_ptr of the Laplacian rows [row_begin, row_end): the
+// on-device generator and the matrix-free stencil use the same cgx::lap_rp.
+long long cgx_laplacian_row_ptr(int dim, int nx, int ny, int nz, int row_begin,
+                                int row_end, int *row_ptr) {
+  const cgx::LapSpec g{dim, nx, ny, dim == 3 ? nz : 1};
+  const long long n = (long long)nx * ny * g.nz;
+  if ((dim != 2 && dim != 3) || nx < 1 || ny < 1 || g.nz < 1 || n > INT32_MAX ||
+      row_begin < 0 || row_end < row_begin || row_end > n)
+    return CGX_EINVAL;
+  const long long base = cgx::lap_rp(row_begin, g);
+  if (row_ptr)
+    for (long long i = row_begin; i <= row_end; ++i)
+      row_ptr[i - row_begin] = (int)(cgx::lap_rp(i, g) - base);
+  return cgx::lap_rp(row_end, g) - base;
+}
+
 }  // extern "C"

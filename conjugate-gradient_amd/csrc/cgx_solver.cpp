@@ -1071,19 +1071,6 @@ int cgx_solver_set_matrix_f32(cgx_solver *s, int n, int nnz,
   return upload_matrix<float>(s, n, nnz, row_ptr, col, val);
 }
 
-long long cgx_laplacian_row_ptr(int dim, int nx, int ny, int nz, int row_begin,
-                                int row_end, int *row_ptr) {
-  const LapSpec g{dim, nx, ny, dim == 3 ? nz : 1};
-  const long long n = (long long)nx * ny * g.nz;
-  if ((dim != 2 && dim != 3) || nx < 1 || ny < 1 || g.nz < 1 || n > INT32_MAX ||
-      row_begin < 0 || row_end < row_begin || row_end > n)
-    return CGX_EINVAL;
-  const long long base = lap_rp(row_begin, g);
-  if (row_ptr)
-    for (long long i = row_begin; i <= row_end; ++i)
-      row_ptr[i - row_begin] = (int)(lap_rp(i, g) - base);
-  return lap_rp(row_end, g) - base;
-}
 
 int cgx_solver_gen_laplacian(cgx_solver *s, int dim, int nx, int ny, int nz) {
   if (!s) return CGX_EINVAL;
