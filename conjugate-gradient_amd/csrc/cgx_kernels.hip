@@ -1729,16 +1729,27 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
     return hipGetLastError();
   }
-  if (a.bs == 64 && a.dma == 1 && a.capw == 456 && sizeof(T) == 8 && !a.x2) {
-    // 456-entry windows (a 7-point block's 448 + alignment): 5.3 KiB of LDS
-    // per wave, 7 workgroups per CU instead of 6
-    constexpr int WPB = 4, CAPW = 456;
+  if (a.bs == 64 && a.dma == 1 && (a.capw == 456 || a.capw == 328) && sizeof(T) == 8 &&
+      !a.x2) {
+    // smaller windows, sized to the matrix's row blocks (456 = a 7-point
+    // block's 448 + alignment, 328 = a 5-point block's 320 + alignment):
+    // less LDS per wave, more waves per CU
+    constexpr int WPB = 4;
     const int g = (a.nblk + WPB - 1) / WPB;
     const bool epi = a.part != nullptr;
-    if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
-    else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
-    else if (a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
-    else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    if (a.capw == 456) {
+      constexpr int CAPW = 456;
+      if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+      else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+      else if (a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+      else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    } else {
+      constexpr int CAPW = 328;
+      if (epi && a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+      else if (epi) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, true, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+      else if (a.nt) hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false, true>), dim3(g), dim3(WPB * kWave), 0, st, a);
+      else hipLaunchKernelGGL((k_spmv_dma<T, WPB, CAPW, false, false>), dim3(g), dim3(WPB * kWave), 0, st, a);
+    }
     return hipGetLastError();
   }
   if (a.bs == 64 && a.dma) {

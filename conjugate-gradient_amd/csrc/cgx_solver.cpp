@@ -77,6 +77,12 @@ int choose_panels(int n, const int *rp, const int *col, size_t tsize) {
   return (int)std::min<long long>(64, (n + pcols - 1) / pcols);
 }
 
+// The adaptive LDS window applies to plain CSR only (column panels plan
+// their own blocks).
+bool gen_panels_pending(int n, const int *rp, const int *col, const void *gen) {
+  return !gen && col && choose_panels(n, rp, col, 8) > 1;
+}
+
 // Panel-major CSR: panel q holds, for every row, the row's entries with
 // column in [q*pc, (q+1)*pc), in the row's order; prp[q*(n+1) + i] are
 // offsets into the concatenated col/val (panel q's block starts at base q).
@@ -334,10 +340,22 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   const bool half = s->spmv_dma == 4 && s->spmv_bs == 64;  // 32-row blocks
   int cap = half ? spmv_cap(32, sizeof(T) == 8) : spmv_cap(s->spmv_bs, sizeof(T) == 8);
   s->spmv_capw = 0;
-  if (sizeof(T) == 8 && s->spmv_dma == 1 && s->spmv_bs == 64 && s->spmv_wpb == 4 &&
-      env_int("CGX_SPMV_CAPW", 512) == 456) {
-    s->spmv_capw = 456;
-    cap = 456;
+  if (sizeof(T) == 8 && s->spmv_dma == 1 && s->spmv_bs == 64 && s->spmv_wpb == 4 && n > 0 &&
+      !gen_panels_pending(n, rp, col, gen)) {
+    // LDS window sized to the matrix: 328 entries when every 64-row block
+    // fits (C2 5-point: -10% SpMV, -5% per iteration from the occupancy it
+    // frees, sweeps 28-29), else the 512 default (456 for 7-point blocks
+    // measured neutral to -4%); CGX_SPMV_CAPW=328|456|512 overrides
+    int w = env_int("CGX_SPMV_CAPW", 0);
+    if (w == 0) {
+      int m = 0;
+      for (int r = 0; r < n; r += 64) m = std::max(m, rp[std::min(r + 64, n)] - rp[r]);
+      w = m + kPad <= 328 ? 328 : 512;
+    }
+    if (w == 456 || w == 328) {
+      s->spmv_capw = w;
+      cap = w;
+    }
   }
   std::vector<int> blk, blkk;
   std::vector<int> prp, pcol;
@@ -623,7 +641,7 @@ bool fused(const cgx_solver *s) {
   return s->fuse_xpay && s->alg == CGX_ALG_HS && (s->spmv_bs == 64 || s->sell) &&
          s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1 &&
          !(s->spmv_dma == 1 && s->spmv_wpb == 8) &&  // no fused variant at 8 waves
-         s->spmv_capw != 456 &&
+         s->spmv_capw == 0 &&
          !s->is_stencil;
 }
 

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void k_mb(Args a) {
   for (; b < a.nblk; b += (MODE == 6 ? nwaves : a.nblk)) {
     const int k0 = a.blk_k[b], k1 = a.blk_k[b + 1];
     const int kb = k0 & ~3;
-    if (MODE == 1 || MODE == 2 || MODE == 6 || MODE >= 9) {
+    if (MODE == 1 || MODE == 2 || MODE == 6 || MODE >= 9) {  // (12, 13 too)
       const double4 *vv = (const double4 *)(a.val + kb);  // 32 B/lane x 2 = 4 KB
       const int4 *cc = (const int4 *)(a.col + kb);
       double2 v0 = ((const double2 *)(a.val + kb))[lane];
@@ -78,6 +78,19 @@ __global__ __launch_bounds__(256) void k_mb(Args a) {
         __builtin_nontemporal_store(acc + (double)(j1 - j0), a.y + r0 + lane);
       }
     }
+    if (MODE == 13) {  // row_ptr + y as 16 B per lane from half the lanes
+      const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
+      double v = 0;
+      if (lane < nr) {
+        const int j0 = a.rp[r0 + lane], j1 = a.rp[r0 + lane + 1];
+        v = acc + (double)(j1 - j0);
+      }
+      const double w = __shfl_down(v, 1);
+      if ((lane & 1) == 0 && lane + 1 < nr)
+        *(double2 *)(a.y + r0 + lane) = make_double2(v, w);
+      else if ((lane & 1) == 0 && lane < nr)
+        a.y[r0 + lane] = v;
+    }
     if (MODE == 2 || MODE == 4 || MODE == 5 || MODE == 6) {
       const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
       if (lane < nr) {
@@ -87,6 +100,32 @@ __global__ __launch_bounds__(256) void k_mb(Args a) {
     }
   }
   if (MODE == 1 || MODE == 3 || MODE == 10) if (acc == 12345.678) a.sink[0] = acc;
+}
+
+// mode 12: stream + row_ptr per wave; y staged in LDS and written by the
+// whole workgroup as one contiguous 256-row (2 KiB) burst after a barrier
+__global__ __launch_bounds__(256) void k_mb12(Args a) {
+  __shared__ double ys[256];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + wid;
+  double acc = 0;
+  if (b < a.nblk) {
+    const int k0 = a.blk_k[b];
+    const int kb = k0 & ~3;
+    double2 v0 = ((const double2 *)(a.val + kb))[lane];
+    double2 v1 = ((const double2 *)(a.val + kb))[lane + 64];
+    double2 v2 = ((const double2 *)(a.val + kb))[lane + 128];
+    double2 v3 = ((const double2 *)(a.val + kb))[lane + 192];
+    const int4 *cc = (const int4 *)(a.col + kb);
+    int4 c0 = cc[lane], c1 = cc[lane + 64];
+    acc += v0.x + v1.y + v2.x + v3.y + (double)(c0.x + c1.w);
+    const int r0 = a.blk_row[b], nr = a.blk_row[b + 1] - r0;
+    if (lane < nr) acc += (double)(a.rp[r0 + lane + 1] - a.rp[r0 + lane]);
+  }
+  ys[threadIdx.x] = acc;
+  __syncthreads();
+  const int row = blockIdx.x * 256 + threadIdx.x;  // 64-row blocks: contiguous rows
+  if (row < a.nblk * 64 && row < (int)(a.nblk) * 64) a.y[row] = ys[threadIdx.x];
 }
 
 __global__ void k_copy(const double2 *__restrict__ s, double2 *__restrict__ d, size_t n) {
@@ -146,6 +185,8 @@ int main() {
   run("9 vgpr window + y", [&] { hipLaunchKernelGGL(k_mb<9>, dim3(g1), dim3(256), 0, 0, a); }, stream + (double)n * 8);
   run("10 vgpr window + rp", [&] { hipLaunchKernelGGL(k_mb<10>, dim3(g1), dim3(256), 0, 0, a); }, stream + (double)n * 4);
   run("11 vgpr window + rp + nt y", [&] { hipLaunchKernelGGL(k_mb<11>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
+  run("12 vgpr window + rp + y (WG 2 KiB burst)", [&] { hipLaunchKernelGGL(k_mb12, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
+  run("13 vgpr window + rp + y (16 B/lane)", [&] { hipLaunchKernelGGL(k_mb<13>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
   run("1 vgpr window (again)", [&] { hipLaunchKernelGGL(k_mb<1>, dim3(g1), dim3(256), 0, 0, a); }, stream);
   run("2 vgpr window + rp + y (again)", [&] { hipLaunchKernelGGL(k_mb<2>, dim3(g1), dim3(256), 0, 0, a); }, stream + ry);
   for (int m : {4})
