@@ -432,6 +432,7 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   if (a.dma != 1) a.dma = 0;  // grids below assume one block per wave, 4 waves per WG
   a.nt = env_int("CGX_SPMV_NT", -1);
   if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes;
+  a.xcd = a.dma ? env_int("CGX_SPMV_XCD", 1) : 0;  // XCD-contiguous blocks, as the solver
   a.tk = TicketArgs{};
   return a;
 }
