@@ -141,7 +141,8 @@ struct SpmvArgs {
   // entries of a row are ascending in column, so summing panel after panel
   // is the reference's sequential order.  May alias y.
   const T *yacc;
-  int capw;            // k_spmv_dma fp64 window entries: 0 = 512, or 456
+  int capw;            // k_spmv_dma fp64 window entries: 0 = 512, or 456 / 328
+  int epi_last;        // k_spmv_dma: last-arriving wave writes the partial
   int dma;             // 1: k_spmv_dma (LDS-DMA stream, one block per wave)
                        // 2: k_spmv_pipe (persistent waves, rbw blocks each,
                        //    next block's stream prefetched by LDS-DMA)

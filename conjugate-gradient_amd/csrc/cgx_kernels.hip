@@ -608,7 +608,14 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
   __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
   __shared__ double red[WPB];
+  __shared__ int arrived;
   if (a.done && *a.done) return;
+  // epilogue without a closing barrier: the last wave to arrive sums the
+  // workgroup's wave partials (fixed order), the others leave at once
+  if (EPI && a.epi_last) {
+    if (threadIdx.x == 0) arrived = 0;
+    __syncthreads();
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   T *lval = lval_all + wid * CAPW;
@@ -681,7 +688,22 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dma(SpmvArgs<T> a) {
       if (EPI) dot = (double)xrow * (double)acc;
     }
   }
-  if (EPI) {
+  if (EPI && a.epi_last) {
+    dot = wave_sum(dot);
+    if (lane == 0) {
+      red[wid] = dot;
+      // LDS ops of one wave complete in order, so a peer's red[] store is
+      // done before its increment; acq_rel orders ours and the reads below
+      const int prev = __hip_atomic_fetch_add(&arrived, 1, __ATOMIC_ACQ_REL,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (prev == WPB - 1) {
+        double s = red[0];
+#pragma unroll
+        for (int w = 1; w < WPB; ++w) s = s + red[w];
+        a.part[blockIdx.x] = s;
+      }
+    }
+  } else if (EPI) {
     dot = wave_sum(dot);
     if (lane == 0) red[wid] = dot;
     __syncthreads();

@@ -200,6 +200,7 @@ struct cgx_solver {
   std::vector<int> panel_off, panel_nblk, panel_grid;
   bool panel_win512 = false;  // fp32 panels: 512-entry LDS windows
   int spmv_capw = 0;           // CGX_SPMV_CAPW: fp64 LDS-DMA window (456 or 512)
+  int epi_last = 0;            // CGX_SPMV_EPI_LAST: barrier-free SpMV epilogue
   // matrix-free Laplacian (cgx_solver_set_stencil): no CSR arrays at all
   bool is_stencil = false;
   cgx::LapSpec lap{};
@@ -592,6 +593,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.dma = s->spmv_dma;
   a.yacc = nullptr;
   a.capw = s->spmv_capw;
+  a.epi_last = s->epi_last;
   return a;
 }
 
@@ -1028,8 +1030,9 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->use_graph = cgx::env_int("CGX_GRAPH", 1) != 0;
   s->graph_batch = std::max(1, cgx::env_int("CGX_GRAPH_BATCH", 16));
   s->fuse_xpay = cgx::env_int("CGX_FUSE_XPAY", 0) != 0;
-  s->xdefer = cgx::env_int("CGX_XDEFER", 1) != 0;
-  s->fold = cgx::env_int("CGX_FOLD", 1) != 0;  // C3 -1%, C2 -8% (sweep22), bit-identical  // -4.4% per C3 iteration (sweep20), bit-identical
+  s->xdefer = cgx::env_int("CGX_XDEFER", 1) != 0;  // -4.4% per C3 iteration (sweep20), bit-identical
+  s->fold = cgx::env_int("CGX_FOLD", 1) != 0;      // C3 -1%, C2 -8% (sweep22), bit-identical
+  s->epi_last = cgx::env_int("CGX_SPMV_EPI_LAST", 0);
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {

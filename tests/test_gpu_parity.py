@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "dmalast", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -73,10 +73,13 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     per-row order, fp64 and fp32, including long rows."""
     monkeypatch.setenv("CGX_SPMV_VEC", vec)
     monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
-    if bs in ("dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512"):
+    if bs in ("dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512",
+              "dmalast"):
         monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4", "dmaw8": "1",
                                             "dmaxcd": "1", "dma456": "1", "dma328": "1",
-                                            "dma512": "1"}[bs])
+                                            "dma512": "1", "dmalast": "1"}[bs])
+        if bs == "dmalast":
+            monkeypatch.setenv("CGX_SPMV_EPI_LAST", "1")
         if bs in ("dma456", "dma328", "dma512"):
             monkeypatch.setenv("CGX_SPMV_CAPW", bs[3:])
         if bs == "dmaw8":
