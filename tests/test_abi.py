@@ -199,3 +199,54 @@ def test_laplacian_row_ptr_c4_total():
     nnz = cgx.lib().cgx_laplacian_row_ptr(3, 400, 400, 400, 0, 64_000_000, None)
     assert nnz == 447_040_000
     assert cgx.lib().cgx_laplacian_row_ptr(3, 216, 216, 216, 0, 216 ** 3, None) == 70_263_936
+
+
+def test_null_handles_fail_cleanly():
+    """Every handle-taking entry point rejects a NULL handle (and NULL
+    out-pointers) with an error code instead of crashing -- the drop-in
+    contract for C callers (mv_ops.c's -1 convention, CGX_EINVAL here)."""
+    L = cgx.lib()
+    vp = ctypes.c_void_p
+    i, d = ctypes.c_int(0), ctypes.c_double(0.0)
+    null = None
+    assert L.cgx_solver_set_mode(null, 0, 0) < 0
+    assert L.cgx_solver_set_matrix(null, 1, 1, null, null, null) < 0
+    assert L.cgx_solver_set_matrix_f32(null, 1, 1, null, null, null) < 0
+    assert L.cgx_solver_set_rhs(null, null) < 0
+    assert L.cgx_solver_set_rhs_f32(null, null) < 0
+    assert L.cgx_solver_run(null, 5, 0.0, ctypes.byref(i)) < 0
+    assert L.cgx_solver_get_x(null, null) < 0
+    assert L.cgx_solver_get_x_f32(null, null) < 0
+    assert L.cgx_solver_get_history(null, null, 4) < 0
+    assert L.cgx_solver_spmv(null, null, null) < 0
+    assert L.cgx_solver_spmv_f32(null, null, null) < 0
+    assert L.cgx_solver_info(null, null) < 0
+    assert L.cgx_solver_bench_prepare(null, 1) < 0
+    assert L.cgx_solver_gen_laplacian(null, 3, 4, 4, 4) < 0
+    assert L.cgx_solver_set_stencil(null, 3, 4, 4, 4) < 0
+    assert L.cgx_solver_get_matrix(null, null, null, null) < 0
+    assert L.cgx_dist_set_rhs(null, null) < 0
+    assert L.cgx_dist_run(null, 5, 0.0, ctypes.byref(i)) < 0
+    assert L.cgx_dist_get_x(null, null) < 0
+    assert L.cgx_dist_get_history(null, null, 4) < 0
+    assert L.cgx_dist_bench_prepare(null, 1) < 0
+    assert L.cgx_dist_info(null, null) < 0
+    assert L.cgx_dist_set_matrix(null, 4, 1, 1, null, null, null) < 0
+    assert L.cgx_solver_bench_run(null, 1, 0, ctypes.byref(d), ctypes.byref(d)) < 0
+    assert L.cgx_dist_bench_run(null, 1, 0, ctypes.byref(d), ctypes.byref(d)) < 0
+    assert L.cgx_part_info(null, null, null, null, null) < 0
+    assert L.cgx_part_ghosts(null, null) < 0
+    assert L.cgx_part_recv_counts(null, null) < 0
+    assert L.cgx_part_send_counts(null, null) < 0
+    assert L.cgx_part_send_local(null, null) < 0
+    assert L.cgx_part_local_cols(null, null) < 0
+    assert L.cgx_solver_create(0, null) < 0
+    assert L.cgx_dist_create(0, 1, 0, null, null) < 0
+    assert L.cgx_dist_create_local(0, 1, null) < 0
+    assert L.cgx_stream_bench(0, 0, 1 << 20, 1, null) < 0
+    # destroy functions accept NULL like free()
+    L.cgx_solver_destroy(null)
+    L.cgx_dist_destroy(null)
+    L.cgx_part_destroy(null)
+    L.cgx_free_mv_deep(null)
+    assert d.value == 0.0 and vp is not None
