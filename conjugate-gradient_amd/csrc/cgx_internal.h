@@ -57,6 +57,8 @@ static_assert(sizeof(CgState) == 112, "CgState layout");
 // SpMV row block: bs (256 or 512) rows, one per lane, and at most
 // spmv_cap(bs) products staged in LDS (16 KiB per 256 lanes).
 inline int spmv_cap(int bs, bool f64) { return bs * (f64 ? 8 : 16); }
+// Resident workgroups per CU of the engine SpMV's ring shapes (k_spmv_eng).
+inline int eng_wg_per_cu(int shape) { return shape == 1 ? 4 : shape >= 2 ? 2 : 3; }
 // Workgroups of one SpMV launch (= fused-dot partials it writes).
 inline int spmv_launch_grid(int bs, int wpb, int rbw, int nblk, int grid,
                             int dma = 0) {

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <algorithm>
+#include <cstring>
 
 #include "cgx_internal.h"
 
@@ -939,6 +940,173 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_pipe(SpmvArgs<T> a) {
   }
 }
 
+// ------------------------------------------------ LDS-DMA engine SpMV (fp64)
+// Persistent workgroups of 1 loader wave + NC consumer waves sharing an
+// S-slot LDS ring (the guide's loader/consumer engine).  The loader only
+// issues LDS-DMA -- val (4 KiB), col (2 KiB) and row_ptr (256 B) windows of
+// one 64-row block per slot, a fixed ENG_OPS instructions per block, in one
+// asm block so the compiler's waitcnt pass never sees them -- and keeps
+// D - 1 blocks in flight: after issuing block i it waits
+// vmcnt((D-1) * ENG_OPS), i.e. for block i-D+1, and publishes that
+// slot (full[slot] = block).  Consumers take blocks round-robin, poll their
+// slot's full flag, do the gathers and the row sums (same order as the CSR
+// row: bit-exact), store y, and release the slot (free[slot] = block).  Their
+// vmcnt only ever tracks their own gathers.  Progress: the loader reuses a
+// slot only after the block S earlier is released, and D <= S, so
+// every wait is on a block that is already published or issued.
+// Shapes (CGX_ENG_SHAPE selects; workgroups per CU from the ring's LDS):
+//   0: NC 3, S 8, D 6 (3/CU)   1: NC 3, S 6, D 3 (4/CU)
+//   2: NC 7, S 12, D 5 (2/CU)  3: NC 7, S 12, D 9 (2/CU)
+constexpr int ENG_OPS = 7;
+constexpr int ENG_CAPW = 512;                            // doubles per window
+constexpr int ENG_SLOT = ENG_CAPW * 8 + ENG_CAPW * 4 + 64 * 4;  // 6400 B
+
+#define CGX_ENG_DMA(NTS)                                                          \
+  asm volatile(                                                                   \
+      "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" NTS "\n\t"       \
+      "s_add_u32 m0, %7, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" NTS "\n\t" \
+      "s_add_u32 m0, %7, 0x800\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off" NTS "\n\t" \
+      "s_add_u32 m0, %7, 0xc00\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, off" NTS "\n\t" \
+      "s_add_u32 m0, %7, 0x1000\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, off" NTS "\n\t"\
+      "s_add_u32 m0, %7, 0x1400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, off" NTS "\n\t"\
+      "s_add_u32 m0, %7, 0x1800\n\ts_nop 0\n\tglobal_load_lds_dword %6, off"            \
+      :                                                                           \
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(c0), "v"(c1), "v"(r), "s"(lds)       \
+      : "memory", "m0", "scc")
+
+template <bool NT>
+__device__ __forceinline__ void eng_dma_block(const void *v0, const void *v1, const void *v2,
+                                              const void *v3, const void *c0, const void *c1,
+                                              const void *r, unsigned lds) {
+  if (NT) CGX_ENG_DMA(" nt");  // the once-read matrix stream, non-temporal
+  else CGX_ENG_DMA("");
+}
+
+// two consecutive ints by a SCALAR load (a vector load would make the
+// compiler wait vmcnt(0) -- draining the loader's in-flight DMA)
+__device__ __forceinline__ void eng_sload2(const int *p, int &lo, int &hi) {
+  unsigned long long v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  lo = (int)(unsigned)(v & 0xffffffffu);
+  hi = (int)(unsigned)(v >> 32);
+}
+
+template <bool EPI, bool NT, int NC, int S, int D>
+__global__ __launch_bounds__((1 + NC) * kWave) void k_spmv_eng(SpmvArgs<double> a) {
+  __shared__ __attribute__((aligned(16))) char ring[S * ENG_SLOT];
+  __shared__ int desc[S][4];  // r0, nr, kb, k1 of the slot's block
+  __shared__ int full[S], freed[S];
+  __shared__ double red[NC];
+  if (a.done && *a.done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  // this workgroup's contiguous block range (XCD-contiguous order)
+  const int q = xcd_block(1), G = gridDim.x;
+  const int b0 = (int)((long long)a.nblk * q / G), b1 = (int)((long long)a.nblk * (q + 1) / G);
+  static_assert(D <= S && (D - 1) * ENG_OPS <= 63, "engine ring shape");
+  if (threadIdx.x < S) {
+    full[threadIdx.x] = -1;
+    freed[threadIdx.x] = -1;
+  }
+  __syncthreads();
+  const unsigned ring_lds = (unsigned)(uintptr_t)(lds_void *)ring;
+  double dot = 0.0;
+  if (wid == 0) {
+    // ------------------------------------------------------------- loader
+    for (int i = b0; i < b1; ++i) {
+      const int slot = (i - b0) % S;
+      if (i - S >= b0)
+        while (__hip_atomic_load(&freed[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+               i - S)
+          __builtin_amdgcn_s_sleep(1);
+      const int rb = a.blk_first + i;
+      int r0, r1, k0, k1;
+      eng_sload2(a.blk_row + rb, r0, r1);
+      eng_sload2(a.blk_k + rb, k0, k1);
+      const int nr = r1 - r0;
+      const int kb = k0 & ~3;
+      const double *vb = a.val + kb + lane * 2;
+      const int *cb = a.col + kb + lane * 4;
+      eng_dma_block<NT>(vb, vb + 128, vb + 256, vb + 384, cb, cb + 256, a.rp + r0 + lane,
+                        ring_lds + slot * ENG_SLOT);
+      if (lane == 0) {
+        desc[slot][0] = r0;
+        desc[slot][1] = nr;
+        desc[slot][2] = kb;
+        desc[slot][3] = k1;
+      }
+      const int pub = i - (D - 1);
+      if (pub >= b0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * ENG_OPS) : "memory");
+        if (lane == 0)
+          __hip_atomic_store(&full[(pub - b0) % S], pub, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      for (int pub = (b1 - (D - 1) > b0 ? b1 - (D - 1) : b0); pub < b1; ++pub)
+        __hip_atomic_store(&full[(pub - b0) % S], pub, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    // ----------------------------------------------------------- consumers
+    const int c = wid - 1;
+    for (int i = b0 + c; i < b1; i += NC) {
+      const int slot = (i - b0) % S;
+      while (__hip_atomic_load(&full[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != i)
+        __builtin_amdgcn_s_sleep(1);
+      const int r0 = desc[slot][0], nr = desc[slot][1], kb = desc[slot][2], k1 = desc[slot][3];
+      const char *sb = ring + slot * ENG_SLOT;
+      const double *lval = (const double *)sb;
+      const int *lcol = (const int *)(sb + ENG_CAPW * 8);
+      const int *lrp = (const int *)(sb + ENG_CAPW * 12);
+      double acc = 0.0;
+      double xrow = 0.0;
+      if (k1 - kb <= ENG_CAPW) {
+        if (lane < nr) {
+          const int j0 = lrp[lane];
+          const int j1 = lane + 1 < kWave ? lrp[lane + 1] : k1;
+          acc = row_sum_lds<double, 4, false>(a, 0.0, lval, lcol, j0 - kb, j1 - kb, acc);
+        }
+      } else if (lane == 0) {  // one long row: straight from global, in order
+        for (int j = lrp[0]; j < k1; ++j) {
+          const double prod = a.val[j] * a.x[a.col[j]];
+          acc = acc + prod;
+        }
+      }
+      if (lane < nr) {
+        if (EPI) xrow = a.x[r0 + lane];
+        a.y[r0 + lane] = acc;
+        if (EPI) dot = dot + xrow * acc;
+      }
+      // every LDS read of the slot is complete before it is handed back
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_store(&freed[slot], i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (wid > 0 && lane == 0) red[wid - 1] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < NC; ++w) s = s + red[w];
+      a.part[blockIdx.x] = s;
+    }
+  }
+}
+
+template <int NC, int S, int D>
+void launch_eng(const SpmvArgs<double> &b, int g, hipStream_t st) {
+  const dim3 blk((1 + NC) * kWave);
+  if (b.part && b.nt) hipLaunchKernelGGL((k_spmv_eng<true, true, NC, S, D>), dim3(g), blk, 0, st, b);
+  else if (b.part) hipLaunchKernelGGL((k_spmv_eng<true, false, NC, S, D>), dim3(g), blk, 0, st, b);
+  else if (b.nt) hipLaunchKernelGGL((k_spmv_eng<false, true, NC, S, D>), dim3(g), blk, 0, st, b);
+  else hipLaunchKernelGGL((k_spmv_eng<false, false, NC, S, D>), dim3(g), blk, 0, st, b);
+}
+
 // SELL-64 (sliced ELLPACK, one 64-row slice per wave, column-major inside the
 // slice): lane t owns row t of its slice and walks the row's nonzeros in
 // column order, so every load is a coalesced wave-wide line (val 512 B, col
@@ -1719,6 +1887,18 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     return hipGetLastError();
   }
   if (a.nblk <= 0) return hipSuccess;
+  if (a.bs == 64 && a.dma == 5 && sizeof(T) == 8 && !a.blk_list && !a.x2) {  // DMA engine
+    SpmvArgs<double> b;
+    memcpy(&b, &a, sizeof b);
+    const int g = grid > 0 ? grid : 1;
+    switch (a.rbw) {
+      case 1: launch_eng<3, 6, 3>(b, g, st); break;
+      case 2: launch_eng<7, 12, 5>(b, g, st); break;
+      case 3: launch_eng<7, 12, 9>(b, g, st); break;
+      default: launch_eng<3, 8, 6>(b, g, st); break;
+    }
+    return hipGetLastError();
+  }
   if (a.bs == 64 && a.dma == 2 && !a.blk_list && !a.x2) {  // pipelined LDS-DMA
     constexpr int WPB = 2;
     constexpr int CAPW = sizeof(T) == 8 ? 512 : 1024;

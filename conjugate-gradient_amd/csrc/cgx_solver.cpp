@@ -399,7 +399,8 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
   const size_t nv = (size_t)n + kPad;
   int rc;
-  if ((rc = dalloc(s, (void **)&s->d_rp, rp_len * 4)) ||
+  // + 64 entries: the engine SpMV DMAs row_ptr[r0 .. r0+63] for every block
+  if ((rc = dalloc(s, (void **)&s->d_rp, rp_len * 4 + 256)) ||
       (rc = dalloc(s, (void **)&s->d_col, nnz_pad * 4)) ||
       (rc = dalloc(s, &s->d_val, nnz_pad * sizeof(T)))) {
     free_matrix(s);
@@ -425,6 +426,8 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
                                   s->spmv_grid, s->spmv_dma);
   if (s->npanel > 1)  // the last panel's launch writes the epilogue partials
     s->spmv_grid = s->panel_grid.back();
+  else if (s->spmv_dma == 5 && sizeof(T) == 8)  // engine: persistent, as many as fit per CU
+    s->spmv_grid = std::max(1, std::min(s->cus * eng_wg_per_cu(s->spmv_rbw), s->nblk));
   s->vec_grid = env_int("CGX_VEC_GRID", vec_grid_for(n, s->cus));
   s->vec_grid = (std::max(s->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
   s->part_cap = std::max(s->spmv_grid, s->vec_grid) + 1;
@@ -644,7 +647,7 @@ bool fused(const cgx_solver *s) {
          s->spmv_dma != 2 && s->spmv_dma != 4 && s->npanel == 1 &&
          !(s->spmv_dma == 1 && s->spmv_wpb == 8) &&  // no fused variant at 8 waves
          s->spmv_capw == 0 &&
-         !s->is_stencil;
+         !s->is_stencil && s->spmv_dma != 5;
 }
 
 // Prologue: x = 0, r = b, p = b (HS) / p = s = 0, w = A r (CG1); b.b; state.
@@ -1014,6 +1017,8 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_dma = cgx::env_int("CGX_SPMV_DMA", 1);
   s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", s->spmv_dma == 2 ? 8 : 1));
   if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
+  if (s->spmv_dma == 5)  // engine ring shape (k_spmv_eng), carried in rbw
+    s->spmv_rbw = std::min(std::max(cgx::env_int("CGX_ENG_SHAPE", 2), 0), 3);
   // XCD-contiguous block order for the LDS-DMA kernel: time-neutral, but the
   // x lines shared by neighbouring row blocks stay in one XCD's L2 (EA reads
   // 1265 -> 976 MB per C3 SpMV = the algorithmic 965 MB; sweep25)
@@ -1021,7 +1026,10 @@ int cgx_solver_create(int device, cgx_solver **out) {
   // nt helps the LDS-DMA stream, hurts the register-staged one (sweep15)
   // -1 = by size at set_matrix (kNtStreamBytes; nt helps the LDS-DMA stream
   // only, it hurts the register-staged one: sweep15)
-  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 || s->spmv_dma == 4 ? -1 : 0);
+  s->spmv_nt = cgx::env_int("CGX_SPMV_NT", s->spmv_dma == 1 || s->spmv_dma == 3 ||
+                                                   s->spmv_dma == 4 || s->spmv_dma == 5
+                                               ? -1
+                                               : 0);
   {
     const int bs = cgx::env_int("CGX_SPMV_BS", 64);
     s->spmv_bs = (bs == 512 || bs == 64) ? bs : 256;

@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "dmalast", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "dmalast", "eng", "eng0", "eng1", "eng3", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -90,6 +90,10 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
         if bs != "pipe":
             monkeypatch.setenv("CGX_SPMV_RBW", bs[4:])
+    elif bs.startswith("eng"):
+        monkeypatch.setenv("CGX_SPMV_DMA", "5")
+        if bs != "eng":
+            monkeypatch.setenv("CGX_ENG_SHAPE", bs[3:])
     elif bs == "notg":
         monkeypatch.setenv("CGX_SPMV_TG", "0")
     else:
@@ -115,13 +119,15 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
         assert rel(s.x(), x_ref) <= FAST_RTOL
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "dma32", "pipe"])
+@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "dma32", "pipe", "eng"])
 def test_spmv_long_rows_variants(bs, monkeypatch):
     monkeypatch.setenv("CGX_SPMV_DMA", "0")
     if bs in ("dma", "dma8", "dma32"):
         monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4"}[bs])
     elif bs == "pipe":
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
+    elif bs == "eng":
+        monkeypatch.setenv("CGX_SPMV_DMA", "5")
     else:
         monkeypatch.setenv("CGX_SPMV_BS", bs)
     n = 3000
@@ -178,7 +184,7 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "8", "1x", "1w"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
