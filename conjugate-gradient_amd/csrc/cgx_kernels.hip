@@ -957,7 +957,9 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_pipe(SpmvArgs<T> a) {
 // Shapes (CGX_ENG_SHAPE selects; workgroups per CU from the ring's LDS):
 //   0: NC 3, S 8, D 6 (3/CU)   1: NC 3, S 6, D 3 (4/CU)
 //   2: NC 7, S 12, D 5 (2/CU)  3: NC 7, S 12, D 9 (2/CU)
+//   4-7 (REG): NC 7/5/7/11, S 12, D 10/10/8/10 (2/CU; 4-6 256-512 threads)
 constexpr int ENG_OPS = 7;
+constexpr int ENG_RL = 8;  // REG: rows up to this long leave the slot early
 constexpr int ENG_CAPW = 512;                            // doubles per window
 constexpr int ENG_SLOT = ENG_CAPW * 8 + ENG_CAPW * 4 + 64 * 4;  // 6400 B
 
@@ -991,7 +993,7 @@ __device__ __forceinline__ void eng_sload2(const int *p, int &lo, int &hi) {
   hi = (int)(unsigned)(v >> 32);
 }
 
-template <bool EPI, bool NT, int NC, int S, int D>
+template <bool EPI, bool NT, int NC, int S, int D, bool REG>
 __global__ __launch_bounds__((1 + NC) * kWave) void k_spmv_eng(SpmvArgs<double> a) {
   __shared__ __attribute__((aligned(16))) char ring[S * ENG_SLOT];
   __shared__ int desc[S][4];  // r0, nr, kb, k1 of the slot's block
@@ -1062,11 +1064,37 @@ __global__ __launch_bounds__((1 + NC) * kWave) void k_spmv_eng(SpmvArgs<double> 
       const int *lrp = (const int *)(sb + ENG_CAPW * 12);
       double acc = 0.0;
       double xrow = 0.0;
+      bool held = true;
       if (k1 - kb <= ENG_CAPW) {
+        int j0 = kb, len = 0;
         if (lane < nr) {
-          const int j0 = lrp[lane];
-          const int j1 = lane + 1 < kWave ? lrp[lane + 1] : k1;
-          acc = row_sum_lds<double, 4, false>(a, 0.0, lval, lcol, j0 - kb, j1 - kb, acc);
+          j0 = lrp[lane];
+          len = (lane + 1 < kWave ? lrp[lane + 1] : k1) - j0;
+        }
+        if (REG && !__any(len > ENG_RL)) {
+          // rows of <= ENG_RL entries: copy them to registers and hand the
+          // slot back before the gathers, so the ring stays DMA in flight
+          double vv[ENG_RL], xx[ENG_RL];
+          int cc[ENG_RL];
+#pragma unroll
+          for (int u = 0; u < ENG_RL; ++u) {
+            const int idx = u < len ? j0 - kb + u : 0;
+            vv[u] = lval[idx];
+            cc[u] = lcol[idx];
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0)
+            __hip_atomic_store(&freed[slot], i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          held = false;
+#pragma unroll
+          for (int u = 0; u < ENG_RL; ++u) xx[u] = a.x[cc[u]];  // a valid column, masked below
+#pragma unroll
+          for (int u = 0; u < ENG_RL; ++u) {  // the row's order, products rounded
+            const double prod = vv[u] * xx[u];
+            acc = acc + (u < len ? prod : 0.0);
+          }
+        } else if (lane < nr) {
+          acc = row_sum_lds<double, 4, false>(a, 0.0, lval, lcol, j0 - kb, j0 + len - kb, acc);
         }
       } else if (lane == 0) {  // one long row: straight from global, in order
         for (int j = lrp[0]; j < k1; ++j) {
@@ -1080,9 +1108,11 @@ __global__ __launch_bounds__((1 + NC) * kWave) void k_spmv_eng(SpmvArgs<double> 
         if (EPI) dot = dot + xrow * acc;
       }
       // every LDS read of the slot is complete before it is handed back
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0)
-        __hip_atomic_store(&freed[slot], i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (held) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(&freed[slot], i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   }
   if (EPI) {
@@ -1098,13 +1128,13 @@ __global__ __launch_bounds__((1 + NC) * kWave) void k_spmv_eng(SpmvArgs<double> 
   }
 }
 
-template <int NC, int S, int D>
+template <int NC, int S, int D, bool REG = false>
 void launch_eng(const SpmvArgs<double> &b, int g, hipStream_t st) {
   const dim3 blk((1 + NC) * kWave);
-  if (b.part && b.nt) hipLaunchKernelGGL((k_spmv_eng<true, true, NC, S, D>), dim3(g), blk, 0, st, b);
-  else if (b.part) hipLaunchKernelGGL((k_spmv_eng<true, false, NC, S, D>), dim3(g), blk, 0, st, b);
-  else if (b.nt) hipLaunchKernelGGL((k_spmv_eng<false, true, NC, S, D>), dim3(g), blk, 0, st, b);
-  else hipLaunchKernelGGL((k_spmv_eng<false, false, NC, S, D>), dim3(g), blk, 0, st, b);
+  if (b.part && b.nt) hipLaunchKernelGGL((k_spmv_eng<true, true, NC, S, D, REG>), dim3(g), blk, 0, st, b);
+  else if (b.part) hipLaunchKernelGGL((k_spmv_eng<true, false, NC, S, D, REG>), dim3(g), blk, 0, st, b);
+  else if (b.nt) hipLaunchKernelGGL((k_spmv_eng<false, true, NC, S, D, REG>), dim3(g), blk, 0, st, b);
+  else hipLaunchKernelGGL((k_spmv_eng<false, false, NC, S, D, REG>), dim3(g), blk, 0, st, b);
 }
 
 // SELL-64 (sliced ELLPACK, one 64-row slice per wave, column-major inside the
@@ -1895,6 +1925,10 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
       case 1: launch_eng<3, 6, 3>(b, g, st); break;
       case 2: launch_eng<7, 12, 5>(b, g, st); break;
       case 3: launch_eng<7, 12, 9>(b, g, st); break;
+      case 4: launch_eng<7, 12, 10, true>(b, g, st); break;
+      case 5: launch_eng<5, 12, 10, true>(b, g, st); break;
+      case 6: launch_eng<7, 12, 8, true>(b, g, st); break;
+      case 7: launch_eng<11, 12, 10, true>(b, g, st); break;
       default: launch_eng<3, 8, 6>(b, g, st); break;
     }
     return hipGetLastError();

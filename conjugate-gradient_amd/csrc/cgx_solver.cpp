@@ -1018,7 +1018,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_rbw = std::max(1, cgx::env_int("CGX_SPMV_RBW", s->spmv_dma == 2 ? 8 : 1));
   if (s->spmv_dma == 2) s->spmv_rbw = std::min(s->spmv_rbw, 63);  // descriptors in lanes
   if (s->spmv_dma == 5)  // engine ring shape (k_spmv_eng), carried in rbw
-    s->spmv_rbw = std::min(std::max(cgx::env_int("CGX_ENG_SHAPE", 2), 0), 3);
+    s->spmv_rbw = std::min(std::max(cgx::env_int("CGX_ENG_SHAPE", 4), 0), 7);
   // XCD-contiguous block order for the LDS-DMA kernel: time-neutral, but the
   // x lines shared by neighbouring row blocks stay in one XCD's L2 (EA reads
   // 1265 -> 976 MB per C3 SpMV = the algorithmic 965 MB; sweep25)

@@ -65,7 +65,7 @@ def test_spmv_bit_exact_vs_reference(solver, name):
     assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "dmalast", "eng", "eng0", "eng1", "eng3", "notg", "pipe", "pipe1", "pipe63"])
+@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "dmalast", "eng", "eng0", "eng1", "eng3", "eng4", "eng5", "eng6", "eng7", "notg", "pipe", "pipe1", "pipe63"])
 @pytest.mark.parametrize("vec", ["1", "2", "4"])
 def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
     """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
@@ -119,15 +119,17 @@ def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
         assert rel(s.x(), x_ref) <= FAST_RTOL
 
 
-@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "dma32", "pipe", "eng"])
+@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "dma32", "pipe", "eng", "eng4"])
 def test_spmv_long_rows_variants(bs, monkeypatch):
     monkeypatch.setenv("CGX_SPMV_DMA", "0")
     if bs in ("dma", "dma8", "dma32"):
         monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4"}[bs])
     elif bs == "pipe":
         monkeypatch.setenv("CGX_SPMV_DMA", "2")
-    elif bs == "eng":
+    elif bs.startswith("eng"):
         monkeypatch.setenv("CGX_SPMV_DMA", "5")
+        if bs != "eng":
+            monkeypatch.setenv("CGX_ENG_SHAPE", bs[3:])
     else:
         monkeypatch.setenv("CGX_SPMV_BS", bs)
     n = 3000
