@@ -211,11 +211,11 @@ hipError_t launch_stencil(const LapSpec &g, int n, const T *x, T *y, double *par
 
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
-                            int nps, double *rr_part, int grid, hipStream_t st);
+                            int nps, double *rr_part, int grid, hipStream_t st, bool pf);
 template <typename T>
 hipError_t launch_xpay_xf(int n, T *x, T *p, const T *r, CgState *stt,
                           const double *rr_part, int nrr, double *hist, int grid,
-                          hipStream_t st);
+                          hipStream_t st, bool pf);
 template <typename T>
 hipError_t launch_update_r(int n, T *r, const T *s, const CgState *stt,
                            double *part, int grid, hipStream_t st);

@@ -1409,7 +1409,10 @@ __device__ __forceinline__ void sum_parts2(const double *pa, int na, const doubl
 // there was written by its own workgroup 0 during this launch).
 constexpr int kFoldBS = 1024;
 
-template <typename T>
+// PF: the first grid-stride element's loads are issued before the partial
+// sum, so the HBM round trip overlaps the L2 round trip of the partials
+// (same elements, same order: bit-identical).
+template <typename T, bool PF>
 __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
                                                        const T *__restrict__ s,
                                                        CgState *__restrict__ st,
@@ -1421,6 +1424,15 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
   if (done) {
     if (done == 1 && blockIdx.x == 0 && threadIdx.x == 0) st->done = 2;
     return;
+  }
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const int nv = n / W;
+  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+  V rv0 = V(), sv0 = V();
+  if (PF && gid < nv) {
+    rv0 = reinterpret_cast<const V *>(r)[gid];
+    sv0 = reinterpret_cast<const V *>(s)[gid];
   }
   const double ps = sum_parts<kFoldBS>(ps_part, nps, red);
   if (threadIdx.x == 0) {
@@ -1435,15 +1447,9 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
     }
   }
   __syncthreads();
-  typedef typename Vec16<T>::type V;
-  constexpr int W = Vec16<T>::W;
   const T alpha = (T)bcast;
-  const int nv = n / W;
-  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
   double acc = 0.0;
-  for (int i = gid; i < nv; i += stride) {
-    V rv = reinterpret_cast<const V *>(r)[i];
-    const V sv = reinterpret_cast<const V *>(s)[i];
+  auto step = [&](int i, V rv, const V sv) {
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const T as = alpha * sv[j];
@@ -1451,7 +1457,14 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
       acc = acc + (double)rv[j] * (double)rv[j];
     }
     reinterpret_cast<V *>(r)[i] = rv;
+  };
+  int i = gid;
+  if (PF && i < nv) {
+    step(i, rv0, sv0);
+    i += stride;
   }
+  for (; i < nv; i += stride)
+    step(i, reinterpret_cast<const V *>(r)[i], reinterpret_cast<const V *>(s)[i]);
   if (gid == 0)
     for (int i = nv * W; i < n; ++i) {
       const T as = alpha * s[i];
@@ -1475,7 +1488,7 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
   }
 }
 
-template <typename T>
+template <typename T, bool PF>
 __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x,
                                                      T *__restrict__ p,
                                                      const T *__restrict__ r,
@@ -1486,6 +1499,16 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x,
   __shared__ double bcast;
   __shared__ int bstop;
   if (st->done > 1) return;
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const int nv = n / W;
+  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+  V pv0 = V(), xv0 = V(), rv0 = V();
+  if (PF && gid < nv) {
+    pv0 = reinterpret_cast<const V *>(p)[gid];
+    xv0 = reinterpret_cast<const V *>(x)[gid];
+    rv0 = reinterpret_cast<const V *>(r)[gid];
+  }
   const double rr_new = sum_parts<kFoldBS>(rr_part, nrr, red);
   if (threadIdx.x == 0) {
     const int k = st->k_u;
@@ -1509,14 +1532,8 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x,
   }
   __syncthreads();
   const bool stop = bstop != 0;
-  typedef typename Vec16<T>::type V;
-  constexpr int W = Vec16<T>::W;
   const T alpha = (T)st->alpha, beta = (T)bcast;
-  const int nv = n / W;
-  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
-  for (int i = gid; i < nv; i += stride) {
-    V pv = reinterpret_cast<const V *>(p)[i];
-    V xv = reinterpret_cast<const V *>(x)[i];
+  auto step = [&](int i, V pv, V xv, const V rv) {
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const T ap = alpha * pv[j];
@@ -1524,7 +1541,6 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x,
     }
     reinterpret_cast<V *>(x)[i] = xv;
     if (!stop) {
-      const V rv = reinterpret_cast<const V *>(r)[i];
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         const T bp = beta * pv[j];
@@ -1532,6 +1548,16 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x,
       }
       reinterpret_cast<V *>(p)[i] = pv;
     }
+  };
+  int i = gid;
+  if (PF && i < nv) {
+    step(i, pv0, xv0, rv0);
+    i += stride;
+  }
+  for (; i < nv; i += stride) {
+    const V pv = reinterpret_cast<const V *>(p)[i];
+    const V xv = reinterpret_cast<const V *>(x)[i];
+    step(i, pv, xv, stop ? V() : reinterpret_cast<const V *>(r)[i]);
   }
   if (gid == 0)
     for (int i = nv * W; i < n; ++i) {
@@ -2077,18 +2103,26 @@ hipError_t launch_xpay_x(int n, T *x, T *p, const T *r, const CgState *stt,
 
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
-                            int nps, double *rr_part, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((k_update_rf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt,
-                     ps_part, nps, rr_part);
+                            int nps, double *rr_part, int grid, hipStream_t st, bool pf) {
+  if (pf)
+    hipLaunchKernelGGL((k_update_rf<T, true>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt,
+                       ps_part, nps, rr_part);
+  else
+    hipLaunchKernelGGL((k_update_rf<T, false>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt,
+                       ps_part, nps, rr_part);
   return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_xpay_xf(int n, T *x, T *p, const T *r, CgState *stt,
                           const double *rr_part, int nrr, double *hist, int grid,
-                          hipStream_t st) {
-  hipLaunchKernelGGL((k_xpay_xf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, r, stt,
-                     rr_part, nrr, hist);
+                          hipStream_t st, bool pf) {
+  if (pf)
+    hipLaunchKernelGGL((k_xpay_xf<T, true>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, r, stt,
+                       rr_part, nrr, hist);
+  else
+    hipLaunchKernelGGL((k_xpay_xf<T, false>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, r, stt,
+                       rr_part, nrr, hist);
   return hipGetLastError();
 }
 
@@ -2289,10 +2323,10 @@ hipError_t launch_stencil(const LapSpec &g, int n, const T *x, T *y, double *par
                                         hipStream_t);                          \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *,     \
                                           const double *, int, double *, int,  \
-                                          hipStream_t);                        \
+                                          hipStream_t, bool);                  \
   template hipError_t launch_xpay_xf<T>(int, T *, T *, const T *, CgState *,  \
                                         const double *, int, double *, int,    \
-                                        hipStream_t);                          \
+                                        hipStream_t, bool);                    \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *,           \
                                            const T *, const CgState *,        \
                                            double *, int, hipStream_t);        \

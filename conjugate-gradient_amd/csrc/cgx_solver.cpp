@@ -201,6 +201,7 @@ struct cgx_solver {
   bool panel_win512 = false;  // fp32 panels: 512-entry LDS windows
   int spmv_capw = 0;           // CGX_SPMV_CAPW: fp64 LDS-DMA window (456 or 512)
   int epi_last = 0;            // CGX_SPMV_EPI_LAST: barrier-free SpMV epilogue
+  bool vec_pf = false;         // CGX_VEC_PF: folded kernels issue loads before the partial sum
   // matrix-free Laplacian (cgx_solver_set_stencil): no CSR arrays at all
   bool is_stencil = false;
   cgx::LapSpec lap{};
@@ -728,9 +729,9 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
       // (no finalize launches; bit-identical scalars, see k_update_rf)
       const int gf = s->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
       CGX_HIP(launch_update_rf<T>(s->n, r, sv, s->d_st, s->d_pa, sg, s->d_pb, gf,
-                                  st));                           // cg.c:113, 118-123
+                                  st, s->vec_pf));                // cg.c:113, 118-123
       CGX_HIP(launch_xpay_xf<T>(s->n, x, p, r, s->d_st, s->d_pb, 4 * gf, s->d_hist,
-                                gf, st));                         // cg.c:115-116, 125-132
+                                gf, st, s->vec_pf));              // cg.c:115-116, 125-132
       return 0;
     } else if (s->xdefer && !fx) {
       // deferred x: r-update alone, x += alpha p_old folded into the p-update
@@ -1041,6 +1042,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->xdefer = cgx::env_int("CGX_XDEFER", 1) != 0;  // -4.4% per C3 iteration (sweep20), bit-identical
   s->fold = cgx::env_int("CGX_FOLD", 1) != 0;      // C3 -1%, C2 -8% (sweep22), bit-identical
   s->epi_last = cgx::env_int("CGX_SPMV_EPI_LAST", 0);
+  s->vec_pf = cgx::env_int("CGX_VEC_PF", 1) != 0;  // C3 -1.7 us, C2 -0.44 us per iteration (sweep36), bit-identical
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {

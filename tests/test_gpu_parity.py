@@ -490,11 +490,14 @@ def test_deferred_x_bit_identical(dma, monkeypatch):
     cases[1] = (g["row_ptr"], g["col"], g["val"], g["b"])
     for rp, col, val, b in cases:
         out = {}
-        for xd in ("0", "1", "fold"):
+        for xd in ("0", "1", "fold", "foldpf"):
             # "fold": CGX_FOLD, the alpha/beta/stop steps inside the vector
-            # kernels (no finalize launches) -- same scalars bit for bit
+            # kernels (no finalize launches) -- same scalars bit for bit;
+            # "foldpf": the same with the first loads issued before the
+            # partial sums (CGX_VEC_PF)
             monkeypatch.setenv("CGX_XDEFER", "0" if xd == "0" else "1")
-            monkeypatch.setenv("CGX_FOLD", "1" if xd == "fold" else "0")
+            monkeypatch.setenv("CGX_FOLD", "1" if xd.startswith("fold") else "0")
+            monkeypatch.setenv("CGX_VEC_PF", "1" if xd == "foldpf" else "0")
             with cgx.Solver(0) as s:
                 s.set_matrix(rp, col, val)
                 res = []
@@ -503,7 +506,7 @@ def test_deferred_x_bit_identical(dma, monkeypatch):
                     its = s.run(maxit, tol)
                     res.append((its, s.x(), s.history(its)))
                 out[xd] = res
-        for other in ("1", "fold"):
+        for other in ("1", "fold", "foldpf"):
             for (i0, x0, h0), (i1, x1, h1) in zip(out["0"], out[other]):
                 assert i0 == i1, other
                 assert H.same_bits_or_both_nan(x0, x1), other
