@@ -148,7 +148,24 @@ struct SpmvArgs {
   int dma;             // 1: k_spmv_dma (LDS-DMA stream, one block per wave)
                        // 2: k_spmv_pipe (persistent waves, rbw blocks each,
                        //    next block's stream prefetched by LDS-DMA)
+  // dictionary-coded columns (k_spmv_dc) when code != nullptr: col[k] ==
+  // row + dict[code[k]], one byte per nonzero instead of four (matrices with
+  // <= 256 distinct column offsets col - row: stencils, banded matrices).
+  // dict holds ndict_cap (64 | 256) entries, unused ones 0.
+  const unsigned char *code;
+  const int *dict;
+  int ndict_cap;
+  int dc_u;            // k_spmv_dc: gathers in flight per row chunk (4 | 8)
 };
+
+// Dictionary-coded columns (host side, cgx_solver.cpp): the distinct column
+// offsets col[k] - row of a CSR matrix, first-seen order, and one code byte per
+// nonzero.  Returns the dictionary size (1..256), or 0 when the matrix has
+// more than 256 distinct offsets (or no nonzeros): then it stays plain CSR.
+int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict,
+                    unsigned char *code);
+// Dictionary capacity the SpMV kernel is instantiated for.
+inline int dict_cap(int ndict) { return ndict <= 64 ? 64 : 256; }
 
 inline int spmv_sell_grid(int nslices) { return (nslices + 3) / 4; }
 

@@ -1137,6 +1137,165 @@ void launch_eng(const SpmvArgs<double> &b, int g, hipStream_t st) {
   else hipLaunchKernelGGL((k_spmv_eng<false, false, NC, S, D, REG>), dim3(g), blk, 0, st, b);
 }
 
+// Dictionary-coded columns (CSR-DC).  A matrix whose nonzeros use at most 256
+// distinct column offsets col - row (every stencil, every banded matrix of
+// half-bandwidth < 128) stores one code byte per nonzero instead of a 4-byte
+// column: col[k] = row + dict[code[k]].  The stream per nonzero drops from
+// 12 to 9 bytes (fp64); C3: 281 -> 70 MB of the SpMV's 1045.  Everything
+// else is k_spmv_dma: one 64-row block per wave, val and code windows land in
+// the wave's LDS slice by LDS-DMA, lane t sums row t from LDS sequentially in
+// column order (the reference's order, mv_ops.c:190-194), so y is bit-identical
+// to the CSR kernels'.  The dictionary is copied into each wave's LDS slice
+// (ND/64 L2-resident loads per lane) and decoded with one LDS read per entry.
+// The smaller slice (4.9 KiB instead of 6 KiB at CAPW 512) also lets 8
+// workgroups (32 waves, the hardware limit) share a CU instead of 6.
+template <typename T, int U>
+__device__ __forceinline__ T row_sum_dc(const T *__restrict__ x, int row, const T *lval,
+                                        const unsigned char *lcode, const int *ldict,
+                                        int jb, int je, T acc) {
+  for (int j = jb; j < je; j += U) {
+    const int cnt = min(U, je - j);
+    int code[U];
+    T vv[U], xx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = u < cnt ? j + u : j;  // clamped: every LDS read is valid
+      code[u] = lcode[idx];
+      vv[u] = lval[idx];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) xx[u] = x[u < cnt ? row + ldict[code[u]] : 0];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const T prod = vv[u] * xx[u];
+      acc = acc + (u < cnt ? prod : T(0));  // +0 never changes the sum
+    }
+  }
+  return acc;
+}
+
+template <typename T, int WPB, int CAPW, int ND, bool EPI, bool NT, int U>
+__global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
+  constexpr int AUX = NT ? 2 : 0;
+  static_assert(CAPW % 4 == 0 && ND % kWave == 0, "window / dictionary");
+  // code window: starts at k0 & ~15 (16-B DMA granules), so up to 15 more
+  // bytes than the val window in front
+  constexpr int CAPC = (CAPW + 16 + 15) & ~15;
+  __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
+  __shared__ __attribute__((aligned(16))) unsigned char lcode_all[WPB * CAPC];
+  __shared__ int ldict_all[WPB * ND];
+  __shared__ double red[WPB];
+  if (a.done && *a.done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  T *lval = lval_all + wid * CAPW;
+  unsigned char *lcode = lcode_all + wid * CAPC;
+  int *ldict = ldict_all + wid * ND;
+  const int wb = xcd_block(a.xcd) * WPB + wid;
+  double dot = 0.0;
+  if (wb < a.nblk) {
+    int dv[ND / kWave];
+#pragma unroll
+    for (int i = 0; i < ND / kWave; ++i) dv[i] = a.dict[i * kWave + lane];
+    const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : a.blk_first + wb);
+    const int r0 = __builtin_amdgcn_readfirstlane(a.blk_row[rb]);
+    const int nr = __builtin_amdgcn_readfirstlane(a.blk_row[rb + 1]) - r0;
+    const int k0 = __builtin_amdgcn_readfirstlane(a.blk_k[rb]);
+    const int k1 = __builtin_amdgcn_readfirstlane(a.blk_k[rb + 1]);
+    const int kb = k0 & ~3;   // val window: 16-B aligned for double and float
+    const int kc = k0 & ~15;  // code window: 16-B aligned bytes
+    const bool fits = k1 - kb <= CAPW;
+    if (fits) {
+      constexpr int EV = 16 / sizeof(T);
+      const int m = k1 - kb;
+#pragma unroll
+      for (int i = 0; i < (int)((CAPW * sizeof(T) + 1023) / 1024); ++i)
+        if ((i * kWave + lane) * EV < m)
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(a.val + kb + i * kWave * EV + lane * EV),
+              (lds_void *)(lval + i * kWave * EV), 16, 0, AUX);
+      const int mc = k1 - kc;
+#pragma unroll
+      for (int i = 0; i < (CAPC + 1023) / 1024; ++i)
+        if ((i * kWave + lane) * 16 < mc)
+          __builtin_amdgcn_global_load_lds(
+              (const void *)(a.code + kc + i * kWave * 16 + lane * 16),
+              (lds_void *)(lcode + i * kWave * 16), 16, 0, AUX);
+    }
+    int j0 = 0, j1 = 0;
+    T xrow = T(0);
+    T acc = T(0);
+    if (lane < nr) {
+      j0 = a.rp[r0 + lane];
+      j1 = a.rp[r0 + lane + 1];
+      if (EPI) xrow = a.x[r0 + lane];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < ND / kWave; ++i) ldict[i * kWave + lane] = dv[i];
+    wave_lds_sync();
+    if (fits) {
+      if (lane < nr)
+        acc = row_sum_dc<T, U>(a.x, r0 + lane, lval, lcode + (kb - kc),
+                               ldict, j0 - kb, j1 - kb, acc);
+    } else {
+      // a single row longer than the window (nr == 1): chunked, lane 0 keeps
+      // the sequential sum; codes decoded from memory
+      for (int c0 = k0; c0 < k1; c0 += CAPW) {
+        const int mm = min(CAPW, k1 - c0);
+        for (int t = lane; t < mm; t += kWave)
+          lval[t] = a.val[c0 + t] * a.x[r0 + ldict[a.code[c0 + t]]];
+        wave_lds_sync();
+        if (lane == 0)
+          for (int j = 0; j < mm; ++j) acc = acc + lval[j];
+        wave_lds_sync();
+      }
+    }
+    if (lane < nr) {
+      a.y[r0 + lane] = acc;
+      if (EPI) dot = (double)xrow * (double)acc;
+    }
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) s = s + red[w];
+      a.part[blockIdx.x] = s;
+    }
+  }
+}
+
+template <typename T, int CAPW, int ND>
+void launch_dc_nd(const SpmvArgs<T> &a, hipStream_t st) {
+  constexpr int WPB = 4;
+  const int g = (a.nblk + WPB - 1) / WPB;
+  const bool epi = a.part != nullptr;
+#define CGX_DC(E, N, UU) \
+  hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU>), dim3(g), dim3(WPB * kWave), 0, st, a)
+  if (a.dc_u == 4) {
+    if (epi && a.nt) CGX_DC(true, true, 4);
+    else if (epi) CGX_DC(true, false, 4);
+    else if (a.nt) CGX_DC(false, true, 4);
+    else CGX_DC(false, false, 4);
+  } else {
+    if (epi && a.nt) CGX_DC(true, true, 8);
+    else if (epi) CGX_DC(true, false, 8);
+    else if (a.nt) CGX_DC(false, true, 8);
+    else CGX_DC(false, false, 8);
+  }
+#undef CGX_DC
+}
+
+template <typename T, int CAPW>
+void launch_dc_w(const SpmvArgs<T> &a, hipStream_t st) {
+  if (a.ndict_cap <= 64) launch_dc_nd<T, CAPW, 64>(a, st);
+  else launch_dc_nd<T, CAPW, 256>(a, st);
+}
+
 // SELL-64 (sliced ELLPACK, one 64-row slice per wave, column-major inside the
 // slice): lane t owns row t of its slice and walks the row's nonzeros in
 // column order, so every load is a coalesced wave-wide line (val 512 B, col
@@ -1943,6 +2102,14 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
     return hipGetLastError();
   }
   if (a.nblk <= 0) return hipSuccess;
+  if (a.code) {  // dictionary-coded columns (k_spmv_dc)
+    if (a.bs != 64 || a.dma != 1 || a.x2 || a.yacc) return hipErrorInvalidValue;
+    if (sizeof(T) == 4) launch_dc_w<T, 1024>(a, st);
+    else if (a.capw == 328) launch_dc_w<T, 328>(a, st);
+    else if (a.capw == 0 || a.capw == 512) launch_dc_w<T, 512>(a, st);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (a.bs == 64 && a.dma == 5 && sizeof(T) == 8 && !a.blk_list && !a.x2) {  // DMA engine
     SpmvArgs<double> b;
     memcpy(&b, &a, sizeof b);

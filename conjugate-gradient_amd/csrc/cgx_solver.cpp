@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cgx_internal.h"
@@ -163,6 +164,81 @@ bool csr_to_sell64(int n, const int *rp, const int *col, const T *val,
   return true;
 }
 
+// Dictionary-coded columns (cgx_internal.h).  Two passes over the nonzeros,
+// each split over host threads by row ranges: (1) the distinct offsets
+// col - row, in small open-addressing sets, giving up past 256; (2) the code
+// bytes.  The dictionary is sorted, so it does not depend on the thread count.
+namespace {
+constexpr int kDcSlots = 1024;  // > 4 x 256: short probe chains
+inline unsigned dc_hash(int key) { return ((unsigned)key * 2654435761u) >> 22; }
+struct DcSet {
+  int key[kDcSlots];
+  short val[kDcSlots];
+  bool used[kDcSlots];
+  int count = 0;
+  DcSet() { memset(used, 0, sizeof used); }
+  // index of key, inserting it (-1 when full past 256 distinct keys)
+  int find_or_add(int k, bool add) {
+    unsigned h = dc_hash(k);
+    while (used[h]) {
+      if (key[h] == k) return val[h];
+      h = (h + 1) & (kDcSlots - 1);
+    }
+    if (!add || count == 256) return -1;
+    used[h] = true;
+    key[h] = k;
+    val[h] = (short)count;
+    return count++;
+  }
+};
+}  // namespace
+
+int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict,
+                    unsigned char *code) {
+  dict.clear();
+  if (n <= 0 || rp[n] <= 0) return 0;
+  const long long nnz = rp[n];
+  int nt = (int)std::min<long long>(16, std::max<long long>(1, nnz >> 22));
+  nt = std::max(1, std::min(nt, (int)std::thread::hardware_concurrency()));
+  auto row_begin = [&](int t) { return (int)((long long)n * t / nt); };
+  std::vector<DcSet> sets((size_t)nt);
+  std::vector<int> ok((size_t)nt, 1);
+  auto pass1 = [&](int t) {
+    DcSet &S = sets[(size_t)t];
+    for (int r = row_begin(t); r < row_begin(t + 1) && ok[(size_t)t]; ++r)
+      for (int k = rp[r]; k < rp[r + 1]; ++k)
+        if (S.find_or_add(col[k] - r, true) < 0) {
+          ok[(size_t)t] = 0;
+          break;
+        }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(pass1, t);
+  pass1(0);
+  for (auto &x : th) x.join();
+  th.clear();
+  DcSet all;
+  for (int t = 0; t < nt; ++t) {
+    if (!ok[(size_t)t]) return 0;
+    for (int h = 0; h < kDcSlots; ++h)
+      if (sets[(size_t)t].used[h] && all.find_or_add(sets[(size_t)t].key[h], true) < 0) return 0;
+  }
+  for (int h = 0; h < kDcSlots; ++h)
+    if (all.used[h]) dict.push_back(all.key[h]);
+  std::sort(dict.begin(), dict.end());
+  DcSet idx;  // offset -> code (position in the sorted dictionary)
+  for (int k : dict) idx.find_or_add(k, true);
+  auto pass2 = [&](int t) {
+    for (int r = row_begin(t); r < row_begin(t + 1); ++r)
+      for (int k = rp[r]; k < rp[r + 1]; ++k)
+        code[k] = (unsigned char)idx.find_or_add(col[k] - r, false);
+  };
+  for (int t = 1; t < nt; ++t) th.emplace_back(pass2, t);
+  pass2(0);
+  for (auto &x : th) x.join();
+  return (int)dict.size();
+}
+
 int vec_grid_for(int n, int cus) {
   const long long vecs = (n + 1) / 2;
   long long g = (vecs + kVecBS - 1) / kVecBS;
@@ -207,6 +283,13 @@ struct cgx_solver {
   cgx::LapSpec lap{};
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
+  // dictionary-coded columns (k_spmv_dc; CGX_DC, default on where it applies):
+  // d_code[k] = index of col[k] - row in d_dict (ndict entries, 256 allocated)
+  bool want_dc = true;
+  int dc_u = 8;
+  int ndict = 0;
+  unsigned char *d_code = nullptr;
+  int *d_dict = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
   bool want_sell = false, sell = false;
   int *d_soff = nullptr, *d_slen = nullptr;
@@ -276,6 +359,9 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_blkk);
   dfree((void **)&s->d_soff);
   dfree((void **)&s->d_slen);
+  dfree((void **)&s->d_code);
+  dfree((void **)&s->d_dict);
+  s->ndict = 0;
   s->sell = false;
   s->nslices = 0;
   s->sell_elems = 0;
@@ -493,6 +579,28 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       }
     }
   }
+  if (s->want_dc && n > 0 && nnz > 0 && !gen && s->npanel == 1 && !s->sell &&
+      s->spmv_dma == 1 && s->spmv_bs == 64 && s->spmv_wpb == 4 &&
+      (s->spmv_capw == 0 || s->spmv_capw == 328)) {
+    std::vector<unsigned char> code((size_t)nnz);
+    std::vector<int> dict;
+    const int nd = build_col_codes(n, rp, col, dict, code.data());
+    if (nd > 0) {
+      if ((rc = dalloc(s, (void **)&s->d_code, nnz_pad)) ||
+          (rc = dalloc(s, (void **)&s->d_dict, 256 * 4))) {
+        free_matrix(s);
+        return rc;
+      }
+      dict.resize(256, 0);
+      CGX_HIP(hipMemsetAsync(s->d_code, 0, nnz_pad, s->stream));
+      CGX_HIP(hipMemcpyAsync(s->d_code, code.data(), (size_t)nnz, hipMemcpyHostToDevice,
+                             s->stream));
+      CGX_HIP(hipMemcpyAsync(s->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice,
+                             s->stream));
+      CGX_HIP(hipStreamSynchronize(s->stream));
+      s->ndict = nd;
+    }
+  }
   s->have_matrix = true;
   return 0;
 }
@@ -566,6 +674,7 @@ template <typename T>
 SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
                       bool with_done) {
   SpmvArgs<T> a;
+  memset(&a, 0, sizeof a);
   a.rp = s->d_rp;
   a.col = s->d_col;
   a.val = (const T *)s->d_val;
@@ -598,6 +707,12 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.yacc = nullptr;
   a.capw = s->spmv_capw;
   a.epi_last = s->epi_last;
+  if (s->ndict > 0) {
+    a.code = s->d_code;
+    a.dict = s->d_dict;
+    a.ndict_cap = dict_cap(s->ndict);
+    a.dc_u = s->dc_u;
+  }
   return a;
 }
 
@@ -1044,10 +1159,13 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->epi_last = cgx::env_int("CGX_SPMV_EPI_LAST", 0);
   s->vec_pf = cgx::env_int("CGX_VEC_PF", 1) != 0;  // C3 -1.7 us, C2 -0.44 us per iteration (sweep36), bit-identical
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
+  s->want_dc = cgx::env_int("CGX_DC", 1) != 0;
+  s->dc_u = cgx::env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {
     const char *l = getenv("CGX_LAYOUT");
     s->want_sell = l && strcmp(l, "sell") == 0;
+    if (l && (strcmp(l, "csr") == 0 || strcmp(l, "sell") == 0)) s->want_dc = false;
   }
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
@@ -1224,8 +1342,12 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
     info->spmv_iter_bytes = (double)s->nnz * (sv + 4) + 4.0 * s->npanel * (s->n + 1.0) +
                             (double)s->n * sv * (1.0 + 2.0 * s->npanel - 1.0);
   if (fused(s)) info->spmv_iter_bytes += 2.0 * s->n * sv;
+  if (s->ndict > 0)  // coded columns: one byte per nonzero + the dictionary
+    info->spmv_iter_bytes = (double)s->nnz * (sv + 1) + 4.0 * (s->n + 1) + 2.0 * s->n * sv +
+                            4.0 * s->ndict;
   info->device_bytes = s->dev_bytes;
   info->n_panels = s->npanel;
+  info->n_dict = s->ndict;
   return 0;
 }
 

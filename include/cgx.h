@@ -87,6 +87,9 @@ typedef struct {
                              column panels: + P row_ptrs, y round trips)    */
   size_t device_bytes;  /* device memory held by the solver                  */
   int n_panels;         /* column panels of the SpMV (1: plain CSR)          */
+  int n_dict;           /* dictionary-coded columns: distinct col - row
+                           offsets (1..256, one code byte per nonzero on the
+                           device); 0: plain 4-byte columns                  */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);

@@ -186,11 +186,15 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1u4"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
-    monkeypatch.setenv("CGX_SPMV_DMA", dma.rstrip("xw"))
+    monkeypatch.setenv("CGX_SPMV_DMA", dma[0])
+    if dma.endswith("c"):
+        monkeypatch.setenv("CGX_LAYOUT", "csr")
+    if dma.endswith("u4"):
+        monkeypatch.setenv("CGX_DC_U", "4")
     if dma.endswith("x"):
         monkeypatch.setenv("CGX_SPMV_XCD", "1")
     if dma.endswith("w"):
@@ -199,7 +203,105 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     x = np.random.default_rng(2).standard_normal(len(rp) - 1)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
+        # dictionary-coded columns on the default kernel (7 offsets), CSR otherwise
+        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1u4") else 0)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+
+
+def banded_spd(n, offsets, seed, f32=False):
+    """Symmetric banded SPD matrix with the given positive column offsets (and
+    their negatives), random values, diagonally dominant; CSR, rows ascending."""
+    rng = np.random.default_rng(seed)
+    offs = sorted(set([-o for o in offsets] + [0] + list(offsets)))
+    rows, cols = [], []
+    for o in offs:
+        r = np.arange(max(0, -o), min(n, n - o))
+        rows.append(r)
+        cols.append(r + o)
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    v = -rng.random(len(r))
+    order = np.lexsort((c, r))
+    r, c, v = r[order], c[order], v[order]
+    upper = c > r
+    vu = dict(zip(zip(r[upper].tolist(), c[upper].tolist()), v[upper].tolist()))
+    for i in range(len(r)):
+        if c[i] < r[i]:
+            v[i] = vu[(int(c[i]), int(r[i]))]
+    diag = np.zeros(n)
+    np.add.at(diag, r[c != r], np.abs(v[c != r]))
+    v[c == r] = diag[r[c == r]] + 1.0
+    rp = np.zeros(n + 1, dtype=np.int32)
+    np.add.at(rp, r + 1, 1)
+    rp = np.cumsum(rp).astype(np.int32)
+    if f32:
+        return rp, c.astype(np.int32), v.astype(np.float32)
+    return rp, c.astype(np.int32), v
+
+
+@pytest.mark.parametrize("u", ["4", "8"])
+@pytest.mark.parametrize("capw", ["", "328", "456"])
+def test_dictionary_coded_columns_bit_exact(u, capw, monkeypatch):
+    """CSR-DC (k_spmv_dc): selected exactly when the matrix has <= 256
+    distinct column offsets col - row, and bit-identical to the oracle's
+    sequential row sums (fp64 and fp32, 64- and 256-entry dictionaries,
+    adaptive 328/512 windows; 456 keeps plain CSR)."""
+    monkeypatch.setenv("CGX_DC_U", u)
+    if capw:
+        monkeypatch.setenv("CGX_SPMV_CAPW", capw)
+    rng = np.random.default_rng(5)
+    cases = [("lap3d_12", None), ("lap2d_32", None), ("dense128", None)]
+    with cgx.Solver(0) as s:
+        for name, _ in cases:
+            g = H.load_golden(name)
+            s.set_matrix(g["row_ptr"], g["col"], g["val"])
+            nd = s.info()["n_dict"]
+            want = len(np.unique(g["col"] - np.repeat(np.arange(len(g["row_ptr"]) - 1),
+                                                      np.diff(g["row_ptr"]))))
+            assert nd == (0 if capw == "456" else want), name
+            x = rng.standard_normal(len(g["row_ptr"]) - 1)
+            assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(g["row_ptr"], g["col"], g["val"], x))
+            assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"])
+        # 127 positive offsets -> 255 distinct: the 256-entry dictionary
+        offs = sorted(rng.choice(np.arange(1, 3000), 127, replace=False).tolist())
+        rp, col, val = banded_spd(5000, offs, 7)
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_dict"] == (0 if capw == "456" else 255)
+        x = rng.standard_normal(5000)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        # 257 distinct offsets: stays plain CSR, still bit-exact
+        rp, col, val = banded_spd(3000, list(range(1, 129)), 8)
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_dict"] == 0
+        x = rng.standard_normal(3000)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        # fp32 banded
+        rp, col, v32 = banded_spd(6000, [1, 77, 500], 9, f32=True)
+        s.set_matrix(rp, col, v32)
+        assert s.info()["n_dict"] == 7  # fp32 windows are not resized: CGX_SPMV_CAPW is fp64-only
+        x32 = rng.standard_normal(6000).astype(np.float32)
+        assert np.array_equal(s.spmv(x32).view(np.uint32),
+                              H.o_spmv_f32(rp, col, v32, x32).view(np.uint32))
+
+
+def test_dictionary_coded_cg_identical_to_csr(monkeypatch):
+    """The coded layout changes only how columns are stored: a CG run is
+    bit-identical to the plain-CSR run (x and the r.r history)."""
+    g = H.load_golden("lap3d_12")
+    out = {}
+    for layout in ("csr", "auto"):
+        if layout == "csr":
+            monkeypatch.setenv("CGX_LAYOUT", "csr")
+        else:
+            monkeypatch.delenv("CGX_LAYOUT", raising=False)
+        with cgx.Solver(0) as s:
+            s.set_matrix(g["row_ptr"], g["col"], g["val"])
+            assert (s.info()["n_dict"] > 0) == (layout == "auto")
+            s.set_rhs(g["b"])
+            s.run(40)
+            out[layout] = (s.x(), s.history(41))
+    assert H.same_bits_or_both_nan(out["csr"][0], out["auto"][0])
+    assert H.same_bits_or_both_nan(out["csr"][1], out["auto"][1])
 
 
 # -------------------------------------------------------- mv_ops.h op list
