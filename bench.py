@@ -231,7 +231,7 @@ def main():
         s.set_rhs(sysm["b"])
         dinfo = s.info()
         info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"],
-                    spmv_iter_bytes=dinfo["spmv_bytes"])
+                    spmv_iter_bytes=dinfo["spmv_iter_bytes"], n_dict=dinfo["n_dict"])
     else:
         s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
@@ -263,14 +263,24 @@ def main():
         _, spmv_ms = s.bench_run(args.steps, spmv_events=True)
     else:
         _, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
+    # achieved: the bytes the SpMV must move in the layout it runs on (coded
+    # columns: 1 byte per nonzero instead of 4) over its measured time; the
+    # CSR-equivalent rate (SURVEY.md 8d's B_spmv over the same time) beside it
     achieved = info["spmv_iter_bytes"] / (spmv_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload, alg)
+    nd = info.get("n_dict", 0)
+    label = spmv_kernel_label(len(sysm["col"]) * (4 + sysm["val"].itemsize))
+    if nd:
+        label = label.replace("k_spmv_dma (LDS-DMA CSR-stream",
+                              f"k_spmv_dc (LDS-DMA CSR-stream, dictionary-coded columns: "
+                              f"{nd} offsets, 1 B/nnz")
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                    traffic=traffic,
-                    kernel=spmv_kernel_label(len(sysm["col"]) * (4 + sysm["val"].itemsize)),
+                    traffic=traffic, kernel=label,
                     spmv_us=round(spmv_ms * 1e3, 2),
-                    algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]))
+                    algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
+                    csr_bytes_per_launch=int(info["spmv_bytes"]),
+                    csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1))
 
     # on-box HBM ceilings: STREAM triad (1/3 writes) and a
     # read-only stream, 512 MiB arrays.  The SpMV is 92% reads (its only

@@ -55,7 +55,8 @@ class CgxDistStats(ctypes.Structure):
                 ("nnz", ctypes.c_int), ("interior_blocks", ctypes.c_int),
                 ("boundary_blocks", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
                 ("iter_bytes", ctypes.c_double), ("halo_bytes", ctypes.c_double),
-                ("device_bytes", ctypes.c_size_t)]
+                ("device_bytes", ctypes.c_size_t), ("spmv_iter_bytes", ctypes.c_double),
+                ("n_dict", ctypes.c_int)]
 
 
 _MVP = ctypes.POINTER(MvSparse)

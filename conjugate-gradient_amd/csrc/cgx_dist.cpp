@@ -67,6 +67,12 @@ struct cgx_dist {
   int vec = 4, wpb = 4;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   int *d_list_int = nullptr, *d_list_bnd = nullptr;
+  // dictionary-coded columns (k_spmv_dc), as the single-GPU solver: the
+  // local numbering keeps them (a slab's ghosts sit at constant offsets)
+  unsigned char *d_code = nullptr;
+  int *d_dict = nullptr;
+  unsigned char *d_rlen = nullptr;  // byte row lengths (rows <= 255 entries)
+  int ndict = 0;
   int n_int = 0, n_bnd = 0, g_int = 0, g_bnd = 0;
   // interior / boundary row blocks as contiguous runs {first, count} when
   // there are few of them (slab partitions: 1 interior + 2 boundary runs);
@@ -134,6 +140,8 @@ void dfree(P **p) {
   *p = nullptr;
 }
 
+bool dc_wanted(const cgx_dist *d);
+
 void free_system(cgx_dist *d) {
   if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
   d->gexec = nullptr;
@@ -142,6 +150,8 @@ void free_system(cgx_dist *d) {
   dfree(&d->d_b); dfree(&d->d_x); dfree(&d->d_r); dfree(&d->d_p);
   dfree(&d->d_s); dfree(&d->d_w); dfree(&d->d_send_idx); dfree(&d->d_sendbuf);
   dfree(&d->d_pa); dfree(&d->d_pb); dfree(&d->d_hist);
+  dfree(&d->d_code); dfree(&d->d_dict); dfree(&d->d_rlen);
+  d->ndict = 0;
   d->hist_alloc = 0;
   if (d->part) cgx_part_destroy(d->part);
   d->part = nullptr;
@@ -276,6 +286,31 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
   }
   CGX_HIP(hipMemcpyAsync(d->d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
   CGX_HIP(hipMemcpyAsync(d->d_blkk, blkk.data(), blkk.size() * 4, hipMemcpyHostToDevice, st));
+  if (n_loc > 0 && nnz > 0 && dc_wanted(d)) {
+    std::vector<unsigned char> code((size_t)nnz);
+    std::vector<int> dict;
+    const int nd = build_col_codes(n_loc, rp, col_local.data(), dict, code.data());
+    if (nd > 0) {
+      if ((rc = dalloc(d, &d->d_code, nnz_pad)) || (rc = dalloc(d, &d->d_dict, 256 * 4))) {
+        free_system(d);
+        return rc;
+      }
+      dict.resize(256, 0);
+      CGX_HIP(hipMemsetAsync(d->d_code, 0, nnz_pad, st));
+      CGX_HIP(hipMemcpyAsync(d->d_code, code.data(), (size_t)nnz, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice, st));
+      std::vector<unsigned char> rl((size_t)n_loc);
+      if (env_int("CGX_DC_RLEN", 1) && build_row_lengths(n_loc, rp, rl.data())) {
+        if ((rc = dalloc(d, &d->d_rlen, (size_t)n_loc + 64))) {
+          free_system(d);
+          return rc;
+        }
+        CGX_HIP(hipMemcpyAsync(d->d_rlen, rl.data(), (size_t)n_loc, hipMemcpyHostToDevice, st));
+      }
+      CGX_HIP(hipStreamSynchronize(st));  // the host vectors go out of scope
+      d->ndict = nd;
+    }
+  }
   if (!lint.empty())
     CGX_HIP(hipMemcpyAsync(d->d_list_int, lint.data(), lint.size() * 4, hipMemcpyHostToDevice, st));
   if (!lbnd.empty())
@@ -408,6 +443,13 @@ int ensure_connected(Group *g) {
 
 // ---------------------------------------------------------- phase helpers
 
+// Coded columns on the default LDS-DMA kernel unless CGX_DC=0 / CGX_LAYOUT=csr.
+bool dc_wanted(const cgx_dist *d) {
+  const char *l = getenv("CGX_LAYOUT");
+  return d->wpb == 4 && env_int("CGX_SPMV_DMA", 1) == 1 && env_int("CGX_DC", 1) != 0 &&
+         !(l && strcmp(l, "csr") == 0);
+}
+
 SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   SpmvArgs<double> a;
   memset(&a, 0, sizeof a);
@@ -434,6 +476,13 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes;
   a.xcd = a.dma ? env_int("CGX_SPMV_XCD", 1) : 0;  // XCD-contiguous blocks, as the solver
   a.tk = TicketArgs{};
+  if (a.dma == 1 && d->ndict > 0) {
+    a.code = d->d_code;
+    a.dict = d->d_dict;
+    a.ndict_cap = dict_cap(d->ndict);
+    a.dc_u = env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
+    a.rlen = d->d_rlen;
+  }
   return a;
 }
 
@@ -910,6 +959,11 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   s->iter_bytes = s->spmv_bytes + 72.0 * d->n_loc;
   s->halo_bytes = 8.0 * (d->n_ghost + d->n_send);
   s->device_bytes = d->dev_bytes;
+  s->spmv_iter_bytes = d->ndict > 0 ? (double)d->nnz * 9.0 +
+                                          (d->d_rlen ? 1.0 * d->n_loc : 4.0 * (d->n_loc + 1)) +
+                                          16.0 * d->n_loc + 4.0 * d->ndict
+                                    : s->spmv_bytes;
+  s->n_dict = d->ndict;
   return 0;
 }
 

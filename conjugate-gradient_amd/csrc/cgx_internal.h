@@ -156,6 +156,10 @@ struct SpmvArgs {
   const int *dict;
   int ndict_cap;
   int dc_u;            // k_spmv_dc: gathers in flight per row chunk (4 | 8)
+  // k_spmv_dc: row lengths as one byte per row (every row <= 255 entries);
+  // the kernel derives row bounds from blk_k and a wave prefix sum instead
+  // of reading rp (nullptr: rp)
+  const unsigned char *rlen;
 };
 
 // Dictionary-coded columns (host side, cgx_solver.cpp): the distinct column
@@ -164,6 +168,9 @@ struct SpmvArgs {
 // more than 256 distinct offsets (or no nonzeros): then it stays plain CSR.
 int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict,
                     unsigned char *code);
+// Row lengths as bytes for k_spmv_dc; false (nothing written) when a row has
+// more than 255 entries.
+bool build_row_lengths(int n, const int *rp, unsigned char *rlen);
 // Dictionary capacity the SpMV kernel is instantiated for.
 inline int dict_cap(int ndict) { return ndict <= 64 ? 64 : 256; }
 

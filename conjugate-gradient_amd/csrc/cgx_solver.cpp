@@ -239,6 +239,13 @@ int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict
   return (int)dict.size();
 }
 
+bool build_row_lengths(int n, const int *rp, unsigned char *rlen) {
+  for (int r = 0; r < n; ++r)
+    if (rp[r + 1] - rp[r] > 255) return false;
+  for (int r = 0; r < n; ++r) rlen[r] = (unsigned char)(rp[r + 1] - rp[r]);
+  return true;
+}
+
 int vec_grid_for(int n, int cus) {
   const long long vecs = (n + 1) / 2;
   long long g = (vecs + kVecBS - 1) / kVecBS;
@@ -290,6 +297,8 @@ struct cgx_solver {
   int ndict = 0;
   unsigned char *d_code = nullptr;
   int *d_dict = nullptr;
+  bool want_rlen = true;           // CGX_DC_RLEN: byte row lengths instead of rp
+  unsigned char *d_rlen = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
   bool want_sell = false, sell = false;
   int *d_soff = nullptr, *d_slen = nullptr;
@@ -361,6 +370,7 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_slen);
   dfree((void **)&s->d_code);
   dfree((void **)&s->d_dict);
+  dfree((void **)&s->d_rlen);
   s->ndict = 0;
   s->sell = false;
   s->nslices = 0;
@@ -597,6 +607,19 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
                              s->stream));
       CGX_HIP(hipMemcpyAsync(s->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice,
                              s->stream));
+      std::vector<unsigned char> rl;
+      if (s->want_rlen) {
+        rl.resize((size_t)n);
+        if (!build_row_lengths(n, rp, rl.data())) rl.clear();
+      }
+      if (!rl.empty()) {
+        if ((rc = dalloc(s, (void **)&s->d_rlen, (size_t)n + 64))) {
+          free_matrix(s);
+          return rc;
+        }
+        CGX_HIP(hipMemcpyAsync(s->d_rlen, rl.data(), (size_t)n, hipMemcpyHostToDevice,
+                               s->stream));
+      }
       CGX_HIP(hipStreamSynchronize(s->stream));
       s->ndict = nd;
     }
@@ -712,6 +735,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
     a.dict = s->d_dict;
     a.ndict_cap = dict_cap(s->ndict);
     a.dc_u = s->dc_u;
+    a.rlen = s->d_rlen;
   }
   return a;
 }
@@ -1161,6 +1185,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->want_dc = cgx::env_int("CGX_DC", 1) != 0;
   s->dc_u = cgx::env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
+  s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {
     const char *l = getenv("CGX_LAYOUT");
@@ -1343,8 +1368,8 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                             (double)s->n * sv * (1.0 + 2.0 * s->npanel - 1.0);
   if (fused(s)) info->spmv_iter_bytes += 2.0 * s->n * sv;
   if (s->ndict > 0)  // coded columns: one byte per nonzero + the dictionary
-    info->spmv_iter_bytes = (double)s->nnz * (sv + 1) + 4.0 * (s->n + 1) + 2.0 * s->n * sv +
-                            4.0 * s->ndict;
+    info->spmv_iter_bytes = (double)s->nnz * (sv + 1) + (s->d_rlen ? 1.0 * s->n : 4.0 * (s->n + 1)) +
+                            2.0 * s->n * sv + 4.0 * s->ndict;
   info->device_bytes = s->dev_bytes;
   info->n_panels = s->npanel;
   info->n_dict = s->ndict;

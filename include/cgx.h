@@ -218,6 +218,11 @@ typedef struct {
   double spmv_bytes, iter_bytes;         /* algorithmic, this rank        */
   double halo_bytes;                     /* sent + received per iteration */
   size_t device_bytes;
+  double spmv_iter_bytes;                /* algorithmic bytes of the SpMV in
+                                            the layout it runs on (coded
+                                            columns: 1 byte per nonzero)  */
+  int n_dict;                            /* coded-column dictionary size,
+                                            0: plain 4-byte columns      */
 } cgx_dist_stats;
 
 /* Rank 0 creates the id and distributes it (e.g. torch.distributed). */

@@ -140,3 +140,27 @@ def test_history_after_buffer_growth():
         d.close()
     assert its == its2
     assert H.same_bits_or_both_nan(h, h2)
+
+
+@pytest.mark.parametrize("P", [1, 2, 4])
+def test_coded_columns_partitions_identical_to_csr(P, monkeypatch):
+    """Partitions of a Laplacian keep <= 256 distinct local column offsets
+    (owned rows: the stencil's; ghost columns: constant offsets per face), so
+    each part runs the coded-column SpMV; x and the history are bit-identical
+    to the plain-CSR layout."""
+    rp, col, val, b = system("lap3d")
+    out = {}
+    for layout in ("csr", "auto"):
+        if layout == "csr":
+            monkeypatch.setenv("CGX_LAYOUT", "csr")
+        else:
+            monkeypatch.delenv("CGX_LAYOUT", raising=False)
+        x, its, hist, stats = solve_local(rp, col, val, b, P, 50, 0.0)
+        if layout == "csr":
+            assert all(s["n_dict"] == 0 for s in stats)
+        else:
+            assert all(0 < s["n_dict"] <= 21 for s in stats)  # <= 7 stencil + 7 per ghost face
+            assert all(s["spmv_iter_bytes"] < s["spmv_bytes"] for s in stats)
+        out[layout] = (x, hist)
+    assert H.same_bits_or_both_nan(out["csr"][0], out["auto"][0])
+    assert H.same_bits_or_both_nan(out["csr"][1], out["auto"][1])

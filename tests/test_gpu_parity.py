@@ -186,7 +186,7 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1u4"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1u4", "1r0"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
@@ -195,6 +195,8 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
         monkeypatch.setenv("CGX_LAYOUT", "csr")
     if dma.endswith("u4"):
         monkeypatch.setenv("CGX_DC_U", "4")
+    if dma.endswith("r0"):
+        monkeypatch.setenv("CGX_DC_RLEN", "0")
     if dma.endswith("x"):
         monkeypatch.setenv("CGX_SPMV_XCD", "1")
     if dma.endswith("w"):
@@ -204,7 +206,7 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         # dictionary-coded columns on the default kernel (7 offsets), CSR otherwise
-        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1u4") else 0)
+        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1u4", "1r0") else 0)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
@@ -239,14 +241,17 @@ def banded_spd(n, offsets, seed, f32=False):
     return rp, c.astype(np.int32), v
 
 
+@pytest.mark.parametrize("rlen", ["1", "0"])
 @pytest.mark.parametrize("u", ["4", "8"])
 @pytest.mark.parametrize("capw", ["", "328", "456"])
-def test_dictionary_coded_columns_bit_exact(u, capw, monkeypatch):
+def test_dictionary_coded_columns_bit_exact(u, capw, rlen, monkeypatch):
     """CSR-DC (k_spmv_dc): selected exactly when the matrix has <= 256
     distinct column offsets col - row, and bit-identical to the oracle's
     sequential row sums (fp64 and fp32, 64- and 256-entry dictionaries,
-    adaptive 328/512 windows; 456 keeps plain CSR)."""
+    adaptive 328/512 windows; 456 keeps plain CSR; row bounds from byte row
+    lengths or from row_ptr)."""
     monkeypatch.setenv("CGX_DC_U", u)
+    monkeypatch.setenv("CGX_DC_RLEN", rlen)
     if capw:
         monkeypatch.setenv("CGX_SPMV_CAPW", capw)
     rng = np.random.default_rng(5)
@@ -274,6 +279,18 @@ def test_dictionary_coded_columns_bit_exact(u, capw, monkeypatch):
         s.set_matrix(rp, col, val)
         assert s.info()["n_dict"] == 0
         x = rng.standard_normal(3000)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        # 256 distinct offsets, one row of 256 entries (> 255: row_ptr bounds),
+        # empty rows, non-symmetric
+        n = 700
+        rows = [list(range(0, 256))] + [[] if r % 5 == 0 else [r] for r in range(1, n)]
+        rp = np.zeros(n + 1, dtype=np.int32)
+        rp[1:] = np.cumsum([len(c) for c in rows])
+        col = np.array([c for cs in rows for c in cs], dtype=np.int32)
+        val = rng.standard_normal(len(col))
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_dict"] == (0 if capw == "456" else 256)
+        x = rng.standard_normal(n)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
         # fp32 banded
         rp, col, v32 = banded_spd(6000, [1, 77, 500], 9, f32=True)
