@@ -73,6 +73,7 @@ struct cgx_dist {
   int *d_dict = nullptr;
   unsigned char *d_rlen = nullptr;  // byte row lengths (rows <= 255 entries)
   int ndict = 0;
+  int code_bits = 8;                 // 4: nibble codes (<= 16 offsets)
   int n_int = 0, n_bnd = 0, g_int = 0, g_bnd = 0;
   // interior / boundary row blocks as contiguous runs {first, count} when
   // there are few of them (slab partitions: 1 interior + 2 boundary runs);
@@ -296,8 +297,14 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
         return rc;
       }
       dict.resize(256, 0);
+      d->code_bits = nd <= 16 && env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;
+      size_t code_bytes = (size_t)nnz;
+      if (d->code_bits == 4) {
+        pack_nibbles(nnz, code.data(), code.data());
+        code_bytes = ((size_t)nnz + 1) / 2;
+      }
       CGX_HIP(hipMemsetAsync(d->d_code, 0, nnz_pad, st));
-      CGX_HIP(hipMemcpyAsync(d->d_code, code.data(), (size_t)nnz, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d->d_code, code.data(), code_bytes, hipMemcpyHostToDevice, st));
       CGX_HIP(hipMemcpyAsync(d->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice, st));
       std::vector<unsigned char> rl((size_t)n_loc);
       if (env_int("CGX_DC_RLEN", 1) && build_row_lengths(n_loc, rp, rl.data())) {
@@ -482,6 +489,7 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
     a.ndict_cap = dict_cap(d->ndict);
     a.dc_u = env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
     a.rlen = d->d_rlen;
+    a.code_bits = d->code_bits;
   }
   return a;
 }
@@ -959,7 +967,7 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   s->iter_bytes = s->spmv_bytes + 72.0 * d->n_loc;
   s->halo_bytes = 8.0 * (d->n_ghost + d->n_send);
   s->device_bytes = d->dev_bytes;
-  s->spmv_iter_bytes = d->ndict > 0 ? (double)d->nnz * 9.0 +
+  s->spmv_iter_bytes = d->ndict > 0 ? (double)d->nnz * (8.0 + d->code_bits / 8.0) +
                                           (d->d_rlen ? 1.0 * d->n_loc : 4.0 * (d->n_loc + 1)) +
                                           16.0 * d->n_loc + 4.0 * d->ndict
                                     : s->spmv_bytes;

@@ -160,6 +160,7 @@ struct SpmvArgs {
   // the kernel derives row bounds from blk_k and a wave prefix sum instead
   // of reading rp (nullptr: rp)
   const unsigned char *rlen;
+  int code_bits;       // k_spmv_dc: 8 (byte codes) or 4 (nibbles, <= 16 offsets)
 };
 
 // Dictionary-coded columns (host side, cgx_solver.cpp): the distinct column
@@ -168,6 +169,9 @@ struct SpmvArgs {
 // more than 256 distinct offsets (or no nonzeros): then it stays plain CSR.
 int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict,
                     unsigned char *code);
+// Nibble codes (dictionaries of <= 16 offsets): entry k in bits 4*(k&1) of
+// byte k/2; out holds (nnz + 1) / 2 bytes.
+void pack_nibbles(long long nnz, const unsigned char *code, unsigned char *out);
 // Row lengths as bytes for k_spmv_dc; false (nothing written) when a row has
 // more than 255 entries.
 bool build_row_lengths(int n, const int *rp, unsigned char *rlen);

@@ -1149,9 +1149,18 @@ void launch_eng(const SpmvArgs<double> &b, int g, hipStream_t st) {
 // (ND/64 L2-resident loads per lane) and decoded with one LDS read per entry.
 // The smaller slice (4.9 KiB instead of 6 KiB at CAPW 512) also lets 8
 // workgroups (32 waves, the hardware limit) share a CU instead of 6.
-template <typename T, int U>
+// Code of entry i of a code window: a byte (CB 8) or a nibble (CB 4, entry
+// i in bits 4*(i&1) of byte i/2; dictionaries of <= 16 offsets).
+template <int CB>
+__device__ __forceinline__ int dc_code(const unsigned char *c, int i) {
+  if (CB == 8) return c[i];
+  return (c[i >> 1] >> ((i & 1) << 2)) & 15;
+}
+
+// co: position of the val window's first entry in the code window
+template <typename T, int U, int CB>
 __device__ __forceinline__ T row_sum_dc(const T *__restrict__ x, int row, const T *lval,
-                                        const unsigned char *lcode, const int *ldict,
+                                        const unsigned char *lcode, int co, const int *ldict,
                                         int jb, int je, T acc) {
   for (int j = jb; j < je; j += U) {
     const int cnt = min(U, je - j);
@@ -1160,7 +1169,7 @@ __device__ __forceinline__ T row_sum_dc(const T *__restrict__ x, int row, const 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = u < cnt ? j + u : j;  // clamped: every LDS read is valid
-      code[u] = lcode[idx];
+      code[u] = dc_code<CB>(lcode, idx + co);
       vv[u] = lval[idx];
     }
 #pragma unroll
@@ -1187,13 +1196,14 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // RL: row bounds from one byte per row (a.rlen, rows of <= 255 entries) and a
 // wave prefix sum from the block's first nonzero, instead of two int32
 // row_ptr reads per row (C3: 40 -> 10 MB per SpMV).
-template <typename T, int WPB, int CAPW, int ND, bool EPI, bool NT, int U, bool RL>
+template <typename T, int WPB, int CAPW, int ND, bool EPI, bool NT, int U, bool RL, int CB>
 __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
   constexpr int AUX = NT ? 2 : 0;
-  static_assert(CAPW % 4 == 0 && ND % kWave == 0, "window / dictionary");
-  // code window: starts at k0 & ~15 (16-B DMA granules), so up to 15 more
-  // bytes than the val window in front
-  constexpr int CAPC = (CAPW + 16 + 15) & ~15;
+  static_assert(CAPW % 4 == 0 && ND % kWave == 0 && (CB == 8 || CB == 4), "window / dictionary");
+  // code window: starts at the 16-B granule holding entry k0 (KA entries per
+  // granule), so up to KA - 1 more entries than the val window in front
+  constexpr int KA = 16 * 8 / CB;
+  constexpr int CAPC = ((CAPW + KA) * CB / 8 + 15) & ~15;
   __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) unsigned char lcode_all[WPB * CAPC];
   __shared__ int ldict_all[WPB * ND];
@@ -1216,7 +1226,7 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
     const int k0 = __builtin_amdgcn_readfirstlane(a.blk_k[rb]);
     const int k1 = __builtin_amdgcn_readfirstlane(a.blk_k[rb + 1]);
     const int kb = k0 & ~3;   // val window: 16-B aligned for double and float
-    const int kc = k0 & ~15;  // code window: 16-B aligned bytes
+    const int kc = k0 & ~(KA - 1);  // code window: 16-B aligned
     const bool fits = k1 - kb <= CAPW;
     if (fits) {
       constexpr int EV = 16 / sizeof(T);
@@ -1227,12 +1237,13 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
           __builtin_amdgcn_global_load_lds(
               (const void *)(a.val + kb + i * kWave * EV + lane * EV),
               (lds_void *)(lval + i * kWave * EV), 16, 0, AUX);
-      const int mc = k1 - kc;
+      const int mc = ((k1 - kc) * CB + 7) / 8;  // code bytes
+      const unsigned char *cbase = a.code + (size_t)kc * CB / 8;
 #pragma unroll
       for (int i = 0; i < (CAPC + 1023) / 1024; ++i)
         if ((i * kWave + lane) * 16 < mc)
           __builtin_amdgcn_global_load_lds(
-              (const void *)(a.code + kc + i * kWave * 16 + lane * 16),
+              (const void *)(cbase + i * kWave * 16 + lane * 16),
               (lds_void *)(lcode + i * kWave * 16), 16, 0, AUX);
     }
     int j0 = 0, j1 = 0, len = 0;
@@ -1257,15 +1268,15 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
     wave_lds_sync();
     if (fits) {
       if (lane < nr)
-        acc = row_sum_dc<T, U>(a.x, r0 + lane, lval, lcode + (kb - kc),
-                               ldict, j0 - kb, j1 - kb, acc);
+        acc = row_sum_dc<T, U, CB>(a.x, r0 + lane, lval, lcode, kb - kc, ldict, j0 - kb,
+                                   j1 - kb, acc);
     } else {
       // a single row longer than the window (nr == 1): chunked, lane 0 keeps
       // the sequential sum; codes decoded from memory
       for (int c0 = k0; c0 < k1; c0 += CAPW) {
         const int mm = min(CAPW, k1 - c0);
         for (int t = lane; t < mm; t += kWave)
-          lval[t] = a.val[c0 + t] * a.x[r0 + ldict[a.code[c0 + t]]];
+          lval[t] = a.val[c0 + t] * a.x[r0 + ldict[dc_code<CB>(a.code, c0 + t)]];
         wave_lds_sync();
         if (lane == 0)
           for (int j = 0; j < mm; ++j) acc = acc + lval[j];
@@ -1297,11 +1308,17 @@ void launch_dc_nd(const SpmvArgs<T> &a, hipStream_t st) {
   const bool epi = a.part != nullptr;
 #define CGX_DC(E, N, UU)                                                                   \
   do {                                                                                     \
-    if (a.rlen)                                                                            \
-      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, true>), dim3(g),           \
+    if (a.rlen && a.code_bits == 4)                                                        \
+      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, true, 4>), dim3(g),        \
+                         dim3(WPB * kWave), 0, st, a);                                     \
+    else if (a.rlen)                                                                       \
+      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, true, 8>), dim3(g),        \
+                         dim3(WPB * kWave), 0, st, a);                                     \
+    else if (a.code_bits == 4)                                                             \
+      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, false, 4>), dim3(g),       \
                          dim3(WPB * kWave), 0, st, a);                                     \
     else                                                                                   \
-      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, false>), dim3(g),          \
+      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, false, 8>), dim3(g),       \
                          dim3(WPB * kWave), 0, st, a);                                     \
   } while (0)
   if (a.dc_u == 4) {

@@ -239,6 +239,12 @@ int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict
   return (int)dict.size();
 }
 
+void pack_nibbles(long long nnz, const unsigned char *code, unsigned char *out) {
+  for (long long i = 0; i + 1 < nnz; i += 2)
+    out[i >> 1] = (unsigned char)(code[i] | (code[i + 1] << 4));
+  if (nnz & 1) out[nnz >> 1] = code[nnz - 1];
+}
+
 bool build_row_lengths(int n, const int *rp, unsigned char *rlen) {
   for (int r = 0; r < n; ++r)
     if (rp[r + 1] - rp[r] > 255) return false;
@@ -298,6 +304,8 @@ struct cgx_solver {
   unsigned char *d_code = nullptr;
   int *d_dict = nullptr;
   bool want_rlen = true;           // CGX_DC_RLEN: byte row lengths instead of rp
+  int want_bits = 8;               // CGX_DC_BITS=4: nibble codes when <= 16 offsets
+  int code_bits = 8;
   unsigned char *d_rlen = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
   bool want_sell = false, sell = false;
@@ -602,8 +610,14 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
         return rc;
       }
       dict.resize(256, 0);
+      s->code_bits = nd <= 16 && s->want_bits == 4 ? 4 : 8;
+      size_t code_bytes = (size_t)nnz;
+      if (s->code_bits == 4) {  // in place: byte i/2 is written after entry i is read
+        pack_nibbles(nnz, code.data(), code.data());
+        code_bytes = ((size_t)nnz + 1) / 2;
+      }
       CGX_HIP(hipMemsetAsync(s->d_code, 0, nnz_pad, s->stream));
-      CGX_HIP(hipMemcpyAsync(s->d_code, code.data(), (size_t)nnz, hipMemcpyHostToDevice,
+      CGX_HIP(hipMemcpyAsync(s->d_code, code.data(), code_bytes, hipMemcpyHostToDevice,
                              s->stream));
       CGX_HIP(hipMemcpyAsync(s->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice,
                              s->stream));
@@ -736,6 +750,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
     a.ndict_cap = dict_cap(s->ndict);
     a.dc_u = s->dc_u;
     a.rlen = s->d_rlen;
+    a.code_bits = s->code_bits;
   }
   return a;
 }
@@ -1186,6 +1201,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->want_dc = cgx::env_int("CGX_DC", 1) != 0;
   s->dc_u = cgx::env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
   s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
+  s->want_bits = cgx::env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;  // nibbles: neutral at C3 (dc3 sweep)
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {
     const char *l = getenv("CGX_LAYOUT");
@@ -1368,7 +1384,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                             (double)s->n * sv * (1.0 + 2.0 * s->npanel - 1.0);
   if (fused(s)) info->spmv_iter_bytes += 2.0 * s->n * sv;
   if (s->ndict > 0)  // coded columns: one byte per nonzero + the dictionary
-    info->spmv_iter_bytes = (double)s->nnz * (sv + 1) + (s->d_rlen ? 1.0 * s->n : 4.0 * (s->n + 1)) +
+    info->spmv_iter_bytes = (double)s->nnz * (sv + s->code_bits / 8.0) + (s->d_rlen ? 1.0 * s->n : 4.0 * (s->n + 1)) +
                             2.0 * s->n * sv + 4.0 * s->ndict;
   info->device_bytes = s->dev_bytes;
   info->n_panels = s->npanel;
