@@ -186,7 +186,15 @@ int init_common(cgx_dist *d, int device) {
   d->graph_batch = env_int("CGX_GRAPH", 1) ? std::max(1, env_int("CGX_GRAPH_BATCH", 16)) : 0;
   CGX_HIP(hipSetDevice(device));
   CGX_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
-  CGX_HIP(hipStreamCreateWithFlags(&d->st_comm, hipStreamNonBlocking));
+  {
+    // halo traffic on a high-priority stream: its RCCL kernel is dispatched
+    // ahead of the interior SpMV's remaining workgroups, so the ghosts arrive
+    // while the interior rows are still being summed
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    CGX_HIP(hipStreamCreateWithPriority(&d->st_comm, hipStreamNonBlocking,
+                                        env_int("CGX_COMM_PRIO", 1) ? greatest : 0));
+  }
   CGX_HIP(hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums, hipEventDisableTiming));

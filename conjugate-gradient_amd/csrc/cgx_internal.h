@@ -233,6 +233,11 @@ __host__ __device__ inline long long lap_rp(long long i, const LapSpec &g) {
 
 hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
                                 hipStream_t st);
+// Device-side coded columns against a sorted dictionary (err |= 1 on a miss).
+hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dict, int nd,
+                            unsigned char *code, int *err, hipStream_t st);
+// The column offsets col - row a generated Laplacian can hold, sorted.
+std::vector<int> lap_offsets(const LapSpec &g);
 template <typename T>
 hipError_t launch_stencil(const LapSpec &g, int n, const T *x, T *y, double *part,
                           const int *done, int grid, hipStream_t st);

@@ -2463,6 +2463,36 @@ hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
   return hipGetLastError();
 }
 
+// Coded columns for a matrix already in device memory (the generated
+// Laplacian): row r's entries get the position of col - r in the sorted
+// dictionary; an offset missing from it raises *err.
+__global__ __launch_bounds__(256) void k_dc_encode(int n, const int *__restrict__ rp,
+                                                   const int *__restrict__ col,
+                                                   const int *__restrict__ dict, int nd,
+                                                   unsigned char *__restrict__ code,
+                                                   int *__restrict__ err) {
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < n; r += gridDim.x * 256) {
+    for (int k = rp[r]; k < rp[r + 1]; ++k) {
+      const int off = col[k] - r;
+      int lo = 0, hi = nd - 1;
+      while (lo < hi) {  // first entry >= off
+        const int mid = (lo + hi) >> 1;
+        if (dict[mid] < off) lo = mid + 1;
+        else hi = mid;
+      }
+      if (dict[lo] != off) atomicOr(err, 1);
+      code[k] = (unsigned char)lo;
+    }
+  }
+}
+
+hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dict, int nd,
+                            unsigned char *code, int *err, hipStream_t st) {
+  const int grid = std::max(1, std::min((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_dc_encode, dim3(grid), dim3(256), 0, st, n, rp, col, dict, nd, code, err);
+  return hipGetLastError();
+}
+
 // Matrix-free SpMV of the same operator: row r sums its products in the CSR
 // row's column order from 0 with the same values (-1 products are exact), so
 // y is bit-identical to the CSR SpMV.  Only x (once, coalesced along rows)

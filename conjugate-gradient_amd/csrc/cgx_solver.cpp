@@ -245,6 +245,17 @@ void pack_nibbles(long long nnz, const unsigned char *code, unsigned char *out) 
   if (nnz & 1) out[nnz >> 1] = code[nnz - 1];
 }
 
+std::vector<int> lap_offsets(const LapSpec &g) {
+  std::vector<int> d{0};
+  const int pl = g.nx * g.ny;
+  if (g.nx > 1) d.insert(d.end(), {-1, 1});
+  if (g.ny > 1) d.insert(d.end(), {-g.nx, g.nx});
+  if (g.dim == 3 && g.nz > 1) d.insert(d.end(), {-pl, pl});
+  std::sort(d.begin(), d.end());
+  d.erase(std::unique(d.begin(), d.end()), d.end());
+  return d;
+}
+
 bool build_row_lengths(int n, const int *rp, unsigned char *rlen) {
   for (int r = 0; r < n; ++r)
     if (rp[r + 1] - rp[r] > 255) return false;
@@ -597,12 +608,19 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       }
     }
   }
-  if (s->want_dc && n > 0 && nnz > 0 && !gen && s->npanel == 1 && !s->sell &&
+  if (s->want_dc && n > 0 && nnz > 0 && s->npanel == 1 && !s->sell &&
       s->spmv_dma == 1 && s->spmv_bs == 64 && s->spmv_wpb == 4 &&
       (s->spmv_capw == 0 || s->spmv_capw == 328)) {
-    std::vector<unsigned char> code((size_t)nnz);
+    std::vector<unsigned char> code;
     std::vector<int> dict;
-    const int nd = build_col_codes(n, rp, col, dict, code.data());
+    int nd;
+    if (gen) {  // generated on the device: the stencil's offsets, encoded there
+      dict = lap_offsets(*gen);
+      nd = (int)dict.size();
+    } else {
+      code.resize((size_t)nnz);
+      nd = build_col_codes(n, rp, col, dict, code.data());
+    }
     if (nd > 0) {
       if ((rc = dalloc(s, (void **)&s->d_code, nnz_pad)) ||
           (rc = dalloc(s, (void **)&s->d_dict, 256 * 4))) {
@@ -610,17 +628,32 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
         return rc;
       }
       dict.resize(256, 0);
-      s->code_bits = nd <= 16 && s->want_bits == 4 ? 4 : 8;
+      s->code_bits = nd <= 16 && s->want_bits == 4 && !gen ? 4 : 8;
       size_t code_bytes = (size_t)nnz;
       if (s->code_bits == 4) {  // in place: byte i/2 is written after entry i is read
         pack_nibbles(nnz, code.data(), code.data());
         code_bytes = ((size_t)nnz + 1) / 2;
       }
       CGX_HIP(hipMemsetAsync(s->d_code, 0, nnz_pad, s->stream));
-      CGX_HIP(hipMemcpyAsync(s->d_code, code.data(), code_bytes, hipMemcpyHostToDevice,
-                             s->stream));
       CGX_HIP(hipMemcpyAsync(s->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice,
                              s->stream));
+      if (gen) {
+        int *d_err = (int *)s->d_pb;  // scratch: partials are rewritten before use
+        CGX_HIP(hipMemsetAsync(d_err, 0, 4, s->stream));
+        CGX_HIP(launch_dc_encode(n, s->d_rp, s->d_col, s->d_dict, nd, s->d_code, d_err,
+                                 s->stream));
+        int err = 0;
+        CGX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, s->stream));
+        CGX_HIP(hipStreamSynchronize(s->stream));
+        if (err) {
+          set_error("internal: generated Laplacian has an offset outside its dictionary");
+          free_matrix(s);
+          return CGX_EINVAL;
+        }
+      } else {
+        CGX_HIP(hipMemcpyAsync(s->d_code, code.data(), code_bytes, hipMemcpyHostToDevice,
+                               s->stream));
+      }
       std::vector<unsigned char> rl;
       if (s->want_rlen) {
         rl.resize((size_t)n);

@@ -730,6 +730,17 @@ def test_column_panels_auto_c5():
         assert s.info()["n_panels"] == 1
 
 
+def lap_dict(dim, nx, ny, nz):
+    d = {0}
+    if nx > 1:
+        d |= {-1, 1}
+    if ny > 1:
+        d |= {-nx, nx}
+    if dim == 3 and nz > 1:
+        d |= {-nx * ny, nx * ny}
+    return sorted(d)
+
+
 @pytest.mark.parametrize("dim,shape", [(3, (12, 12, 12)), (3, (7, 5, 9)), (3, (1, 6, 4)),
                                        (2, (32, 32, 1)), (2, (17, 9, 1)), (3, (216, 216, 216))])
 def test_device_generated_laplacian_bit_exact(dim, shape):
@@ -742,6 +753,14 @@ def test_device_generated_laplacian_bit_exact(dim, shape):
         rp, col, val = s.matrix()
         assert np.array_equal(rp, host[0]) and np.array_equal(col, host[1])
         assert H.same_bits_or_both_nan(val, host[2])
+        # coded columns encoded on the device against the stencil's offsets
+        n = len(rp) - 1
+        offs = np.unique(col - np.repeat(np.arange(n), np.diff(rp)))
+        assert s.info()["n_dict"] == len(lap_dict(dim, nx, ny, nz))
+        assert set(offs.tolist()) <= set(lap_dict(dim, nx, ny, nz))
+        x = np.random.default_rng(6).standard_normal(n)
+        if n <= 200_000:
+            assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(*host, x))
         if len(rp) - 1 <= 2000:
             b = np.random.default_rng(4).standard_normal(len(rp) - 1)
             s.set_rhs(b)
@@ -788,6 +807,7 @@ def test_c4_full_size_spmv_device_generated():
     with cgx.Solver(0) as s:
         s.gen_laplacian(3, 400, 400, 400)
         assert s.info()["nnz"] == 447_040_000
+        assert s.info()["n_dict"] == 7  # coded columns, encoded on the device
         y = s.spmv(x)
     with cgx.Solver(0) as s:
         s.set_stencil(3, 400, 400, 400)
