@@ -293,6 +293,33 @@ def main():
 
     # matrix-free upper bound for the Laplacian runs -- the same
     # operator as a stencil (bit-identical SpMV), only x and y move
+    # the same solve with plain 4-byte CSR columns (CGX_LAYOUT=csr): the
+    # layout SURVEY.md 8d's B_spmv prices, measured beside the coded one
+    csr_plain = None
+    if world == 1 and not use_dist and info.get("n_dict", 0) > 0:
+        old_layout = os.environ.get("CGX_LAYOUT")
+        os.environ["CGX_LAYOUT"] = "csr"
+        try:
+            with cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS) as cs:
+                cs.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+                cs.set_rhs(sysm["b"])
+                cs.bench_prepare(args.warmup)
+                c_ms = cs.bench_run(args.steps, graph=True)[0]
+                _, c_spmv = cs.bench_run(args.steps, graph=False, spmv_events=True)
+                cinfo = cs.info()
+        finally:
+            if old_layout is None:
+                os.environ.pop("CGX_LAYOUT", None)
+            else:
+                os.environ["CGX_LAYOUT"] = old_layout
+        c_gbs = cinfo["spmv_iter_bytes"] / (c_spmv * 1e-3) / 1e9
+        csr_plain = dict(value=round(args.steps / (c_ms * 1e-3), 2), unit="it/s",
+                         spmv_us=round(c_spmv * 1e3, 2), spmv_gbs=round(c_gbs, 1),
+                         frac=round(c_gbs / HBM_PEAK_GBS, 4),
+                         kernel=spmv_kernel_label(len(sysm["col"]) * (4 + sysm["val"].itemsize)),
+                         note="same system, plain int32 CSR columns (CGX_LAYOUT=csr): "
+                              "B_spmv of SURVEY.md 8d")
+
     mf = None
     if world == 1 and wl["kind"] in ("lap3d", "lap2d"):
         with cgx.Solver(local_rank) as ms:
@@ -328,13 +355,17 @@ def main():
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz_local=int(len(sysm["col"])),
                     alg=alg, graph=not use_dist or world == 1,
                     parallelism=f"row-partition x{world}",
+                    layout=(f"CSR with dictionary-coded columns ({info['n_dict']} col-row "
+                            f"offsets, 1 B/nnz) + byte row lengths"
+                            if info.get("n_dict", 0) else "CSR (int32 columns)"),
                     halo_bytes_per_iter=(dinfo or {}).get("halo_bytes")),
         device_ms_per_step=round(dev_ms / args.steps, 4),
         # the C boundary takes host CSR buffers: one-time upload + plan, not in `value`
         upload_ms=round(upload_ms, 1),
         iter_bytes=int(info["iter_bytes"]),
         iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),
-        roofline=roofline, cpu_baseline=cpu, matrix_free_upper_bound=mf,
+        roofline=roofline, cpu_baseline=cpu, csr_plain=csr_plain,
+        matrix_free_upper_bound=mf,
     )
     if rank == 0:
         print(json.dumps(out), flush=True)
