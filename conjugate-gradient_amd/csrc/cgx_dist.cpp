@@ -66,6 +66,7 @@ struct cgx_dist {
   int row_begin = 0, n_loc = 0, n_ghost = 0, nnz = 0;
   int vec = 4, wpb = 4;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
+  int *d_blkrk = nullptr;  // (blk_row, blk_k) pairs for the coded-column kernel
   int *d_list_int = nullptr, *d_list_bnd = nullptr;
   // dictionary-coded columns (k_spmv_dc), as the single-GPU solver: the
   // local numbering keeps them (a slab's ghosts sit at constant offsets)
@@ -147,6 +148,7 @@ void free_system(cgx_dist *d) {
   if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
   d->gexec = nullptr;
   dfree(&d->d_rp); dfree(&d->d_col); dfree(&d->d_blk); dfree(&d->d_blkk);
+  dfree(&d->d_blkrk);
   dfree(&d->d_list_int); dfree(&d->d_list_bnd); dfree(&d->d_val);
   dfree(&d->d_b); dfree(&d->d_x); dfree(&d->d_r); dfree(&d->d_p);
   dfree(&d->d_s); dfree(&d->d_w); dfree(&d->d_send_idx); dfree(&d->d_sendbuf);
@@ -271,6 +273,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
       (rc = dalloc(d, &d->d_val, nnz_pad * 8)) ||
       (rc = dalloc(d, &d->d_blk, blk.size() * 4)) ||
       (rc = dalloc(d, &d->d_blkk, blk.size() * 4)) ||
+      (rc = dalloc(d, &d->d_blkrk, blk.size() * 8)) ||
       (rc = dalloc(d, &d->d_list_int, (lint.size() + 1) * 4)) ||
       (rc = dalloc(d, &d->d_list_bnd, (lbnd.size() + 1) * 4)) ||
       (rc = dalloc(d, &d->d_b, nv * 8)) || (rc = dalloc(d, &d->d_x, nv * 8)) ||
@@ -295,6 +298,12 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
   }
   CGX_HIP(hipMemcpyAsync(d->d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
   CGX_HIP(hipMemcpyAsync(d->d_blkk, blkk.data(), blkk.size() * 4, hipMemcpyHostToDevice, st));
+  std::vector<int> blkrk(2 * blk.size());
+  for (size_t i = 0; i < blk.size(); ++i) {
+    blkrk[2 * i] = blk[i];
+    blkrk[2 * i + 1] = blkk[i];
+  }
+  CGX_HIP(hipMemcpyAsync(d->d_blkrk, blkrk.data(), blkrk.size() * 4, hipMemcpyHostToDevice, st));
   if (n_loc > 0 && nnz > 0 && dc_wanted(d)) {
     std::vector<unsigned char> code((size_t)nnz);
     std::vector<int> dict;
@@ -475,6 +484,7 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.y = d->d_w;
   a.blk_row = d->d_blk;
   a.blk_k = d->d_blkk;
+  a.blk_rk = d->d_blkrk;
   a.blk_list = boundary ? d->d_list_bnd : d->d_list_int;
   a.blk_first = 0;
   a.nblk = boundary ? d->n_bnd : d->n_int;
@@ -495,7 +505,6 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
     a.code = d->d_code;
     a.dict = d->d_dict;
     a.ndict_cap = dict_cap(d->ndict);
-    a.dc_u = env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
     a.rlen = d->d_rlen;
     a.code_bits = d->code_bits;
   }

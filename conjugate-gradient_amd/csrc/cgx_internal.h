@@ -112,6 +112,8 @@ struct SpmvArgs {
   T *y;
   const int *blk_row;  // row-block boundaries, nblk_total+1 entries
   const int *blk_k;    // rp[blk_row[i]]: nonzero offset of each row block
+  const int *blk_rk;   // k_spmv_dc: (blk_row[i], blk_k[i]) pairs, so a block's
+                       // whole descriptor is one 16-byte scalar load
   const int *blk_list; // optional subset of row blocks (nullptr: a contiguous
                        // run blk_first .. blk_first+nblk-1)
   int blk_first;
@@ -155,12 +157,12 @@ struct SpmvArgs {
   const unsigned char *code;
   const int *dict;
   int ndict_cap;
-  int dc_u;            // k_spmv_dc: gathers in flight per row chunk (4 | 8)
   // k_spmv_dc: row lengths as one byte per row (every row <= 255 entries);
   // the kernel derives row bounds from blk_k and a wave prefix sum instead
   // of reading rp (nullptr: rp)
   const unsigned char *rlen;
   int code_bits;       // k_spmv_dc: 8 (byte codes) or 4 (nibbles, <= 16 offsets)
+  int lds_pad;         // k_spmv_dc diagnostic: extra dynamic LDS bytes per workgroup
 };
 
 // Dictionary-coded columns (host side, cgx_solver.cpp): the distinct column

@@ -1196,7 +1196,8 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // RL: row bounds from one byte per row (a.rlen, rows of <= 255 entries) and a
 // wave prefix sum from the block's first nonzero, instead of two int32
 // row_ptr reads per row (C3: 40 -> 10 MB per SpMV).
-template <typename T, int WPB, int CAPW, int ND, bool EPI, bool NT, int U, bool RL, int CB>
+template <typename T, int WPB, int CAPW, int ND, bool EPI, bool NT, int U, bool RL, int CB,
+          bool LIST>
 __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
   constexpr int AUX = NT ? 2 : 0;
   static_assert(CAPW % 4 == 0 && ND % kWave == 0 && (CB == 8 || CB == 4), "window / dictionary");
@@ -1208,23 +1209,35 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
   __shared__ __attribute__((aligned(16))) unsigned char lcode_all[WPB * CAPC];
   __shared__ int ldict_all[WPB * ND];
   __shared__ double red[WPB];
-  if (a.done && *a.done) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   T *lval = lval_all + wid * CAPW;
   unsigned char *lcode = lcode_all + wid * CAPC;
   int *ldict = ldict_all + wid * ND;
-  const int wb = xcd_block(a.xcd) * WPB + wid;
+  // Prologue in as few dependent round trips as possible: the early-exit
+  // flag and the block descriptor are scalar loads issued together (the
+  // flag is tested only once both are in), the dictionary is loaded after
+  // the window DMA is on its way.  (The naive order -- flag, then
+  // dictionary, then descriptor, then DMA -- costs two more memory round
+  // trips per wave, and the kernel is latency-bound: its time tracks the
+  // resident waves per CU.)
+  const int wb = __builtin_amdgcn_readfirstlane(xcd_block(a.xcd) * WPB + wid);
   double dot = 0.0;
   if (wb < a.nblk) {
-    int dv[ND / kWave];
-#pragma unroll
-    for (int i = 0; i < ND / kWave; ++i) dv[i] = a.dict[i * kWave + lane];
-    const int rb = __builtin_amdgcn_readfirstlane(a.blk_list ? a.blk_list[wb] : a.blk_first + wb);
-    const int r0 = __builtin_amdgcn_readfirstlane(a.blk_row[rb]);
-    const int nr = __builtin_amdgcn_readfirstlane(a.blk_row[rb + 1]) - r0;
-    const int k0 = __builtin_amdgcn_readfirstlane(a.blk_k[rb]);
-    const int k1 = __builtin_amdgcn_readfirstlane(a.blk_k[rb + 1]);
+    // no early-exit flag (op-level SpMV): read blk_k[0], which is 0 -- a
+    // select, not a branch, so the load goes out with the descriptor's
+    const int *dp = a.done ? a.done : a.blk_k;
+    const int stop = *dp;
+    const int rb = LIST ? a.blk_list[wb] : a.blk_first + wb;
+    const int *d = a.blk_rk + 2 * rb;  // row, k of this block and the next
+    const int r0 = d[0];
+    const int k0 = d[1];
+    const int nr = d[2] - r0;
+    const int k1 = d[3];
+    // make the descriptor live before the flag's branch, so its loads are
+    // issued with the flag's instead of being sunk past it
+    asm volatile("" ::"s"(r0), "s"(nr), "s"(k0), "s"(k1));
+    if (stop) return;  // every wave of the grid sees the same flag
     const int kb = k0 & ~3;   // val window: 16-B aligned for double and float
     const int kc = k0 & ~(KA - 1);  // code window: 16-B aligned
     const bool fits = k1 - kb <= CAPW;
@@ -1258,6 +1271,9 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
       }
       if (EPI) xrow = a.x[r0 + lane];
     }
+    int dv[ND / kWave];
+#pragma unroll
+    for (int i = 0; i < ND / kWave; ++i) dv[i] = a.dict[i * kWave + lane];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (RL) {
       j1 = k0 + wave_incl_scan(len, lane);
@@ -1301,37 +1317,38 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_dc(SpmvArgs<T> a) {
   }
 }
 
+template <typename T, int CAPW, int ND, bool EPI, bool NT, bool LIST>
+void launch_dc_k(const SpmvArgs<T> &a, int g, hipStream_t st) {
+  constexpr int WPB = 4;
+  const dim3 blk(WPB * kWave);
+  const int lds_pad = a.lds_pad;  // diagnostic: fewer resident workgroups per CU
+  if (a.rlen && a.code_bits == 4 && ND == 64)
+    hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, EPI, NT, 8, true, 4, LIST>), dim3(g), blk,
+                       lds_pad, st, a);
+  else if (a.rlen)
+    hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, EPI, NT, 8, true, 8, LIST>), dim3(g), blk,
+                       lds_pad, st, a);
+  else if (a.code_bits == 4 && ND == 64)
+    hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, EPI, NT, 8, false, 4, LIST>), dim3(g), blk,
+                       lds_pad, st, a);
+  else
+    hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, EPI, NT, 8, false, 8, LIST>), dim3(g), blk,
+                       lds_pad, st, a);
+}
+
 template <typename T, int CAPW, int ND>
 void launch_dc_nd(const SpmvArgs<T> &a, hipStream_t st) {
-  constexpr int WPB = 4;
-  const int g = (a.nblk + WPB - 1) / WPB;
-  const bool epi = a.part != nullptr;
-#define CGX_DC(E, N, UU)                                                                   \
-  do {                                                                                     \
-    if (a.rlen && a.code_bits == 4)                                                        \
-      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, true, 4>), dim3(g),        \
-                         dim3(WPB * kWave), 0, st, a);                                     \
-    else if (a.rlen)                                                                       \
-      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, true, 8>), dim3(g),        \
-                         dim3(WPB * kWave), 0, st, a);                                     \
-    else if (a.code_bits == 4)                                                             \
-      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, false, 4>), dim3(g),       \
-                         dim3(WPB * kWave), 0, st, a);                                     \
-    else                                                                                   \
-      hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, E, N, UU, false, 8>), dim3(g),       \
-                         dim3(WPB * kWave), 0, st, a);                                     \
+  const int g = (a.nblk + 3) / 4;
+  const bool epi = a.part != nullptr, list = a.blk_list != nullptr;
+#define CGX_DC(E, N)                                        \
+  do {                                                      \
+    if (list) launch_dc_k<T, CAPW, ND, E, N, true>(a, g, st); \
+    else launch_dc_k<T, CAPW, ND, E, N, false>(a, g, st);     \
   } while (0)
-  if (a.dc_u == 4) {
-    if (epi && a.nt) CGX_DC(true, true, 4);
-    else if (epi) CGX_DC(true, false, 4);
-    else if (a.nt) CGX_DC(false, true, 4);
-    else CGX_DC(false, false, 4);
-  } else {
-    if (epi && a.nt) CGX_DC(true, true, 8);
-    else if (epi) CGX_DC(true, false, 8);
-    else if (a.nt) CGX_DC(false, true, 8);
-    else CGX_DC(false, false, 8);
-  }
+  if (epi && a.nt) CGX_DC(true, true);
+  else if (epi) CGX_DC(true, false);
+  else if (a.nt) CGX_DC(false, true);
+  else CGX_DC(false, false);
 #undef CGX_DC
 }
 

@@ -307,16 +307,17 @@ struct cgx_solver {
   cgx::LapSpec lap{};
   int graph_batch = 16;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
+  int *d_blkrk = nullptr;  // (blk_row, blk_k) pairs: one scalar load per descriptor
   // dictionary-coded columns (k_spmv_dc; CGX_DC, default on where it applies):
   // d_code[k] = index of col[k] - row in d_dict (ndict entries, 256 allocated)
   bool want_dc = true;
-  int dc_u = 8;
   int ndict = 0;
   unsigned char *d_code = nullptr;
   int *d_dict = nullptr;
   bool want_rlen = true;           // CGX_DC_RLEN: byte row lengths instead of rp
   int want_bits = 8;               // CGX_DC_BITS=4: nibble codes when <= 16 offsets
   int code_bits = 8;
+  int dc_lds_pad = 0;              // CGX_DC_LDS_PAD (diagnostic: fewer workgroups per CU)
   unsigned char *d_rlen = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
   bool want_sell = false, sell = false;
@@ -385,6 +386,7 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_col);
   dfree((void **)&s->d_blk);
   dfree((void **)&s->d_blkk);
+  dfree((void **)&s->d_blkrk);
   dfree((void **)&s->d_soff);
   dfree((void **)&s->d_slen);
   dfree((void **)&s->d_code);
@@ -524,6 +526,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   }
   if ((rc = dalloc(s, (void **)&s->d_blk, blk.size() * 4)) ||
       (rc = dalloc(s, (void **)&s->d_blkk, blk.size() * 4)) ||
+      (rc = dalloc(s, (void **)&s->d_blkrk, blk.size() * 8)) ||
       (rc = dalloc(s, &s->d_b, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_x, nv * sizeof(T))) ||
       (rc = dalloc(s, &s->d_r, nv * sizeof(T))) ||
@@ -576,6 +579,13 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
   }
   CGX_HIP(hipMemcpyAsync(s->d_blk, blk.data(), blk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
+  std::vector<int> blkrk(2 * blk.size());
+  for (size_t i = 0; i < blk.size(); ++i) {
+    blkrk[2 * i] = blk[i];
+    blkrk[2 * i + 1] = blkk[i];
+  }
+  CGX_HIP(hipMemcpyAsync(s->d_blkrk, blkrk.data(), blkrk.size() * 4, hipMemcpyHostToDevice,
+                         s->stream));
   CGX_HIP(hipMemcpyAsync(s->d_blkk, blkk.data(), blkk.size() * 4,
                          hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
@@ -752,6 +762,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.y = (T *)y;
   a.blk_row = s->d_blk;
   a.blk_k = s->d_blkk;
+  a.blk_rk = s->d_blkrk;
   a.blk_list = nullptr;
   a.blk_first = 0;
   a.nblk = s->nblk;
@@ -781,9 +792,9 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
     a.code = s->d_code;
     a.dict = s->d_dict;
     a.ndict_cap = dict_cap(s->ndict);
-    a.dc_u = s->dc_u;
     a.rlen = s->d_rlen;
     a.code_bits = s->code_bits;
+    a.lds_pad = s->dc_lds_pad;
   }
   return a;
 }
@@ -1232,8 +1243,8 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->vec_pf = cgx::env_int("CGX_VEC_PF", 1) != 0;  // C3 -1.7 us, C2 -0.44 us per iteration (sweep36), bit-identical
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->want_dc = cgx::env_int("CGX_DC", 1) != 0;
-  s->dc_u = cgx::env_int("CGX_DC_U", 8) == 4 ? 4 : 8;
   s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
+  s->dc_lds_pad = std::max(0, std::min(cgx::env_int("CGX_DC_LDS_PAD", 0), 65536));
   s->want_bits = cgx::env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;  // nibbles: neutral at C3 (dc3 sweep)
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
   {

@@ -186,15 +186,13 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1u4", "1r0", "1b4"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1r0", "1b4"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
     monkeypatch.setenv("CGX_SPMV_DMA", dma[0])
     if dma.endswith("c"):
         monkeypatch.setenv("CGX_LAYOUT", "csr")
-    if dma.endswith("u4"):
-        monkeypatch.setenv("CGX_DC_U", "4")
     if dma.endswith("r0"):
         monkeypatch.setenv("CGX_DC_RLEN", "0")
     if dma.endswith("b4"):
@@ -208,7 +206,7 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         # dictionary-coded columns on the default kernel (7 offsets), CSR otherwise
-        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1u4", "1r0", "1b4") else 0)
+        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1r0", "1b4") else 0)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
@@ -245,16 +243,14 @@ def banded_spd(n, offsets, seed, f32=False):
 
 @pytest.mark.parametrize("bits", ["4", "8"])
 @pytest.mark.parametrize("rlen", ["1", "0"])
-@pytest.mark.parametrize("u", ["4", "8"])
 @pytest.mark.parametrize("capw", ["", "328", "456"])
-def test_dictionary_coded_columns_bit_exact(u, capw, rlen, bits, monkeypatch):
+def test_dictionary_coded_columns_bit_exact(capw, rlen, bits, monkeypatch):
     """CSR-DC (k_spmv_dc): selected exactly when the matrix has <= 256
     distinct column offsets col - row, and bit-identical to the oracle's
     sequential row sums (fp64 and fp32, 64- and 256-entry dictionaries,
     adaptive 328/512 windows; 456 keeps plain CSR; row bounds from byte row
     lengths or from row_ptr; nibble codes for <= 16 offsets or bytes)."""
     monkeypatch.setenv("CGX_DC_BITS", bits)
-    monkeypatch.setenv("CGX_DC_U", u)
     monkeypatch.setenv("CGX_DC_RLEN", rlen)
     if capw:
         monkeypatch.setenv("CGX_SPMV_CAPW", capw)
