@@ -177,6 +177,11 @@ void pack_nibbles(long long nnz, const unsigned char *code, unsigned char *out);
 // Row lengths as bytes for k_spmv_dc; false (nothing written) when a row has
 // more than 255 entries.
 bool build_row_lengths(int n, const int *rp, unsigned char *rlen);
+// Per-solver switch for coded columns at the next set_matrix (the op-level
+// mv_mult turns it off: one product per upload).  Respects CGX_DC /
+// CGX_LAYOUT: `on` restores the environment's choice.
+void solver_want_dc(cgx_solver *s, bool on);
+bool env_wants_dc();
 // Dictionary capacity the SpMV kernel is instantiated for.
 inline int dict_cap(int ndict) { return ndict <= 64 ? 64 : 256; }
 

@@ -338,9 +338,13 @@ int mv_mult(struct __mv_sparse *A, struct __mv_sparse *b, struct __mv_sparse **r
   if (n > 0) {
     cgx_solver *s = nullptr;
     rc = default_solver(&s);
+    // one product per upload: coding the columns would cost more host time
+    // than it saves on a single SpMV (the solvers below keep it)
+    if (rc == 0) cgx::solver_want_dc(s, false);
     if (rc == 0)
       rc = cgx_solver_set_matrix(s, n, A->row_ptr[n], A->row_ptr,
                                  A->col_indices, A->values);
+    if (rc == 0) cgx::solver_want_dc(s, true);
     if (rc == 0) rc = cgx_solver_spmv(s, b->values, tmp);
   }
   if (rc == 0) rc = prepare_out(r, n, b->nnz, true);

@@ -263,6 +263,11 @@ bool build_row_lengths(int n, const int *rp, unsigned char *rlen) {
   return true;
 }
 
+bool env_wants_dc() {
+  const char *l = getenv("CGX_LAYOUT");
+  return env_int("CGX_DC", 1) != 0 && !(l && (strcmp(l, "csr") == 0 || strcmp(l, "sell") == 0));
+}
+
 int vec_grid_for(int n, int cus) {
   const long long vecs = (n + 1) / 2;
   long long g = (vecs + kVecBS - 1) / kVecBS;
@@ -348,6 +353,8 @@ struct cgx_solver {
   int gexec_key[2] = {-1, -1};
   std::vector<hipEvent_t> events;
 };
+
+void cgx::solver_want_dc(cgx_solver *s, bool on) { s->want_dc = on && env_wants_dc(); }
 
 namespace {
 
@@ -1242,7 +1249,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->epi_last = cgx::env_int("CGX_SPMV_EPI_LAST", 0);
   s->vec_pf = cgx::env_int("CGX_VEC_PF", 1) != 0;  // C3 -1.7 us, C2 -0.44 us per iteration (sweep36), bit-identical
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
-  s->want_dc = cgx::env_int("CGX_DC", 1) != 0;
+  s->want_dc = cgx::env_wants_dc();
   s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
   s->dc_lds_pad = std::max(0, std::min(cgx::env_int("CGX_DC_LDS_PAD", 0), 65536));
   s->want_bits = cgx::env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;  // nibbles: neutral at C3 (dc3 sweep)
@@ -1250,7 +1257,6 @@ int cgx_solver_create(int device, cgx_solver **out) {
   {
     const char *l = getenv("CGX_LAYOUT");
     s->want_sell = l && strcmp(l, "sell") == 0;
-    if (l && (strcmp(l, "csr") == 0 || strcmp(l, "sell") == 0)) s->want_dc = false;
   }
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
