@@ -1322,6 +1322,13 @@ void launch_dc_k(const SpmvArgs<T> &a, int g, hipStream_t st) {
   constexpr int WPB = 4;
   const dim3 blk(WPB * kWave);
   const int lds_pad = a.lds_pad;  // diagnostic: fewer resident workgroups per CU
+  if constexpr (EPI && !LIST && ND == 64 && CAPW == 512 && sizeof(T) == 8) {
+    if (a.wpb == 8 && a.rlen && a.code_bits == 8) {  // 8 waves: half the partials
+      hipLaunchKernelGGL((k_spmv_dc<T, 8, CAPW, ND, EPI, NT, 8, true, 8, LIST>),
+                         dim3((a.nblk + 7) / 8), dim3(8 * kWave), lds_pad, st, a);
+      return;
+    }
+  }
   if (a.rlen && a.code_bits == 4 && ND == 64)
     hipLaunchKernelGGL((k_spmv_dc<T, WPB, CAPW, ND, EPI, NT, 8, true, 4, LIST>), dim3(g), blk,
                        lds_pad, st, a);

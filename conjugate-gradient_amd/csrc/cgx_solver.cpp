@@ -626,7 +626,8 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
     }
   }
   if (s->want_dc && n > 0 && nnz > 0 && s->npanel == 1 && !s->sell &&
-      s->spmv_dma == 1 && s->spmv_bs == 64 && s->spmv_wpb == 4 &&
+      s->spmv_dma == 1 && s->spmv_bs == 64 &&
+      (s->spmv_wpb == 4 || (s->spmv_wpb == 8 && sizeof(T) == 8)) &&
       (s->spmv_capw == 0 || s->spmv_capw == 328)) {
     std::vector<unsigned char> code;
     std::vector<int> dict;
@@ -686,6 +687,14 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       }
       CGX_HIP(hipStreamSynchronize(s->stream));
       s->ndict = nd;
+      if (s->spmv_wpb == 8 && (!s->d_rlen || s->code_bits != 8 || nd > 64)) {
+        // the 8-wave coded kernel covers byte codes + row lengths + <= 64
+        // offsets only; otherwise plain CSR at 8 waves (same partial count)
+        dfree((void **)&s->d_code);
+        dfree((void **)&s->d_dict);
+        dfree((void **)&s->d_rlen);
+        s->ndict = 0;
+      }
     }
   }
   s->have_matrix = true;

@@ -186,7 +186,7 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1r0", "1b4"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1r0", "1b4", "1w8"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
@@ -197,6 +197,8 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
         monkeypatch.setenv("CGX_DC_RLEN", "0")
     if dma.endswith("b4"):
         monkeypatch.setenv("CGX_DC_BITS", "4")
+    if dma.endswith("w8"):
+        monkeypatch.setenv("CGX_SPMV_WPB", "8")
     if dma.endswith("x"):
         monkeypatch.setenv("CGX_SPMV_XCD", "1")
     if dma.endswith("w"):
@@ -206,7 +208,7 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         # dictionary-coded columns on the default kernel (7 offsets), CSR otherwise
-        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1r0", "1b4") else 0)
+        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1r0", "1b4", "1w8") else 0)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
