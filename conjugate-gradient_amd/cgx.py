@@ -150,6 +150,7 @@ _SIGS = {
     "cgx_dist_set_matrix": (ctypes.c_int, [_vp, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
                                            _i32p, _i32p, _f64p]),
     "cgx_dist_set_rhs": (ctypes.c_int, [_vp, _f64p]),
+    "cgx_dist_set_alg": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
                                     ctypes.POINTER(ctypes.c_int)]),
     "cgx_dist_get_x": (ctypes.c_int, [_vp, _f64p]),
@@ -564,6 +565,10 @@ class DistSolver:
     def set_rhs(self, b):
         b = np.ascontiguousarray(b, np.float64)
         check(lib().cgx_dist_set_rhs(self._h, _p(b, _f64p)), "dist_set_rhs")
+
+    def set_alg(self, alg):
+        """CGX_ALG_CG1 (one all-reduce per iteration) or CGX_ALG_HS (two)."""
+        check(lib().cgx_dist_set_alg(self._h, alg), "dist_set_alg")
 
     def run(self, maxit, tol=0.0):
         it = ctypes.c_int(0)

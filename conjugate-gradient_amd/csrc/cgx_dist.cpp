@@ -60,11 +60,15 @@ struct cgx_dist {
   ncclComm_t comm = nullptr;
   int cus = 256;
   hipStream_t st = nullptr, st_comm = nullptr;
-  hipEvent_t ev_packed = nullptr, ev_halo = nullptr, ev_sums = nullptr;
+  hipEvent_t ev_packed = nullptr, ev_halo = nullptr, ev_sums = nullptr, ev_sums2 = nullptr;
   cgx_part *part = nullptr;
   long long n_global = 0;
   int row_begin = 0, n_loc = 0, n_ghost = 0, nnz = 0;
   int vec = 4, wpb = 4;
+  // recurrence (cgx_dist_set_alg): CGX_ALG_CG1 (Chronopoulos-Gear, one
+  // all-reduce of 2 doubles per iteration) or CGX_ALG_HS (the reference's
+  // recurrence, two all-reduces of 1 double, 8 B per row less vector traffic)
+  int alg = CGX_ALG_CG1;
   int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
   int *d_blkrk = nullptr;  // (blk_row, blk_k) pairs for the coded-column kernel
   int *d_list_int = nullptr, *d_list_bnd = nullptr;
@@ -111,7 +115,11 @@ namespace {
 
 using namespace cgx;
 
-bool solo(const cgx_dist *d) { return d->nranks == 1 && !d->local; }
+// One rank with no transport: no halo, scalars straight from the partials,
+// graph replay.  A 1-rank RCCL communicator (cgx_dist_create with an id at
+// nranks 1) keeps the transport phases -- the multi-GPU code path, all-reduce
+// included, on one GPU.
+bool solo(const cgx_dist *d) { return !d->local && d->comm == nullptr; }
 
 #define CGX_NCCL(call)                                                       \
   do {                                                                       \
@@ -186,6 +194,10 @@ int init_common(cgx_dist *d, int device) {
   if (d->vec != 1 && d->vec != 2 && d->vec != 4) d->vec = 4;
   d->wpb = env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
   d->graph_batch = env_int("CGX_GRAPH", 1) ? std::max(1, env_int("CGX_GRAPH_BATCH", 16)) : 0;
+  {
+    const char *al = getenv("CGX_DIST_ALG");
+    d->alg = al && strcmp(al, "hs") == 0 ? CGX_ALG_HS : CGX_ALG_CG1;
+  }
   CGX_HIP(hipSetDevice(device));
   CGX_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
   {
@@ -200,6 +212,7 @@ int init_common(cgx_dist *d, int device) {
   CGX_HIP(hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums, hipEventDisableTiming));
+  CGX_HIP(hipEventCreateWithFlags(&d->ev_sums2, hipEventDisableTiming));
   CGX_HIP(hipMalloc((void **)&d->d_st, sizeof(CgState)));
   CGX_HIP(hipMalloc((void **)&d->d_sums, 4 * sizeof(double)));
   CGX_HIP(hipHostMalloc((void **)&d->h_st, sizeof(CgState), hipHostMallocDefault));
@@ -278,9 +291,9 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
       (rc = dalloc(d, &d->d_list_bnd, (lbnd.size() + 1) * 4)) ||
       (rc = dalloc(d, &d->d_b, nv * 8)) || (rc = dalloc(d, &d->d_x, nv * 8)) ||
       (rc = dalloc(d, &d->d_r, (nv + d->n_ghost) * 8)) ||
-      (rc = dalloc(d, &d->d_p, nv * 8)) || (rc = dalloc(d, &d->d_s, nv * 8)) ||
+      (rc = dalloc(d, &d->d_p, (nv + d->n_ghost) * 8)) || (rc = dalloc(d, &d->d_s, nv * 8)) ||
       (rc = dalloc(d, &d->d_w, nv * 8)) ||
-      (rc = dalloc(d, &d->d_pa, ((size_t)d->vec_grid + 1) * 8)) ||
+      (rc = dalloc(d, &d->d_pa, ((size_t)d->vec_grid + 8) * 8)) ||
       (rc = dalloc(d, &d->d_pb, ((size_t)d->g_int + d->g_bnd + 1) * 8))) {
     free_system(d);
     return rc;
@@ -289,6 +302,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
   CGX_HIP(hipMemsetAsync(d->d_col, 0, nnz_pad * 4, st));
   CGX_HIP(hipMemsetAsync(d->d_val, 0, nnz_pad * 8, st));
   CGX_HIP(hipMemsetAsync(d->d_r, 0, (nv + d->n_ghost) * 8, st));
+  CGX_HIP(hipMemsetAsync(d->d_p, 0, (nv + d->n_ghost) * 8, st));
   if (n_loc > 0) {
     CGX_HIP(hipMemcpyAsync(d->d_rp, rp, ((size_t)n_loc + 1) * 4, hipMemcpyHostToDevice, st));
     if (nnz > 0) {
@@ -480,8 +494,10 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.rp = d->d_rp;
   a.col = d->d_col;
   a.val = d->d_val;
-  a.x = d->d_r;
-  a.y = d->d_w;
+  // CG1: w = A r;  HS: s = A p (cg.c:111).  The gathered vector carries the
+  // ghost tail the halo exchange fills.
+  a.x = d->alg == CGX_ALG_HS ? d->d_p : d->d_r;
+  a.y = d->alg == CGX_ALG_HS ? d->d_s : d->d_w;
   a.blk_row = d->d_blk;
   a.blk_k = d->d_blkk;
   a.blk_rk = d->d_blkrk;
@@ -533,7 +549,7 @@ int phase_halo(cgx_dist *d) {
   if (solo(d)) return 0;
   CGX_HIP(hipSetDevice(d->device));
   CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_packed, 0));
-  double *ghost = d->d_r + d->n_loc;
+  double *ghost = (d->alg == CGX_ALG_HS ? d->d_p : d->d_r) + d->n_loc;
   if (d->local) {
     for (cgx_dist *o : d->group->parts) {
       if (o == d || d->recv_count[o->rank] == 0) continue;
@@ -596,9 +612,13 @@ int phase_spmv(cgx_dist *d) {
     d->ev_i += 4;
   }
   if (solo(d)) return 0;  // phase_reduce finalizes straight from the partials
-  CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, d->vec_grid, d->d_pb,
-                          d->g_int + d->g_bnd, d->d_st, d->d_hist, d->d_sums,
-                          d->st));
+  if (d->alg == CGX_ALG_HS)  // local p.s -> sums[0]
+    CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, d->g_int + d->g_bnd, nullptr, 0, d->d_st,
+                            d->d_hist, d->d_sums, d->st));
+  else
+    CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, d->vec_grid, d->d_pb,
+                            d->g_int + d->g_bnd, d->d_st, d->d_hist, d->d_sums,
+                            d->st));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
@@ -617,8 +637,8 @@ int phase_reduce(cgx_dist *d, bool init) {
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_sums, 0));
     CGX_HIP(launch_group_sum(d->group->d_srcs, (int)d->group->parts.size(), 2,
-                             d->d_gsums, d->st));
-  } else if (d->nranks > 1) {
+                             d->d_gsums, d->st, 0));
+  } else if (d->comm) {
     CGX_NCCL(ncclAllReduce(d->d_sums, d->d_gsums, 2, ncclFloat64, ncclSum,
                            d->comm, d->st));
   } else {
@@ -658,8 +678,116 @@ int run_phases(Group *g, bool init, long long iters) {
   return run_phases_eager(g, init, iters);
 }
 
+// ---- HS recurrence (CGX_ALG_HS): the single-GPU folded kernels, with the
+// two scalar steps fed by all-reduced sums instead of local partials.  Per
+// iteration: halo of p (packed at the end of the previous one) || interior
+// SpMV s = A p; boundary SpMV; p.s -> all-reduce -> k_update_rf (alpha,
+// r -= alpha s, r.r partials) -> r.r -> all-reduce -> k_xpay_xf (beta, stop,
+// x += alpha p, p = r + beta p) -> pack p.  Every rank computes alpha, beta
+// and the stop test from the same global sums, so they agree bit for bit.
+
+// one scalar of the iteration summed over the ranks: sums[i] -> gsums[i]
+int reduce_one(cgx_dist *d, int i, hipEvent_t ev) {
+  if (d->local) {
+    for (cgx_dist *o : d->group->parts)
+      if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, i == 0 ? o->ev_sums : o->ev_sums2, 0));
+    CGX_HIP(launch_group_sum(d->group->d_srcs, (int)d->group->parts.size(), 1, d->d_gsums,
+                             d->st, i));
+  } else {
+    CGX_NCCL(ncclAllReduce(d->d_sums + i, d->d_gsums + i, 1, ncclFloat64, ncclSum, d->comm,
+                           d->st));
+  }
+  (void)ev;
+  return 0;
+}
+
+int hs_pack(cgx_dist *d) {
+  if (solo(d)) return 0;
+  CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, d->d_p, d->d_sendbuf, d->st));
+  CGX_HIP(hipEventRecord(d->ev_packed, d->st));
+  return 0;
+}
+
+// prologue: x = 0, r = p = b, b.b (cg.c:104-107)
+int hs_init(cgx_dist *d) {
+  CGX_HIP(hipSetDevice(d->device));
+  CGX_HIP(launch_init_hs<double>(d->n_loc, d->d_b, d->d_x, d->d_r, d->d_p, d->d_pa,
+                                 d->vec_grid, d->st));
+  if (solo(d)) {
+    CGX_HIP(launch_finalize(FIN_INIT_HS, d->d_pa, d->vec_grid, nullptr, 0, d->d_st,
+                            d->d_hist, nullptr, d->st));
+    return 0;
+  }
+  CGX_HIP(launch_finalize(FIN_SUM, d->d_pa, d->vec_grid, nullptr, 0, d->d_st, d->d_hist,
+                          d->d_sums, d->st));
+  CGX_HIP(hipEventRecord(d->ev_sums, d->st));
+  return 0;
+}
+
+int hs_init_reduce(cgx_dist *d) {
+  if (solo(d)) return hs_pack(d);
+  int rc = reduce_one(d, 0, d->ev_sums);
+  if (rc) return rc;
+  CGX_HIP(launch_finalize(FIN_INIT_HS, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist,
+                          nullptr, d->st));
+  return hs_pack(d);
+}
+
+// alpha step: all-reduced p.s, r -= alpha s, local r.r
+int hs_alpha(cgx_dist *d) {
+  CGX_HIP(hipSetDevice(d->device));
+  const int gf = (d->vec_grid + 3) / 4;  // 1024-thread workgroups, 4 partials each
+  const double *ps = d->d_pb;
+  int nps = d->g_int + d->g_bnd;
+  if (!solo(d)) {
+    int rc = reduce_one(d, 0, d->ev_sums);
+    if (rc) return rc;
+    ps = d->d_gsums;
+    nps = 1;
+  }
+  CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, ps, nps, d->d_pa, gf,
+                                   d->st, true));              // cg.c:113, 118-123
+  if (solo(d)) return 0;
+  CGX_HIP(launch_finalize(FIN_SUM, d->d_pa, 4 * gf, nullptr, 0, d->d_st, d->d_hist,
+                          d->d_sums + 1, d->st));
+  CGX_HIP(hipEventRecord(d->ev_sums2, d->st));
+  return 0;
+}
+
+// beta step: all-reduced r.r, stop test, x += alpha p, p = r + beta p
+int hs_beta(cgx_dist *d) {
+  CGX_HIP(hipSetDevice(d->device));
+  const int gf = (d->vec_grid + 3) / 4;
+  const double *rr = d->d_pa;
+  int nrr = 4 * gf;
+  if (!solo(d)) {
+    int rc = reduce_one(d, 1, d->ev_sums2);
+    if (rc) return rc;
+    rr = d->d_gsums + 1;
+    nrr = 1;
+  }
+  CGX_HIP(launch_xpay_xf<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_st, rr, nrr,
+                                 d->d_hist, gf, d->st, true));  // cg.c:115-116, 125-132
+  return hs_pack(d);
+}
+
 int run_phases_eager(Group *g, bool init, long long iters) {
   auto &P = g->parts;
+  if (P[0]->alg == CGX_ALG_HS) {
+    int rc;
+    if (init) {
+      for (cgx_dist *d : P) if ((rc = hs_init(d))) return rc;
+      for (cgx_dist *d : P) if ((rc = hs_init_reduce(d))) return rc;
+      return 0;
+    }
+    for (long long it = 0; it < iters; ++it) {
+      for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
+      for (cgx_dist *d : P) if ((rc = phase_spmv(d))) return rc;
+      for (cgx_dist *d : P) if ((rc = hs_alpha(d))) return rc;
+      for (cgx_dist *d : P) if ((rc = hs_beta(d))) return rc;
+    }
+    return 0;
+  }
   for (long long it = 0; it < (init ? 1 : iters); ++it) {
     int rc;
     for (cgx_dist *d : P) if ((rc = phase_update(d, init))) return rc;
@@ -822,6 +950,7 @@ void destroy_one(cgx_dist *d) {
   if (d->ev_packed) (void)hipEventDestroy(d->ev_packed);
   if (d->ev_halo) (void)hipEventDestroy(d->ev_halo);
   if (d->ev_sums) (void)hipEventDestroy(d->ev_sums);
+  if (d->ev_sums2) (void)hipEventDestroy(d->ev_sums2);
   for (hipEvent_t e : d->spmv_ev) (void)hipEventDestroy(e);
   if (d->d_st) (void)hipFree(d->d_st);
   if (d->d_sums) (void)hipFree(d->d_sums);
@@ -860,7 +989,7 @@ int cgx_dist_create(int device, int nranks, int rank,
     destroy_one(d);
     return rc;
   }
-  if (nranks > 1) {
+  if (id) {  // nranks == 1 with an id: a 1-rank communicator (see solo())
     ncclUniqueId u;
     memcpy(u.internal, id, sizeof u.internal);
     ncclResult_t r = ncclCommInitRank(&d->comm, nranks, u, rank);
@@ -968,6 +1097,21 @@ int cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms,
   if (!d || iters < 1 || !total_ms || !spmv_ms || (d->local && !d->owns_group))
     return CGX_EINVAL;
   return group_bench_run(d->group, iters, flags, total_ms, spmv_ms);
+}
+
+int cgx_dist_set_alg(cgx_dist *d, int alg) {
+  if (!d || (alg != CGX_ALG_HS && alg != CGX_ALG_CG1) || (d->local && !d->owns_group))
+    return CGX_EINVAL;
+  for (cgx_dist *o : d->group->parts) {
+    if (o->alg != alg && o->gexec) {  // a captured graph holds the other recurrence
+      (void)hipStreamSynchronize(o->st);
+      (void)hipGraphExecDestroy(o->gexec);
+      o->gexec = nullptr;
+    }
+    o->alg = alg;
+    o->bench_ready = false;
+  }
+  return 0;
 }
 
 int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {

@@ -290,7 +290,7 @@ hipError_t launch_gather(int m, const int *idx, const T *x, T *buf,
                          hipStream_t st);
 
 hipError_t launch_group_sum(const double *const *srcs, int P, int count,
-                            double *dst, hipStream_t st);
+                            double *dst, hipStream_t st, int off = 0);
 
 int vec_grid_for(int n, int cus);
 int env_int(const char *name, int dflt);

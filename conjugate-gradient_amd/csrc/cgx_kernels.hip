@@ -2079,9 +2079,9 @@ __global__ __launch_bounds__(BS) void k_axpby(int op, int n, double sc,
 // In-process all-reduce of the multi-partition transport: every partition
 // adds the partitions' local sums in the same fixed order (0..P-1).
 __global__ void k_group_sum(const double *const *srcs, int P, int count,
-                            double *dst) {
-  const int c = threadIdx.x;
-  if (c >= count) return;
+                            double *dst, int off) {
+  const int c = threadIdx.x + off;
+  if (threadIdx.x >= count) return;
   double acc = srcs[0][c];
   for (int q = 1; q < P; ++q) acc = acc + srcs[q][c];
   dst[c] = acc;
@@ -2404,8 +2404,8 @@ hipError_t launch_axpby(int op, int n, double s, const T *a, const T *b, T *r,
 }
 
 hipError_t launch_group_sum(const double *const *srcs, int P, int count,
-                            double *dst, hipStream_t st) {
-  hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, st, srcs, P, count, dst);
+                            double *dst, hipStream_t st, int off) {
+  hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, st, srcs, P, count, dst, off);
   return hipGetLastError();
 }
 

@@ -239,6 +239,13 @@ int  cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
                          const int *row_ptr, const int *col_global,
                          const double *val);
 int  cgx_dist_set_rhs(cgx_dist *d, const double *b_local);
+/* Recurrence: CGX_ALG_CG1 (default; Chronopoulos-Gear, ONE all-reduce of two
+ * doubles per iteration) or CGX_ALG_HS (the reference's cg.c:88-141
+ * recurrence, two all-reduces of one double, 8 bytes per row less vector
+ * traffic).  Every rank (every part of a local group) must use the same one;
+ * on a local group, setting it on part 0 sets the group.  The environment
+ * default is CGX_DIST_ALG=cg1|hs. */
+int  cgx_dist_set_alg(cgx_dist *d, int alg);
 int  cgx_dist_run(cgx_dist *d, int maxit, double tol, int *iters);
 int  cgx_dist_get_x(cgx_dist *d, double *x_local);
 int  cgx_dist_get_history(cgx_dist *d, double *rr, int cap);

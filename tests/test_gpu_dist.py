@@ -27,10 +27,11 @@ def system(kind):
     return rp, col, val, b
 
 
-def solve_local(rp, col, val, b, P, maxit, tol):
+def solve_local(rp, col, val, b, P, maxit, tol, alg=cgx.CGX_ALG_CG1):
     n = len(rp) - 1
     parts = cgx.DistSolver.local_group(0, P)
     try:
+        parts[0].set_alg(alg)
         for g, d in enumerate(parts):
             rb, re_ = cgx.partition_rows(n, P, g)
             d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]],
@@ -164,3 +165,97 @@ def test_coded_columns_partitions_identical_to_csr(P, monkeypatch):
         out[layout] = (x, hist)
     assert H.same_bits_or_both_nan(out["csr"][0], out["auto"][0])
     assert H.same_bits_or_both_nan(out["csr"][1], out["auto"][1])
+
+
+@pytest.mark.parametrize("kind", ["lap3d", "lap2d", "rand"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_hs_partitions_match_oracle(kind, P):
+    """The HS recurrence across partitions (two all-reduced scalars per
+    iteration, the single-GPU folded kernels): x within 1e-9 of the oracle's
+    HS solve (the reference's recurrence), stop iteration within 1."""
+    rp, col, val, b = system(kind)
+    x, its, hist, stats = solve_local(rp, col, val, b, P, 2000, 1e-10, alg=cgx.CGX_ALG_HS)
+    x_ref, its_ref, hist_ref = H.o_solve(2000, 1e-10, rp, col, val, b)
+    assert abs(its - its_ref) <= 1
+    assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
+    m = min(len(hist), len(hist_ref)) - 2
+    assert np.allclose(hist[:m], hist_ref[:m], rtol=1e-6, atol=0)
+    res = b - H.o_spmv(rp, col, val, x)
+    assert np.linalg.norm(res) <= 2e-10 * np.linalg.norm(b)
+
+
+def test_hs_single_part_identical_to_solver():
+    """One partition, no transport: the HS recurrence runs the single-GPU
+    solver's kernels with the same grids, so x and the r.r history are
+    bit-identical to cgx.Solver's."""
+    rp, col, val, b = system("lap3d")
+    x, its, hist, _ = solve_local(rp, col, val, b, 1, 40, 0.0, alg=cgx.CGX_ALG_HS)
+    d = cgx.DistSolver(0, 1, 0, None)
+    try:
+        d.set_alg(cgx.CGX_ALG_HS)
+        d.set_matrix(len(rp) - 1, rp, col, val)
+        d.set_rhs(b)
+        its2 = d.run(40)
+        x2 = d.x()
+    finally:
+        d.close()
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        its3 = s.run(40)
+        x3 = s.x()
+        h3 = s.history(41)
+    assert its == its2 == its3 == 41
+    assert H.same_bits_or_both_nan(x, x3)
+    assert H.same_bits_or_both_nan(x2, x3)
+    assert H.same_bits_or_both_nan(hist, h3[:len(hist)])
+
+
+def test_hs_fixed_iterations_and_bench():
+    rp, col, val, b = system("lap3d")
+    xs = [solve_local(rp, col, val, b, P, 60, 0.0, alg=cgx.CGX_ALG_HS) for P in (1, 2, 4)]
+    assert all(x[1] == 61 for x in xs)
+    for x in xs[1:]:
+        assert np.linalg.norm(x[0] - xs[0][0]) <= 1e-11 * np.linalg.norm(xs[0][0])
+    n = len(rp) - 1
+    parts = cgx.DistSolver.local_group(0, 3)
+    try:
+        parts[0].set_alg(cgx.CGX_ALG_HS)
+        for g, d in enumerate(parts):
+            rb, re_ = cgx.partition_rows(n, 3, g)
+            d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+            d.set_rhs(b[rb:re_])
+        parts[0].bench_prepare(2)
+        ms, sp = parts[0].bench_run(5, spmv_events=True)
+        assert ms > 0 and 0 < sp < ms
+    finally:
+        parts[0].close()
+
+
+@pytest.mark.parametrize("alg", [cgx.CGX_ALG_CG1, cgx.CGX_ALG_HS])
+def test_rccl_one_rank_communicator(alg):
+    """A 1-rank RCCL communicator (an id at world size 1) runs the multi-GPU
+    phase code on one GPU: pack, grouped send/recv loop (no peers), local
+    sums, ncclAllReduce, scalar steps.  Bit-identical to the in-process
+    1-partition group (the same phases with a fixed-order group sum), within
+    tolerance of the oracle, and the eager bench path runs."""
+    rp, col, val, b = system("lap3d")
+    n = len(rp) - 1
+    d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+    try:
+        d.set_alg(alg)
+        d.set_matrix(n, rp, col, val)
+        d.set_rhs(b)
+        its = d.run(500, 1e-10)
+        x = d.x()
+        d.bench_prepare(2)
+        ms, sp = d.bench_run(5, spmv_events=True)
+        assert ms > 0 and 0 < sp < ms
+    finally:
+        d.close()
+    x1, its1, _, _ = solve_local(rp, col, val, b, 1, 500, 1e-10, alg=alg)
+    assert its == its1
+    assert H.same_bits_or_both_nan(x, x1)
+    x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=alg == cgx.CGX_ALG_CG1)
+    assert abs(its - its_ref) <= 1
+    assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
