@@ -190,7 +190,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--alg", default=None, choices=["hs", "cg1", "cg1-dist"])
+    ap.add_argument("--alg", default=None, choices=["hs", "cg1", "cg1-dist", "hs-dist", "auto-dist"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -215,12 +215,15 @@ def main():
     wl = WORKLOADS[args.workload]
     if world > 1 and wl["kind"] == "rand":
         raise SystemExit("bench: C5 (random SPD) is a single-GPU configuration (BASELINE.json)")
-    alg = args.alg or ("cg1-dist" if world > 1 else "hs")
+    # N > 1: the partitioned solver; its recurrence is chosen by a short
+    # timed trial of both (below) unless --alg names one
+    alg = args.alg or ("auto-dist" if world > 1 else "hs")
     sysm = make_system(wl, rank, world)
 
-    use_dist = world > 1 or alg == "cg1-dist"
+    use_dist = world > 1 or alg.endswith("-dist")
     torch.cuda.synchronize()
     t_up = time.perf_counter()  # host -> HBM upload + row-block plan (outside `value`)
+    trial = None
     if use_dist:
         # one rank per GPU; RCCL communicator from an id rank 0 broadcasts
         uid = [cgx.dist_unique_id() if (rank == 0 and world > 1) else None]
@@ -230,6 +233,23 @@ def main():
         s.set_matrix(sysm["n_global"], sysm["rp"], sysm["col"], sysm["val"])
         s.set_rhs(sysm["b"])
         dinfo = s.info()
+        if alg == "auto-dist":
+            # HS needs two all-reduces per iteration, CG1 one but 8 B/row more
+            # vector traffic: which wins depends on the node's all-reduce
+            # latency, so time both (max over ranks, same choice everywhere)
+            trial = {}
+            for name, a in (("hs-dist", cgx.CGX_ALG_HS), ("cg1-dist", cgx.CGX_ALG_CG1)):
+                s.set_alg(a)
+                s.bench_prepare(3)
+                barrier()
+                tms = s.bench_run(20)[0] / 20
+                if world > 1:
+                    t = torch.tensor([tms], device="cuda", dtype=torch.float64)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    tms = float(t.item())
+                trial[name] = round(tms, 4)
+            alg = min(trial, key=trial.get)
+        s.set_alg(cgx.CGX_ALG_HS if alg == "hs-dist" else cgx.CGX_ALG_CG1)
         info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"],
                     spmv_iter_bytes=dinfo["spmv_iter_bytes"], n_dict=dinfo["n_dict"])
     else:
@@ -353,7 +373,8 @@ def main():
         higher_is_better=True, scaling="strong" if strong else "weak", vs_baseline=None,
         dtype=wl["dtype"], data="synthetic",
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz_local=int(len(sysm["col"])),
-                    alg=alg, graph=not use_dist or world == 1,
+                    alg=alg, alg_trial_ms_per_iter=trial if use_dist else None,
+                    graph=not use_dist or world == 1,
                     parallelism=f"row-partition x{world}",
                     layout=(f"CSR with dictionary-coded columns ({info['n_dict']} col-row "
                             f"offsets, 1 B/nnz) + byte row lengths"
