@@ -1,9 +1,9 @@
 """World-size-2 rehearsal of the multi-GPU path on CPU (gloo): each process
 builds its partition with libcgx's partition layer, exchanges ghost requests,
-then runs the distributed Chronopoulos-Gear recurrence with the same
-communication pattern as the GPU solver -- halo point-to-point, ONE
-all-reduce of (gamma, delta) per iteration -- and the gathered x is checked
-against the serial oracle."""
+then runs the distributed recurrence with the same communication pattern as
+the GPU solver -- Chronopoulos-Gear: halo of r point-to-point, ONE all-reduce
+of (gamma, delta) per iteration; HS: halo of p, one all-reduce of p.s and one
+of r.r -- and the gathered x is checked against the serial oracle."""
 import os
 import socket
 
@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, out_path):
+def _worker(rank, world, port, kind, out_path, alg="cg1"):
     import sys
     from pathlib import Path
     repo = Path(__file__).resolve().parent.parent
@@ -87,6 +87,34 @@ def _worker(rank, world, port, kind, out_path):
         return float(t[0]), float(t[1])
 
     maxit, tol = 500, 1e-10
+    if alg == "hs":  # cg.c:88-141 with the two dots all-reduced
+        def allreduce1(a):
+            t = torch.tensor([a], dtype=torch.float64)
+            dist.all_reduce(t)
+            return float(t[0])
+        x = np.zeros(n_loc)
+        r = b.copy()
+        p = b.copy()
+        rr = allreduce1(float(np.dot(r, r)))
+        bb, k = rr, 0
+        while True:
+            s = H.o_spmv(rp, lcol, val, halo(p))
+            alpha = rr / allreduce1(float(np.dot(p, s)))
+            x = x + alpha * p
+            r = r - alpha * s
+            rr_new = allreduce1(float(np.dot(r, r)))
+            if k == maxit or rr_new <= tol * tol * bb:
+                break
+            p = r + (rr_new / rr) * p
+            rr = rr_new
+            k += 1
+        xs = [None] * world
+        dist.all_gather_object(xs, x.tolist())
+        if rank == 0:
+            np.save(out_path, np.array(sum(xs, [])))
+            np.save(out_path + ".its.npy", np.array([k + 1]))
+        dist.destroy_process_group()
+        return
     x = np.zeros(n_loc)
     r = b.copy()
     p = np.zeros(n_loc)
@@ -116,12 +144,13 @@ def _worker(rank, world, port, kind, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("alg", ["cg1", "hs"])
 @pytest.mark.parametrize("kind", ["lap3d", "rand"])
-def test_distributed_cg1_world2_gloo(kind, tmp_path):
+def test_distributed_world2_gloo(kind, alg, tmp_path):
     import helpers as H
     import cgx
     out = str(tmp_path / "x.npy")
-    mp.start_processes(_worker, args=(2, _free_port(), kind, out), nprocs=2,
+    mp.start_processes(_worker, args=(2, _free_port(), kind, out, alg), nprocs=2,
                        join=True, start_method="spawn")
     x = np.load(out)
     its = int(np.load(out + ".its.npy")[0])
@@ -131,7 +160,7 @@ def test_distributed_cg1_world2_gloo(kind, tmp_path):
     else:
         rp, col, val = cgx.random_spd(1200, 6, 3)
         b = np.random.default_rng(9).standard_normal(1200)
-    x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=True)
+    x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=alg == "cg1")
     assert abs(its - its_ref) <= 1
     assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
     res = b - H.o_spmv(rp, col, val, x)
