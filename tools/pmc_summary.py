@@ -16,6 +16,8 @@ Both count L2 misses, including those the Infinity Cache serves: an upper
 bound of DRAM traffic.
 
   python tools/pmc_summary.py <tag> <round> <workload> [algorithmic_spmv_bytes]
+(the SpMV it reports is k_spmv_dc when the run has it, else the k_spmv* kernel
+with the most launches)
 """
 import csv
 import collections
@@ -68,7 +70,11 @@ for s in stats:
                  ea_rd / 1e6, ea_wr / 1e6, guide / 1e6, ea / avg_ns if avg_ns else 0))
     if "k_stream_read" in name:
         calib = ea_rd
-    if "k_spmv" in name and (spmv is None or int(s["Calls"]) > spmv["calls"]):
+    # the solver's default SpMV: the coded-column kernel when present (the bench
+    # also runs the plain-CSR kernel for its csr_plain line), else the SpMV
+    # kernel with the most launches
+    prefer = "k_spmv_dc" if any("k_spmv_dc" in t["Name"] for t in stats) else "k_spmv"
+    if prefer in name and (spmv is None or int(s["Calls"]) > spmv["calls"]):
         spmv = dict(kernel=short(name), calls=int(s["Calls"]), avg_us=avg_ns / 1e3,
                     ea_read_bytes=ea_rd, ea_write_bytes=ea_wr,
                     guide_bytes_2fetch_plus_write=guide,
