@@ -65,6 +65,8 @@ struct cgx_dist {
   long long n_global = 0;
   int row_begin = 0, n_loc = 0, n_ghost = 0, nnz = 0;
   int vec = 4, wpb = 4;
+  // SpMV knobs, read from the environment once (CGX_SPMV_TG/DMA/NT/XCD)
+  int spmv_tg = 1, spmv_dma = 1, spmv_nt = -1, spmv_xcd = 1;
   // recurrence (cgx_dist_set_alg): CGX_ALG_CG1 (Chronopoulos-Gear, one
   // all-reduce of 2 doubles per iteration) or CGX_ALG_HS (the reference's
   // recurrence, two all-reduces of 1 double, 8 B per row less vector traffic)
@@ -193,6 +195,10 @@ int init_common(cgx_dist *d, int device) {
   d->vec = env_int("CGX_SPMV_VEC", 4);
   if (d->vec != 1 && d->vec != 2 && d->vec != 4) d->vec = 4;
   d->wpb = env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
+  d->spmv_tg = env_int("CGX_SPMV_TG", 1);
+  d->spmv_dma = d->wpb == 4 && env_int("CGX_SPMV_DMA", 1) == 1 ? 1 : 0;  // as the solver
+  d->spmv_nt = env_int("CGX_SPMV_NT", -1);
+  d->spmv_xcd = env_int("CGX_SPMV_XCD", 1);
   d->graph_batch = env_int("CGX_GRAPH", 1) ? std::max(1, env_int("CGX_GRAPH_BATCH", 16)) : 0;
   {
     const char *al = getenv("CGX_DIST_ALG");
@@ -484,7 +490,7 @@ int ensure_connected(Group *g) {
 // Coded columns on the default LDS-DMA kernel unless CGX_DC=0 / CGX_LAYOUT=csr.
 bool dc_wanted(const cgx_dist *d) {
   const char *l = getenv("CGX_LAYOUT");
-  return d->wpb == 4 && env_int("CGX_SPMV_DMA", 1) == 1 && env_int("CGX_DC", 1) != 0 &&
+  return d->wpb == 4 && d->spmv_dma == 1 && env_int("CGX_DC", 1) != 0 &&
          !(l && strcmp(l, "csr") == 0);
 }
 
@@ -510,12 +516,11 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.wpb = d->wpb;
   a.rbw = 1;
   a.st = d->d_st;
-  a.tg = env_int("CGX_SPMV_TG", 1);
-  a.dma = d->wpb == 4 ? env_int("CGX_SPMV_DMA", 1) : 0;  // as the single-GPU solver
-  if (a.dma != 1) a.dma = 0;  // grids below assume one block per wave, 4 waves per WG
-  a.nt = env_int("CGX_SPMV_NT", -1);
+  a.tg = d->spmv_tg;
+  a.dma = d->spmv_dma;  // 1 or 0: the grids assume one block per wave, 4 waves per WG
+  a.nt = d->spmv_nt;
   if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes;
-  a.xcd = a.dma ? env_int("CGX_SPMV_XCD", 1) : 0;  // XCD-contiguous blocks, as the solver
+  a.xcd = a.dma ? d->spmv_xcd : 0;  // XCD-contiguous blocks, as the solver
   a.tk = TicketArgs{};
   if (a.dma == 1 && d->ndict > 0) {
     a.code = d->d_code;
