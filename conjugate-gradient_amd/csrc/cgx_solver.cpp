@@ -320,6 +320,10 @@ struct cgx_solver {
   unsigned char *d_code = nullptr;
   int *d_dict = nullptr;
   bool want_rlen = true;           // CGX_DC_RLEN: byte row lengths instead of rp
+  bool want_tile = true;           // CGX_DC_TILE: L2-tiled block order for wide stencils
+  int tile_kb = 1536;              // CGX_DC_TILE_KB: x budget of a band sweep per XCD
+  int tile_bands = 0;
+  int *d_blklist = nullptr;        // the tiled block order (nullptr: natural)
   int want_bits = 8;               // CGX_DC_BITS=4: nibble codes when <= 16 offsets
   int code_bits = 8;
   int dc_lds_pad = 0;              // CGX_DC_LDS_PAD (diagnostic: fewer workgroups per CU)
@@ -399,6 +403,8 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_code);
   dfree((void **)&s->d_dict);
   dfree((void **)&s->d_rlen);
+  dfree((void **)&s->d_blklist);
+  s->tile_bands = 0;
   s->ndict = 0;
   s->sell = false;
   s->nslices = 0;
@@ -693,7 +699,40 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
         dfree((void **)&s->d_code);
         dfree((void **)&s->d_dict);
         dfree((void **)&s->d_rlen);
+  dfree((void **)&s->d_blklist);
+  s->tile_bands = 0;
         s->ndict = 0;
+      }
+      if (s->ndict > 0 && s->spmv_wpb == 4 && s->want_tile) {
+        // L2 tiling of the block order.  The x lines a row needs sit at its
+        // offsets; with P = the largest |offset| (a 3-D stencil's plane), an
+        // XCD sweeping rows in order needs ~3 P x-values resident to hit its
+        // 4 MiB L2 on every re-read.  When that exceeds the budget, sweep the
+        // rows in T bands of the P-periodic position instead (all planes of
+        // band 0, then band 1, ...): ~3 P / T values in flight.  Only the
+        // order of the row blocks changes -- each row's sum is the same.
+        long long P = 0;
+        for (int v : dict) P = std::max(P, (long long)std::abs(v));
+        const long long budget = (long long)s->tile_kb * 1024;
+        const long long need = 3 * P * (long long)sizeof(T);
+        if (P > 0 && need > budget && s->nblk > 0) {
+          const long long T_ = (need + budget - 1) / budget;
+          std::vector<int> order((size_t)s->nblk);
+          for (int b = 0; b < s->nblk; ++b) order[(size_t)b] = b;
+          auto band = [&](int b) { return (long long)blk[(size_t)b] % P * T_ / P; };
+          auto plane = [&](int b) { return (long long)blk[(size_t)b] / P; };
+          std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+            const long long bx = band(x), by = band(y);
+            return bx != by ? bx < by : plane(x) < plane(y);
+          });
+          if ((rc = dalloc(s, (void **)&s->d_blklist, (size_t)s->nblk * 4))) {
+            free_matrix(s);
+            return rc;
+          }
+          CGX_HIP(hipMemcpy(s->d_blklist, order.data(), (size_t)s->nblk * 4,
+                            hipMemcpyHostToDevice));
+          s->tile_bands = (int)T_;
+        }
       }
     }
   }
@@ -810,6 +849,7 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
     a.ndict_cap = dict_cap(s->ndict);
     a.rlen = s->d_rlen;
     a.code_bits = s->code_bits;
+    a.blk_list = s->d_blklist;
     a.lds_pad = s->dc_lds_pad;
   }
   return a;
@@ -1260,6 +1300,8 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->want_dc = cgx::env_wants_dc();
   s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
+  s->want_tile = cgx::env_int("CGX_DC_TILE", 1) != 0;
+  s->tile_kb = std::max(64, cgx::env_int("CGX_DC_TILE_KB", 1536));
   s->dc_lds_pad = std::max(0, std::min(cgx::env_int("CGX_DC_LDS_PAD", 0), 65536));
   s->want_bits = cgx::env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;  // nibbles: neutral at C3 (dc3 sweep)
   s->ticket = cgx::env_int("CGX_TICKET", 0) != 0 && s->spmv_dma == 0;  // DMA/pipe: partials only
@@ -1448,6 +1490,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->device_bytes = s->dev_bytes;
   info->n_panels = s->npanel;
   info->n_dict = s->ndict;
+  info->tile_bands = s->tile_bands;
   return 0;
 }
 

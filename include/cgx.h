@@ -90,6 +90,9 @@ typedef struct {
   int n_dict;           /* dictionary-coded columns: distinct col - row
                            offsets (1..256, one code byte per nonzero on the
                            device); 0: plain 4-byte columns                  */
+  int tile_bands;       /* L2-tiled row-block order: bands of the widest
+                           offset's period swept one after another (0: the
+                           natural order)                                    */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);

@@ -796,6 +796,29 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
         assert abs(its - its_o) <= 1
 
 
+@pytest.mark.parametrize("kb", ["", "64", "0"])
+def test_tiled_block_order_bit_exact(kb, monkeypatch):
+    """L2-tiled row-block order (CGX_DC_TILE_KB budget; 0 = off): the SpMV
+    is bit-identical to the oracle whatever the order, and a CG run stays
+    within the fast-mode tolerance."""
+    if kb == "0":
+        monkeypatch.setenv("CGX_DC_TILE", "0")
+    elif kb:
+        monkeypatch.setenv("CGX_DC_TILE_KB", kb)
+    rp, col, val = cgx.laplacian3d(120, 100, 20)  # plane 12000 rows: 288 KB of x per 3 planes
+    n = len(rp) - 1
+    x = np.random.default_rng(8).standard_normal(n)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_dict"] == 7
+        assert s.info()["tile_bands"] == {"": 0, "64": 5, "0": 0}[kb]
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        s.set_rhs(x)
+        s.run(30)
+        x_ref, _ = H.o_conj_grad(30, rp, col, val, x)
+        assert rel(s.x(), x_ref) <= FAST_RTOL
+
+
 def test_c4_full_size_spmv_device_generated():
     """C4 at full size (400^3: 64,000,000 rows, 447,040,000 nnz -- the largest
     BASELINE config, int32 offsets up to 2^28.7): the device-generated CSR
