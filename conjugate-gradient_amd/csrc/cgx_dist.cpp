@@ -279,6 +279,9 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
     d->g_int = d->g_bnd = 0;
     for (auto &r : d->runs_int) d->g_int += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
     for (auto &r : d->runs_bnd) d->g_bnd += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
+    // several boundary runs (a middle slab's first and last plane): one launch
+    // over the boundary block list instead of one per run
+    if (d->runs_bnd.size() > 1) d->g_bnd = spmv_launch_grid(64, d->wpb, 1, d->n_bnd, 0);
   } else {
     d->g_int = spmv_launch_grid(64, d->wpb, 1, d->n_int, 0);
     d->g_bnd = spmv_launch_grid(64, d->wpb, 1, d->n_bnd, 0);
@@ -586,7 +589,7 @@ int phase_halo(cgx_dist *d) {
 // contiguous run, partials packed after each other from d_pb + part_off.
 int spmv_set(cgx_dist *d, bool boundary) {
   SpmvArgs<double> a = spmv_args(d, boundary);
-  if (!d->use_runs) {
+  if (!d->use_runs || (boundary && d->runs_bnd.size() > 1)) {
     CGX_HIP(launch_spmv<double>(a, boundary ? d->g_bnd : d->g_int, d->vec, d->st));
     return 0;
   }
