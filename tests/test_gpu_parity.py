@@ -303,6 +303,35 @@ def test_dictionary_coded_columns_bit_exact(capw, rlen, bits, monkeypatch):
                               H.o_spmv_f32(rp, col, v32, x32).view(np.uint32))
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_dictionary_coded_random_patterns(seed):
+    """Randomised sparsity patterns for the coded-column encoder and kernel:
+    n not a multiple of 64, empty and ragged rows (0-40 entries), 1-256
+    distinct offsets drawn from a random band, unsorted offset draws (the
+    CSR columns are sorted per row); the SpMV is bit-identical to the oracle,
+    and a pattern with 257 offsets stays plain CSR."""
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(1, 9000))
+    nd = int(rng.integers(1, 258))
+    offs = rng.choice(np.arange(-4000, 4001), size=nd, replace=False)
+    rows = []
+    for r in range(n):
+        k = int(rng.integers(0, 41)) if rng.random() > 0.1 else 0
+        cand = r + offs
+        cand = cand[(cand >= 0) & (cand < n)]
+        rows.append(np.sort(rng.choice(cand, size=min(k, len(cand)), replace=False)))
+    rp = np.zeros(n + 1, dtype=np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32) if rp[-1] else np.zeros(0, np.int32)
+    val = rng.standard_normal(len(col))
+    x = rng.standard_normal(n)
+    used = len(np.unique(col - np.repeat(np.arange(n), np.diff(rp)))) if len(col) else 0
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["n_dict"] == (used if 0 < used <= 256 else 0)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+
+
 def test_dictionary_coded_cg_identical_to_csr(monkeypatch):
     """The coded layout changes only how columns are stored: a CG run is
     bit-identical to the plain-CSR run (x and the r.r history)."""
