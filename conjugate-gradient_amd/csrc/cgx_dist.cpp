@@ -136,7 +136,12 @@ bool solo(const cgx_dist *d) { return !d->local && d->comm == nullptr; }
 template <typename P>
 int dalloc(cgx_dist *d, P **p, size_t bytes) {
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipMalloc((void **)p, bytes);
+  hipError_t e = hipErrorUnknown;
+  if (env_int("CGX_CONTIG", 1)) {  // physically contiguous, as the solver (fallback: hipMalloc)
+    e = hipExtMallocWithFlags((void **)p, bytes, hipDeviceMallocContiguous);
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  if (e != hipSuccess) e = hipMalloc((void **)p, bytes);
   if (e != hipSuccess) {
     set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     *p = nullptr;

@@ -327,6 +327,7 @@ struct cgx_solver {
   int want_bits = 8;               // CGX_DC_BITS=4: nibble codes when <= 16 offsets
   int code_bits = 8;
   int dc_lds_pad = 0;              // CGX_DC_LDS_PAD (diagnostic: fewer workgroups per CU)
+  bool contig = false;             // CGX_CONTIG: physically contiguous device allocations
   unsigned char *d_rlen = nullptr;
   // SELL-64 internal layout (CGX_LAYOUT=sell): d_col/d_val hold the slices
   bool want_sell = false, sell = false;
@@ -368,7 +369,12 @@ size_t tsize(int dtype) { return dtype == CGX_F32 ? 4 : 8; }
 
 int dalloc(cgx_solver *s, void **p, size_t bytes) {
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipMalloc(p, bytes);
+  hipError_t e = hipErrorUnknown;
+  if (s->contig) {  // physically contiguous (CGX_CONTIG), falling back to hipMalloc
+    e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  if (e != hipSuccess) e = hipMalloc(p, bytes);
   if (e != hipSuccess) {
     set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     *p = nullptr;
@@ -1300,6 +1306,9 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->want_dc = cgx::env_wants_dc();
   s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
+  // physically contiguous allocations: -1 to -2% per C3 iteration in two
+  // order-swapped A/Bs with 4 allocations per variant (tools/gpu_contig1.sh)
+  s->contig = cgx::env_int("CGX_CONTIG", 1) != 0;
   s->want_tile = cgx::env_int("CGX_DC_TILE", 1) != 0;
   s->tile_kb = std::max(64, cgx::env_int("CGX_DC_TILE_KB", 1536));
   s->dc_lds_pad = std::max(0, std::min(cgx::env_int("CGX_DC_LDS_PAD", 0), 65536));
