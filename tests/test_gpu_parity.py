@@ -825,6 +825,27 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
         assert abs(its - its_o) <= 1
 
 
+@pytest.mark.parametrize("wpb", ["8"])
+def test_coded_wide_workgroups_cg(wpb, monkeypatch):
+    """The 8-wave coded-column kernel (half the epilogue partials) inside
+    the HS iteration: x within the fast-mode tolerance, runs reproducible."""
+    monkeypatch.setenv("CGX_SPMV_WPB", wpb)
+    rp, col, val = cgx.laplacian3d(60, 50, 40)
+    b = np.random.default_rng(12).standard_normal(len(rp) - 1)
+    xs = []
+    for _ in range(2):
+        with cgx.Solver(0) as s:
+            s.set_matrix(rp, col, val)
+            assert s.info()["n_dict"] == 7
+            assert s.info()["spmv_grid"] == -(-s.info()["n_rowblocks"] // int(wpb))
+            s.set_rhs(b)
+            s.run(30)
+            xs.append(s.x())
+    x_ref, _ = H.o_conj_grad(30, rp, col, val, b)
+    assert rel(xs[0], x_ref) <= FAST_RTOL
+    assert H.same_bits_or_both_nan(xs[0], xs[1])
+
+
 @pytest.mark.parametrize("kb", ["", "64", "0"])
 def test_tiled_block_order_bit_exact(kb, monkeypatch):
     """L2-tiled row-block order (CGX_DC_TILE_KB budget; 0 = off): the SpMV
