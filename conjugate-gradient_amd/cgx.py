@@ -46,7 +46,8 @@ class CgxInfo(ctypes.Structure):
                 ("vec_grid", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
                 ("iter_bytes", ctypes.c_double), ("spmv_iter_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("n_panels", ctypes.c_int),
-                ("n_dict", ctypes.c_int), ("tile_bands", ctypes.c_int)]
+                ("n_dict", ctypes.c_int), ("tile_bands", ctypes.c_int),
+                ("dict_vals", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):
@@ -56,7 +57,7 @@ class CgxDistStats(ctypes.Structure):
                 ("boundary_blocks", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
                 ("iter_bytes", ctypes.c_double), ("halo_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("spmv_iter_bytes", ctypes.c_double),
-                ("n_dict", ctypes.c_int)]
+                ("n_dict", ctypes.c_int), ("dict_vals", ctypes.c_int)]
 
 
 _MVP = ctypes.POINTER(MvSparse)

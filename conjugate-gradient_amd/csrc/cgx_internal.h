@@ -163,6 +163,12 @@ struct SpmvArgs {
   const unsigned char *rlen;
   int code_bits;       // k_spmv_dc: 8 (byte codes) or 4 (nibbles, <= 16 offsets)
   int lds_pad;         // k_spmv_dc diagnostic: extra dynamic LDS bytes per workgroup
+  // k_spmv_vi (value-indexed pairs, CSR-VI) when dval != nullptr: the
+  // dictionary entries are (dict[c], dval[c]) pairs and val[k] ==
+  // dval[code[k]] bit for bit, so val is not read (needs rlen, <= 64 pairs,
+  // 4 waves per workgroup, every block's code window inside the kernel's)
+  const T *dval;
+  int bpw;             // k_spmv_vi: row blocks per wave (1 | 2 | 4; byte codes)
 };
 
 // Dictionary-coded columns (host side, cgx_solver.cpp): the distinct column
@@ -171,6 +177,14 @@ struct SpmvArgs {
 // more than 256 distinct offsets (or no nonzeros): then it stays plain CSR.
 int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict,
                     unsigned char *code);
+// Value-indexed pairs (CSR-VI): from offset codes (dict = the offsets), the
+// distinct (offset, value bit pattern) pairs, sorted by offset then bits.  On
+// success (<= cap pairs) code is rewritten to pair codes, dict to the pairs'
+// offsets, dval to their values, and the pair count returned; 0 (code, dict
+// untouched) otherwise.
+template <typename T>
+int build_val_pairs(long long nnz, const T *val, unsigned char *code, std::vector<int> &dict,
+                    std::vector<T> &dval, int cap);
 // Nibble codes (dictionaries of <= 16 offsets): entry k in bits 4*(k&1) of
 // byte k/2; out holds (nnz + 1) / 2 bytes.
 void pack_nibbles(long long nnz, const unsigned char *code, unsigned char *out);
@@ -241,8 +255,11 @@ __host__ __device__ inline long long lap_rp(long long i, const LapSpec &g) {
 hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
                                 hipStream_t st);
 // Device-side coded columns against a sorted dictionary (err |= 1 on a miss).
+// With dval (value-indexed pairs, one value per offset): also err |= 1 when
+// val[k] differs from dval[code] in any bit.
 hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dict, int nd,
-                            unsigned char *code, int *err, hipStream_t st);
+                            unsigned char *code, int *err, hipStream_t st,
+                            const double *val = nullptr, const double *dval = nullptr);
 // The column offsets col - row a generated Laplacian can hold, sorted.
 std::vector<int> lap_offsets(const LapSpec &g);
 template <typename T>

@@ -1365,6 +1365,160 @@ void launch_dc_w(const SpmvArgs<T> &a, hipStream_t st) {
   else launch_dc_nd<T, CAPW, 256>(a, st);
 }
 
+// Value-indexed pairs (CSR-VI).  When a matrix has <= 64 distinct
+// (col - row, value) pairs -- constant-coefficient stencils, small value
+// sets -- one code per nonzero names both the offset and the value:
+// col[k] = row + dict[code[k]], val[k] = dval[code[k]] (bit for bit), and
+// the val stream disappears.  C3's SpMV moves 241 MB instead of 804 MB
+// (codes 70, row lengths 10, x 81, y 81).  Without the val window a wave's
+// LDS slice is a few hundred bytes, so a wave takes BPW row blocks at once
+// (lane t sums row t of each; their gathers are issued together), which
+// divides the waves -- and the epilogue partials -- by BPW while each wave
+// keeps the same three dependent memory round trips (descriptor; codes, row
+// lengths and dictionary; x gathers).  Every row is summed sequentially in
+// column order from 0 (mv_ops.c:190-194), as in every other SpMV kernel.
+// The host guarantees every row block's code window fits CAPC bytes
+// (rows <= 255 entries, blocks <= CAPW entries).
+template <typename T, int CAPW, bool EPI, bool NT, int CB, bool LIST, int BPW>
+__global__ __launch_bounds__(4 * kWave) void k_spmv_vi(SpmvArgs<T> a) {
+  constexpr int WPB = 4, ND = 64, U = 8;
+  constexpr int AUX = NT ? 2 : 0;
+  constexpr int KA = 16 * 8 / CB;  // entries per 16-B code granule
+  constexpr int CAPC = ((CAPW + KA) * CB / 8 + 15) & ~15;
+  __shared__ __attribute__((aligned(16))) unsigned char lcode_all[WPB * BPW * CAPC];
+  __shared__ int ldict_all[WPB * ND];
+  __shared__ T ldv_all[WPB * ND];
+  __shared__ double red[WPB];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  unsigned char *lcode = lcode_all + wid * BPW * CAPC;
+  int *ldict = ldict_all + wid * ND;
+  T *ldv = ldv_all + wid * ND;
+  const int wb0 = __builtin_amdgcn_readfirstlane(xcd_block(a.xcd) * WPB + wid) * BPW;
+  double dot = 0.0;
+  if (wb0 < a.nblk) {
+    const int *dp = a.done ? a.done : a.blk_k;
+    const int stop = *dp;
+    int r0[BPW], nr[BPW], k0[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      const int wb = wb0 + b < a.nblk ? wb0 + b : wb0;  // past the end: a copy, no rows
+      const int rb = LIST ? a.blk_list[wb] : a.blk_first + wb;
+      const int *d = a.blk_rk + 2 * rb;
+      r0[b] = d[0];
+      k0[b] = d[1];
+      nr[b] = wb0 + b < a.nblk ? d[2] - d[0] : 0;
+      const int k1 = d[3];
+      asm volatile("" ::"s"(r0[b]), "s"(nr[b]), "s"(k0[b]), "s"(k1));
+      if (b == BPW - 1 && stop) return;  // every wave of the grid sees the same flag
+      const int kc = k0[b] & ~(KA - 1);
+      const int mc = nr[b] ? ((k1 - kc) * CB + 7) / 8 : 0;
+      const unsigned char *cbase = a.code + (size_t)kc * CB / 8;
+#pragma unroll
+      for (int i = 0; i < (CAPC + 1023) / 1024; ++i)
+        if ((i * kWave + lane) * 16 < mc)
+          __builtin_amdgcn_global_load_lds((const void *)(cbase + i * kWave * 16 + lane * 16),
+                                           (lds_void *)(lcode + b * CAPC + i * kWave * 16), 16,
+                                           0, AUX);
+    }
+    int len[BPW];
+    T xrow[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      len[b] = lane < nr[b] ? a.rlen[r0[b] + lane] : 0;
+      xrow[b] = EPI && lane < nr[b] ? a.x[r0[b] + lane] : T(0);
+    }
+    const int dv = a.dict[lane];
+    const T dvv = a.dval[lane];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ldict[lane] = dv;
+    ldv[lane] = dvv;
+    int jb[BPW], maxlen = 0;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      // entry index of the row's first code inside block b's window
+      jb[b] = k0[b] + wave_incl_scan(len[b], lane) - len[b] - (k0[b] & ~(KA - 1));
+      maxlen = max(maxlen, len[b]);
+    }
+    wave_lds_sync();
+    T acc[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) acc[b] = T(0);
+    for (int j = 0; j < maxlen; j += U) {
+      int code[BPW][U];
+      T xx[BPW][U];
+#pragma unroll
+      for (int b = 0; b < BPW; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          code[b][u] = dc_code<CB>(lcode + b * CAPC, j + u < len[b] ? jb[b] + j + u : 0);
+#pragma unroll
+      for (int b = 0; b < BPW; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          xx[b][u] = a.x[j + u < len[b] ? r0[b] + lane + ldict[code[b][u]] : 0];
+#pragma unroll
+      for (int b = 0; b < BPW; ++b)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const T prod = ldv[code[b][u]] * xx[b][u];
+          acc[b] = acc[b] + (j + u < len[b] ? prod : T(0));  // +0 never changes the sum
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < BPW; ++b)
+      if (lane < nr[b]) {
+        a.y[r0[b] + lane] = acc[b];
+        if (EPI) dot = dot + (double)xrow[b] * (double)acc[b];
+      }
+  }
+  if (EPI) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) s = s + red[w];
+      a.part[blockIdx.x] = s;
+    }
+  }
+}
+
+template <typename T, int CAPW, int CB, int BPW>
+void launch_vi_b(const SpmvArgs<T> &a, hipStream_t st) {
+  const int g = (a.nblk + 4 * BPW - 1) / (4 * BPW);
+  const dim3 blk(4 * kWave);
+  const bool epi = a.part != nullptr, list = a.blk_list != nullptr;
+#define CGX_VI(E, N, L) \
+  hipLaunchKernelGGL((k_spmv_vi<T, CAPW, E, N, CB, L, BPW>), dim3(g), blk, 0, st, a)
+  if (list) {
+    if (epi && a.nt) CGX_VI(true, true, true);
+    else if (epi) CGX_VI(true, false, true);
+    else if (a.nt) CGX_VI(false, true, true);
+    else CGX_VI(false, false, true);
+  } else {
+    if (epi && a.nt) CGX_VI(true, true, false);
+    else if (epi) CGX_VI(true, false, false);
+    else if (a.nt) CGX_VI(false, true, false);
+    else CGX_VI(false, false, false);
+  }
+#undef CGX_VI
+}
+
+template <typename T, int CAPW>
+void launch_vi(const SpmvArgs<T> &a, hipStream_t st) {
+  if (a.code_bits == 4) {
+    launch_vi_b<T, CAPW, 4, 1>(a, st);
+  } else {
+    switch (a.bpw) {
+      case 2: launch_vi_b<T, CAPW, 8, 2>(a, st); break;
+      case 4: launch_vi_b<T, CAPW, 8, 4>(a, st); break;
+      default: launch_vi_b<T, CAPW, 8, 1>(a, st); break;
+    }
+  }
+}
+
 // SELL-64 (sliced ELLPACK, one 64-row slice per wave, column-major inside the
 // slice): lane t owns row t of its slice and walks the row's nonzeros in
 // column order, so every load is a coalesced wave-wide line (val 512 B, col
@@ -2173,6 +2327,17 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, int grid, int vec, hipStream_t st) 
   if (a.nblk <= 0) return hipSuccess;
   if (a.code) {  // dictionary-coded columns (k_spmv_dc)
     if (a.bs != 64 || a.dma != 1 || a.x2 || a.yacc) return hipErrorInvalidValue;
+    if (a.dval) {  // value-indexed pairs (k_spmv_vi)
+      if (!a.rlen || a.ndict_cap > 64 || a.wpb != 4) return hipErrorInvalidValue;
+      if constexpr (sizeof(T) == 4) {
+        launch_vi<T, 1024>(a, st);
+      } else {
+        if (a.capw == 328) launch_vi<T, 328>(a, st);
+        else if (a.capw == 0 || a.capw == 512) launch_vi<T, 512>(a, st);
+        else return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
     if (sizeof(T) == 4) launch_dc_w<T, 1024>(a, st);
     else if (a.capw == 328) launch_dc_w<T, 328>(a, st);
     else if (a.capw == 0 || a.capw == 512) launch_dc_w<T, 512>(a, st);
@@ -2494,7 +2659,9 @@ __global__ __launch_bounds__(256) void k_dc_encode(int n, const int *__restrict_
                                                    const int *__restrict__ col,
                                                    const int *__restrict__ dict, int nd,
                                                    unsigned char *__restrict__ code,
-                                                   int *__restrict__ err) {
+                                                   int *__restrict__ err,
+                                                   const double *__restrict__ val,
+                                                   const double *__restrict__ dval) {
   for (int r = blockIdx.x * 256 + threadIdx.x; r < n; r += gridDim.x * 256) {
     for (int k = rp[r]; k < rp[r + 1]; ++k) {
       const int off = col[k] - r;
@@ -2505,15 +2672,19 @@ __global__ __launch_bounds__(256) void k_dc_encode(int n, const int *__restrict_
         else hi = mid;
       }
       if (dict[lo] != off) atomicOr(err, 1);
+      if (dval && __double_as_longlong(val[k]) != __double_as_longlong(dval[lo]))
+        atomicOr(err, 1);
       code[k] = (unsigned char)lo;
     }
   }
 }
 
 hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dict, int nd,
-                            unsigned char *code, int *err, hipStream_t st) {
+                            unsigned char *code, int *err, hipStream_t st,
+                            const double *val, const double *dval) {
   const int grid = std::max(1, std::min((n + 255) / 256, 8192));
-  hipLaunchKernelGGL(k_dc_encode, dim3(grid), dim3(256), 0, st, n, rp, col, dict, nd, code, err);
+  hipLaunchKernelGGL(k_dc_encode, dim3(grid), dim3(256), 0, st, n, rp, col, dict, nd, code, err,
+                     val, dval);
   return hipGetLastError();
 }
 

@@ -239,6 +239,93 @@ int build_col_codes(int n, const int *rp, const int *col, std::vector<int> &dict
   return (int)dict.size();
 }
 
+template <typename T>
+int build_val_pairs(long long nnz, const T *val, unsigned char *code, std::vector<int> &dict,
+                    std::vector<T> &dval, int cap) {
+  const int nd = (int)dict.size();
+  dval.clear();
+  if (nnz <= 0 || nd <= 0) return 0;
+  auto bits = [](T v) {
+    unsigned long long b = 0;
+    memcpy(&b, &v, sizeof v);
+    return b;
+  };
+  int nt = (int)std::min<long long>(16, std::max<long long>(1, nnz >> 22));
+  nt = std::max(1, std::min(nt, (int)std::thread::hardware_concurrency()));
+  auto beg = [&](int t) { return nnz * t / nt; };
+  // per thread: the distinct value bit patterns of each offset code
+  std::vector<std::vector<std::vector<unsigned long long>>> seen(
+      (size_t)nt, std::vector<std::vector<unsigned long long>>((size_t)nd));
+  std::vector<int> ok((size_t)nt, 1);
+  auto pass1 = [&](int t) {
+    auto &S = seen[(size_t)t];
+    int tot = 0;
+    unsigned long long last_b = 0;
+    int last_c = -1;
+    for (long long k = beg(t); k < beg(t + 1); ++k) {
+      const int c = code[k];
+      const unsigned long long b = bits(val[k]);
+      if (c == last_c && b == last_b) continue;
+      auto &L = S[(size_t)c];
+      if (std::find(L.begin(), L.end(), b) == L.end()) {
+        if (++tot > cap) {
+          ok[(size_t)t] = 0;
+          return;
+        }
+        L.push_back(b);
+      }
+      last_c = c;
+      last_b = b;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(pass1, t);
+  pass1(0);
+  for (auto &x : th) x.join();
+  th.clear();
+  for (int t = 0; t < nt; ++t)
+    if (!ok[(size_t)t]) return 0;
+  std::vector<std::vector<unsigned long long>> all((size_t)nd);
+  std::vector<int> base((size_t)nd + 1, 0);
+  for (int c = 0; c < nd; ++c) {
+    auto &A = all[(size_t)c];
+    for (int t = 0; t < nt; ++t)
+      for (unsigned long long b : seen[(size_t)t][(size_t)c])
+        if (std::find(A.begin(), A.end(), b) == A.end()) A.push_back(b);
+    std::sort(A.begin(), A.end());
+    base[(size_t)c + 1] = base[(size_t)c] + (int)A.size();
+  }
+  const int np = base[(size_t)nd];
+  if (np > cap) return 0;
+  std::vector<int> pd((size_t)np);
+  dval.resize((size_t)np);
+  for (int c = 0; c < nd; ++c)
+    for (size_t i = 0; i < all[(size_t)c].size(); ++i) {
+      pd[(size_t)base[(size_t)c] + i] = dict[(size_t)c];
+      T v;
+      const unsigned long long b = all[(size_t)c][i];
+      memcpy(&v, &b, sizeof v);
+      dval[(size_t)base[(size_t)c] + i] = v;
+    }
+  auto pass2 = [&](int t) {
+    for (long long k = beg(t); k < beg(t + 1); ++k) {
+      const int c = code[k];
+      const auto &A = all[(size_t)c];
+      const unsigned long long b = bits(val[k]);
+      code[k] = (unsigned char)(base[(size_t)c] + (std::find(A.begin(), A.end(), b) - A.begin()));
+    }
+  };
+  for (int t = 1; t < nt; ++t) th.emplace_back(pass2, t);
+  pass2(0);
+  for (auto &x : th) x.join();
+  dict = pd;
+  return np;
+}
+template int build_val_pairs<double>(long long, const double *, unsigned char *,
+                                     std::vector<int> &, std::vector<double> &, int);
+template int build_val_pairs<float>(long long, const float *, unsigned char *,
+                                    std::vector<int> &, std::vector<float> &, int);
+
 void pack_nibbles(long long nnz, const unsigned char *code, unsigned char *out) {
   for (long long i = 0; i + 1 < nnz; i += 2)
     out[i >> 1] = (unsigned char)(code[i] | (code[i + 1] << 4));
@@ -319,6 +406,12 @@ struct cgx_solver {
   int ndict = 0;
   unsigned char *d_code = nullptr;
   int *d_dict = nullptr;
+  // value-indexed pairs (CGX_DC_VALS, default on where it applies): the
+  // dictionary holds (offset, value) pairs and the SpMV does not read val
+  bool want_vi = true;
+  bool vi = false;
+  void *d_dval = nullptr;
+  int vi_bpw = 1;                  // CGX_VI_BPW: row blocks per wave of k_spmv_vi
   bool want_rlen = true;           // CGX_DC_RLEN: byte row lengths instead of rp
   bool want_tile = true;           // CGX_DC_TILE: L2-tiled block order for wide stencils
   int tile_kb = 1536;              // CGX_DC_TILE_KB: x budget of a band sweep per XCD
@@ -408,6 +501,8 @@ void free_matrix(cgx_solver *s) {
   dfree((void **)&s->d_slen);
   dfree((void **)&s->d_code);
   dfree((void **)&s->d_dict);
+  dfree(&s->d_dval);
+  s->vi = false;
   dfree((void **)&s->d_rlen);
   dfree((void **)&s->d_blklist);
   s->tile_bands = 0;
@@ -651,13 +746,46 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       code.resize((size_t)nnz);
       nd = build_col_codes(n, rp, col, dict, code.data());
     }
+    std::vector<unsigned char> rl;
+    if (nd > 0 && s->want_rlen) {
+      rl.resize((size_t)n);
+      if (!build_row_lengths(n, rp, rl.data())) rl.clear();
+    }
+    // value-indexed pairs: 4-wave kernel with row lengths, <= 64 pairs
+    std::vector<T> dv;
+    // (rows <= 255 entries < every window, so each block's code window fits
+    // the kernel's; checked anyway)
+    bool vi_fits = true;
+    {
+      const int capw = sizeof(T) == 4 ? 1024 : (s->spmv_capw == 328 ? 328 : 512);
+      const int cb = nd <= 16 && s->want_bits == 4 && !gen ? 4 : 8, ka = 128 / cb;
+      const long long capc = ((long long)(capw + ka) * cb / 8 + 15) & ~15LL;
+      for (int b = 0; b < s->nblk && vi_fits; ++b)
+        vi_fits = ((long long)(blkk[(size_t)b + 1] - (blkk[(size_t)b] & ~(ka - 1))) * cb + 7) / 8 <= capc;
+    }
+    if (nd > 0 && s->want_vi && !rl.empty() && s->spmv_wpb == 4 && vi_fits) {
+      if (gen) {  // one value per offset: 2 dim on the diagonal, -1 off it
+        dv.resize((size_t)nd);
+        for (int c = 0; c < nd; ++c) dv[(size_t)c] = dict[(size_t)c] == 0 ? T(2 * gen->dim) : T(-1);
+      } else {
+        const int np = build_val_pairs<T>(nnz, val, code.data(), dict, dv, 64);
+        if (np > 0) nd = np;
+      }
+    }
     if (nd > 0) {
       if ((rc = dalloc(s, (void **)&s->d_code, nnz_pad)) ||
-          (rc = dalloc(s, (void **)&s->d_dict, 256 * 4))) {
+          (rc = dalloc(s, (void **)&s->d_dict, 256 * 4)) ||
+          (!dv.empty() && (rc = dalloc(s, &s->d_dval, 256 * sizeof(T))))) {
         free_matrix(s);
         return rc;
       }
       dict.resize(256, 0);
+      if (!dv.empty()) {
+        dv.resize(256, T(0));
+        CGX_HIP(hipMemcpyAsync(s->d_dval, dv.data(), 256 * sizeof(T), hipMemcpyHostToDevice,
+                               s->stream));
+        s->vi = true;
+      }
       s->code_bits = nd <= 16 && s->want_bits == 4 && !gen ? 4 : 8;
       size_t code_bytes = (size_t)nnz;
       if (s->code_bits == 4) {  // in place: byte i/2 is written after entry i is read
@@ -671,7 +799,8 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
         int *d_err = (int *)s->d_pb;  // scratch: partials are rewritten before use
         CGX_HIP(hipMemsetAsync(d_err, 0, 4, s->stream));
         CGX_HIP(launch_dc_encode(n, s->d_rp, s->d_col, s->d_dict, nd, s->d_code, d_err,
-                                 s->stream));
+                                 s->stream, (const double *)s->d_val,
+                                 s->vi ? (const double *)s->d_dval : nullptr));
         int err = 0;
         CGX_HIP(hipMemcpyAsync(&err, d_err, 4, hipMemcpyDeviceToHost, s->stream));
         CGX_HIP(hipStreamSynchronize(s->stream));
@@ -683,11 +812,6 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
       } else {
         CGX_HIP(hipMemcpyAsync(s->d_code, code.data(), code_bytes, hipMemcpyHostToDevice,
                                s->stream));
-      }
-      std::vector<unsigned char> rl;
-      if (s->want_rlen) {
-        rl.resize((size_t)n);
-        if (!build_row_lengths(n, rp, rl.data())) rl.clear();
       }
       if (!rl.empty()) {
         if ((rc = dalloc(s, (void **)&s->d_rlen, (size_t)n + 64))) {
@@ -704,10 +828,16 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
         // offsets only; otherwise plain CSR at 8 waves (same partial count)
         dfree((void **)&s->d_code);
         dfree((void **)&s->d_dict);
+        dfree(&s->d_dval);
+        s->vi = false;
         dfree((void **)&s->d_rlen);
   dfree((void **)&s->d_blklist);
   s->tile_bands = 0;
         s->ndict = 0;
+      }
+      if (s->ndict > 0 && s->vi) {  // k_spmv_vi: bpw row blocks per wave
+        const int bpw = s->code_bits == 8 ? s->vi_bpw : 1;
+        s->spmv_grid = (s->nblk + 4 * bpw - 1) / (4 * bpw);
       }
       if (s->ndict > 0 && s->spmv_wpb == 4 && s->want_tile) {
         // L2 tiling of the block order.  The x lines a row needs sit at its
@@ -857,6 +987,8 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
     a.code_bits = s->code_bits;
     a.blk_list = s->d_blklist;
     a.lds_pad = s->dc_lds_pad;
+    a.dval = s->vi ? (const T *)s->d_dval : nullptr;
+    a.bpw = s->code_bits == 8 ? s->vi_bpw : 1;
   }
   return a;
 }
@@ -1306,6 +1438,9 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->spmv_tg = cgx::env_int("CGX_SPMV_TG", 1);
   s->want_dc = cgx::env_wants_dc();
   s->want_rlen = cgx::env_int("CGX_DC_RLEN", 1) != 0;
+  s->want_vi = cgx::env_int("CGX_DC_VALS", 1) != 0;
+  s->vi_bpw = cgx::env_int("CGX_VI_BPW", 1);
+  if (s->vi_bpw != 2 && s->vi_bpw != 4) s->vi_bpw = 1;
   // physically contiguous allocations: -1 to -2% per C3 iteration in two
   // order-swapped A/Bs with 4 allocations per variant (tools/gpu_contig1.sh)
   s->contig = cgx::env_int("CGX_CONTIG", 1) != 0;
@@ -1498,7 +1633,11 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                             2.0 * s->n * sv + 4.0 * s->ndict;
   info->device_bytes = s->dev_bytes;
   info->n_panels = s->npanel;
+  if (s->ndict > 0 && s->vi)  // value-indexed pairs: no val stream
+    info->spmv_iter_bytes = (double)s->nnz * (s->code_bits / 8.0) + (double)s->n +
+                            2.0 * s->n * sv + (4.0 + sv) * s->ndict;
   info->n_dict = s->ndict;
+  info->dict_vals = s->ndict > 0 && s->vi;
   info->tile_bands = s->tile_bands;
   return 0;
 }

@@ -93,6 +93,9 @@ typedef struct {
   int tile_bands;       /* L2-tiled row-block order: bands of the widest
                            offset's period swept one after another (0: the
                            natural order)                                    */
+  int dict_vals;        /* 1: the dictionary holds (offset, value) pairs and
+                           the codes name both -- the SpMV streams no values
+                           (CSR-VI; <= 64 distinct pairs)                    */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);
@@ -226,6 +229,8 @@ typedef struct {
                                             columns: 1 byte per nonzero)  */
   int n_dict;                            /* coded-column dictionary size,
                                             0: plain 4-byte columns      */
+  int dict_vals;                         /* 1: (offset, value) pairs, no
+                                            value stream (see cgx_info)  */
 } cgx_dist_stats;
 
 /* Rank 0 creates the id and distributes it (e.g. torch.distributed). */

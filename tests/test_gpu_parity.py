@@ -186,7 +186,7 @@ def test_spmv_f32_bit_exact(solver):
     assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1r0", "1b4", "1w8"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1r0", "1b4", "1w8", "1v0", "1v2", "1v4"])
 def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size (default and pipelined kernels)."""
@@ -197,6 +197,10 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
         monkeypatch.setenv("CGX_DC_RLEN", "0")
     if dma.endswith("b4"):
         monkeypatch.setenv("CGX_DC_BITS", "4")
+    if dma.endswith("v0"):
+        monkeypatch.setenv("CGX_DC_VALS", "0")
+    if dma.endswith("v2") or dma.endswith("v4"):
+        monkeypatch.setenv("CGX_VI_BPW", dma[-1])
     if dma.endswith("w8"):
         monkeypatch.setenv("CGX_SPMV_WPB", "8")
     if dma.endswith("x"):
@@ -208,7 +212,8 @@ def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         # dictionary-coded columns on the default kernel (7 offsets), CSR otherwise
-        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1r0", "1b4", "1w8") else 0)
+        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1r0", "1b4", "1w8", "1v0", "1v2", "1v4") else 0)
+        assert s.info()["dict_vals"] == (1 if dma in ("1", "1x", "1b4", "1v2", "1v4") else 0)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
@@ -243,6 +248,26 @@ def banded_spd(n, offsets, seed, f32=False):
     return rp, c.astype(np.int32), v
 
 
+def expect_dict(rp, col, val, vi_ok=True):
+    """(n_dict, dict_vals) the solver should pick for a CSR matrix: coded
+    columns for <= 256 distinct col - row offsets; value-indexed pairs when
+    also <= 64 distinct (offset, value bit pattern) pairs and every row has
+    <= 255 entries (the byte row lengths the pair kernel needs)."""
+    rp, col = np.asarray(rp), np.asarray(col)
+    n = len(rp) - 1
+    if len(col) == 0:
+        return 0, 0
+    off = col.astype(np.int64) - np.repeat(np.arange(n), np.diff(rp))
+    noff = len(np.unique(off))
+    if noff > 256:
+        return 0, 0
+    bits = np.asarray(val).view(np.uint64 if np.asarray(val).dtype == np.float64 else np.uint32)
+    npair = np.unique(np.stack([off, bits.astype(np.int64)]), axis=1).shape[1]
+    if vi_ok and npair <= 64 and np.diff(rp).max() <= 255:
+        return npair, 1
+    return noff, 0
+
+
 @pytest.mark.parametrize("bits", ["4", "8"])
 @pytest.mark.parametrize("rlen", ["1", "0"])
 @pytest.mark.parametrize("capw", ["", "328", "456"])
@@ -262,10 +287,10 @@ def test_dictionary_coded_columns_bit_exact(capw, rlen, bits, monkeypatch):
         for name, _ in cases:
             g = H.load_golden(name)
             s.set_matrix(g["row_ptr"], g["col"], g["val"])
-            nd = s.info()["n_dict"]
-            want = len(np.unique(g["col"] - np.repeat(np.arange(len(g["row_ptr"]) - 1),
-                                                      np.diff(g["row_ptr"]))))
-            assert nd == (0 if capw == "456" else want), name
+            nd, vi = s.info()["n_dict"], s.info()["dict_vals"]
+            want, want_vi = expect_dict(g["row_ptr"], g["col"], g["val"],
+                                        vi_ok=rlen == "1")
+            assert (nd, vi) == ((0, 0) if capw == "456" else (want, want_vi)), name
             x = rng.standard_normal(len(g["row_ptr"]) - 1)
             assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(g["row_ptr"], g["col"], g["val"], x))
             assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"])
@@ -323,13 +348,70 @@ def test_dictionary_coded_random_patterns(seed):
     rp = np.zeros(n + 1, dtype=np.int32)
     rp[1:] = np.cumsum([len(c) for c in rows])
     col = np.concatenate(rows).astype(np.int32) if rp[-1] else np.zeros(0, np.int32)
-    val = rng.standard_normal(len(col))
+    # odd seeds: values from a small set (value-indexed pairs when <= 64
+    # (offset, value) pairs), even seeds: all distinct
+    if seed % 2:
+        val = rng.choice(np.array([-1.0, 2.5, -0.0, 0.0, 1e-300, -3.25]), size=len(col))
+    else:
+        val = rng.standard_normal(len(col))
     x = rng.standard_normal(n)
-    used = len(np.unique(col - np.repeat(np.arange(n), np.diff(rp)))) if len(col) else 0
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
-        assert s.info()["n_dict"] == (used if 0 < used <= 256 else 0)
+        assert (s.info()["n_dict"], s.info()["dict_vals"]) == expect_dict(rp, col, val)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+
+
+@pytest.mark.parametrize("bits,bpw", [("8", "1"), ("8", "2"), ("8", "4"), ("4", "1")])
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_value_indexed_pairs_bit_exact(bits, bpw, dtype, monkeypatch):
+    """CSR-VI: (offset, value) pair codes -- the SpMV reads no val stream.
+    Selected for constant-coefficient stencils and small value sets, off with
+    CGX_DC_VALS=0 or > 64 pairs; y bit-identical to the oracle in every case
+    (signed zeros and a denormal-range value keep their bit patterns; nibble
+    codes for <= 16 pairs)."""
+    monkeypatch.setenv("CGX_DC_BITS", bits)
+    monkeypatch.setenv("CGX_VI_BPW", bpw)
+    rng = np.random.default_rng(77)
+    with cgx.Solver(0) as s:
+        for name in ("lap3d_12", "lap2d_32"):
+            g = H.load_golden(name)
+            v = g["val"].astype(np.float32) if dtype == "f32" else g["val"]
+            s.set_matrix(g["row_ptr"], g["col"], v)
+            assert (s.info()["n_dict"], s.info()["dict_vals"]) == expect_dict(g["row_ptr"], g["col"], v)
+            assert s.info()["dict_vals"] == 1
+            x = rng.standard_normal(len(g["row_ptr"]) - 1)
+            if dtype == "f32":
+                x = x.astype(np.float32)
+                assert np.array_equal(s.spmv(x).view(np.uint32),
+                                      H.o_spmv_f32(g["row_ptr"], g["col"], v, x).view(np.uint32))
+            else:
+                assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(g["row_ptr"], g["col"], v, x))
+        # a banded matrix whose values per offset take a few values: 5 offsets
+        # x 12 values = 60 pairs (VI), then 65 pairs (offset codes only)
+        for nv, want_vi in ((12, 1), (13, 0)):
+            n = 5000
+            rp, col, _ = banded_spd(n, [1, 300], 3)
+            vals = np.linspace(-2, 2, nv)
+            off = col - np.repeat(np.arange(n), np.diff(rp))
+            val = vals[(np.arange(len(col)) * 7 + off) % nv]
+            if dtype == "f32":
+                val = val.astype(np.float32)
+            s.set_matrix(rp, col, val)
+            nd, vi = s.info()["n_dict"], s.info()["dict_vals"]
+            assert (nd, vi) == expect_dict(rp, col, val)
+            assert vi == want_vi
+            x = rng.standard_normal(n)
+            if dtype == "f32":
+                x = x.astype(np.float32)
+                assert np.array_equal(s.spmv(x).view(np.uint32),
+                                      H.o_spmv_f32(rp, col, val, x).view(np.uint32))
+            else:
+                assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+    monkeypatch.setenv("CGX_DC_VALS", "0")
+    g = H.load_golden("lap3d_12")
+    with cgx.Solver(0) as s:
+        s.set_matrix(g["row_ptr"], g["col"], g["val"])
+        assert (s.info()["n_dict"], s.info()["dict_vals"]) == (7, 0)
 
 
 def test_dictionary_coded_cg_identical_to_csr(monkeypatch):
@@ -823,6 +905,32 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
             its = s.run(3000, 1e-10)
         _, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
         assert abs(its - its_o) <= 1
+
+
+@pytest.mark.parametrize("bpw", ["1", "2", "4"])
+def test_value_indexed_cg(bpw, monkeypatch):
+    """CG on value-indexed pairs: with one row block per wave the SpMV
+    partials group exactly as the offset-coded kernel's, so the run is
+    bit-identical to CGX_DC_VALS=0; 2 and 4 blocks per wave regroup p.s
+    (fast-mode tolerance against the oracle, reproducible)."""
+    monkeypatch.setenv("CGX_VI_BPW", bpw)
+    rp, col, val = cgx.laplacian3d(60, 50, 40)
+    b = np.random.default_rng(13).standard_normal(len(rp) - 1)
+    out = {}
+    for vals in ("1", "0", "1"):
+        monkeypatch.setenv("CGX_DC_VALS", vals)
+        with cgx.Solver(0) as s:
+            s.set_matrix(rp, col, val)
+            assert s.info()["dict_vals"] == int(vals)
+            s.set_rhs(b)
+            s.run(30)
+            out.setdefault(vals, []).append((s.x(), s.history(31)))
+    x_ref, _ = H.o_conj_grad(30, rp, col, val, b)
+    assert rel(out["1"][0][0], x_ref) <= FAST_RTOL
+    assert H.same_bits_or_both_nan(out["1"][0][0], out["1"][1][0])
+    if bpw == "1":
+        assert H.same_bits_or_both_nan(out["1"][0][0], out["0"][0][0])
+        assert H.same_bits_or_both_nan(out["1"][0][1], out["0"][0][1])
 
 
 @pytest.mark.parametrize("wpb", ["8"])
