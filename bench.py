@@ -85,6 +85,20 @@ def load_traffic(workload, alg):
         return None
 
 
+def spmv_layout_label(info, stream_bytes):
+    """Kernel label for the layout a solver picked (coded columns, pairs)."""
+    nd = info.get("n_dict", 0)
+    label = spmv_kernel_label(stream_bytes)
+    if nd and info.get("dict_vals", 0):
+        return (f"k_spmv_vi (LDS-DMA code stream, value-indexed (offset, value) pairs: "
+                f"{nd} pairs, 1 B/nnz, no value stream; one 64-row block per wave)")
+    if nd:
+        return label.replace("k_spmv_dma (LDS-DMA CSR-stream",
+                             f"k_spmv_dc (LDS-DMA CSR-stream, dictionary-coded columns: "
+                             f"{nd} offsets, 1 B/nnz")
+    return label
+
+
 def spmv_kernel_label(stream_bytes):
     """The SpMV kernel the solver selects (cgx_solver.cpp defaults, CGX_* knobs;
     nt by default only above kNtStreamBytes = 160 MiB of val+col)."""
@@ -251,7 +265,8 @@ def main():
             alg = min(trial, key=trial.get)
         s.set_alg(cgx.CGX_ALG_HS if alg == "hs-dist" else cgx.CGX_ALG_CG1)
         info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"],
-                    spmv_iter_bytes=dinfo["spmv_iter_bytes"], n_dict=dinfo["n_dict"])
+                    spmv_iter_bytes=dinfo["spmv_iter_bytes"], n_dict=dinfo["n_dict"],
+                    dict_vals=dinfo["dict_vals"])
     else:
         s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
@@ -288,12 +303,7 @@ def main():
     # CSR-equivalent rate (SURVEY.md 8d's B_spmv over the same time) beside it
     achieved = info["spmv_iter_bytes"] / (spmv_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload, alg)
-    nd = info.get("n_dict", 0)
-    label = spmv_kernel_label(len(sysm["col"]) * (4 + sysm["val"].itemsize))
-    if nd:
-        label = label.replace("k_spmv_dma (LDS-DMA CSR-stream",
-                              f"k_spmv_dc (LDS-DMA CSR-stream, dictionary-coded columns: "
-                              f"{nd} offsets, 1 B/nnz")
+    label = spmv_layout_label(info, len(sysm["col"]) * (4 + sysm["val"].itemsize))
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                     traffic=traffic, kernel=label,
@@ -315,10 +325,10 @@ def main():
     # operator as a stencil (bit-identical SpMV), only x and y move
     # the same solve with plain 4-byte CSR columns (CGX_LAYOUT=csr): the
     # layout SURVEY.md 8d's B_spmv prices, measured beside the coded one
-    csr_plain = None
-    if world == 1 and not use_dist and info.get("n_dict", 0) > 0:
-        old_layout = os.environ.get("CGX_LAYOUT")
-        os.environ["CGX_LAYOUT"] = "csr"
+    def alt_layout(env, note):
+        """The same solve with other layout knobs (env), measured like the main line."""
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         try:
             with cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS) as cs:
                 cs.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
@@ -328,17 +338,31 @@ def main():
                 _, c_spmv = cs.bench_run(args.steps, graph=False, spmv_events=True)
                 cinfo = cs.info()
         finally:
-            if old_layout is None:
-                os.environ.pop("CGX_LAYOUT", None)
-            else:
-                os.environ["CGX_LAYOUT"] = old_layout
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         c_gbs = cinfo["spmv_iter_bytes"] / (c_spmv * 1e-3) / 1e9
-        csr_plain = dict(value=round(args.steps / (c_ms * 1e-3), 2), unit="it/s",
-                         spmv_us=round(c_spmv * 1e3, 2), spmv_gbs=round(c_gbs, 1),
-                         frac=round(c_gbs / HBM_PEAK_GBS, 4),
-                         kernel=spmv_kernel_label(len(sysm["col"]) * (4 + sysm["val"].itemsize)),
-                         note="same system, plain int32 CSR columns (CGX_LAYOUT=csr): "
-                              "B_spmv of SURVEY.md 8d")
+        return dict(value=round(args.steps / (c_ms * 1e-3), 2), unit="it/s",
+                    spmv_us=round(c_spmv * 1e3, 2), spmv_gbs=round(c_gbs, 1),
+                    frac=round(c_gbs / HBM_PEAK_GBS, 4),
+                    algorithmic_bytes_per_launch=int(cinfo["spmv_iter_bytes"]),
+                    kernel=spmv_layout_label(cinfo, len(sysm["col"]) * (4 + sysm["val"].itemsize)),
+                    note=note)
+
+    # the same solve with plain 4-byte CSR columns (CGX_LAYOUT=csr): the
+    # layout SURVEY.md 8d's B_spmv prices, measured beside the coded one; and
+    # with offset codes but the value stream kept (CGX_DC_VALS=0)
+    csr_plain = coded_offsets = None
+    if world == 1 and not use_dist and info.get("n_dict", 0) > 0:
+        csr_plain = alt_layout({"CGX_LAYOUT": "csr"},
+                               "same system, plain int32 CSR columns (CGX_LAYOUT=csr): "
+                               "B_spmv of SURVEY.md 8d")
+        if info.get("dict_vals", 0):
+            coded_offsets = alt_layout({"CGX_DC_VALS": "0"},
+                                       "same system, offset codes + the fp64 value stream "
+                                       "(CGX_DC_VALS=0)")
 
     mf = None
     if world == 1 and wl["kind"] in ("lap3d", "lap2d"):
@@ -376,7 +400,10 @@ def main():
                     alg=alg, alg_trial_ms_per_iter=trial if use_dist else None,
                     graph=not use_dist or world == 1,
                     parallelism=f"row-partition x{world}",
-                    layout=(f"CSR with dictionary-coded columns ({info['n_dict']} col-row "
+                    layout=(f"CSR-VI: value-indexed coded columns ({info['n_dict']} "
+                            f"(col-row, value) pairs, 1 B/nnz, no value stream) + byte row lengths"
+                            if info.get("dict_vals", 0) else
+                            f"CSR with dictionary-coded columns ({info['n_dict']} col-row "
                             f"offsets, 1 B/nnz) + byte row lengths"
                             if info.get("n_dict", 0) else "CSR (int32 columns)"),
                     halo_bytes_per_iter=(dinfo or {}).get("halo_bytes")),
@@ -385,7 +412,11 @@ def main():
         upload_ms=round(upload_ms, 1),
         iter_bytes=int(info["iter_bytes"]),
         iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),
-        roofline=roofline, cpu_baseline=cpu, csr_plain=csr_plain,
+        # the iteration's bytes in the layout it runs on (SpMV as above + the
+        # vector kernels' 8d bytes) over the measured step
+        iter_layout_gbs=round((info["iter_bytes"] - info["spmv_bytes"] + info["spmv_iter_bytes"])
+                              / (ms_per_step * 1e-3) / 1e9, 1),
+        roofline=roofline, cpu_baseline=cpu, csr_plain=csr_plain, coded_offsets=coded_offsets,
         matrix_free_upper_bound=mf,
     )
     if rank == 0:

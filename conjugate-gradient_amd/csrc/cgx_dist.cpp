@@ -81,6 +81,8 @@ struct cgx_dist {
   unsigned char *d_rlen = nullptr;  // byte row lengths (rows <= 255 entries)
   int ndict = 0;
   int code_bits = 8;                 // 4: nibble codes (<= 16 offsets)
+  void *d_dval = nullptr;            // value-indexed pairs (CGX_DC_VALS): pair values
+  bool vi = false;
   int n_int = 0, n_bnd = 0, g_int = 0, g_bnd = 0;
   // interior / boundary row blocks as contiguous runs {first, count} when
   // there are few of them (slab partitions: 1 interior + 2 boundary runs);
@@ -168,8 +170,9 @@ void free_system(cgx_dist *d) {
   dfree(&d->d_b); dfree(&d->d_x); dfree(&d->d_r); dfree(&d->d_p);
   dfree(&d->d_s); dfree(&d->d_w); dfree(&d->d_send_idx); dfree(&d->d_sendbuf);
   dfree(&d->d_pa); dfree(&d->d_pb); dfree(&d->d_hist);
-  dfree(&d->d_code); dfree(&d->d_dict); dfree(&d->d_rlen);
+  dfree(&d->d_code); dfree(&d->d_dict); dfree(&d->d_rlen); dfree(&d->d_dval);
   d->ndict = 0;
+  d->vi = false;
   d->hist_alloc = 0;
   if (d->part) cgx_part_destroy(d->part);
   d->part = nullptr;
@@ -335,13 +338,38 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
   if (n_loc > 0 && nnz > 0 && dc_wanted(d)) {
     std::vector<unsigned char> code((size_t)nnz);
     std::vector<int> dict;
-    const int nd = build_col_codes(n_loc, rp, col_local.data(), dict, code.data());
+    int nd = build_col_codes(n_loc, rp, col_local.data(), dict, code.data());
+    std::vector<unsigned char> rl;
+    if (nd > 0 && env_int("CGX_DC_RLEN", 1)) {
+      rl.resize((size_t)n_loc);
+      if (!build_row_lengths(n_loc, rp, rl.data())) rl.clear();
+    }
+    // value-indexed pairs (k_spmv_vi) as the solver: byte row lengths, <= 64
+    // (offset, value) pairs, every block's code window inside the kernel's
+    std::vector<double> dv;
+    if (nd > 0 && !rl.empty() && env_int("CGX_DC_VALS", 1) != 0) {
+      const int cb = nd <= 16 && env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8, ka = 128 / cb;
+      const long long capc = ((512LL + ka) * cb / 8 + 15) & ~15LL;
+      bool fits = true;
+      for (size_t b = 0; b + 1 < blkk.size() && fits; ++b)
+        fits = ((long long)(blkk[b + 1] - (blkk[b] & ~(ka - 1))) * cb + 7) / 8 <= capc;
+      if (fits) {
+        const int np = build_val_pairs<double>(nnz, val, code.data(), dict, dv, 64);
+        if (np > 0) nd = np;
+      }
+    }
     if (nd > 0) {
-      if ((rc = dalloc(d, &d->d_code, nnz_pad)) || (rc = dalloc(d, &d->d_dict, 256 * 4))) {
+      if ((rc = dalloc(d, &d->d_code, nnz_pad)) || (rc = dalloc(d, &d->d_dict, 256 * 4)) ||
+          (!dv.empty() && (rc = dalloc(d, &d->d_dval, 256 * 8)))) {
         free_system(d);
         return rc;
       }
       dict.resize(256, 0);
+      if (!dv.empty()) {
+        dv.resize(256, 0.0);
+        CGX_HIP(hipMemcpyAsync(d->d_dval, dv.data(), 256 * 8, hipMemcpyHostToDevice, st));
+        d->vi = true;
+      }
       d->code_bits = nd <= 16 && env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;
       size_t code_bytes = (size_t)nnz;
       if (d->code_bits == 4) {
@@ -351,8 +379,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
       CGX_HIP(hipMemsetAsync(d->d_code, 0, nnz_pad, st));
       CGX_HIP(hipMemcpyAsync(d->d_code, code.data(), code_bytes, hipMemcpyHostToDevice, st));
       CGX_HIP(hipMemcpyAsync(d->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice, st));
-      std::vector<unsigned char> rl((size_t)n_loc);
-      if (env_int("CGX_DC_RLEN", 1) && build_row_lengths(n_loc, rp, rl.data())) {
+      if (!rl.empty()) {
         if ((rc = dalloc(d, &d->d_rlen, (size_t)n_loc + 64))) {
           free_system(d);
           return rc;
@@ -536,6 +563,8 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
     a.ndict_cap = dict_cap(d->ndict);
     a.rlen = d->d_rlen;
     a.code_bits = d->code_bits;
+    a.dval = d->vi ? (const double *)d->d_dval : nullptr;
+    a.bpw = 1;
   }
   return a;
 }
@@ -1145,7 +1174,11 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
                                           (d->d_rlen ? 1.0 * d->n_loc : 4.0 * (d->n_loc + 1)) +
                                           16.0 * d->n_loc + 4.0 * d->ndict
                                     : s->spmv_bytes;
+  if (d->ndict > 0 && d->vi)  // value-indexed pairs: no val stream
+    s->spmv_iter_bytes = (double)d->nnz * (d->code_bits / 8.0) + 1.0 * d->n_loc +
+                         16.0 * d->n_loc + 12.0 * d->ndict;
   s->n_dict = d->ndict;
+  s->dict_vals = d->ndict > 0 && d->vi;
   return 0;
 }
 

@@ -60,6 +60,11 @@ inline int spmv_cap(int bs, bool f64) { return bs * (f64 ? 8 : 16); }
 // Resident workgroups per CU of the engine SpMV's ring shapes (k_spmv_eng).
 inline int eng_wg_per_cu(int shape) { return shape == 1 ? 4 : shape >= 2 ? 2 : 3; }
 // Workgroups of one SpMV launch (= fused-dot partials it writes).
+// k_spmv_vi's grid (and epilogue partial count)
+inline int vi_grid(int nblk, int code_bits, int bpw) {
+  if (code_bits != 8) bpw = 1;
+  return (nblk + 4 * bpw - 1) / (4 * bpw);
+}
 inline int spmv_launch_grid(int bs, int wpb, int rbw, int nblk, int grid,
                             int dma = 0) {
   if (bs == 64 && dma == 2) return (nblk + 2 * rbw - 1) / (2 * rbw);

@@ -1379,9 +1379,9 @@ void launch_dc_w(const SpmvArgs<T> &a, hipStream_t st) {
 // column order from 0 (mv_ops.c:190-194), as in every other SpMV kernel.
 // The host guarantees every row block's code window fits CAPC bytes
 // (rows <= 255 entries, blocks <= CAPW entries).
-template <typename T, int CAPW, bool EPI, bool NT, int CB, bool LIST, int BPW>
-__global__ __launch_bounds__(4 * kWave) void k_spmv_vi(SpmvArgs<T> a) {
-  constexpr int WPB = 4, ND = 64, U = 8;
+template <typename T, int CAPW, bool EPI, bool NT, int CB, bool LIST, int BPW, int WPB = 4>
+__global__ __launch_bounds__(WPB * kWave) void k_spmv_vi(SpmvArgs<T> a) {
+  constexpr int ND = 64, U = 8;
   constexpr int AUX = NT ? 2 : 0;
   constexpr int KA = 16 * 8 / CB;  // entries per 16-B code granule
   constexpr int CAPC = ((CAPW + KA) * CB / 8 + 15) & ~15;
@@ -1485,13 +1485,13 @@ __global__ __launch_bounds__(4 * kWave) void k_spmv_vi(SpmvArgs<T> a) {
   }
 }
 
-template <typename T, int CAPW, int CB, int BPW>
+template <typename T, int CAPW, int CB, int BPW, int WPB = 4>
 void launch_vi_b(const SpmvArgs<T> &a, hipStream_t st) {
-  const int g = (a.nblk + 4 * BPW - 1) / (4 * BPW);
-  const dim3 blk(4 * kWave);
+  const int g = (a.nblk + WPB * BPW - 1) / (WPB * BPW);
+  const dim3 blk(WPB * kWave);
   const bool epi = a.part != nullptr, list = a.blk_list != nullptr;
 #define CGX_VI(E, N, L) \
-  hipLaunchKernelGGL((k_spmv_vi<T, CAPW, E, N, CB, L, BPW>), dim3(g), blk, 0, st, a)
+  hipLaunchKernelGGL((k_spmv_vi<T, CAPW, E, N, CB, L, BPW, WPB>), dim3(g), blk, 0, st, a)
   if (list) {
     if (epi && a.nt) CGX_VI(true, true, true);
     else if (epi) CGX_VI(true, false, true);

@@ -836,8 +836,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col,
         s->ndict = 0;
       }
       if (s->ndict > 0 && s->vi) {  // k_spmv_vi: bpw row blocks per wave
-        const int bpw = s->code_bits == 8 ? s->vi_bpw : 1;
-        s->spmv_grid = (s->nblk + 4 * bpw - 1) / (4 * bpw);
+        s->spmv_grid = vi_grid(s->nblk, s->code_bits, s->vi_bpw);
       }
       if (s->ndict > 0 && s->spmv_wpb == 4 && s->want_tile) {
         // L2 tiling of the block order.  The x lines a row needs sit at its

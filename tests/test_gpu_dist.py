@@ -147,11 +147,13 @@ def test_history_after_buffer_growth():
 def test_coded_columns_partitions_identical_to_csr(P, monkeypatch):
     """Partitions of a Laplacian keep <= 256 distinct local column offsets
     (owned rows: the stencil's; ghost columns: constant offsets per face), so
-    each part runs the coded-column SpMV; x and the history are bit-identical
-    to the plain-CSR layout."""
+    each part runs the coded-column SpMV -- value-indexed pairs by default
+    (one value per offset: <= 21 pairs), offset codes with CGX_DC_VALS=0; x
+    and the history are bit-identical to the plain-CSR layout in both."""
     rp, col, val, b = system("lap3d")
     out = {}
-    for layout in ("csr", "auto"):
+    for layout in ("csr", "auto", "dc"):
+        monkeypatch.setenv("CGX_DC_VALS", "0" if layout == "dc" else "1")
         if layout == "csr":
             monkeypatch.setenv("CGX_LAYOUT", "csr")
         else:
@@ -162,9 +164,11 @@ def test_coded_columns_partitions_identical_to_csr(P, monkeypatch):
         else:
             assert all(0 < s["n_dict"] <= 21 for s in stats)  # <= 7 stencil + 7 per ghost face
             assert all(s["spmv_iter_bytes"] < s["spmv_bytes"] for s in stats)
+            assert all(s["dict_vals"] == (layout == "auto") for s in stats)
         out[layout] = (x, hist)
-    assert H.same_bits_or_both_nan(out["csr"][0], out["auto"][0])
-    assert H.same_bits_or_both_nan(out["csr"][1], out["auto"][1])
+    for layout in ("auto", "dc"):
+        assert H.same_bits_or_both_nan(out["csr"][0], out[layout][0])
+        assert H.same_bits_or_both_nan(out["csr"][1], out[layout][1])
 
 
 @pytest.mark.parametrize("kind", ["lap3d", "lap2d", "rand"])

@@ -928,6 +928,12 @@ def test_value_indexed_cg(bpw, monkeypatch):
     x_ref, _ = H.o_conj_grad(30, rp, col, val, b)
     assert rel(out["1"][0][0], x_ref) <= FAST_RTOL
     assert H.same_bits_or_both_nan(out["1"][0][0], out["1"][1][0])
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        want = -(-s.info()["n_rowblocks"] // (int(bpw) * 4))
+        assert s.info()["spmv_grid"] == want
+        y = s.spmv(b)
+        assert H.same_bits_or_both_nan(y, H.o_spmv(rp, col, val, b))
     if bpw == "1":
         assert H.same_bits_or_both_nan(out["1"][0][0], out["0"][0][0])
         assert H.same_bits_or_both_nan(out["1"][0][1], out["0"][0][1])

@@ -73,7 +73,8 @@ for s in stats:
     # the solver's default SpMV: the coded-column kernel when present (the bench
     # also runs the plain-CSR kernel for its csr_plain line), else the SpMV
     # kernel with the most launches
-    prefer = "k_spmv_dc" if any("k_spmv_dc" in t["Name"] for t in stats) else "k_spmv"
+    prefer = next((k for k in ("k_spmv_vi", "k_spmv_dc") if any(k in t["Name"] for t in stats)),
+                  "k_spmv")
     if prefer in name and (spmv is None or int(s["Calls"]) > spmv["calls"]):
         spmv = dict(kernel=short(name), calls=int(s["Calls"]), avg_us=avg_ns / 1e3,
                     ea_read_bytes=ea_rd, ea_write_bytes=ea_wr,
