@@ -8,5 +8,5 @@ tail -1 gpurun_out/vi_tests.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py -x -q --timeout 300 --timeout-method thread > gpurun_out/vi_dist.log 2>&1 || { tail -40 gpurun_out/vi_dist.log; exit 1; }
 tail -1 gpurun_out/vi_dist.log
 timeout -k 10 900 python tools/sweep.py --workload c3 --rounds 6 --iters 30 --instances 2 --control \
-  --variant vi4w: --variant vi8w:CGX_VI_WPB=8 --variant vi16w:CGX_VI_WPB=16 > gpurun_out/vi.log 2>&1 || exit 1
+  --variant vw1: --variant vw2:CGX_VI_BPW=2 --variant vs:CGX_VI_WIN=0 > gpurun_out/vi.log 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/vi.log | tail -6
