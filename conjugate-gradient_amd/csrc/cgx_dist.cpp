@@ -554,7 +554,7 @@ SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
   a.tg = d->spmv_tg;
   a.dma = d->spmv_dma;  // 1 or 0: the grids assume one block per wave, 4 waves per WG
   a.nt = d->spmv_nt;
-  if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes;
+  if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes ? 2 : 0;
   a.xcd = a.dma ? d->spmv_xcd : 0;  // XCD-contiguous blocks, as the solver
   a.tk = TicketArgs{};
   if (a.dma == 1 && d->ndict > 0) {

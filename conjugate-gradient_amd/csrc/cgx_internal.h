@@ -126,7 +126,7 @@ struct SpmvArgs {
   double *part;        // per-workgroup partial of x[row]*y[row] (nullptr: none)
   const int *done;     // early-exit flag (nullptr: never)
   int xcd;             // XCD-aware chunk mapping (speed only)
-  int nt;              // non-temporal val/col stream loads
+  int nt;              // non-temporal val/col stream loads (2: + CSR-VI y store)
   int bs;              // rows per row block: 256 | 512 (workgroup-wide block),
                        // 64 (one row block per wave, k_spmv_wave)
   int wpb;             // k_spmv_wave: waves per workgroup (4 | 8)

@@ -1468,7 +1468,10 @@ __global__ __launch_bounds__(WPB * kWave) void k_spmv_vi(SpmvArgs<T> a) {
 #pragma unroll
     for (int b = 0; b < BPW; ++b)
       if (lane < nr[b]) {
-        a.y[r0[b] + lane] = acc[b];
+        if (NT && a.nt == 2)  // y streamed past the caches too (nt=2)
+          __builtin_nontemporal_store(acc[b], a.y + r0[b] + lane);
+        else
+          a.y[r0[b] + lane] = acc[b];
         if (EPI) dot = dot + (double)xrow[b] * (double)acc[b];
       }
   }

@@ -959,8 +959,10 @@ SpmvArgs<T> spmv_args(cgx_solver *s, const void *x, void *y, double *part,
   a.part = part;
   a.done = with_done ? &s->d_st->done : nullptr;
   a.xcd = s->spmv_xcd;
+  // by size: 2 = code stream AND the CSR-VI y store past the caches (C3 SpMV
+  // 95.0 -> 92.5 us, iteration 195.2 -> 192.4 us; tools/gpu_vi_nt.sh)
   a.nt = s->spmv_nt < 0
-             ? (double)s->nnz * (double)(sizeof(T) + 4) > cgx::kNtStreamBytes
+             ? ((double)s->nnz * (double)(sizeof(T) + 4) > cgx::kNtStreamBytes ? 2 : 0)
              : s->spmv_nt;
   a.bs = s->spmv_bs;
   a.wpb = s->spmv_wpb;
