@@ -21,7 +21,12 @@ CGX_EINVAL, CGX_ENODEV, CGX_ENOMEM, CGX_ECOMM = -1, -2, -3, -4
 CGX_MODE_FAST, CGX_MODE_EXACT = 0, 1
 CGX_ALG_HS, CGX_ALG_CG1 = 0, 1
 CGX_F64, CGX_F32 = 0, 1
-CGX_BENCH_GRAPH, CGX_BENCH_SPMV_EVENTS = 1, 2
+CGX_BENCH_GRAPH, CGX_BENCH_SPMV_EVENTS, CGX_BENCH_SPMV_ONLY = 1, 2, 4
+(CGX_LAYOUT_AUTO, CGX_LAYOUT_CSR, CGX_LAYOUT_DC, CGX_LAYOUT_VI, CGX_LAYOUT_PANEL,
+ CGX_LAYOUT_STENCIL) = range(6)
+LAYOUT_NAMES = {CGX_LAYOUT_AUTO: "auto", CGX_LAYOUT_CSR: "csr", CGX_LAYOUT_DC: "dc",
+                CGX_LAYOUT_VI: "vi", CGX_LAYOUT_PANEL: "panel", CGX_LAYOUT_STENCIL: "stencil"}
+LAYOUTS = {v: k for k, v in LAYOUT_NAMES.items()}
 
 _i32p = ctypes.POINTER(ctypes.c_int)
 _f64p = ctypes.POINTER(ctypes.c_double)
@@ -41,23 +46,25 @@ class MvSparse(ctypes.Structure):
 
 class CgxInfo(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("nnz", ctypes.c_int), ("dtype", ctypes.c_int),
-                ("mode", ctypes.c_int), ("alg", ctypes.c_int),
-                ("n_rowblocks", ctypes.c_int), ("spmv_grid", ctypes.c_int),
+                ("mode", ctypes.c_int), ("alg", ctypes.c_int), ("layout", ctypes.c_int),
+                ("n_items", ctypes.c_int), ("spmv_grid", ctypes.c_int),
                 ("vec_grid", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
                 ("iter_bytes", ctypes.c_double), ("spmv_iter_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("n_panels", ctypes.c_int),
-                ("n_dict", ctypes.c_int), ("tile_bands", ctypes.c_int),
-                ("dict_vals", ctypes.c_int)]
+                ("n_dict", ctypes.c_int), ("tile_bands", ctypes.c_int), ("nt", ctypes.c_int),
+                ("row_width", ctypes.c_int), ("encode_fallback", ctypes.c_int),
+                ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double)]
 
 
 class CgxDistStats(ctypes.Structure):
     _fields_ = [("n_global", ctypes.c_longlong), ("row_begin", ctypes.c_int),
                 ("n_loc", ctypes.c_int), ("n_ghost", ctypes.c_int), ("n_send", ctypes.c_int),
-                ("nnz", ctypes.c_int), ("interior_blocks", ctypes.c_int),
-                ("boundary_blocks", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
+                ("nnz", ctypes.c_int), ("interior_items", ctypes.c_int),
+                ("boundary_items", ctypes.c_int), ("spmv_bytes", ctypes.c_double),
                 ("iter_bytes", ctypes.c_double), ("halo_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("spmv_iter_bytes", ctypes.c_double),
-                ("n_dict", ctypes.c_int), ("dict_vals", ctypes.c_int)]
+                ("layout", ctypes.c_int), ("n_dict", ctypes.c_int), ("graph", ctypes.c_int),
+                ("alg", ctypes.c_int)]
 
 
 _MVP = ctypes.POINTER(MvSparse)
@@ -81,6 +88,7 @@ _SIGS = {
     "conj_grad": (ctypes.c_int, [ctypes.c_int, _MVP, _MVP, _MVPP]),
     "solve": (ctypes.c_int, [_MVP, _MVP, _MVPP, ctypes.c_double, ctypes.c_int]),
     "cgx_free_mv_deep": (None, [_MVP]),
+    "cgx_ops_counters": (ctypes.c_int, [ctypes.POINTER(ctypes.c_longlong)] * 2),
     "cgx_last_error": (ctypes.c_char_p, []),
     "cgx_device_count": (ctypes.c_int, []),
     "cgx_stream_bench": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
@@ -88,6 +96,7 @@ _SIGS = {
     "cgx_solver_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "cgx_solver_destroy": (None, [_vp]),
     "cgx_solver_set_mode": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    "cgx_solver_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_matrix": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                              _i32p, _i32p, _f64p]),
     "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
@@ -152,6 +161,8 @@ _SIGS = {
                                            _i32p, _i32p, _f64p]),
     "cgx_dist_set_rhs": (ctypes.c_int, [_vp, _f64p]),
     "cgx_dist_set_alg": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_set_graph": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
                                     ctypes.POINTER(ctypes.c_int)]),
     "cgx_dist_get_x": (ctypes.c_int, [_vp, _f64p]),
@@ -269,10 +280,11 @@ def is_chained(rp, col):
 class Solver:
     """Device-resident CG solver (cgx_solver_*)."""
 
-    def __init__(self, device=0, mode=CGX_MODE_FAST, alg=CGX_ALG_HS):
+    def __init__(self, device=0, mode=CGX_MODE_FAST, alg=CGX_ALG_HS, layout=CGX_LAYOUT_AUTO):
         self._h = _vp()
         check(lib().cgx_solver_create(device, ctypes.byref(self._h)), "cgx_solver_create")
         self.set_mode(mode, alg)
+        self.set_layout(layout)
         self.n = 0
         self.f32 = False
 
@@ -295,6 +307,12 @@ class Solver:
 
     def set_mode(self, mode, alg=CGX_ALG_HS):
         check(lib().cgx_solver_set_mode(self._h, mode, alg), "set_mode")
+
+    def set_layout(self, layout):
+        """CGX_LAYOUT_* (or its name) for the next set_matrix / gen_laplacian."""
+        if isinstance(layout, str):
+            layout = LAYOUTS[layout]
+        check(lib().cgx_solver_set_layout(self._h, layout), "set_layout")
 
     def gen_laplacian(self, dim, nx, ny, nz=1):
         """Laplacian CSR generated in device memory (cgx_solver_gen_laplacian)."""
@@ -378,16 +396,20 @@ class Solver:
     def info(self):
         i = CgxInfo()
         check(lib().cgx_solver_info(self._h, ctypes.byref(i)), "info")
-        return {k: getattr(i, k) for k, _ in CgxInfo._fields_}
+        d = {k: getattr(i, k) for k, _ in CgxInfo._fields_}
+        d["layout_name"] = LAYOUT_NAMES.get(d["layout"], "?")
+        return d
 
     def bench_prepare(self, warmup):
         check(lib().cgx_solver_bench_prepare(self._h, warmup), "bench_prepare")
 
-    def bench_run(self, iters, graph=True, spmv_events=False):
-        """Returns (device ms for all iters, average SpMV ms or -1)."""
+    def bench_run(self, iters, graph=True, spmv_events=False, spmv_only=False):
+        """Returns (device ms for all iters, average SpMV ms or -1).
+        spmv_only: back-to-back SpMVs y = A p instead of CG iterations."""
         tot = ctypes.c_double(0)
         sp = ctypes.c_double(0)
-        flags = (CGX_BENCH_GRAPH if graph else 0) | (CGX_BENCH_SPMV_EVENTS if spmv_events else 0)
+        flags = ((CGX_BENCH_GRAPH if graph else 0) | (CGX_BENCH_SPMV_EVENTS if spmv_events else 0)
+                 | (CGX_BENCH_SPMV_ONLY if spmv_only else 0))
         check(lib().cgx_solver_bench_run(self._h, iters, flags, ctypes.byref(tot),
                                          ctypes.byref(sp)), "bench_run")
         return tot.value, sp.value
@@ -447,6 +469,22 @@ def solve(A: Mv, b: Mv, tol, maxit):
     x = mv_values(out)
     lib().cgx_free_mv_deep(out)
     return x, its
+
+
+def mv_mult(A: Mv, b: Mv):
+    """mv_ops.h mv_mult through the C ABI (the op-level drop-in)."""
+    out = _MVP()
+    check(lib().mv_mult(A.ptr, b.ptr, ctypes.byref(out)), "mv_mult")
+    y = mv_values(out)
+    lib().cgx_free_mv_deep(out)
+    return y
+
+
+def ops_counters():
+    """(uploads, reuses) of the op-level matrix residency (cgx_ops_counters)."""
+    u, r = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    check(lib().cgx_ops_counters(ctypes.byref(u), ctypes.byref(r)), "ops_counters")
+    return u.value, r.value
 
 
 # ------------------------------------------------------------ partitioning
@@ -568,8 +606,16 @@ class DistSolver:
         check(lib().cgx_dist_set_rhs(self._h, _p(b, _f64p)), "dist_set_rhs")
 
     def set_alg(self, alg):
-        """CGX_ALG_CG1 (one all-reduce per iteration) or CGX_ALG_HS (two)."""
+        """CGX_ALG_HS (default, two all-reduces) or CGX_ALG_CG1 (one)."""
         check(lib().cgx_dist_set_alg(self._h, alg), "dist_set_alg")
+
+    def set_layout(self, layout):
+        if isinstance(layout, str):
+            layout = LAYOUTS[layout]
+        check(lib().cgx_dist_set_layout(self._h, layout), "dist_set_layout")
+
+    def set_graph(self, on):
+        check(lib().cgx_dist_set_graph(self._h, 1 if on else 0), "dist_set_graph")
 
     def run(self, maxit, tol=0.0):
         it = ctypes.c_int(0)
@@ -589,15 +635,18 @@ class DistSolver:
     def bench_prepare(self, warmup):
         check(lib().cgx_dist_bench_prepare(self._h, warmup), "dist_bench_prepare")
 
-    def bench_run(self, iters, spmv_events=False):
-        """Returns (device ms for all iters, average SpMV ms or -1)."""
+    def bench_run(self, iters, spmv_events=False, graph=True):
+        """Returns (device ms for all iters, average SpMV ms or -1).
+        SpMV events run the iterations eagerly."""
         ms, sp = ctypes.c_double(0), ctypes.c_double(0)
-        check(lib().cgx_dist_bench_run(self._h, iters,
-                                       CGX_BENCH_SPMV_EVENTS if spmv_events else 0,
+        flags = (CGX_BENCH_SPMV_EVENTS if spmv_events else 0) | (CGX_BENCH_GRAPH if graph else 0)
+        check(lib().cgx_dist_bench_run(self._h, iters, flags,
                                        ctypes.byref(ms), ctypes.byref(sp)), "dist_bench_run")
         return ms.value, sp.value
 
     def info(self):
         st = CgxDistStats()
         check(lib().cgx_dist_info(self._h, ctypes.byref(st)), "dist_info")
-        return {k: getattr(st, k) for k, _ in CgxDistStats._fields_}
+        d = {k: getattr(st, k) for k, _ in CgxDistStats._fields_}
+        d["layout_name"] = LAYOUT_NAMES.get(d["layout"], "?")
+        return d

@@ -1,32 +1,38 @@
-// cgx_dist.cpp -- the multi-GPU CG solver: one rank per GPU, rows
-// partitioned into contiguous blocks (cgx_partition.cpp), halo x segments
-// exchanged point to point, and the iteration's two dot products fused into
-// ONE all-reduce (north star in BASELINE.json).
+// cgx_dist.cpp -- the multi-GPU CG solver: one rank per GPU, rows partitioned
+// into contiguous blocks (cgx_partition.cpp), halo x segments exchanged point
+// to point, the iteration's dot products all-reduced over RCCL (SURVEY.md
+// 8e; north star in BASELINE.json).  Each rank's rows live in a DevMatrix
+// (cgx_matrix.h) with local column numbering: owned rows -> [0, n_loc),
+// ghosts -> n_loc + position, so the halo exchange writes the gathered
+// vector's ghost tail directly and every layout (CSR, CSR-DC, CSR-VI) works
+// unchanged -- a slab's ghost columns are one more constant offset per face.
 //
-// Recurrence: Chronopoulos-Gear CG (one reduction per iteration; the
-// reference's Hestenes-Stiefel form, cg.c:113 and cg.c:129, needs two
-// dependent reductions).  Per iteration, on the rank's compute stream A and
-// communication stream B:
+// Recurrences (cgx_dist_set_alg):
+//   HS  (default; the reference's cg.c:88-141): per iteration
+//       st_comm: halo of p (ncclSend/Recv with each neighbour, into p's
+//                ghost tail), created at the device's highest priority so its
+//                kernel is dispatched ahead of the interior SpMV's workgroups
+//       st:      SpMV s = A p over INTERIOR work items (no ghost columns)
+//                || halo; wait; SpMV over BOUNDARY items -- its last
+//                workgroup also sums every p.s partial (local p.s)
+//                ncclAllReduce(p.s)
+//                k_update_rf (alpha, r -= alpha s; its last workgroup sums
+//                the r.r partials) -> ncclAllReduce(r.r)
+//                k_xpay_xf (beta, stop test, x += alpha p, p = r + beta p)
+//                pack p[send rows] for the next halo
+//   CG1 (Chronopoulos-Gear): ONE all-reduce of (gamma, delta) per iteration,
+//       rounding-level different from HS, 8 B per row more vector traffic.
+// Every rank derives alpha, beta and the stop test from the same all-reduced
+// sums, so they agree bit for bit.  With RCCL, batches of iterations --
+// halo, all-reduces and kernels -- are captured once as a hipGraph and
+// replayed (eager fallback if the capture fails).
 //
-//   A: k_cg1_update   p = r + beta p, s = w + beta s, x += alpha p,
-//                     r -= alpha s, gamma partials              -> ev_packed
-//   A: k_gather       pack r[send rows] into the send buffer
-//   B: halo           ncclSend/ncclRecv with each neighbour (RCCL over xGMI)
-//                     straight into r's ghost tail               -> ev_halo
-//   A: k_spmv_wave    w = A r over INTERIOR row blocks (no ghost columns),
-//                     overlapping the halo on B; delta = w.r partials
-//   A: wait ev_halo;  k_spmv_wave over BOUNDARY row blocks
-//   A: k_finalize     local (gamma, delta)
-//   A: ncclAllReduce  2 doubles, sum
-//   A: k_finalize     alpha, beta, stop test on the global sums
-//
-// Transports: RCCL (one process per GPU, ncclCommInitRank from an id the
+// Transports: RCCL (one process per GPU; ncclCommInitRank from an id the
 // caller distributes), or "local": P partitions driven by one host thread on
-// one device (device-to-device copies for the halo, a fixed-order sum kernel
-// for the all-reduce) -- the same phase code, used to validate the
-// partitioned path on a single GPU.  The host driver runs the iteration as
-// phases over all partitions it owns (one in RCCL mode), so every wait is on
-// an event that has already been recorded.
+// one device (device copies for the halo, a fixed-order sum kernel for the
+// all-reduce) -- the same phase code, used to validate the partitioned path
+// on a single GPU.  The host driver runs each phase over all partitions it
+// owns (one in RCCL mode), so every wait is on an already recorded event.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -37,15 +43,21 @@
 #include <vector>
 
 #include "cgx_internal.h"
+#include "cgx_matrix.h"
 
 using cgx::CgState;
+using cgx::DevMatrix;
 
 struct cgx_dist;
+
+namespace cgx {
+int public_layout(const DevMatrix &m);
+}
 
 namespace {
 
 struct Group {
-  std::vector<cgx_dist *> parts;  // RCCL mode: just this rank
+  std::vector<cgx_dist *> parts;    // RCCL mode: just this rank
   const double **d_srcs = nullptr;  // local mode: every part's d_sums
   bool connected = false;
 };
@@ -55,7 +67,7 @@ struct Group {
 struct cgx_dist {
   int device = 0, nranks = 1, rank = 0;
   bool local = false;
-  Group *group = nullptr;     // owned by part 0 in local mode, by self in RCCL
+  Group *group = nullptr;  // owned by part 0 in local mode, by self in RCCL
   bool owns_group = false;
   ncclComm_t comm = nullptr;
   int cus = 256;
@@ -64,154 +76,95 @@ struct cgx_dist {
   cgx_part *part = nullptr;
   long long n_global = 0;
   int row_begin = 0, n_loc = 0, n_ghost = 0, nnz = 0;
-  int vec = 4, wpb = 4;
-  // SpMV knobs, read from the environment once (CGX_SPMV_TG/DMA/NT/XCD)
-  int spmv_tg = 1, spmv_dma = 1, spmv_nt = -1, spmv_xcd = 1;
-  // recurrence (cgx_dist_set_alg): CGX_ALG_CG1 (Chronopoulos-Gear, one
-  // all-reduce of 2 doubles per iteration) or CGX_ALG_HS (the reference's
-  // recurrence, two all-reduces of 1 double, 8 B per row less vector traffic)
-  int alg = CGX_ALG_CG1;
-  int *d_rp = nullptr, *d_col = nullptr, *d_blk = nullptr, *d_blkk = nullptr;
-  int *d_blkrk = nullptr;  // (blk_row, blk_k) pairs for the coded-column kernel
+  int alg = CGX_ALG_HS;
+  int want_layout = CGX_LAYOUT_AUTO;
+  DevMatrix A;
+  cgx::Items it_int{}, it_bnd{};
   int *d_list_int = nullptr, *d_list_bnd = nullptr;
-  // dictionary-coded columns (k_spmv_dc), as the single-GPU solver: the
-  // local numbering keeps them (a slab's ghosts sit at constant offsets)
-  unsigned char *d_code = nullptr;
-  int *d_dict = nullptr;
-  unsigned char *d_rlen = nullptr;  // byte row lengths (rows <= 255 entries)
-  int ndict = 0;
-  int code_bits = 8;                 // 4: nibble codes (<= 16 offsets)
-  void *d_dval = nullptr;            // value-indexed pairs (CGX_DC_VALS): pair values
-  bool vi = false;
-  int n_int = 0, n_bnd = 0, g_int = 0, g_bnd = 0;
-  // interior / boundary row blocks as contiguous runs {first, count} when
-  // there are few of them (slab partitions: 1 interior + 2 boundary runs);
-  // otherwise the index lists above are used (one launch each)
-  std::vector<std::pair<int, int>> runs_int, runs_bnd;
-  bool use_runs = false;
-  double *d_val = nullptr;
-  double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr,
-         *d_s = nullptr, *d_w = nullptr;
+  int g_int = 0, g_bnd = 0;  // SpMV partials of each launch
+  double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
+         *d_w = nullptr;
   int *d_send_idx = nullptr;
   double *d_sendbuf = nullptr;
   std::vector<int> send_count, send_off, recv_count, recv_off;
   int n_send = 0;
-  double *d_pa = nullptr, *d_pb = nullptr, *d_sums = nullptr, *d_gsums = nullptr;
+  double *d_pa = nullptr, *d_pb = nullptr;
+  double *d_sums = nullptr, *d_gsums = nullptr;  // [0, 1] local, [2, 3] all-reduced
+  unsigned *d_tick = nullptr;                    // last-arriver counters
   int vec_grid = 1;
   CgState *d_st = nullptr, *h_st = nullptr;
   double *d_hist = nullptr;
   int hist_alloc = 0;
-  size_t dev_bytes = 0;
+  size_t vec_bytes = 0;
   bool have_matrix = false, have_rhs = false, bench_ready = false;
   int last_iters = 0;
   // optional SpMV timing: 4 events per iteration (interior start/end,
-  // boundary start/end) while rec_spmv is set
+  // boundary start/end) while rec_spmv is set (eager only)
   std::vector<hipEvent_t> spmv_ev;
   bool rec_spmv = false;
   size_t ev_i = 0;
-  // single rank, no transport: the iteration is [update, SpMV, finalize] on
-  // one stream, replayed as hipGraphs of graph_batch iterations
+  // batches of graph_batch iterations replayed as a hipGraph (solo and
+  // RCCL; the in-process group runs eager)
   hipGraphExec_t gexec = nullptr;
+  int gexec_alg = -1;
   int graph_batch = 16;
+  bool use_graph = true;
+  int graph_state = 0;  // 1 captured, -1 capture failed (eager from then on)
 };
 
 namespace {
 
 using namespace cgx;
 
-// One rank with no transport: no halo, scalars straight from the partials,
-// graph replay.  A 1-rank RCCL communicator (cgx_dist_create with an id at
-// nranks 1) keeps the transport phases -- the multi-GPU code path, all-reduce
-// included, on one GPU.
+// One rank with no transport: no halo, scalars straight from the partials.
+// A 1-rank RCCL communicator (cgx_dist_create with an id at nranks 1) keeps
+// the transport phases -- the multi-GPU code path, all-reduce included.
 bool solo(const cgx_dist *d) { return !d->local && d->comm == nullptr; }
 
-#define CGX_NCCL(call)                                                       \
-  do {                                                                       \
-    ncclResult_t r_ = (call);                                                \
-    if (r_ != ncclSuccess) {                                                 \
-      set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call,           \
-                ncclGetErrorString(r_));                                     \
-      return CGX_ECOMM;                                                      \
-    }                                                                        \
+#define CGX_NCCL(call)                                                                  \
+  do {                                                                                  \
+    ncclResult_t r_ = (call);                                                           \
+    if (r_ != ncclSuccess) {                                                            \
+      set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call, ncclGetErrorString(r_)); \
+      return CGX_ECOMM;                                                                 \
+    }                                                                                   \
   } while (0)
 
-template <typename P>
-int dalloc(cgx_dist *d, P **p, size_t bytes) {
-  if (bytes == 0) bytes = 16;
-  hipError_t e = hipErrorUnknown;
-  if (env_int("CGX_CONTIG", 1)) {  // physically contiguous, as the solver (fallback: hipMalloc)
-    e = hipExtMallocWithFlags((void **)p, bytes, hipDeviceMallocContiguous);
-    if (e != hipSuccess) (void)hipGetLastError();
-  }
-  if (e != hipSuccess) e = hipMalloc((void **)p, bytes);
-  if (e != hipSuccess) {
-    set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-    *p = nullptr;
-    return CGX_ENOMEM;
-  }
-  d->dev_bytes += bytes;
-  return 0;
-}
-
-template <typename P>
-void dfree(P **p) {
-  if (*p) (void)hipFree((void *)*p);
-  *p = nullptr;
-}
-
-bool dc_wanted(const cgx_dist *d);
-
-void free_system(cgx_dist *d) {
+void drop_graph(cgx_dist *d) {
   if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
   d->gexec = nullptr;
-  dfree(&d->d_rp); dfree(&d->d_col); dfree(&d->d_blk); dfree(&d->d_blkk);
-  dfree(&d->d_blkrk);
-  dfree(&d->d_list_int); dfree(&d->d_list_bnd); dfree(&d->d_val);
-  dfree(&d->d_b); dfree(&d->d_x); dfree(&d->d_r); dfree(&d->d_p);
-  dfree(&d->d_s); dfree(&d->d_w); dfree(&d->d_send_idx); dfree(&d->d_sendbuf);
-  dfree(&d->d_pa); dfree(&d->d_pb); dfree(&d->d_hist);
-  dfree(&d->d_code); dfree(&d->d_dict); dfree(&d->d_rlen); dfree(&d->d_dval);
-  d->ndict = 0;
-  d->vi = false;
+  d->gexec_alg = -1;
+}
+
+void free_system(cgx_dist *d) {
+  drop_graph(d);
+  d->A.release();
+  dev_free(&d->d_list_int);
+  dev_free(&d->d_list_bnd);
+  dev_free(&d->d_b);
+  dev_free(&d->d_x);
+  dev_free(&d->d_r);
+  dev_free(&d->d_p);
+  dev_free(&d->d_s);
+  dev_free(&d->d_w);
+  dev_free(&d->d_send_idx);
+  dev_free(&d->d_sendbuf);
+  dev_free(&d->d_pa);
+  dev_free(&d->d_pb);
+  dev_free(&d->d_hist);
   d->hist_alloc = 0;
   if (d->part) cgx_part_destroy(d->part);
   d->part = nullptr;
   d->have_matrix = d->have_rhs = d->bench_ready = false;
-  d->dev_bytes = 0;
+  d->vec_bytes = 0;
   if (d->group) d->group->connected = false;
 }
 
 int init_common(cgx_dist *d, int device) {
-  int cnt = 0;
-  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) {
-    set_error("no HIP device available");
-    return CGX_ENODEV;
-  }
-  if (device < 0 || device >= cnt) {
-    set_error("device %d out of range", device);
-    return CGX_EINVAL;
-  }
-  hipDeviceProp_t prop;
-  CGX_HIP(hipGetDeviceProperties(&prop, device));
-  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-    set_error("device %d is %s; libcgx is built for gfx950 only", device,
-              prop.gcnArchName);
-    return CGX_ENODEV;
-  }
+  int rc = check_device(device, &d->cus);
+  if (rc) return rc;
   d->device = device;
-  d->cus = prop.multiProcessorCount;
-  d->vec = env_int("CGX_SPMV_VEC", 4);
-  if (d->vec != 1 && d->vec != 2 && d->vec != 4) d->vec = 4;
-  d->wpb = env_int("CGX_SPMV_WPB", 4) == 8 ? 8 : 4;
-  d->spmv_tg = env_int("CGX_SPMV_TG", 1);
-  d->spmv_dma = d->wpb == 4 && env_int("CGX_SPMV_DMA", 1) == 1 ? 1 : 0;  // as the solver
-  d->spmv_nt = env_int("CGX_SPMV_NT", -1);
-  d->spmv_xcd = env_int("CGX_SPMV_XCD", 1);
-  d->graph_batch = env_int("CGX_GRAPH", 1) ? std::max(1, env_int("CGX_GRAPH_BATCH", 16)) : 0;
-  {
-    const char *al = getenv("CGX_DIST_ALG");
-    d->alg = al && strcmp(al, "hs") == 0 ? CGX_ALG_HS : CGX_ALG_CG1;
-  }
+  d->A.device = device;
   CGX_HIP(hipSetDevice(device));
   CGX_HIP(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
   {
@@ -220,15 +173,18 @@ int init_common(cgx_dist *d, int device) {
     // while the interior rows are still being summed
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-    CGX_HIP(hipStreamCreateWithPriority(&d->st_comm, hipStreamNonBlocking,
-                                        env_int("CGX_COMM_PRIO", 1) ? greatest : 0));
+    CGX_HIP(hipStreamCreateWithPriority(&d->st_comm, hipStreamNonBlocking, greatest));
   }
+  d->A.st = d->st;
   CGX_HIP(hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums2, hipEventDisableTiming));
   CGX_HIP(hipMalloc((void **)&d->d_st, sizeof(CgState)));
   CGX_HIP(hipMalloc((void **)&d->d_sums, 4 * sizeof(double)));
+  CGX_HIP(hipMemset(d->d_sums, 0, 4 * sizeof(double)));
+  CGX_HIP(hipMalloc((void **)&d->d_tick, 4 * sizeof(unsigned)));
+  CGX_HIP(hipMemset(d->d_tick, 0, 4 * sizeof(unsigned)));
   CGX_HIP(hipHostMalloc((void **)&d->h_st, sizeof(CgState), hipHostMallocDefault));
   d->d_gsums = d->d_sums + 2;
   return 0;
@@ -236,13 +192,47 @@ int init_common(cgx_dist *d, int device) {
 
 // ------------------------------------------------------------ system setup
 
-int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
-                 const int *rp, const int *col_global, const double *val) {
+// Interior / boundary work items (blocks or slices) of the local matrix:
+// boundary = any row of the item references a ghost column.  In the
+// matrix's (tiled) item order; one contiguous run needs no device list.
+int split_items(cgx_dist *d, const int *rp, const std::vector<int> &col_local) {
+  const std::vector<int> ir = d->A.item_rows();
+  const int ni = (int)ir.size() - 1;
+  std::vector<char> ghost((size_t)std::max(ni, 0), 0);
+  for (int i = 0; i < ni; ++i)
+    for (int k = rp[ir[(size_t)i]]; k < rp[ir[(size_t)i + 1]] && !ghost[(size_t)i]; ++k)
+      ghost[(size_t)i] = col_local[(size_t)k] >= d->n_loc;
+  std::vector<int> lint, lbnd;
+  for (int j = 0; j < ni; ++j) {
+    const int i = d->A.order.empty() ? j : d->A.order[(size_t)j];
+    (ghost[(size_t)i] ? lbnd : lint).push_back(i);
+  }
+  auto make = [&](const std::vector<int> &l, int **dl, Items &it) -> int {
+    const bool run = !l.empty() && l.back() - l.front() + 1 == (int)l.size() &&
+                     std::is_sorted(l.begin(), l.end());
+    it = Items{nullptr, l.empty() ? 0 : l.front(), (int)l.size()};
+    if (l.empty() || run) return 0;
+    int rc = dev_alloc(dl, l.size() * 4, &d->vec_bytes);
+    if (rc) return rc;
+    CGX_HIP(hipMemcpy(*dl, l.data(), l.size() * 4, hipMemcpyHostToDevice));
+    it.list = *dl;
+    it.first = 0;
+    return 0;
+  };
+  int rc;
+  if ((rc = make(lint, &d->d_list_int, d->it_int)) || (rc = make(lbnd, &d->d_list_bnd, d->it_bnd)))
+    return rc;
+  d->g_int = d->it_int.count ? d->A.partials(d->it_int) : 0;
+  d->g_bnd = d->it_bnd.count ? d->A.partials(d->it_bnd) : 0;
+  return 0;
+}
+
+int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int *rp,
+                 const int *col_global, const double *val) {
   CGX_HIP(hipSetDevice(d->device));
   free_system(d);
   cgx_part *pt = nullptr;
-  int rc = cgx_part_create(n_global, d->nranks, d->rank, n_loc, nnz, rp,
-                           col_global, &pt);
+  int rc = cgx_part_create(n_global, d->nranks, d->rank, n_loc, nnz, rp, col_global, &pt);
   if (rc) return rc;
   d->part = pt;
   d->n_global = n_global;
@@ -254,147 +244,33 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz,
   d->recv_count.assign((size_t)d->nranks, 0);
   cgx_part_recv_counts(pt, d->recv_count.data());
   d->recv_off.assign((size_t)d->nranks, 0);
-  for (int q = 1; q < d->nranks; ++q)
-    d->recv_off[q] = d->recv_off[q - 1] + d->recv_count[q - 1];
+  for (int q = 1; q < d->nranks; ++q) d->recv_off[q] = d->recv_off[q - 1] + d->recv_count[q - 1];
 
-  // wave row blocks of 64 rows, split into interior / boundary lists
-  const int cap = spmv_cap(64, true);
-  std::vector<int> blk = n_loc > 0 ? plan_rowblocks(n_loc, rp, 64, cap - kPad)
-                                   : std::vector<int>{0};
-  const int nblk = (int)blk.size() - 1;
-  std::vector<int> blkk(blk.size()), lint, lbnd;
-  for (size_t i = 0; i < blk.size(); ++i) blkk[i] = n_loc > 0 ? rp[blk[i]] : 0;
-  for (int b = 0; b < nblk; ++b) {
-    bool ghost = false;
-    for (int k = blkk[b]; k < blkk[b + 1] && !ghost; ++k) ghost = col_local[k] >= n_loc;
-    (ghost ? lbnd : lint).push_back(b);
-  }
-  d->n_int = (int)lint.size();
-  d->n_bnd = (int)lbnd.size();
-  auto runs = [](const std::vector<int> &l) {
-    std::vector<std::pair<int, int>> r;
-    for (int b : l) {
-      if (!r.empty() && r.back().first + r.back().second == b) r.back().second++;
-      else r.push_back({b, 1});
-    }
-    return r;
-  };
-  d->runs_int = runs(lint);
-  d->runs_bnd = runs(lbnd);
-  d->use_runs = d->runs_int.size() <= 4 && d->runs_bnd.size() <= 4 &&
-                env_int("CGX_DIST_RUNS", 1) != 0;
-  if (d->use_runs) {
-    d->g_int = d->g_bnd = 0;
-    for (auto &r : d->runs_int) d->g_int += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
-    for (auto &r : d->runs_bnd) d->g_bnd += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
-    // several boundary runs (a middle slab's first and last plane): one launch
-    // over the boundary block list instead of one per run
-    if (d->runs_bnd.size() > 1) d->g_bnd = spmv_launch_grid(64, d->wpb, 1, d->n_bnd, 0);
-  } else {
-    d->g_int = spmv_launch_grid(64, d->wpb, 1, d->n_int, 0);
-    d->g_bnd = spmv_launch_grid(64, d->wpb, 1, d->n_bnd, 0);
-  }
-  d->vec_grid = vec_grid_for(n_loc, d->cus);
-
-  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
-  const size_t nv = (size_t)n_loc + kPad;
-  if ((rc = dalloc(d, &d->d_rp, ((size_t)n_loc + 1) * 4)) ||
-      (rc = dalloc(d, &d->d_col, nnz_pad * 4)) ||
-      (rc = dalloc(d, &d->d_val, nnz_pad * 8)) ||
-      (rc = dalloc(d, &d->d_blk, blk.size() * 4)) ||
-      (rc = dalloc(d, &d->d_blkk, blk.size() * 4)) ||
-      (rc = dalloc(d, &d->d_blkrk, blk.size() * 8)) ||
-      (rc = dalloc(d, &d->d_list_int, (lint.size() + 1) * 4)) ||
-      (rc = dalloc(d, &d->d_list_bnd, (lbnd.size() + 1) * 4)) ||
-      (rc = dalloc(d, &d->d_b, nv * 8)) || (rc = dalloc(d, &d->d_x, nv * 8)) ||
-      (rc = dalloc(d, &d->d_r, (nv + d->n_ghost) * 8)) ||
-      (rc = dalloc(d, &d->d_p, (nv + d->n_ghost) * 8)) || (rc = dalloc(d, &d->d_s, nv * 8)) ||
-      (rc = dalloc(d, &d->d_w, nv * 8)) ||
-      (rc = dalloc(d, &d->d_pa, ((size_t)d->vec_grid + 8) * 8)) ||
-      (rc = dalloc(d, &d->d_pb, ((size_t)d->g_int + d->g_bnd + 1) * 8))) {
+  if ((rc = d->A.upload<double>(n_loc, n_loc + d->n_ghost, nnz, rp, col_local.data(), val,
+                                d->want_layout, false))) {
     free_system(d);
     return rc;
   }
-  hipStream_t st = d->st;
-  CGX_HIP(hipMemsetAsync(d->d_col, 0, nnz_pad * 4, st));
-  CGX_HIP(hipMemsetAsync(d->d_val, 0, nnz_pad * 8, st));
-  CGX_HIP(hipMemsetAsync(d->d_r, 0, (nv + d->n_ghost) * 8, st));
-  CGX_HIP(hipMemsetAsync(d->d_p, 0, (nv + d->n_ghost) * 8, st));
-  if (n_loc > 0) {
-    CGX_HIP(hipMemcpyAsync(d->d_rp, rp, ((size_t)n_loc + 1) * 4, hipMemcpyHostToDevice, st));
-    if (nnz > 0) {
-      CGX_HIP(hipMemcpyAsync(d->d_col, col_local.data(), (size_t)nnz * 4, hipMemcpyHostToDevice, st));
-      CGX_HIP(hipMemcpyAsync(d->d_val, val, (size_t)nnz * 8, hipMemcpyHostToDevice, st));
-    }
+  if ((rc = split_items(d, rp, col_local))) {
+    free_system(d);
+    return rc;
   }
-  CGX_HIP(hipMemcpyAsync(d->d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
-  CGX_HIP(hipMemcpyAsync(d->d_blkk, blkk.data(), blkk.size() * 4, hipMemcpyHostToDevice, st));
-  std::vector<int> blkrk(2 * blk.size());
-  for (size_t i = 0; i < blk.size(); ++i) {
-    blkrk[2 * i] = blk[i];
-    blkrk[2 * i + 1] = blkk[i];
+  d->vec_grid = vec_grid_for(n_loc, d->cus);
+  d->vec_grid = (std::max(d->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
+  const size_t nv = (size_t)n_loc + kPad, ng = nv + (size_t)d->n_ghost;
+  size_t *cb = &d->vec_bytes;
+  if ((rc = dev_alloc(&d->d_b, nv * 8, cb)) || (rc = dev_alloc(&d->d_x, nv * 8, cb)) ||
+      (rc = dev_alloc(&d->d_r, ng * 8, cb)) || (rc = dev_alloc(&d->d_p, ng * 8, cb)) ||
+      (rc = dev_alloc(&d->d_s, nv * 8, cb)) || (rc = dev_alloc(&d->d_w, nv * 8, cb)) ||
+      (rc = dev_alloc(&d->d_pa, ((size_t)d->vec_grid + 8) * 8, cb)) ||
+      (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb))) {
+    free_system(d);
+    return rc;
   }
-  CGX_HIP(hipMemcpyAsync(d->d_blkrk, blkrk.data(), blkrk.size() * 4, hipMemcpyHostToDevice, st));
-  if (n_loc > 0 && nnz > 0 && dc_wanted(d)) {
-    std::vector<unsigned char> code((size_t)nnz);
-    std::vector<int> dict;
-    int nd = build_col_codes(n_loc, rp, col_local.data(), dict, code.data());
-    std::vector<unsigned char> rl;
-    if (nd > 0 && env_int("CGX_DC_RLEN", 1)) {
-      rl.resize((size_t)n_loc);
-      if (!build_row_lengths(n_loc, rp, rl.data())) rl.clear();
-    }
-    // value-indexed pairs (k_spmv_vi) as the solver: byte row lengths, <= 64
-    // (offset, value) pairs, every block's code window inside the kernel's
-    std::vector<double> dv;
-    if (nd > 0 && !rl.empty() && env_int("CGX_DC_VALS", 1) != 0) {
-      const int cb = nd <= 16 && env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8, ka = 128 / cb;
-      const long long capc = ((512LL + ka) * cb / 8 + 15) & ~15LL;
-      bool fits = true;
-      for (size_t b = 0; b + 1 < blkk.size() && fits; ++b)
-        fits = ((long long)(blkk[b + 1] - (blkk[b] & ~(ka - 1))) * cb + 7) / 8 <= capc;
-      if (fits) {
-        const int np = build_val_pairs<double>(nnz, val, code.data(), dict, dv, 64);
-        if (np > 0) nd = np;
-      }
-    }
-    if (nd > 0) {
-      if ((rc = dalloc(d, &d->d_code, nnz_pad)) || (rc = dalloc(d, &d->d_dict, 256 * 4)) ||
-          (!dv.empty() && (rc = dalloc(d, &d->d_dval, 256 * 8)))) {
-        free_system(d);
-        return rc;
-      }
-      dict.resize(256, 0);
-      if (!dv.empty()) {
-        dv.resize(256, 0.0);
-        CGX_HIP(hipMemcpyAsync(d->d_dval, dv.data(), 256 * 8, hipMemcpyHostToDevice, st));
-        d->vi = true;
-      }
-      d->code_bits = nd <= 16 && env_int("CGX_DC_BITS", 8) == 4 ? 4 : 8;
-      size_t code_bytes = (size_t)nnz;
-      if (d->code_bits == 4) {
-        pack_nibbles(nnz, code.data(), code.data());
-        code_bytes = ((size_t)nnz + 1) / 2;
-      }
-      CGX_HIP(hipMemsetAsync(d->d_code, 0, nnz_pad, st));
-      CGX_HIP(hipMemcpyAsync(d->d_code, code.data(), code_bytes, hipMemcpyHostToDevice, st));
-      CGX_HIP(hipMemcpyAsync(d->d_dict, dict.data(), 256 * 4, hipMemcpyHostToDevice, st));
-      if (!rl.empty()) {
-        if ((rc = dalloc(d, &d->d_rlen, (size_t)n_loc + 64))) {
-          free_system(d);
-          return rc;
-        }
-        CGX_HIP(hipMemcpyAsync(d->d_rlen, rl.data(), (size_t)n_loc, hipMemcpyHostToDevice, st));
-      }
-      CGX_HIP(hipStreamSynchronize(st));  // the host vectors go out of scope
-      d->ndict = nd;
-    }
-  }
-  if (!lint.empty())
-    CGX_HIP(hipMemcpyAsync(d->d_list_int, lint.data(), lint.size() * 4, hipMemcpyHostToDevice, st));
-  if (!lbnd.empty())
-    CGX_HIP(hipMemcpyAsync(d->d_list_bnd, lbnd.data(), lbnd.size() * 4, hipMemcpyHostToDevice, st));
-  CGX_HIP(hipStreamSynchronize(st));
+  CGX_HIP(hipMemsetAsync(d->d_r, 0, ng * 8, d->st));
+  CGX_HIP(hipMemsetAsync(d->d_p, 0, ng * 8, d->st));
+  CGX_HIP(hipMemsetAsync(d->d_x, 0, nv * 8, d->st));
+  CGX_HIP(hipStreamSynchronize(d->st));
   d->have_matrix = true;
   return 0;
 }
@@ -406,19 +282,17 @@ int install_sends(cgx_dist *d, const std::vector<int> &req_counts,
   if (rc) return rc;
   d->send_count = req_counts;
   d->send_off.assign((size_t)d->nranks, 0);
-  for (int q = 1; q < d->nranks; ++q)
-    d->send_off[q] = d->send_off[q - 1] + d->send_count[q - 1];
+  for (int q = 1; q < d->nranks; ++q) d->send_off[q] = d->send_off[q - 1] + d->send_count[q - 1];
   d->n_send = d->send_off[d->nranks - 1] + d->send_count[d->nranks - 1];
   std::vector<int> loc((size_t)d->n_send);
   cgx_part_send_local(d->part, loc.data());
-  dfree(&d->d_send_idx);
-  dfree(&d->d_sendbuf);
-  if ((rc = dalloc(d, &d->d_send_idx, ((size_t)d->n_send + 1) * 4)) ||
-      (rc = dalloc(d, &d->d_sendbuf, ((size_t)d->n_send + 1) * 8)))
+  dev_free(&d->d_send_idx);
+  dev_free(&d->d_sendbuf);
+  if ((rc = dev_alloc(&d->d_send_idx, ((size_t)d->n_send + 1) * 4, &d->vec_bytes)) ||
+      (rc = dev_alloc(&d->d_sendbuf, ((size_t)d->n_send + 1) * 8, &d->vec_bytes)))
     return rc;
   if (d->n_send > 0)
-    CGX_HIP(hipMemcpy(d->d_send_idx, loc.data(), (size_t)d->n_send * 4,
-                      hipMemcpyHostToDevice));
+    CGX_HIP(hipMemcpy(d->d_send_idx, loc.data(), (size_t)d->n_send * 4, hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -489,8 +363,7 @@ int connect_local(Group *g) {
       const cgx_dist *o = g->parts[q];
       const int off = o->recv_off[p], cnt = o->recv_count[p];
       req_counts[q] = cnt;
-      req_global.insert(req_global.end(), ghosts[q].begin() + off,
-                        ghosts[q].begin() + off + cnt);
+      req_global.insert(req_global.end(), ghosts[q].begin() + off, ghosts[q].begin() + off + cnt);
     }
     int rc = install_sends(d, req_counts, req_global);
     if (rc) return rc;
@@ -500,8 +373,7 @@ int connect_local(Group *g) {
     for (int q = 0; q < P; ++q) srcs[q] = g->parts[q]->d_sums;
     CGX_HIP(hipSetDevice(g->parts[0]->device));
     CGX_HIP(hipMalloc((void **)&g->d_srcs, (size_t)P * sizeof(double *)));
-    CGX_HIP(hipMemcpy(g->d_srcs, srcs.data(), (size_t)P * sizeof(double *),
-                      hipMemcpyHostToDevice));
+    CGX_HIP(hipMemcpy(g->d_srcs, srcs.data(), (size_t)P * sizeof(double *), hipMemcpyHostToDevice));
   }
   g->connected = true;
   return 0;
@@ -522,95 +394,42 @@ int ensure_connected(Group *g) {
 
 // ---------------------------------------------------------- phase helpers
 
-// Coded columns on the default LDS-DMA kernel unless CGX_DC=0 / CGX_LAYOUT=csr.
-bool dc_wanted(const cgx_dist *d) {
-  const char *l = getenv("CGX_LAYOUT");
-  return d->wpb == 4 && d->spmv_dma == 1 && env_int("CGX_DC", 1) != 0 &&
-         !(l && strcmp(l, "csr") == 0);
-}
+// the vector the SpMV gathers (its ghost tail is the halo) and its output
+double *spmv_x(cgx_dist *d) { return d->alg == CGX_ALG_HS ? d->d_p : d->d_r; }
+double *spmv_y(cgx_dist *d) { return d->alg == CGX_ALG_HS ? d->d_s : d->d_w; }
 
-SpmvArgs<double> spmv_args(cgx_dist *d, bool boundary) {
-  SpmvArgs<double> a;
-  memset(&a, 0, sizeof a);
-  a.rp = d->d_rp;
-  a.col = d->d_col;
-  a.val = d->d_val;
-  // CG1: w = A r;  HS: s = A p (cg.c:111).  The gathered vector carries the
-  // ghost tail the halo exchange fills.
-  a.x = d->alg == CGX_ALG_HS ? d->d_p : d->d_r;
-  a.y = d->alg == CGX_ALG_HS ? d->d_s : d->d_w;
-  a.blk_row = d->d_blk;
-  a.blk_k = d->d_blkk;
-  a.blk_rk = d->d_blkrk;
-  a.blk_list = boundary ? d->d_list_bnd : d->d_list_int;
-  a.blk_first = 0;
-  a.nblk = boundary ? d->n_bnd : d->n_int;
-  a.part = boundary ? d->d_pb + d->g_int : d->d_pb;
-  a.done = &d->d_st->done;
-  a.bs = 64;
-  a.wpb = d->wpb;
-  a.rbw = 1;
-  a.st = d->d_st;
-  a.tg = d->spmv_tg;
-  a.dma = d->spmv_dma;  // 1 or 0: the grids assume one block per wave, 4 waves per WG
-  a.nt = d->spmv_nt;
-  if (a.nt < 0) a.nt = a.dma && (double)d->nnz * 12.0 > kNtStreamBytes ? 2 : 0;
-  a.xcd = a.dma ? d->spmv_xcd : 0;  // XCD-contiguous blocks, as the solver
-  a.tk = TicketArgs{};
-  if (a.dma == 1 && d->ndict > 0) {
-    a.code = d->d_code;
-    a.dict = d->d_dict;
-    a.ndict_cap = dict_cap(d->ndict);
-    a.rlen = d->d_rlen;
-    a.code_bits = d->code_bits;
-    a.dval = d->vi ? (const double *)d->d_dval : nullptr;
-    a.bpw = 1;
-  }
-  return a;
-}
-
-// phase A: the vector update (or the prologue) and the halo pack
-int phase_update(cgx_dist *d, bool init) {
-  CGX_HIP(hipSetDevice(d->device));
-  if (init)
-    CGX_HIP(launch_init_cg1<double>(d->n_loc, d->d_b, d->d_x, d->d_r, d->d_p,
-                                    d->d_s, d->d_pa, d->vec_grid, d->st));
-  else
-    CGX_HIP(launch_cg1_update<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_s,
-                                      d->d_w, d->d_st, d->d_pa, d->vec_grid,
-                                      d->st));
+// pack the send rows of the gathered vector (after its update)
+int phase_pack(cgx_dist *d) {
   if (solo(d)) return 0;
-  CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, d->d_r, d->d_sendbuf,
-                                d->st));
+  CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, spmv_x(d), d->d_sendbuf, d->st));
   CGX_HIP(hipEventRecord(d->ev_packed, d->st));
   return 0;
 }
 
-// phase B: halo exchange on the communication stream
+// halo exchange on the communication stream, straight into the ghost tail
 int phase_halo(cgx_dist *d) {
   if (solo(d)) return 0;
   CGX_HIP(hipSetDevice(d->device));
   CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_packed, 0));
-  double *ghost = (d->alg == CGX_ALG_HS ? d->d_p : d->d_r) + d->n_loc;
+  double *ghost = spmv_x(d) + d->n_loc;
   if (d->local) {
     for (cgx_dist *o : d->group->parts) {
       if (o == d || d->recv_count[o->rank] == 0) continue;
       CGX_HIP(hipStreamWaitEvent(d->st_comm, o->ev_packed, 0));
-      CGX_HIP(hipMemcpyAsync(ghost + d->recv_off[o->rank],
-                             o->d_sendbuf + o->send_off[d->rank],
-                             (size_t)d->recv_count[o->rank] * 8,
-                             hipMemcpyDeviceToDevice, d->st_comm));
+      CGX_HIP(hipMemcpyAsync(ghost + d->recv_off[o->rank], o->d_sendbuf + o->send_off[d->rank],
+                             (size_t)d->recv_count[o->rank] * 8, hipMemcpyDeviceToDevice,
+                             d->st_comm));
     }
   } else if (d->nranks > 1) {
     CGX_NCCL(ncclGroupStart());
     for (int q = 0; q < d->nranks; ++q) {
       if (q == d->rank) continue;
       if (d->recv_count[q])
-        CGX_NCCL(ncclRecv(ghost + d->recv_off[q], d->recv_count[q], ncclFloat64,
-                          q, d->comm, d->st_comm));
+        CGX_NCCL(ncclRecv(ghost + d->recv_off[q], d->recv_count[q], ncclFloat64, q, d->comm,
+                          d->st_comm));
       if (d->send_count[q])
-        CGX_NCCL(ncclSend(d->d_sendbuf + d->send_off[q], d->send_count[q],
-                          ncclFloat64, q, d->comm, d->st_comm));
+        CGX_NCCL(ncclSend(d->d_sendbuf + d->send_off[q], d->send_count[q], ncclFloat64, q,
+                          d->comm, d->st_comm));
     }
     CGX_NCCL(ncclGroupEnd());
   }
@@ -618,146 +437,67 @@ int phase_halo(cgx_dist *d) {
   return 0;
 }
 
-// phase C: SpMV (interior overlapping the halo, then boundary) + local sums
-// SpMV over one set of row blocks (interior or boundary): one launch per
-// contiguous run, partials packed after each other from d_pb + part_off.
-int spmv_set(cgx_dist *d, bool boundary) {
-  SpmvArgs<double> a = spmv_args(d, boundary);
-  if (!d->use_runs || (boundary && d->runs_bnd.size() > 1)) {
-    CGX_HIP(launch_spmv<double>(a, boundary ? d->g_bnd : d->g_int, d->vec, d->st));
-    return 0;
-  }
-  a.blk_list = nullptr;
-  double *part = boundary ? d->d_pb + d->g_int : d->d_pb;
-  for (const auto &r : boundary ? d->runs_bnd : d->runs_int) {
-    a.blk_first = r.first;
-    a.nblk = r.second;
-    a.part = part;
-    CGX_HIP(launch_spmv<double>(a, 0, d->vec, d->st));
-    part += spmv_launch_grid(64, d->wpb, 1, r.second, 0);
-  }
-  return 0;
-}
-
+// SpMV over interior items (overlapping the halo), then boundary items; with
+// a transport, the last launch's last workgroup writes the local sums (HS:
+// p.s -> sums[0]; CG1: gamma, delta -> sums[0..1]).
 int phase_spmv(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
-  int rc;
+  const int np = d->g_int + d->g_bnd;
+  FinArgs fin{};
+  if (!solo(d) && np > 0) {
+    if (d->alg == CGX_ALG_HS) fin = FinArgs{d->d_tick, d->d_pb, np, nullptr, 0, d->d_sums};
+    else fin = FinArgs{d->d_tick, d->d_pa, d->vec_grid, d->d_pb, np, d->d_sums};
+  }
+  const bool bnd_last = d->g_bnd > 0;
+  auto launch = [&](const Items &it, double *part, bool last) -> hipError_t {
+    if (it.count == 0) return hipSuccess;
+    SpmvArgs<double> a = d->A.args<double>(spmv_x(d), spmv_y(d), part, &d->d_st->done, it);
+    if (last) a.fin = fin;
+    return launch_spmv<double>(a, d->st);
+  };
   if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i], d->st));
-  if ((rc = spmv_set(d, false))) return rc;
+  CGX_HIP(launch(d->it_int, d->d_pb, !bnd_last));
   if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 1], d->st));
   if (!solo(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
   if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 2], d->st));
-  if ((rc = spmv_set(d, true))) return rc;
+  CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, bnd_last));
   if (rec) {
     CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 3], d->st));
     d->ev_i += 4;
   }
-  if (solo(d)) return 0;  // phase_reduce finalizes straight from the partials
-  if (d->alg == CGX_ALG_HS)  // local p.s -> sums[0]
-    CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, d->g_int + d->g_bnd, nullptr, 0, d->d_st,
-                            d->d_hist, d->d_sums, d->st));
-  else
-    CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, d->vec_grid, d->d_pb,
-                            d->g_int + d->g_bnd, d->d_st, d->d_hist, d->d_sums,
-                            d->st));
+  if (solo(d)) return 0;
+  if (np == 0)  // no rows here: the local sums are those of empty sets
+    CGX_HIP(launch_finalize(d->alg == CGX_ALG_HS ? FIN_SUM : FIN_SUM2, d->d_pa,
+                            d->alg == CGX_ALG_HS ? 0 : d->vec_grid, d->alg == CGX_ALG_HS ? nullptr : d->d_pb, 0,
+                            d->d_st, d->d_hist, d->d_sums, d->st));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
 
-// phase D: the one all-reduce of the iteration (gamma, delta), then scalars
-int phase_reduce(cgx_dist *d, bool init) {
-  CGX_HIP(hipSetDevice(d->device));
-  if (solo(d)) {
-    CGX_HIP(launch_finalize(init ? FIN_INIT_CG1 : FIN_CG1, d->d_pa, d->vec_grid,
-                            d->d_pb, d->g_int + d->g_bnd, d->d_st, d->d_hist,
-                            nullptr, d->st));
-    return 0;
-  }
-  const double *g = d->d_gsums;
-  if (d->local) {
-    for (cgx_dist *o : d->group->parts)
-      if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_sums, 0));
-    CGX_HIP(launch_group_sum(d->group->d_srcs, (int)d->group->parts.size(), 2,
-                             d->d_gsums, d->st, 0));
-  } else if (d->comm) {
-    CGX_NCCL(ncclAllReduce(d->d_sums, d->d_gsums, 2, ncclFloat64, ncclSum,
-                           d->comm, d->st));
-  } else {
-    g = d->d_sums;
-  }
-  CGX_HIP(launch_finalize(init ? FIN_INIT_CG1 : FIN_CG1, g, 1, g + 1, 1,
-                          d->d_st, d->d_hist, nullptr, d->st));
-  return 0;
-}
-
-int run_phases_eager(Group *g, bool init, long long iters);
-
-int run_phases(Group *g, bool init, long long iters) {
-  cgx_dist *d = g->parts[0];
-  const int B = d->graph_batch;
-  if (!init && solo(d) && B > 0 && iters >= B && !d->rec_spmv) {
-    if (!d->gexec) {
-      hipGraph_t gr = nullptr;
-      CGX_HIP(hipSetDevice(d->device));
-      CGX_HIP(hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal));
-      int rc = run_phases_eager(g, false, B);
-      hipError_t e = hipStreamEndCapture(d->st, &gr);
-      if (rc) {
-        if (gr) (void)hipGraphDestroy(gr);
-        return rc;
-      }
-      CGX_HIP(e);
-      e = hipGraphInstantiate(&d->gexec, gr, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(gr);
-      CGX_HIP(e);
-    }
-    while (iters >= B) {
-      CGX_HIP(hipGraphLaunch(d->gexec, d->st));
-      iters -= B;
-    }
-  }
-  return run_phases_eager(g, init, iters);
-}
-
-// ---- HS recurrence (CGX_ALG_HS): the single-GPU folded kernels, with the
-// two scalar steps fed by all-reduced sums instead of local partials.  Per
-// iteration: halo of p (packed at the end of the previous one) || interior
-// SpMV s = A p; boundary SpMV; p.s -> all-reduce -> k_update_rf (alpha,
-// r -= alpha s, r.r partials) -> r.r -> all-reduce -> k_xpay_xf (beta, stop,
-// x += alpha p, p = r + beta p) -> pack p.  Every rank computes alpha, beta
-// and the stop test from the same global sums, so they agree bit for bit.
-
-// one scalar of the iteration summed over the ranks: sums[i] -> gsums[i]
-int reduce_one(cgx_dist *d, int i, hipEvent_t ev) {
+// the all-reduce of `count` local sums starting at sums[i] -> gsums[i]
+int allreduce(cgx_dist *d, int i, int count) {
   if (d->local) {
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, i == 0 ? o->ev_sums : o->ev_sums2, 0));
-    CGX_HIP(launch_group_sum(d->group->d_srcs, (int)d->group->parts.size(), 1, d->d_gsums,
+    CGX_HIP(launch_group_sum(d->group->d_srcs, (int)d->group->parts.size(), count, d->d_gsums,
                              d->st, i));
   } else {
-    CGX_NCCL(ncclAllReduce(d->d_sums + i, d->d_gsums + i, 1, ncclFloat64, ncclSum, d->comm,
+    CGX_NCCL(ncclAllReduce(d->d_sums + i, d->d_gsums + i, count, ncclFloat64, ncclSum, d->comm,
                            d->st));
   }
-  (void)ev;
   return 0;
 }
 
-int hs_pack(cgx_dist *d) {
-  if (solo(d)) return 0;
-  CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, d->d_p, d->d_sendbuf, d->st));
-  CGX_HIP(hipEventRecord(d->ev_packed, d->st));
-  return 0;
-}
-
+// ---- HS
 // prologue: x = 0, r = p = b, b.b (cg.c:104-107)
 int hs_init(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
-  CGX_HIP(launch_init_hs<double>(d->n_loc, d->d_b, d->d_x, d->d_r, d->d_p, d->d_pa,
-                                 d->vec_grid, d->st));
+  CGX_HIP(launch_init_hs<double>(d->n_loc, d->d_b, d->d_x, d->d_r, d->d_p, d->d_pa, d->vec_grid,
+                                 d->st));
   if (solo(d)) {
-    CGX_HIP(launch_finalize(FIN_INIT_HS, d->d_pa, d->vec_grid, nullptr, 0, d->d_st,
-                            d->d_hist, nullptr, d->st));
+    CGX_HIP(launch_finalize(FIN_INIT_HS, d->d_pa, d->vec_grid, nullptr, 0, d->d_st, d->d_hist,
+                            nullptr, d->st));
     return 0;
   }
   CGX_HIP(launch_finalize(FIN_SUM, d->d_pa, d->vec_grid, nullptr, 0, d->d_st, d->d_hist,
@@ -767,31 +507,28 @@ int hs_init(cgx_dist *d) {
 }
 
 int hs_init_reduce(cgx_dist *d) {
-  if (solo(d)) return hs_pack(d);
-  int rc = reduce_one(d, 0, d->ev_sums);
+  if (solo(d)) return 0;
+  int rc = allreduce(d, 0, 1);
   if (rc) return rc;
-  CGX_HIP(launch_finalize(FIN_INIT_HS, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist,
-                          nullptr, d->st));
-  return hs_pack(d);
+  CGX_HIP(launch_finalize(FIN_INIT_HS, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist, nullptr,
+                          d->st));
+  return 0;
 }
 
-// alpha step: all-reduced p.s, r -= alpha s, local r.r
+// alpha step: all-reduced p.s, r -= alpha s, local r.r (last workgroup)
 int hs_alpha(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
-  const int gf = (d->vec_grid + 3) / 4;  // 1024-thread workgroups, 4 partials each
-  const double *ps = d->d_pb;
-  int nps = d->g_int + d->g_bnd;
-  if (!solo(d)) {
-    int rc = reduce_one(d, 0, d->ev_sums);
-    if (rc) return rc;
-    ps = d->d_gsums;
-    nps = 1;
+  const int gf = d->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
+  if (solo(d)) {
+    CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_pb,
+                                     d->g_int + d->g_bnd, d->d_pa, gf, d->st));
+    return 0;
   }
-  CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, ps, nps, d->d_pa, gf,
-                                   d->st, true));              // cg.c:113, 118-123
-  if (solo(d)) return 0;
-  CGX_HIP(launch_finalize(FIN_SUM, d->d_pa, 4 * gf, nullptr, 0, d->d_st, d->d_hist,
-                          d->d_sums + 1, d->st));
+  int rc = allreduce(d, 0, 1);
+  if (rc) return rc;
+  const FinArgs fin{d->d_tick + 1, d->d_pa, 4 * gf, nullptr, 0, d->d_sums + 1};
+  CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_gsums, 1, d->d_pa, gf,
+                                   d->st, &fin));  // cg.c:113, 118-123
   CGX_HIP(hipEventRecord(d->ev_sums2, d->st));
   return 0;
 }
@@ -799,30 +536,59 @@ int hs_alpha(cgx_dist *d) {
 // beta step: all-reduced r.r, stop test, x += alpha p, p = r + beta p
 int hs_beta(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
-  const int gf = (d->vec_grid + 3) / 4;
+  const int gf = d->vec_grid / 4;
   const double *rr = d->d_pa;
   int nrr = 4 * gf;
   if (!solo(d)) {
-    int rc = reduce_one(d, 1, d->ev_sums2);
+    int rc = allreduce(d, 1, 1);
     if (rc) return rc;
     rr = d->d_gsums + 1;
     nrr = 1;
   }
-  CGX_HIP(launch_xpay_xf<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_st, rr, nrr,
-                                 d->d_hist, gf, d->st, true));  // cg.c:115-116, 125-132
-  return hs_pack(d);
+  CGX_HIP(launch_xpay_xf<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_st, rr, nrr, d->d_hist,
+                                 gf, d->st));  // cg.c:115-116, 125-132
+  return 0;
+}
+
+// ---- CG1
+int cg1_update(cgx_dist *d, bool init) {
+  CGX_HIP(hipSetDevice(d->device));
+  if (init)
+    CGX_HIP(launch_init_cg1<double>(d->n_loc, d->d_b, d->d_x, d->d_r, d->d_p, d->d_s, d->d_pa,
+                                    d->vec_grid, d->st));
+  else
+    CGX_HIP(launch_cg1_update<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_s, d->d_w, d->d_st,
+                                      d->d_pa, d->vec_grid, d->st));
+  return phase_pack(d);
+}
+
+int cg1_reduce(cgx_dist *d, bool init) {
+  CGX_HIP(hipSetDevice(d->device));
+  const int op = init ? FIN_INIT_CG1 : FIN_CG1;
+  if (solo(d)) {
+    CGX_HIP(launch_finalize(op, d->d_pa, d->vec_grid, d->d_pb, d->g_int + d->g_bnd, d->d_st,
+                            d->d_hist, nullptr, d->st));
+    return 0;
+  }
+  int rc = allreduce(d, 0, 2);
+  if (rc) return rc;
+  CGX_HIP(launch_finalize(op, d->d_gsums, 1, d->d_gsums + 1, 1, d->d_st, d->d_hist, nullptr, d->st));
+  return 0;
 }
 
 int run_phases_eager(Group *g, bool init, long long iters) {
   auto &P = g->parts;
+  int rc;
   if (P[0]->alg == CGX_ALG_HS) {
-    int rc;
     if (init) {
       for (cgx_dist *d : P) if ((rc = hs_init(d))) return rc;
       for (cgx_dist *d : P) if ((rc = hs_init_reduce(d))) return rc;
       return 0;
     }
+    // each iteration packs its own halo first, so a captured batch has no
+    // dependency on work outside it
     for (long long it = 0; it < iters; ++it) {
+      for (cgx_dist *d : P) if ((rc = phase_pack(d))) return rc;
       for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
       for (cgx_dist *d : P) if ((rc = phase_spmv(d))) return rc;
       for (cgx_dist *d : P) if ((rc = hs_alpha(d))) return rc;
@@ -831,13 +597,55 @@ int run_phases_eager(Group *g, bool init, long long iters) {
     return 0;
   }
   for (long long it = 0; it < (init ? 1 : iters); ++it) {
-    int rc;
-    for (cgx_dist *d : P) if ((rc = phase_update(d, init))) return rc;
+    for (cgx_dist *d : P) if ((rc = cg1_update(d, init))) return rc;
     for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
     for (cgx_dist *d : P) if ((rc = phase_spmv(d))) return rc;
-    for (cgx_dist *d : P) if ((rc = phase_reduce(d, init))) return rc;
+    for (cgx_dist *d : P) if ((rc = cg1_reduce(d, init))) return rc;
   }
   return 0;
+}
+
+// Capture graph_batch iterations (kernels, halo send/recv on the comm
+// stream forked and joined by events, all-reduces) once; replay.
+int capture(cgx_dist *d, Group *g) {
+  hipGraph_t gr = nullptr;
+  CGX_HIP(hipSetDevice(d->device));
+  CGX_HIP(hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal));
+  const int rc = run_phases_eager(g, false, d->graph_batch);
+  const hipError_t e = hipStreamEndCapture(d->st, &gr);
+  hipError_t ei = hipSuccess;
+  if (rc == 0 && e == hipSuccess) ei = hipGraphInstantiate(&d->gexec, gr, nullptr, nullptr, 0);
+  if (gr) (void)hipGraphDestroy(gr);
+  if (rc || e != hipSuccess || ei != hipSuccess) {
+    d->gexec = nullptr;
+    (void)hipGetLastError();
+    return CGX_ENODEV;
+  }
+  d->gexec_alg = d->alg;
+  return 0;
+}
+
+int run_phases(Group *g, bool init, long long iters) {
+  cgx_dist *d = g->parts[0];
+  const int B = d->graph_batch;
+  if (!init && !d->local && d->use_graph && d->graph_state >= 0 && B > 0 && iters >= B &&
+      !d->rec_spmv) {
+    if (!d->gexec || d->gexec_alg != d->alg) {
+      drop_graph(d);
+      if (capture(d, g)) {
+        // capture not supported here (e.g. a transport call refused it):
+        // stay eager; nothing was enqueued on the stream
+        d->graph_state = -1;
+        return run_phases_eager(g, init, iters);
+      }
+      d->graph_state = 1;
+    }
+    while (iters >= B) {
+      CGX_HIP(hipGraphLaunch(d->gexec, d->st));
+      iters -= B;
+    }
+  }
+  return run_phases_eager(g, init, iters);
 }
 
 int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
@@ -846,11 +654,10 @@ int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
     if (hist_cap > d->hist_alloc) {
       if (d->gexec) {  // the captured graph holds the old history pointer
         CGX_HIP(hipStreamSynchronize(d->st));
-        (void)hipGraphExecDestroy(d->gexec);
-        d->gexec = nullptr;
+        drop_graph(d);
       }
-      dfree(&d->d_hist);
-      int rc = dalloc(d, &d->d_hist, (size_t)hist_cap * 8);
+      dev_free(&d->d_hist);
+      int rc = dev_alloc(&d->d_hist, (size_t)hist_cap * 8, nullptr);
       if (rc) return rc;
       d->hist_alloc = hist_cap;
     }
@@ -859,8 +666,7 @@ int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
     d->h_st->use_tol = tol > 0.0 ? 1 : 0;
     d->h_st->max_iter = maxit;
     d->h_st->hist_cap = std::min(hist_cap, d->hist_alloc);
-    CGX_HIP(hipMemcpyAsync(d->d_st, d->h_st, sizeof(CgState),
-                           hipMemcpyHostToDevice, d->st));
+    CGX_HIP(hipMemcpyAsync(d->d_st, d->h_st, sizeof(CgState), hipMemcpyHostToDevice, d->st));
   }
   return 0;
 }
@@ -868,8 +674,7 @@ int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
 int read_states(Group *g) {
   for (cgx_dist *d : g->parts) {
     CGX_HIP(hipSetDevice(d->device));
-    CGX_HIP(hipMemcpyAsync(d->h_st, d->d_st, sizeof(CgState),
-                           hipMemcpyDeviceToHost, d->st));
+    CGX_HIP(hipMemcpyAsync(d->h_st, d->d_st, sizeof(CgState), hipMemcpyDeviceToHost, d->st));
   }
   for (cgx_dist *d : g->parts) CGX_HIP(hipStreamSynchronize(d->st));
   return 0;
@@ -892,7 +697,7 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
     if ((rc = run_phases(g, false, total))) return rc;
     if ((rc = read_states(g))) return rc;
   } else {
-    long long done = 0, batch = 8;
+    long long done = 0, batch = 16;
     for (;;) {
       const long long b = std::min(batch, total - done);
       if ((rc = run_phases(g, false, b))) return rc;
@@ -928,8 +733,7 @@ int group_bench_prepare(Group *g, int warmup) {
   return 0;
 }
 
-int group_bench_run(Group *g, int iters, int flags, double *ms,
-                    double *spmv_ms) {
+int group_bench_run(Group *g, int iters, int flags, double *ms, double *spmv_ms) {
   for (cgx_dist *d : g->parts)
     if (!d->bench_ready) return CGX_EINVAL;
   cgx_dist *d0 = g->parts[0];
@@ -944,6 +748,8 @@ int group_bench_run(Group *g, int iters, int flags, double *ms,
     d0->ev_i = 0;
     d0->rec_spmv = true;
   }
+  const bool graph_saved = d0->use_graph;
+  d0->use_graph = graph_saved && (flags & CGX_BENCH_GRAPH) != 0;
   hipEvent_t e0, e1;
   CGX_HIP(hipSetDevice(d0->device));
   CGX_HIP(hipEventCreate(&e0));
@@ -951,6 +757,7 @@ int group_bench_run(Group *g, int iters, int flags, double *ms,
   CGX_HIP(hipEventRecord(e0, d0->st));
   int rc = run_phases(g, false, iters);
   d0->rec_spmv = false;
+  d0->use_graph = graph_saved;
   if (rc) return rc;
   for (cgx_dist *d : g->parts)
     if (d != d0) {
@@ -996,6 +803,7 @@ void destroy_one(cgx_dist *d) {
   for (hipEvent_t e : d->spmv_ev) (void)hipEventDestroy(e);
   if (d->d_st) (void)hipFree(d->d_st);
   if (d->d_sums) (void)hipFree(d->d_sums);
+  if (d->d_tick) (void)hipFree(d->d_tick);
   if (d->h_st) (void)hipHostFree(d->h_st);
   if (d->st) (void)hipStreamDestroy(d->st);
   if (d->st_comm) (void)hipStreamDestroy(d->st_comm);
@@ -1016,8 +824,8 @@ int cgx_dist_unique_id(unsigned char id[128]) {
   return 0;
 }
 
-int cgx_dist_create(int device, int nranks, int rank,
-                    const unsigned char id[128], cgx_dist **out) {
+int cgx_dist_create(int device, int nranks, int rank, const unsigned char id[128],
+                    cgx_dist **out) {
   if (!out || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !id)) {
     set_error("cgx_dist_create: bad arguments");
     return CGX_EINVAL;
@@ -1036,8 +844,7 @@ int cgx_dist_create(int device, int nranks, int rank,
     memcpy(u.internal, id, sizeof u.internal);
     ncclResult_t r = ncclCommInitRank(&d->comm, nranks, u, rank);
     if (r != ncclSuccess) {
-      set_error("ncclCommInitRank(%d of %d) failed: %s", rank, nranks,
-                ncclGetErrorString(r));
+      set_error("ncclCommInitRank(%d of %d) failed: %s", rank, nranks, ncclGetErrorString(r));
       destroy_one(d);
       return CGX_ECOMM;
     }
@@ -1088,9 +895,22 @@ void cgx_dist_destroy(cgx_dist *d) {
   delete g;
 }
 
-int cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
-                        const int *row_ptr, const int *col_global,
-                        const double *val) {
+int cgx_dist_set_layout(cgx_dist *d, int layout) {
+  if (!d || layout < CGX_LAYOUT_AUTO || layout > CGX_LAYOUT_VI) return CGX_EINVAL;
+  d->want_layout = layout;
+  return 0;
+}
+
+int cgx_dist_set_graph(cgx_dist *d, int on) {
+  if (!d) return CGX_EINVAL;
+  d->use_graph = on != 0;
+  d->graph_state = 0;  // (re)try a capture at the next run
+  drop_graph(d);
+  return 0;
+}
+
+int cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz, const int *row_ptr,
+                        const int *col_global, const double *val) {
   if (!d) return CGX_EINVAL;
   return upload_local(d, n_global, n_loc, nnz, row_ptr, col_global, val);
 }
@@ -1098,8 +918,7 @@ int cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
 int cgx_dist_set_rhs(cgx_dist *d, const double *b_local) {
   if (!d || !d->have_matrix || (d->n_loc > 0 && !b_local)) return CGX_EINVAL;
   CGX_HIP(hipSetDevice(d->device));
-  if (d->n_loc)
-    CGX_HIP(hipMemcpy(d->d_b, b_local, (size_t)d->n_loc * 8, hipMemcpyHostToDevice));
+  if (d->n_loc) CGX_HIP(hipMemcpy(d->d_b, b_local, (size_t)d->n_loc * 8, hipMemcpyHostToDevice));
   d->have_rhs = true;
   return 0;
 }
@@ -1115,8 +934,7 @@ int cgx_dist_run(cgx_dist *d, int maxit, double tol, int *iters) {
 int cgx_dist_get_x(cgx_dist *d, double *x_local) {
   if (!d || !d->have_matrix || (d->n_loc > 0 && !x_local)) return CGX_EINVAL;
   CGX_HIP(hipSetDevice(d->device));
-  if (d->n_loc)
-    CGX_HIP(hipMemcpy(x_local, d->d_x, (size_t)d->n_loc * 8, hipMemcpyDeviceToHost));
+  if (d->n_loc) CGX_HIP(hipMemcpy(x_local, d->d_x, (size_t)d->n_loc * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1134,10 +952,8 @@ int cgx_dist_bench_prepare(cgx_dist *d, int warmup) {
   return group_bench_prepare(d->group, warmup);
 }
 
-int cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms,
-                       double *spmv_ms) {
-  if (!d || iters < 1 || !total_ms || !spmv_ms || (d->local && !d->owns_group))
-    return CGX_EINVAL;
+int cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms, double *spmv_ms) {
+  if (!d || iters < 1 || !total_ms || !spmv_ms || (d->local && !d->owns_group)) return CGX_EINVAL;
   return group_bench_run(d->group, iters, flags, total_ms, spmv_ms);
 }
 
@@ -1147,8 +963,7 @@ int cgx_dist_set_alg(cgx_dist *d, int alg) {
   for (cgx_dist *o : d->group->parts) {
     if (o->alg != alg && o->gexec) {  // a captured graph holds the other recurrence
       (void)hipStreamSynchronize(o->st);
-      (void)hipGraphExecDestroy(o->gexec);
-      o->gexec = nullptr;
+      drop_graph(o);
     }
     o->alg = alg;
     o->bench_ready = false;
@@ -1158,27 +973,24 @@ int cgx_dist_set_alg(cgx_dist *d, int alg) {
 
 int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   if (!d || !s) return CGX_EINVAL;
+  memset(s, 0, sizeof *s);
   s->n_global = d->n_global;
   s->row_begin = d->row_begin;
   s->n_loc = d->n_loc;
   s->n_ghost = d->n_ghost;
   s->n_send = d->n_send;
   s->nnz = d->nnz;
-  s->interior_blocks = d->n_int;
-  s->boundary_blocks = d->n_bnd;
+  s->interior_items = d->it_int.count;
+  s->boundary_items = d->it_bnd.count;
   s->spmv_bytes = (double)d->nnz * 12.0 + 4.0 * (d->n_loc + 1) + 16.0 * d->n_loc;
   s->iter_bytes = s->spmv_bytes + 72.0 * d->n_loc;
   s->halo_bytes = 8.0 * (d->n_ghost + d->n_send);
-  s->device_bytes = d->dev_bytes;
-  s->spmv_iter_bytes = d->ndict > 0 ? (double)d->nnz * (8.0 + d->code_bits / 8.0) +
-                                          (d->d_rlen ? 1.0 * d->n_loc : 4.0 * (d->n_loc + 1)) +
-                                          16.0 * d->n_loc + 4.0 * d->ndict
-                                    : s->spmv_bytes;
-  if (d->ndict > 0 && d->vi)  // value-indexed pairs: no val stream
-    s->spmv_iter_bytes = (double)d->nnz * (d->code_bits / 8.0) + 1.0 * d->n_loc +
-                         16.0 * d->n_loc + 12.0 * d->ndict;
-  s->n_dict = d->ndict;
-  s->dict_vals = d->ndict > 0 && d->vi;
+  s->device_bytes = d->A.dev_bytes + d->vec_bytes;
+  s->spmv_iter_bytes = d->have_matrix ? d->A.layout_bytes() : 0.0;
+  s->layout = d->have_matrix ? cgx::public_layout(d->A) : CGX_LAYOUT_AUTO;
+  s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_VI ? d->A.npair : 0;
+  s->graph = d->graph_state;
+  s->alg = d->alg;
   return 0;
 }
 

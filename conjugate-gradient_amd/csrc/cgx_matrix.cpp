@@ -1,0 +1,703 @@
+// cgx_matrix.cpp -- DevMatrix (cgx_matrix.h): layout choice, encoding and
+// upload of a CSR matrix, and the SpMV launch over its layout.
+#include "cgx_matrix.h"
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+namespace cgx {
+
+namespace {
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+int host_threads(long long work) {
+  int nt = (int)std::min<long long>(16, std::max<long long>(1, work >> 21));
+  return std::max(1, std::min(nt, (int)std::thread::hardware_concurrency()));
+}
+
+// Runs f(t, lo, hi) over [0, n) split into contiguous ranges on up to 16
+// host threads.
+template <typename F>
+void parallel_rows(long long n, long long work, F f) {
+  const int nt = host_threads(work);
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(f, t, n * t / nt, n * (t + 1) / nt);
+  f(0, 0, n / nt);
+  for (auto &x : th) x.join();
+}
+
+template <typename T>
+unsigned long long bits_of(T v) {
+  unsigned long long b = 0;
+  memcpy(&b, &v, sizeof v);
+  return b;
+}
+
+// Small open-addressing set of (offset, value bits) keys; gives up past cap.
+struct PairSet {
+  static constexpr int kSlots = 1024;
+  int off[kSlots];
+  unsigned long long vb[kSlots];
+  bool used[kSlots];
+  int count = 0;
+  PairSet() { memset(used, 0, sizeof used); }
+  static unsigned hash(int o, unsigned long long b) {
+    const unsigned long long h = ((unsigned long long)(unsigned)o * 0x9e3779b97f4a7c15ULL) ^
+                                 (b * 0xbf58476d1ce4e5b9ULL);
+    return (unsigned)(h >> 54);  // 10 bits
+  }
+  // false when the set is full (more than cap distinct keys)
+  bool add(int o, unsigned long long b, int cap) {
+    unsigned h = hash(o, b);
+    while (used[h]) {
+      if (off[h] == o && vb[h] == b) return true;
+      h = (h + 1) & (kSlots - 1);
+    }
+    if (count >= cap) return false;
+    used[h] = true;
+    off[h] = o;
+    vb[h] = b;
+    ++count;
+    return true;
+  }
+};
+
+// Distinct (col - row, value bits) pairs of rows [lo, hi) -- with_vals false:
+// offsets only (vb = 0).  Returns false past cap distinct keys.
+template <typename T>
+bool scan_pairs(const int *rp, const int *col, const T *val, long long lo, long long hi,
+                long long step, bool with_vals, int cap, PairSet &S) {
+  for (long long r = lo; r < hi; r += step)
+    for (int k = rp[r]; k < rp[r + 1]; ++k)
+      if (!S.add(col[k] - (int)r, with_vals ? bits_of(val[k]) : 0ULL, cap)) return false;
+  return true;
+}
+
+// Candidate keys: sampled rows (sample) or every row, on host threads; the
+// merged set sorted by offset, then value bits (as unsigned).  Empty when
+// more than cap distinct keys were found.
+template <typename T>
+bool find_pairs(int n, const int *rp, const int *col, const T *val, bool with_vals, int cap,
+                bool sample, std::vector<int> &off, std::vector<T> &pv) {
+  off.clear();
+  pv.clear();
+  std::vector<PairSet> sets;
+  std::vector<int> ok;
+  if (sample) {
+    // ~64 K rows: every step-th row plus the first and last 4096 rows
+    sets.resize(1);
+    ok.assign(1, 1);
+    const long long step = std::max<long long>(1, n / 65536);
+    PairSet &S = sets[0];
+    ok[0] = scan_pairs(rp, col, val, 0, std::min(n, 4096), 1, with_vals, cap, S) &&
+            scan_pairs(rp, col, val, 0, n, step, with_vals, cap, S) &&
+            scan_pairs(rp, col, val, std::max(0, n - 4096), n, 1, with_vals, cap, S);
+  } else {
+    const int nt = host_threads(rp[n]);
+    sets.resize(nt);
+    ok.assign(nt, 1);
+    parallel_rows(n, rp[n], [&](int t, long long lo, long long hi) {
+      ok[t] = scan_pairs(rp, col, val, lo, hi, 1, with_vals, cap, sets[t]);
+    });
+  }
+  PairSet all;
+  for (size_t t = 0; t < sets.size(); ++t) {
+    if (!ok[t]) return false;
+    for (int h = 0; h < PairSet::kSlots; ++h)
+      if (sets[t].used[h] && !all.add(sets[t].off[h], sets[t].vb[h], cap)) return false;
+  }
+  std::vector<std::pair<int, unsigned long long>> keys;
+  for (int h = 0; h < PairSet::kSlots; ++h)
+    if (all.used[h]) keys.push_back({all.off[h], all.vb[h]});
+  std::sort(keys.begin(), keys.end());
+  for (auto &k : keys) {
+    off.push_back(k.first);
+    T v{};
+    memcpy(&v, &k.second, sizeof v);
+    pv.push_back(v);
+  }
+  return !keys.empty();
+}
+
+// Column panels for matrices whose gathers have no locality (SURVEY.md C5:
+// random SPD).  x is read through per-XCD L2s of 4 MiB; when x is larger and
+// most entries lie far from the diagonal, every gather is a line fetched
+// from the Infinity Cache.  Splitting the columns into panels whose x slice
+// fits an L2 and running one SpMV pass per panel keeps the gathers
+// L2-resident, for P row_ptr reads and P-1 y round trips more.  Auto: x >
+// 8 MiB and >= 30 % of (sampled) entries more than a panel width (2 MiB of
+// x) from the diagonal.
+int choose_panels(int n, const int *rp, const int *col, size_t tsize, bool force) {
+  const long long pcols = std::max<long long>(1024, 2048LL * 1024 / (long long)tsize);
+  if (n <= pcols) return 1;
+  if (!force) {
+    if ((double)n * (double)tsize <= 8.0 * 1024 * 1024) return 1;
+    long long far = 0, tot = 0;
+    for (int i = 0; i < n; i += 61)
+      for (int k = rp[i]; k < rp[i + 1]; ++k) {
+        ++tot;
+        far += std::llabs((long long)col[k] - i) > pcols;
+      }
+    if (far * 10 < tot * 3) return 1;
+  }
+  return (int)std::min<long long>(64, (n + pcols - 1) / pcols);
+}
+
+// Panel-major CSR: panel q holds, for every row, the row's entries with
+// column in [q*pc, (q+1)*pc), in the row's order; prp[q*(n+1) + i] are
+// offsets into the concatenated col/val.  The entries of a row ascend in
+// column, so summing panel after panel is the reference's sequential order.
+template <typename T>
+void build_panels(int n, int ncols, const int *rp, const int *col, const T *val, int P,
+                  std::vector<int> &prp, std::vector<int> &pcol, std::vector<T> &pval) {
+  const int nnz = rp[n];
+  const long long pc = ((long long)ncols + P - 1) / P;
+  std::vector<long long> base((size_t)P + 1, 0);
+  for (int k = 0; k < nnz; ++k) base[(size_t)(col[k] / pc) + 1]++;
+  for (int q = 0; q < P; ++q) base[q + 1] += base[q];
+  prp.assign((size_t)P * ((size_t)n + 1), 0);
+  std::vector<int> cnt((size_t)P);
+  for (int q = 0; q < P; ++q) prp[(size_t)q * (n + 1)] = (int)base[q];
+  for (int i = 0; i < n; ++i) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int k = rp[i]; k < rp[i + 1]; ++k) cnt[(size_t)(col[k] / pc)]++;
+    for (int q = 0; q < P; ++q) {
+      const size_t o = (size_t)q * (n + 1) + i;
+      prp[o + 1] = prp[o] + cnt[q];
+    }
+  }
+  pcol.resize((size_t)nnz);
+  pval.resize((size_t)nnz);
+  std::vector<int> cur((size_t)P);
+  for (int i = 0; i < n; ++i) {
+    for (int q = 0; q < P; ++q) cur[q] = prp[(size_t)q * (n + 1) + i];
+    for (int k = rp[i]; k < rp[i + 1]; ++k) {
+      const int q = (int)(col[k] / pc);
+      pcol[(size_t)cur[q]] = col[k];
+      pval[(size_t)cur[q]++] = val[k];
+    }
+  }
+}
+
+// CSR-VI slice widths: the widest row of each 512-row slice in dwords (4
+// codes each), rounded to 1, 2 or a multiple of 4; dword offsets 16-B
+// aligned.  False when the padded codes would exceed 2x the compact bytes
+// (nnz + n) -- irregular row lengths, where CSR-DC's compact codes win.
+bool plan_slices(int n, const int *rp, std::vector<int2> &sd, int &wdmax, double &bytes) {
+  const int ns = (n + kViSliceRows - 1) / kViSliceRows;
+  sd.resize((size_t)ns + 1);
+  long long off = 0;
+  wdmax = 0;
+  for (int s = 0; s < ns; ++s) {
+    const int r0 = s * kViSliceRows, r1 = std::min(n, r0 + kViSliceRows);
+    int m = 0;
+    for (int r = r0; r < r1; ++r) m = std::max(m, rp[r + 1] - rp[r]);
+    int wd = (m + 3) / 4;
+    if (wd == 0) wd = 1;
+    if (wd == 3) wd = 4;
+    if (wd > 4) wd = (wd + 3) / 4 * 4;
+    sd[(size_t)s] = make_int2((int)off, wd);
+    off += (long long)wd * kViSliceRows;
+    off = (off + 3) & ~3LL;
+    wdmax = std::max(wdmax, wd);
+    if (off > INT32_MAX) return false;
+  }
+  sd[(size_t)ns] = make_int2((int)off, 0);
+  bytes = 4.0 * (double)off;
+  const double compact = (double)rp[n] + (double)n;
+  return bytes <= 2.0 * compact + 4096.0;
+}
+
+// L2 tiling of the item order for a wide stencil: the x lines a row needs sit
+// at its offsets; with P = the largest |offset| (a 3-D stencil's plane), an
+// XCD sweeping rows in order needs ~3 P x-values resident to hit its 4 MiB
+// L2 on every re-read.  When that exceeds the budget, sweep the rows in T
+// bands of the P-periodic position instead (all planes of band 0, then band
+// 1, ...): ~3 P / T values in flight.  Only the order of the work items
+// changes -- each row's sum is the same.
+std::vector<int> tile_order(const std::vector<int> &item_row, long long P, size_t tsize,
+                            int &bands) {
+  bands = 0;
+  const long long budget = 1536LL * 1024;
+  const long long need = 3 * P * (long long)tsize;
+  const int ni = (int)item_row.size() - 1;
+  if (P <= 0 || need <= budget || ni <= 0) return {};
+  const long long T_ = (need + budget - 1) / budget;
+  std::vector<int> order((size_t)ni);
+  for (int b = 0; b < ni; ++b) order[(size_t)b] = b;
+  auto band = [&](int b) { return (long long)item_row[(size_t)b] % P * T_ / P; };
+  auto plane = [&](int b) { return (long long)item_row[(size_t)b] / P; };
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+    const long long bx = band(x), by = band(y);
+    return bx != by ? bx < by : plane(x) < plane(y);
+  });
+  bands = (int)T_;
+  return order;
+}
+
+}  // namespace
+
+std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap) {
+  std::vector<int> blk;
+  blk.reserve((size_t)n / 48 + 2);
+  blk.push_back(0);
+  int r = 0;
+  while (r < n) {
+    const int start = r;
+    const int k0 = rp[r];
+    if (rp[r + 1] - k0 > cap) {  // long row: a block of its own
+      blk.push_back(++r);
+      continue;
+    }
+    while (r < n && r - start < rows && rp[r + 1] - k0 <= cap) ++r;
+    blk.push_back(r);
+  }
+  return blk;
+}
+
+std::vector<int> lap_offsets(const LapSpec &g) {
+  std::vector<int> d{0};
+  const int pl = g.nx * g.ny;
+  if (g.nx > 1) d.insert(d.end(), {-1, 1});
+  if (g.ny > 1) d.insert(d.end(), {-g.nx, g.nx});
+  if (g.dim == 3 && g.nz > 1) d.insert(d.end(), {-pl, pl});
+  std::sort(d.begin(), d.end());
+  d.erase(std::unique(d.begin(), d.end()), d.end());
+  return d;
+}
+
+void DevMatrix::release() {
+  dev_free(&d_rp);
+  dev_free(&d_col);
+  dev_free(&d_val);
+  dev_free(&d_blkrk);
+  dev_free(&d_code);
+  dev_free(&d_rlen);
+  dev_free(&d_dict);
+  dev_free(&d_vcode);
+  dev_free(&d_sdesc);
+  dev_free(&d_vdict);
+  dev_free(&d_vval);
+  dev_free(&d_order);
+  order.clear();
+  blk_row.clear();
+  panel_first.clear();
+  panel_count.clear();
+  n = nnz = ncols = nblk = ndict = npair = nslice = wdmax = tile_bands = 0;
+  npanel = 1;
+  layout = L_CSR;
+  nt = false;
+  dev_bytes = 0;
+  vcode_bytes = 0;
+  encode_fallback = 0;
+  setup_host_ms = setup_dev_ms = 0;
+}
+
+int DevMatrix::set_stencil(const LapSpec &g) {
+  release();
+  const long long nn = (long long)g.nx * g.ny * g.nz;
+  if ((g.dim != 2 && g.dim != 3) || g.nx < 1 || g.ny < 1 || g.nz < 1 ||
+      (g.dim == 2 && g.nz != 1) || nn > INT32_MAX || lap_rp(nn, g) > INT32_MAX) {
+    set_error("set_stencil: bad grid");
+    return CGX_EINVAL;
+  }
+  dtype = CGX_F64;
+  n = ncols = (int)nn;
+  nnz = (int)lap_rp(nn, g);
+  layout = L_STENCIL;
+  lap = g;
+  nt = 16.0 * n + 40.0 * n > kMallBytes;
+  return 0;
+}
+
+template <typename T>
+int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *col, const T *val,
+                      int want, bool allow_panels, const LapSpec *gen) {
+  const double t0 = now_ms();
+  if (n_ < 0 || nnz_ < 0 || ncols_ < n_ ||
+      (n_ > 0 && (!rp || (nnz_ > 0 && !gen && (!col || !val))))) {
+    set_error("set_matrix: invalid arguments");
+    return CGX_EINVAL;
+  }
+  if (n_ > 0 && (rp[0] != 0 || rp[n_] != nnz_)) {
+    set_error("set_matrix: row_ptr[0] must be 0 and row_ptr[n] == nnz");
+    return CGX_EINVAL;
+  }
+  // row_ptr non-decreasing and columns inside x: a bad index would be an
+  // out-of-bounds gather on the device, so it is rejected here
+  for (int r = 0; r < n_; ++r)
+    if (rp[r + 1] < rp[r]) {
+      set_error("set_matrix: row_ptr decreases at row %d", r);
+      return CGX_EINVAL;
+    }
+  if (!gen && nnz_ > 0) {
+    std::vector<int> bad((size_t)host_threads(nnz_), 0);
+    parallel_rows(nnz_, nnz_, [&](int t, long long lo, long long hi) {
+      for (long long k = lo; k < hi; ++k)
+        if ((unsigned)col[k] >= (unsigned)ncols_) {
+          bad[t] = 1;
+          return;
+        }
+    });
+    for (int b : bad)
+      if (b) {
+        set_error("set_matrix: a column index is outside [0, %d)", ncols_);
+        return CGX_EINVAL;
+      }
+  }
+  release();
+  dtype = sizeof(T) == 4 ? CGX_F32 : CGX_F64;
+  n = n_;
+  ncols = ncols_;
+  nnz = nnz_;
+  const size_t ts = sizeof(T);
+  const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
+  int rc;
+
+  // ---- which layout: candidates from a sample (or the generator's stencil)
+  const bool want_vi = want == CGX_LAYOUT_AUTO || want == CGX_LAYOUT_VI;
+  const bool want_dc = want_vi || want == CGX_LAYOUT_DC;
+  std::vector<int> poff;  // VI pair offsets / DC offsets, sorted
+  std::vector<T> pval;
+  std::vector<int2> sd;
+  int maxlen = 0;
+  for (int r = 0; r < n; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
+  bool vi_ok = false, dc_ok = false;
+  if (n > 0 && nnz > 0 && want_vi) {
+    int wdm = 0;
+    double vb = 0;
+    if (plan_slices(n, rp, sd, wdm, vb)) {
+      if (gen) {  // one value per offset: 2 dim on the diagonal, -1 off it
+        poff = lap_offsets(*gen);
+        for (int o : poff) pval.push_back(o == 0 ? T(2 * gen->dim) : T(-1));
+        vi_ok = true;
+      } else {
+        vi_ok = find_pairs(n, rp, col, val, true, 255, true, poff, pval);
+      }
+      wdmax = wdm;
+      vcode_bytes = vb;
+    }
+  }
+  std::vector<int> doff;
+  if (!vi_ok && n > 0 && nnz > 0 && want_dc && maxlen <= 255) {
+    std::vector<T> dummy;
+    if (gen) {
+      doff = lap_offsets(*gen);
+      dc_ok = true;
+    } else {
+      dc_ok = find_pairs(n, rp, col, val, false, 256, true, doff, dummy);
+    }
+  }
+
+  // ---- CSR arrays (panels for irregular fp matrices on one GPU)
+  std::vector<int> prp, pcol;
+  std::vector<T> pval_panel;
+  const bool want_panel = want == CGX_LAYOUT_PANEL;
+  npanel = 1;
+  if (!vi_ok && !dc_ok && !gen && n > 0 && nnz > 0 && allow_panels &&
+      (want == CGX_LAYOUT_AUTO || want_panel))
+    npanel = choose_panels(n, rp, col, ts, want_panel);
+  if (npanel > 1) {
+    build_panels<T>(n, ncols, rp, col, val, npanel, prp, pcol, pval_panel);
+  }
+  const int *urp = npanel > 1 ? prp.data() : rp;
+  const int *ucol = npanel > 1 ? pcol.data() : col;
+  const T *uval = npanel > 1 ? pval_panel.data() : val;
+  const size_t rp_len = (size_t)npanel * ((size_t)n + 1);
+  if ((rc = dev_alloc(&d_rp, rp_len * 4 + 256, &dev_bytes)) ||
+      (rc = dev_alloc(&d_col, nnz_pad * 4, &dev_bytes)) ||
+      (rc = dev_alloc(&d_val, nnz_pad * ts, &dev_bytes))) {
+    release();
+    return rc;
+  }
+  CGX_HIP(hipMemsetAsync(d_col + nnz, 0, (nnz_pad - nnz) * 4, st));
+  CGX_HIP(hipMemsetAsync((char *)d_val + (size_t)nnz * ts, 0, (nnz_pad - nnz) * ts, st));
+  if (n > 0) {
+    CGX_HIP(hipMemcpyAsync(d_rp, urp, rp_len * 4, hipMemcpyHostToDevice, st));
+    if (nnz > 0 && gen) {
+      CGX_HIP(launch_gen_laplacian(*gen, n, d_col, (double *)d_val, st));
+    } else if (nnz > 0) {
+      CGX_HIP(hipMemcpyAsync(d_col, ucol, (size_t)nnz * 4, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d_val, uval, (size_t)nnz * ts, hipMemcpyHostToDevice, st));
+    }
+  }
+
+  int *d_err = nullptr;
+  CGX_HIP(hipMalloc((void **)&d_err, 16));
+  auto read_err = [&](int *out) -> int {
+    CGX_HIP(hipMemcpyAsync(out, d_err, 4, hipMemcpyDeviceToHost, st));
+    CGX_HIP(hipStreamSynchronize(st));
+    return 0;
+  };
+  auto fail = [&](int code) {
+    (void)hipFree(d_err);
+    release();
+    return code;
+  };
+
+  // ---- CSR-VI: device encode against the candidates, exact host scan on a miss
+  if (vi_ok) {
+    nslice = (int)sd.size() - 1;
+    const size_t words = (size_t)sd.back().x + 4;
+    if ((rc = dev_alloc(&d_vcode, words * 4, &dev_bytes)) ||
+        (rc = dev_alloc(&d_sdesc, sd.size() * sizeof(int2), &dev_bytes)) ||
+        (rc = dev_alloc(&d_vdict, 256 * 4, &dev_bytes)) ||
+        (rc = dev_alloc(&d_vval, 256 * ts, &dev_bytes)))
+      return fail(rc);
+    CGX_HIP(hipMemcpyAsync(d_sdesc, sd.data(), sd.size() * sizeof(int2), hipMemcpyHostToDevice, st));
+    for (int attempt = 0; attempt < 2 && vi_ok; ++attempt) {
+      std::vector<int> po = poff;
+      std::vector<T> pv = pval;
+      po.resize(256, 0);
+      pv.resize(256, T(0));
+      CGX_HIP(hipMemcpyAsync(d_vdict, po.data(), 256 * 4, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d_vval, pv.data(), 256 * ts, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+      CGX_HIP(launch_vi_encode<T>(n, d_rp, d_col, (const T *)d_val, d_sdesc, d_vdict,
+                                  (const T *)d_vval, (int)poff.size(), d_vcode, d_err, st));
+      int err = 0;
+      if ((rc = read_err(&err))) return fail(rc);
+      if (!err) break;
+      if (attempt == 0 && !gen) {  // the sample missed a pair: exact scan
+        encode_fallback = 1;
+        vi_ok = find_pairs(n, rp, col, val, true, 255, false, poff, pval);
+      } else {
+        vi_ok = false;
+      }
+    }
+    if (vi_ok) {
+      npair = (int)poff.size();
+      layout = L_VI;
+    } else {
+      dev_free(&d_vcode);
+      dev_free(&d_sdesc);
+      dev_free(&d_vdict);
+      dev_free(&d_vval);
+      nslice = 0;
+      if (want_dc && maxlen <= 255 && !dc_ok) {
+        std::vector<T> dummy;
+        if (gen) {
+          doff = lap_offsets(*gen);
+          dc_ok = true;
+        } else {
+          dc_ok = find_pairs(n, rp, col, val, false, 256, true, doff, dummy);
+        }
+      }
+    }
+  }
+
+  // ---- row blocks (CSR / DC)
+  if (layout != L_VI) {
+    capw = ts == 4 ? 1024 : 512;
+    if (ts == 8 && npanel == 1 && n > 0) {
+      // LDS window sized to the matrix: 328 entries when every 64-row block
+      // fits (5-point stencils, C2: one more workgroup per CU)
+      int m = 0;
+      for (int r = 0; r < n; r += 64) m = std::max(m, rp[std::min(r + 64, n)] - rp[r]);
+      if (m + kPad <= 328) capw = 328;
+    }
+    std::vector<int> blkrk;
+    blk_row.clear();
+    panel_first.clear();
+    panel_count.clear();
+    for (int q = 0; q < npanel; ++q) {
+      const int *rq = urp + (size_t)q * (n + 1);
+      std::vector<int> b = n > 0 ? plan_rowblocks(n, rq, 64, capw - kPad) : std::vector<int>{0};
+      panel_first.push_back((int)(blkrk.size() / 2));
+      panel_count.push_back((int)b.size() - 1);
+      for (size_t i = 0; i < b.size(); ++i) {
+        blkrk.push_back(b[i]);
+        blkrk.push_back(rq[b[i]]);
+      }
+      if (q == 0) blk_row = b;
+    }
+    nblk = panel_count.empty() ? 0 : panel_count[0];
+    if ((rc = dev_alloc(&d_blkrk, blkrk.size() * 4 + 16, &dev_bytes))) return fail(rc);
+    CGX_HIP(hipMemcpyAsync(d_blkrk, blkrk.data(), blkrk.size() * 4, hipMemcpyHostToDevice, st));
+    CGX_HIP(hipStreamSynchronize(st));  // blkrk goes out of scope
+  }
+
+  // ---- CSR-DC
+  if (layout != L_VI && dc_ok && npanel == 1) {
+    if ((rc = dev_alloc(&d_code, nnz_pad, &dev_bytes)) ||
+        (rc = dev_alloc(&d_dict, 256 * 4, &dev_bytes)) ||
+        (rc = dev_alloc(&d_rlen, (size_t)n + 64, &dev_bytes)))
+      return fail(rc);
+    std::vector<unsigned char> rl((size_t)n);
+    for (int r = 0; r < n; ++r) rl[(size_t)r] = (unsigned char)(rp[r + 1] - rp[r]);
+    CGX_HIP(hipMemcpyAsync(d_rlen, rl.data(), (size_t)n, hipMemcpyHostToDevice, st));
+    CGX_HIP(hipMemsetAsync(d_code, 0, nnz_pad, st));
+    for (int attempt = 0; attempt < 2 && dc_ok; ++attempt) {
+      std::vector<int> dd = doff;
+      dd.resize(256, 0);
+      CGX_HIP(hipMemcpyAsync(d_dict, dd.data(), 256 * 4, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemsetAsync(d_err, 0, 4, st));
+      CGX_HIP(launch_dc_encode(n, d_rp, d_col, d_dict, (int)doff.size(), d_code, d_err, st));
+      int err = 0;
+      if ((rc = read_err(&err))) return fail(rc);
+      if (!err) break;
+      if (attempt == 0 && !gen) {
+        encode_fallback = 1;
+        std::vector<T> dummy;
+        dc_ok = find_pairs(n, rp, col, val, false, 256, false, doff, dummy);
+      } else {
+        dc_ok = false;
+      }
+    }
+    CGX_HIP(hipStreamSynchronize(st));  // rl goes out of scope
+    if (dc_ok) {
+      ndict = (int)doff.size();
+      layout = L_DC;
+    } else {
+      dev_free(&d_code);
+      dev_free(&d_dict);
+      dev_free(&d_rlen);
+    }
+  }
+  (void)hipFree(d_err);
+
+  // ---- L2-tiled item order for wide stencils (DC / VI)
+  if (layout == L_DC || layout == L_VI) {
+    long long P = 0;
+    for (int v : (layout == L_VI ? poff : doff)) P = std::max(P, (long long)std::abs(v));
+    const std::vector<int> ir = item_rows();
+    order = tile_order(ir, P, ts, tile_bands);
+    if (!order.empty()) {
+      if ((rc = dev_alloc(&d_order, order.size() * 4, &dev_bytes))) {
+        release();
+        return rc;
+      }
+      CGX_HIP(hipMemcpyAsync(d_order, order.data(), order.size() * 4, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipStreamSynchronize(st));
+    }
+  }
+  // the matrix stream and y bypass the caches when the iteration's working
+  // set (this layout's stream + five vectors) cannot stay in the 256 MiB
+  // Infinity Cache anyway: the vectors then keep what residency there is
+  nt = layout_bytes() + 5.0 * ts * n > kMallBytes;
+  const double t1 = now_ms();
+  CGX_HIP(hipStreamSynchronize(st));
+  setup_dev_ms = now_ms() - t1;
+  setup_host_ms = t1 - t0;
+  return 0;
+}
+
+template int DevMatrix::upload<double>(int, int, int, const int *, const int *, const double *,
+                                       int, bool, const LapSpec *);
+template int DevMatrix::upload<float>(int, int, int, const int *, const int *, const float *,
+                                      int, bool, const LapSpec *);
+
+int DevMatrix::items() const {
+  switch (layout) {
+    case L_VI: return nslice;
+    case L_STENCIL: return (n + 255) / 256;
+    default: return nblk;
+  }
+}
+
+std::vector<int> DevMatrix::item_rows() const {
+  if (layout == L_CSR || layout == L_DC) return blk_row;
+  std::vector<int> r;
+  const int step = layout == L_VI ? kViSliceRows : 256;
+  for (int i = 0; i < n; i += step) r.push_back(i);
+  r.push_back(n);
+  return r;
+}
+
+double DevMatrix::csr_bytes() const {
+  const double sv = dtype == CGX_F32 ? 4.0 : 8.0;
+  return (double)nnz * (sv + 4) + 4.0 * (n + 1) + 2.0 * n * sv;
+}
+
+double DevMatrix::layout_bytes() const {
+  const double sv = dtype == CGX_F32 ? 4.0 : 8.0;
+  switch (layout) {
+    case L_VI: return vcode_bytes + 2.0 * n * sv + (4.0 + sv) * npair;
+    case L_DC: return (double)nnz * (sv + 1) + 1.0 * n + 2.0 * n * sv + 4.0 * ndict;
+    case L_STENCIL: return 2.0 * n * sv;
+    default:
+      if (npanel > 1)  // P row_ptrs, y written P times and read P - 1 times
+        return (double)nnz * (sv + 4) + 4.0 * npanel * (n + 1.0) + (double)n * sv * 2.0 * npanel;
+      return csr_bytes();
+  }
+}
+
+template <typename T>
+SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Items it) const {
+  SpmvArgs<T> a;
+  memset(&a, 0, sizeof a);
+  a.layout = layout;
+  a.x = x;
+  a.y = y;
+  a.part = part;
+  a.done = done;
+  a.nt = nt ? 1 : 0;
+  a.items = it;
+  a.blkrk = d_blkrk;
+  a.capw = capw;
+  a.rp = d_rp;
+  a.col = d_col;
+  a.val = (const T *)d_val;
+  a.code = d_code;
+  a.rlen = d_rlen;
+  a.dict = d_dict;
+  a.ndict_cap = ndict <= 64 ? 64 : 256;
+  a.vcode = d_vcode;
+  a.sdesc = d_sdesc;
+  a.vdict = d_vdict;
+  a.vval = (const T *)d_vval;
+  a.npair = npair;
+  a.wdmax = wdmax <= 4 ? wdmax : 0;
+  a.n = n;
+  a.lap = lap;
+  return a;
+}
+
+int DevMatrix::partials(Items it) const {
+  switch (layout) {
+    case L_VI: return it.count;
+    case L_STENCIL: return (n + 255) / 256;
+    default:
+      if (npanel > 1) return (panel_count.back() + 3) / 4;
+      return (it.count + 3) / 4;
+  }
+}
+
+template <typename T>
+hipError_t DevMatrix::spmv(const T *x, T *y, double *part, const int *done, Items it,
+                           hipStream_t s, int *nparts) const {
+  if (nparts) *nparts = partials(it);
+  if (layout == L_STENCIL) it = Items{nullptr, 0, (n + 255) / 256};
+  if (npanel <= 1) return launch_spmv<T>(args<T>(x, y, part, done, it), s);
+  for (int q = 0; q < npanel; ++q) {
+    SpmvArgs<T> a = args<T>(x, y, q + 1 == npanel ? part : nullptr, done,
+                            Items{nullptr, panel_first[q], panel_count[q]});
+    a.rp = d_rp + (size_t)q * ((size_t)n + 1);
+    a.yacc = q ? y : nullptr;
+    a.capw = capw;
+    const hipError_t e = launch_spmv<T>(a, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template SpmvArgs<double> DevMatrix::args<double>(const double *, double *, double *,
+                                                  const int *, Items) const;
+template SpmvArgs<float> DevMatrix::args<float>(const float *, float *, double *, const int *,
+                                                Items) const;
+template hipError_t DevMatrix::spmv<double>(const double *, double *, double *, const int *,
+                                            Items, hipStream_t, int *) const;
+template hipError_t DevMatrix::spmv<float>(const float *, float *, double *, const int *, Items,
+                                           hipStream_t, int *) const;
+
+}  // namespace cgx

@@ -1,0 +1,98 @@
+// cgx_matrix.h -- the device-resident sparse matrix shared by the single-GPU
+// solver, the partitioned (multi-GPU) solver and the op-level mv_mult:
+// layout choice, encoding, upload, and the SpMV launch.
+//
+// The C ABI takes the reference's CSR (mv_ops.h:17-23: int32 row_ptr and
+// col_indices, fp64 values; fp32 for SURVEY.md C5).  The CSR arrays always
+// stay resident; on top of them the matrix picks, once per upload, the
+// layout the SpMV streams (cgx_internal.h, Layout):
+//   auto: CSR-VI when the nonzeros use <= 255 distinct (col - row, value)
+//         pairs and the row widths are regular; else CSR-DC when they use
+//         <= 256 distinct offsets (rows <= 255 entries); else plain CSR,
+//         with column panels when the gathers have no locality (C5).
+// Candidates (pairs / offsets) come from a sample of rows on the host; the
+// device encoder then checks every nonzero against them, and a miss falls
+// back to an exact host scan -- so the setup of a 10 M-row stencil is one
+// pass over row_ptr on the host plus one device pass over col/val.
+#pragma once
+
+#include <vector>
+
+#include "cgx_internal.h"
+
+namespace cgx {
+
+struct DevMatrix {
+  int device = 0;
+  hipStream_t st = nullptr;  // setup stream (owner's)
+  int dtype = CGX_F64;
+  int n = 0, nnz = 0;
+  int ncols = 0;             // columns of x (n, or n_loc + ghosts when partitioned)
+  int layout = L_CSR;
+  bool nt = false;           // matrix stream + y store non-temporal
+  size_t dev_bytes = 0;
+  // CSR (always resident; panels: P row_ptrs back to back, panel-major col/val)
+  int *d_rp = nullptr, *d_col = nullptr;
+  void *d_val = nullptr;
+  // CSR / DC row blocks
+  int *d_blkrk = nullptr;
+  int nblk = 0, capw = 512;
+  std::vector<int> blk_row;  // host: first row of each block, nblk + 1 entries
+  int npanel = 1;
+  std::vector<int> panel_first, panel_count;
+  // DC
+  unsigned char *d_code = nullptr, *d_rlen = nullptr;
+  int *d_dict = nullptr;
+  int ndict = 0;
+  // VI
+  unsigned *d_vcode = nullptr;
+  int2 *d_sdesc = nullptr;
+  int *d_vdict = nullptr;
+  void *d_vval = nullptr;
+  int npair = 0, nslice = 0, wdmax = 0;
+  double vcode_bytes = 0;
+  // L2-tiled order of the work items (DC / VI, wide stencils; nullptr: natural)
+  int *d_order = nullptr;
+  std::vector<int> order;    // host copy of the tiled order (empty: natural)
+  int tile_bands = 0;
+  // stencil
+  LapSpec lap{};
+  // setup record
+  double setup_host_ms = 0, setup_dev_ms = 0;
+  int encode_fallback = 0;   // 1: a sampled candidate set missed, exact host scan used
+
+  // Host CSR -> device.  want: CGX_LAYOUT_* request (a layout that does not
+  // apply falls back along VI -> DC -> CSR).  ncols: columns of x (>= n for
+  // the partitioned solver's ghost tail).  gen: col/val generated on the
+  // device (rp is the host closed form).  allow_panels: single-GPU only.
+  template <typename T>
+  int upload(int n, int ncols, int nnz, const int *rp, const int *col, const T *val, int want,
+             bool allow_panels, const LapSpec *gen = nullptr);
+  int set_stencil(const LapSpec &g);
+  void release();
+
+  int items() const;  // work items of the layout (blocks or slices)
+  // host: first row of each item, items() + 1 entries
+  std::vector<int> item_rows() const;
+  // algorithmic HBM bytes of one SpMV in the layout it runs on
+  double layout_bytes() const;
+  // CSR-basis algorithmic bytes (SURVEY.md 8d B_spmv)
+  double csr_bytes() const;
+
+  template <typename T>
+  SpmvArgs<T> args(const T *x, T *y, double *part, const int *done, Items it) const;
+  Items all_items() const { return Items{d_order, 0, items()}; }
+  // One SpMV (panels: one launch per panel, rows continuing their sums;
+  // the epilogue partials on the last panel).  Returns the partial count.
+  template <typename T>
+  hipError_t spmv(const T *x, T *y, double *part, const int *done, Items it, hipStream_t s,
+                  int *nparts = nullptr) const;
+  // The number of partials spmv() writes for the given items.
+  int partials(Items it) const;
+};
+
+// Row-block plan: consecutive rows, at most `rows` rows and `cap` nonzeros
+// per block; a row longer than `cap` gets a block of its own.
+std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap);
+
+}  // namespace cgx

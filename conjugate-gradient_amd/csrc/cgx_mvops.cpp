@@ -7,6 +7,14 @@
 // iteration runs on the GPU through a process-wide default context (device
 // CGX_DEVICE, default 0), serialised by a mutex.  There is no CPU fallback:
 // without a gfx950 device these calls fail (-2) and cgx_last_error() says why.
+//
+// Matrix residency: the reference's conj_grad calls mv_mult once per
+// iteration on the same A (cg.c:111 -> mv_ops.c:160-201).  The default
+// context keeps the last matrix on the device, keyed by the struct's
+// pointers and sizes plus a 64-bit hash of row_ptr, col_indices and values
+// (one threaded pass over host memory, a fraction of a PCIe upload), so a
+// caller linked at the op level uploads A once, not once per iteration --
+// and a caller that edits A in place between calls still gets its new A.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,6 +22,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "cgx_internal.h"
 
@@ -23,6 +33,15 @@ using namespace cgx;
 
 std::mutex g_mu;
 cgx_solver *g_solver = nullptr;  // for mv_mult / conj_grad / solve
+
+struct Resident {
+  const void *rp = nullptr, *col = nullptr, *val = nullptr;
+  int size = -1, nnz = -1;
+  unsigned long long hash = 0;
+  bool valid = false;
+};
+Resident g_res;
+long long g_uploads = 0, g_reuses = 0;
 
 struct OpsCtx {
   int device = -1;
@@ -57,23 +76,81 @@ int default_solver(cgx_solver **out) {
   return 0;
 }
 
+// 64-bit hash of a byte range: 4 independent multiply-xor lanes per thread
+// over 8-byte words, chunks on host threads, chunk hashes combined in order.
+unsigned long long hash_bytes(const void *p, size_t bytes) {
+  const unsigned char *b = (const unsigned char *)p;
+  const size_t words = bytes / 8;
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>(16, words >> 20));
+  std::vector<unsigned long long> part((size_t)nt);
+  auto work = [&](int t) {
+    const size_t lo = words * t / nt, hi = words * (t + 1) / nt;
+    unsigned long long h[4] = {0x9e3779b97f4a7c15ULL, 0xbf58476d1ce4e5b9ULL,
+                               0x94d049bb133111ebULL, 0x2545f4914f6cdd1dULL};
+    size_t i = lo;
+    for (; i + 4 <= hi; i += 4)
+      for (int l = 0; l < 4; ++l) {
+        unsigned long long w;
+        memcpy(&w, b + 8 * (i + l), 8);
+        h[l] = (h[l] ^ w) * 0x100000001b3ULL;
+      }
+    for (; i < hi; ++i) {
+      unsigned long long w;
+      memcpy(&w, b + 8 * i, 8);
+      h[0] = (h[0] ^ w) * 0x100000001b3ULL;
+    }
+    part[(size_t)t] = h[0] ^ (h[1] * 3) ^ (h[2] * 5) ^ (h[3] * 7);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+  unsigned long long h = 0xcbf29ce484222325ULL ^ bytes;
+  for (unsigned long long x : part) h = (h ^ x) * 0x100000001b3ULL;
+  for (size_t i = words * 8; i < bytes; ++i) h = (h ^ b[i]) * 0x100000001b3ULL;
+  return h;
+}
+
+unsigned long long matrix_hash(const struct __mv_sparse *A) {
+  const int n = A->size, nnz = A->row_ptr[n];
+  unsigned long long h = hash_bytes(A->row_ptr, ((size_t)n + 1) * 4);
+  if (nnz > 0) {
+    h = h * 31 + hash_bytes(A->col_indices, (size_t)nnz * 4);
+    h = h * 31 + hash_bytes(A->values, (size_t)nnz * 8);
+  }
+  return h;
+}
+
+// Makes A the default solver's matrix: a reuse when the struct's arrays,
+// sizes and contents are those already on the device, else one upload.
+int ensure_matrix(cgx_solver *s, const struct __mv_sparse *A) {
+  const int n = A->size, nnz = A->row_ptr[n];
+  const unsigned long long h = matrix_hash(A);
+  if (g_res.valid && g_res.rp == A->row_ptr && g_res.col == A->col_indices &&
+      g_res.val == A->values && g_res.size == n && g_res.nnz == nnz && g_res.hash == h) {
+    ++g_reuses;
+    return 0;
+  }
+  g_res.valid = false;
+  int rc = cgx_solver_set_matrix(s, n, nnz, A->row_ptr, A->col_indices, A->values);
+  if (rc) return rc;
+  ++g_uploads;
+  g_res.rp = A->row_ptr;
+  g_res.col = A->col_indices;
+  g_res.val = A->values;
+  g_res.size = n;
+  g_res.nnz = nnz;
+  g_res.hash = h;
+  g_res.valid = true;
+  return 0;
+}
+
 int ops_ready(size_t n) {
   if (g_ops.device < 0) {
     const int dev = env_device();
-    int cnt = 0;
-    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= dev) {
-      set_error("no HIP device %d available", dev);
-      return CGX_ENODEV;
-    }
+    int rc = check_device(dev, &g_ops.cus);
+    if (rc) return rc;
     CGX_HIP(hipSetDevice(dev));
-    hipDeviceProp_t prop;
-    CGX_HIP(hipGetDeviceProperties(&prop, dev));
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-      set_error("device %d is %s; libcgx targets gfx950 only", dev,
-                prop.gcnArchName);
-      return CGX_ENODEV;
-    }
-    g_ops.cus = prop.multiProcessorCount;
     CGX_HIP(hipStreamCreateWithFlags(&g_ops.st, hipStreamNonBlocking));
     CGX_HIP(hipMalloc((void **)&g_ops.part, (size_t)(g_ops.cus * 4 + 1) * 8));
     g_ops.device = dev;
@@ -102,15 +179,17 @@ int prepare_out(struct __mv_sparse **r, int size, int nnz, bool zero) {
     struct __mv_sparse *v = (struct __mv_sparse *)calloc(1, sizeof *v);
     if (!v) return CGX_ENOMEM;
     v->values = (double *)calloc(size > 0 ? size : 1, sizeof(double));
-    if (!v->values) { free(v); return CGX_ENOMEM; }
+    if (!v->values) {
+      free(v);
+      return CGX_ENOMEM;
+    }
     v->size = size;
     v->nnz = nnz;
     v->col_indices = nullptr;
     v->row_ptr = nullptr;
     *r = v;
   } else {
-    double *nv = (double *)realloc((*r)->values,
-                                   (size_t)(size > 0 ? size : 1) * sizeof(double));
+    double *nv = (double *)realloc((*r)->values, (size_t)(size > 0 ? size : 1) * sizeof(double));
     if (!nv) return CGX_ENOMEM;
     (*r)->values = nv;
     if (zero) memset(nv, 0, (size_t)size * sizeof(double));
@@ -121,17 +200,14 @@ int prepare_out(struct __mv_sparse **r, int size, int nnz, bool zero) {
 }
 
 // r = op(a, b) on the device; op 0: s*a, 1: a+b, 2: a-b.
-int device_axpby(int op, double s, const double *a, const double *b, double *r,
-                 int n) {
+int device_axpby(int op, double s, const double *a, const double *b, double *r, int n) {
   if (n <= 0) return 0;
   int rc = ops_ready((size_t)n);
   if (rc) return rc;
   CGX_HIP(hipMemcpyAsync(g_ops.a, a, (size_t)n * 8, hipMemcpyHostToDevice, g_ops.st));
-  if (b)
-    CGX_HIP(hipMemcpyAsync(g_ops.b, b, (size_t)n * 8, hipMemcpyHostToDevice,
-                           g_ops.st));
-  CGX_HIP(launch_axpby<double>(op, n, s, g_ops.a, b ? g_ops.b : nullptr,
-                               g_ops.r, vec_grid_for(n, g_ops.cus), g_ops.st));
+  if (b) CGX_HIP(hipMemcpyAsync(g_ops.b, b, (size_t)n * 8, hipMemcpyHostToDevice, g_ops.st));
+  CGX_HIP(launch_axpby<double>(op, n, s, g_ops.a, b ? g_ops.b : nullptr, g_ops.r,
+                               vec_grid_for(n, g_ops.cus), g_ops.st));
   CGX_HIP(hipMemcpyAsync(r, g_ops.r, (size_t)n * 8, hipMemcpyDeviceToHost, g_ops.st));
   CGX_HIP(hipStreamSynchronize(g_ops.st));
   return 0;
@@ -151,8 +227,8 @@ int device_dot(const double *a, const double *b, int n, double *out) {
   } else {
     const int g = vec_grid_for(n, g_ops.cus);
     CGX_HIP(launch_dot_part<double>(n, g_ops.a, g_ops.b, g_ops.part, g, g_ops.st));
-    CGX_HIP(launch_finalize(FIN_SUM, g_ops.part, g, nullptr, 0, nullptr,
-                            nullptr, g_ops.r, g_ops.st));
+    CGX_HIP(launch_finalize(FIN_SUM, g_ops.part, g, nullptr, 0, nullptr, nullptr, g_ops.r,
+                            g_ops.st));
   }
   CGX_HIP(hipMemcpyAsync(out, g_ops.r, 8, hipMemcpyDeviceToHost, g_ops.st));
   CGX_HIP(hipStreamSynchronize(g_ops.st));
@@ -163,18 +239,10 @@ bool is_matrix(const struct __mv_sparse *A) {
   return A && A->row_ptr && A->size >= 0 && (A->nnz == 0 || (A->col_indices && A->values));
 }
 
-int load_system(cgx_solver *s, const struct __mv_sparse *A,
-                const struct __mv_sparse *b) {
-  int rc = cgx_solver_set_matrix(s, A->size, A->row_ptr[A->size], A->row_ptr,
-                                 A->col_indices, A->values);
-  if (rc) return rc;
-  return cgx_solver_set_rhs(s, b->values);
-}
-
-int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
-              struct __mv_sparse **x, double tol, int maxit) {
-  if (!is_matrix(A) || !b || !x || (b->size > 0 && !b->values) ||
-      A->size != b->size || maxit < 0) {
+int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct __mv_sparse **x,
+              double tol, int maxit) {
+  if (!is_matrix(A) || !b || !x || (b->size > 0 && !b->values) || A->size != b->size ||
+      maxit < 0) {
     set_error("conj_grad/solve: NULL argument, size mismatch or max_iter < 0");
     return CGX_EINVAL;
   }
@@ -185,7 +253,8 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
   if ((rc = cgx_solver_set_mode(s, env_exact() ? CGX_MODE_EXACT : CGX_MODE_FAST,
                                 env_exact() ? CGX_ALG_HS : env_alg())))
     return rc;
-  if ((rc = load_system(s, A, b))) return rc;
+  if ((rc = ensure_matrix(s, A))) return rc;
+  if ((rc = cgx_solver_set_rhs(s, b->values))) return rc;
   int iters = maxit + 1;
   if (A->size > 0 && (rc = cgx_solver_run(s, maxit, tol, &iters))) return rc;
   struct __mv_sparse *xv = new_mv_struct_with_size(b->size);  // cg.c:104
@@ -240,8 +309,7 @@ struct __mv_sparse *mv_deep_copy(struct __mv_sparse *orig) {  // mv_ops.c:44-74
   if (orig->nnz > 0) memcpy(cp->values, orig->values, (size_t)orig->nnz * 8);
   if (orig->col_indices) {
     cp->col_indices = (int *)calloc(nv, sizeof(int));
-    if (orig->nnz > 0)
-      memcpy(cp->col_indices, orig->col_indices, (size_t)orig->nnz * 4);
+    if (orig->nnz > 0) memcpy(cp->col_indices, orig->col_indices, (size_t)orig->nnz * 4);
   }
   if (orig->row_ptr) {
     cp->row_ptr = (int *)calloc((size_t)orig->size + 1, sizeof(int));
@@ -338,13 +406,7 @@ int mv_mult(struct __mv_sparse *A, struct __mv_sparse *b, struct __mv_sparse **r
   if (n > 0) {
     cgx_solver *s = nullptr;
     rc = default_solver(&s);
-    // one product per upload: coding the columns would cost more host time
-    // than it saves on a single SpMV (the solvers below keep it)
-    if (rc == 0) cgx::solver_want_dc(s, false);
-    if (rc == 0)
-      rc = cgx_solver_set_matrix(s, n, A->row_ptr[n], A->row_ptr,
-                                 A->col_indices, A->values);
-    if (rc == 0) cgx::solver_want_dc(s, true);
+    if (rc == 0) rc = ensure_matrix(s, A);  // resident across calls (see top)
     if (rc == 0) rc = cgx_solver_spmv(s, b->values, tmp);
   }
   if (rc == 0) rc = prepare_out(r, n, b->nnz, true);
@@ -353,16 +415,23 @@ int mv_mult(struct __mv_sparse *A, struct __mv_sparse *b, struct __mv_sparse **r
   return rc;
 }
 
+int cgx_ops_counters(long long *uploads, long long *reuses) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (uploads) *uploads = g_uploads;
+  if (reuses) *reuses = g_reuses;
+  return 0;
+}
+
 // ------------------------------------------------------------- solvers
 
-int conj_grad(int max_iter, struct __mv_sparse *mat_A,
-              struct __mv_sparse *vec_b, struct __mv_sparse **vec_x) {
+int conj_grad(int max_iter, struct __mv_sparse *mat_A, struct __mv_sparse *vec_b,
+              struct __mv_sparse **vec_x) {
   const int rc = run_solve(mat_A, vec_b, vec_x, 0.0, max_iter);
   return rc < 0 ? rc : 0;  // the reference always returns 0 (cg.c:140)
 }
 
-int solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
-          struct __mv_sparse **x, double tol, int maxit) {
+int solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct __mv_sparse **x,
+          double tol, int maxit) {
   return run_solve(A, b, x, tol, maxit);
 }
 

@@ -50,6 +50,14 @@ int solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
  * the shell, mv_ops.c:39-42, which libcgx keeps for drop-in safety). */
 void cgx_free_mv_deep(struct __mv_sparse *m);
 
+/* Matrix residency of the mv_ops.h / conj_grad / solve entry points: the
+ * last matrix stays on the device, keyed by the struct's array pointers,
+ * sizes and a 64-bit hash of row_ptr, col_indices and values.  A call with
+ * the same (unmodified) matrix reuses it -- a cg.c caller linked at the op
+ * level (cg.c:111 -> mv_mult) uploads A once, not once per iteration.
+ * Counts since process start: uploads performed, reuses. */
+int cgx_ops_counters(long long *uploads, long long *reuses);
+
 const char *cgx_last_error(void);
 int cgx_device_count(void);
 
@@ -74,33 +82,57 @@ enum { CGX_ALG_HS = 0,       /* Hestenes-Stiefel, the reference recurrence    */
        CGX_ALG_CG1 = 1 };    /* Chronopoulos-Gear, one fused reduction/iter   */
 enum { CGX_F64 = 0, CGX_F32 = 1 };
 
+/* Device layout of the matrix the SpMV streams (the C ABI always takes the
+ * reference's CSR; the CSR arrays stay resident whatever the layout):
+ *   AUTO     VI where it applies, else DC, else CSR (PANEL for gathers with
+ *            no locality, e.g. random SPD)                       (default)
+ *   CSR      plain CSR, int32 columns: SURVEY.md 8d's B_spmv layout
+ *   DC       dictionary-coded columns: <= 256 distinct col - row offsets,
+ *            one code byte per nonzero + the value stream, rows <= 255
+ *   VI       value-indexed pairs: <= 255 distinct (col - row, value) pairs,
+ *            one code byte per nonzero naming both, no value stream, rows
+ *            in 512-row slices of fixed width (stencils, small value sets)
+ *   PANEL    CSR split into column panels (one SpMV pass per panel)
+ *   STENCIL  matrix-free Laplacian (cgx_solver_set_stencil; info only)
+ * A requested layout that does not apply falls back VI -> DC -> CSR;
+ * cgx_info.layout says which one runs.  Every layout sums each row in the
+ * reference's order: y is bit-identical across layouts. */
+enum { CGX_LAYOUT_AUTO = 0, CGX_LAYOUT_CSR = 1, CGX_LAYOUT_DC = 2, CGX_LAYOUT_VI = 3,
+       CGX_LAYOUT_PANEL = 4, CGX_LAYOUT_STENCIL = 5 };
+
 typedef struct {
   int n, nnz, dtype, mode, alg;
-  int n_rowblocks;      /* LDS-staged row blocks of the SpMV plan            */
-  int spmv_grid;        /* workgroups of the persistent SpMV launch          */
-  int vec_grid;         /* workgroups of the vector-update launches          */
-  double spmv_bytes;    /* algorithmic HBM bytes per SpMV     */
+  int layout;           /* CGX_LAYOUT_* the SpMV runs on                     */
+  int n_items;          /* SpMV work items: 64-row blocks (CSR/DC/PANEL) or
+                           512-row slices (VI)                              */
+  int spmv_grid;        /* workgroups of one SpMV launch (= its partials)    */
+  int vec_grid;         /* 256-thread units of the vector-update launches    */
+  double spmv_bytes;    /* algorithmic HBM bytes per SpMV, CSR basis
+                           (SURVEY.md 8d B_spmv)                             */
   double iter_bytes;    /* algorithmic HBM bytes per CG iteration (8d)       */
-  double spmv_iter_bytes; /* algorithmic bytes of the SpMV as it runs inside
-                             the iteration, in the layout it runs on (fused
-                             p-update: + r, p_old gathered, p_new written;
-                             column panels: + P row_ptrs, y round trips)    */
+  double spmv_iter_bytes; /* algorithmic bytes of one SpMV in the layout it
+                             runs on (VI: padded code rows + x + y + pairs;
+                             DC: codes + values + row lengths + x + y;
+                             PANEL: + P row_ptrs and y round trips)         */
   size_t device_bytes;  /* device memory held by the solver                  */
-  int n_panels;         /* column panels of the SpMV (1: plain CSR)          */
-  int n_dict;           /* dictionary-coded columns: distinct col - row
-                           offsets (1..256, one code byte per nonzero on the
-                           device); 0: plain 4-byte columns                  */
-  int tile_bands;       /* L2-tiled row-block order: bands of the widest
-                           offset's period swept one after another (0: the
-                           natural order)                                    */
-  int dict_vals;        /* 1: the dictionary holds (offset, value) pairs and
-                           the codes name both -- the SpMV streams no values
-                           (CSR-VI; <= 64 distinct pairs)                    */
+  int n_panels;         /* column panels of the SpMV (1: none)               */
+  int n_dict;           /* DC: distinct col - row offsets; VI: distinct
+                           (offset, value) pairs; 0 otherwise               */
+  int tile_bands;       /* L2-tiled item order: bands of the widest offset's
+                           period swept one after another (0: natural)      */
+  int nt;               /* 1: matrix stream and y store non-temporal        */
+  int row_width;        /* VI: codes per row of the widest slice            */
+  int encode_fallback;  /* 1: the sampled pairs/offsets missed one; an exact
+                           host scan was needed                             */
+  double setup_host_ms;   /* set_matrix: host time (checks, plan, submit)    */
+  double setup_device_ms; /* set_matrix: device time after the last submit  */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);
 void cgx_solver_destroy(cgx_solver *s);
 int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
+/* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
+int  cgx_solver_set_layout(cgx_solver *s, int layout);
 /* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.
  * Columns must be ascending within each row for bit-exact SpMV order. */
 int  cgx_solver_set_matrix(cgx_solver *s, int n, int nnz, const int *row_ptr,
@@ -146,9 +178,13 @@ int  cgx_solver_info(cgx_solver *s, cgx_info *info);
  * flags & CGX_BENCH_GRAPH: replay the iteration loop as hipGraphs.
  * flags & CGX_BENCH_SPMV_EVENTS: also bracket every SpMV launch with events
  *   and report its average duration in *spmv_ms (else *spmv_ms = -1).
+ * flags & CGX_BENCH_SPMV_ONLY: `iters` back-to-back SpMVs y = A p instead of
+ *   CG iterations (the standard SpMV benchmark; the iteration state is not
+ *   touched).
  * cgx_solver_bench = prepare + run. */
 #define CGX_BENCH_GRAPH        1
 #define CGX_BENCH_SPMV_EVENTS  2
+#define CGX_BENCH_SPMV_ONLY    4
 int  cgx_solver_bench_prepare(cgx_solver *s, int warmup);
 int  cgx_solver_bench_run(cgx_solver *s, int iters, int flags, double *total_ms,
                           double *spmv_ms);
@@ -212,25 +248,28 @@ int  cgx_part_send_counts(const cgx_part *p, int *counts);     /* nranks  */
 int  cgx_part_send_local(const cgx_part *p, int *send_local);  /* n_send  */
 
 /* ------------------------------------------------------------------------
- * 5. Multi-GPU solver: one rank per GPU, halo exchange + ONE fused
- *    all-reduce per iteration (Chronopoulos-Gear CG) over RCCL.
+ * 5. Multi-GPU solver: one rank per GPU, rows partitioned in contiguous
+ *    blocks, halo x segments exchanged point to point (ncclSend/Recv on a
+ *    high-priority stream, overlapped with the interior SpMV), dot products
+ *    all-reduced over RCCL; batches of iterations replayed as hipGraphs.
  *    Stop rule as solve(); x0 = 0; every rank passes its own rows.
  * ------------------------------------------------------------------------ */
 typedef struct cgx_dist cgx_dist;
 typedef struct {
   long long n_global;
   int row_begin, n_loc, n_ghost, n_send, nnz;
-  int interior_blocks, boundary_blocks;  /* 64-row SpMV blocks            */
-  double spmv_bytes, iter_bytes;         /* algorithmic, this rank        */
+  int interior_items, boundary_items;    /* SpMV work items (cgx_info)    */
+  double spmv_bytes, iter_bytes;         /* algorithmic, CSR basis, rank  */
   double halo_bytes;                     /* sent + received per iteration */
   size_t device_bytes;
   double spmv_iter_bytes;                /* algorithmic bytes of the SpMV in
-                                            the layout it runs on (coded
-                                            columns: 1 byte per nonzero)  */
-  int n_dict;                            /* coded-column dictionary size,
-                                            0: plain 4-byte columns      */
-  int dict_vals;                         /* 1: (offset, value) pairs, no
-                                            value stream (see cgx_info)  */
+                                            the layout it runs on         */
+  int layout;                            /* CGX_LAYOUT_* of the local rows */
+  int n_dict;                            /* as cgx_info                   */
+  int graph;                             /* 1 iterations replayed as a
+                                            hipGraph, 0 not (yet), -1 the
+                                            capture failed: eager        */
+  int alg;                               /* CGX_ALG_* in use              */
 } cgx_dist_stats;
 
 /* Rank 0 creates the id and distributes it (e.g. torch.distributed). */
@@ -243,17 +282,22 @@ int  cgx_dist_create(int device, int nranks, int rank,
  * Run/bench through parts[0]; destroy through parts[0]. */
 int  cgx_dist_create_local(int device, int nparts, cgx_dist **parts);
 void cgx_dist_destroy(cgx_dist *d);
+/* Layout of the local rows for the next set_matrix (AUTO, CSR, DC, VI). */
+int  cgx_dist_set_layout(cgx_dist *d, int layout);
 int  cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
                          const int *row_ptr, const int *col_global,
                          const double *val);
 int  cgx_dist_set_rhs(cgx_dist *d, const double *b_local);
-/* Recurrence: CGX_ALG_CG1 (default; Chronopoulos-Gear, ONE all-reduce of two
- * doubles per iteration) or CGX_ALG_HS (the reference's cg.c:88-141
- * recurrence, two all-reduces of one double, 8 bytes per row less vector
- * traffic).  Every rank (every part of a local group) must use the same one;
- * on a local group, setting it on part 0 sets the group.  The environment
- * default is CGX_DIST_ALG=cg1|hs. */
+/* Recurrence: CGX_ALG_HS (default; the reference's cg.c:88-141 recurrence:
+ * two all-reduces of one double per iteration, bit-identical to the
+ * single-GPU solver at one rank) or CGX_ALG_CG1 (Chronopoulos-Gear: ONE
+ * all-reduce of two doubles, 8 bytes per row more vector traffic).  Every
+ * rank (every part of a local group) must use the same one; on a local
+ * group, setting it on part 0 sets the group. */
 int  cgx_dist_set_alg(cgx_dist *d, int alg);
+/* hipGraph replay of the iteration batches (RCCL calls included); on by
+ * default; 0 runs every iteration eagerly.  Resets a failed capture. */
+int  cgx_dist_set_graph(cgx_dist *d, int on);
 int  cgx_dist_run(cgx_dist *d, int maxit, double tol, int *iters);
 int  cgx_dist_get_x(cgx_dist *d, double *x_local);
 int  cgx_dist_get_history(cgx_dist *d, double *rr, int cap);

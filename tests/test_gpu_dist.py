@@ -27,12 +27,13 @@ def system(kind):
     return rp, col, val, b
 
 
-def solve_local(rp, col, val, b, P, maxit, tol, alg=cgx.CGX_ALG_CG1):
+def solve_local(rp, col, val, b, P, maxit, tol, alg=cgx.CGX_ALG_CG1, layout="auto"):
     n = len(rp) - 1
     parts = cgx.DistSolver.local_group(0, P)
     try:
         parts[0].set_alg(alg)
         for g, d in enumerate(parts):
+            d.set_layout(layout)
             rb, re_ = cgx.partition_rows(n, P, g)
             d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]],
                          val[rp[rb]:rp[re_]])
@@ -46,11 +47,9 @@ def solve_local(rp, col, val, b, P, maxit, tol, alg=cgx.CGX_ALG_CG1):
     return x, its, hist, stats
 
 
-@pytest.mark.parametrize("runs", ["1", "0"])
 @pytest.mark.parametrize("kind", ["lap3d", "lap2d", "rand"])
 @pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
-def test_local_partitions_match_oracle(kind, P, runs, monkeypatch):
-    monkeypatch.setenv("CGX_DIST_RUNS", runs)
+def test_local_partitions_match_oracle(kind, P):
     rp, col, val, b = system(kind)
     x, its, hist, stats = solve_local(rp, col, val, b, P, 2000, 1e-10)
     x_ref, its_ref, hist_ref = H.o_solve(2000, 1e-10, rp, col, val, b, cg1=True)
@@ -109,9 +108,11 @@ def test_local_group_bench_and_interior_split():
         parts[0].close()
     # z-slabs of 16 planes: one ghost plane per neighbour, boundary blocks
     # are the first and last plane's 64-row blocks
+    # VI slices of 512 rows: the first and last plane's 2 slices per face
     assert [s["n_ghost"] for s in st] == [1024, 2048, 2048, 1024]
-    assert all(s["boundary_blocks"] <= 2 * 1024 // 64 + 2 for s in st)
-    assert all(s["interior_blocks"] > 0 for s in st)
+    assert [s["layout_name"] for s in st] == ["vi"] * 4
+    assert [s["boundary_items"] for s in st] == [2, 4, 4, 2]
+    assert all(s["interior_items"] > 0 for s in st)
 
 
 def test_history_after_buffer_growth():
@@ -144,31 +145,23 @@ def test_history_after_buffer_growth():
 
 
 @pytest.mark.parametrize("P", [1, 2, 4])
-def test_coded_columns_partitions_identical_to_csr(P, monkeypatch):
-    """Partitions of a Laplacian keep <= 256 distinct local column offsets
-    (owned rows: the stencil's; ghost columns: constant offsets per face), so
-    each part runs the coded-column SpMV -- value-indexed pairs by default
-    (one value per offset: <= 21 pairs), offset codes with CGX_DC_VALS=0; x
-    and the history are bit-identical to the plain-CSR layout in both."""
+def test_layouts_partitions_identical_in_exact_sums(P):
+    """Partitions of a Laplacian keep a small set of local column offsets
+    (owned rows: the stencil's; ghost columns: one more constant offset per
+    face), so every part runs CSR-DC or CSR-VI like the single-GPU solver.
+    With tol = 0 the layouts only change how A is stored and how the SpMV
+    partials are grouped: x agrees to rounding (1e-12) across CSR, DC, VI."""
     rp, col, val, b = system("lap3d")
     out = {}
-    for layout in ("csr", "auto", "dc"):
-        monkeypatch.setenv("CGX_DC_VALS", "0" if layout == "dc" else "1")
-        if layout == "csr":
-            monkeypatch.setenv("CGX_LAYOUT", "csr")
-        else:
-            monkeypatch.delenv("CGX_LAYOUT", raising=False)
-        x, its, hist, stats = solve_local(rp, col, val, b, P, 50, 0.0)
-        if layout == "csr":
-            assert all(s["n_dict"] == 0 for s in stats)
-        else:
+    for layout in ("csr", "dc", "vi"):
+        x, its, hist, stats = solve_local(rp, col, val, b, P, 50, 0.0, layout=layout)
+        assert all(s["layout_name"] == layout for s in stats)
+        if layout != "csr":
             assert all(0 < s["n_dict"] <= 21 for s in stats)  # <= 7 stencil + 7 per ghost face
             assert all(s["spmv_iter_bytes"] < s["spmv_bytes"] for s in stats)
-            assert all(s["dict_vals"] == (layout == "auto") for s in stats)
-        out[layout] = (x, hist)
-    for layout in ("auto", "dc"):
-        assert H.same_bits_or_both_nan(out["csr"][0], out[layout][0])
-        assert H.same_bits_or_both_nan(out["csr"][1], out[layout][1])
+        out[layout] = x
+    for layout in ("dc", "vi"):
+        assert np.linalg.norm(out[layout] - out["csr"]) <= 1e-12 * np.linalg.norm(out["csr"])
 
 
 @pytest.mark.parametrize("kind", ["lap3d", "lap2d", "rand"])
@@ -240,26 +233,59 @@ def test_hs_fixed_iterations_and_bench():
 def test_rccl_one_rank_communicator(alg):
     """A 1-rank RCCL communicator (an id at world size 1) runs the multi-GPU
     phase code on one GPU: pack, grouped send/recv loop (no peers), local
-    sums, ncclAllReduce, scalar steps.  Bit-identical to the in-process
-    1-partition group (the same phases with a fixed-order group sum), within
-    tolerance of the oracle, and the eager bench path runs."""
+    sums by the producing kernels' last workgroups, ncclAllReduce, scalar
+    steps -- replayed as a hipGraph (RCCL calls captured) and eagerly, the
+    two bit-identical.  Bit-identical to the in-process 1-partition group
+    (the same phases with a fixed-order group sum), within tolerance of the
+    oracle."""
     rp, col, val, b = system("lap3d")
     n = len(rp) - 1
-    d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
-    try:
-        d.set_alg(alg)
-        d.set_matrix(n, rp, col, val)
-        d.set_rhs(b)
-        its = d.run(500, 1e-10)
-        x = d.x()
-        d.bench_prepare(2)
-        ms, sp = d.bench_run(5, spmv_events=True)
-        assert ms > 0 and 0 < sp < ms
-    finally:
-        d.close()
+    res = {}
+    for graph in (True, False):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+        try:
+            d.set_alg(alg)
+            d.set_graph(graph)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            its = d.run(500, 1e-10)
+            x = d.x()
+            h = d.history(its)
+            assert d.info()["graph"] == (1 if graph else 0)
+            d.bench_prepare(2)
+            ms, sp = d.bench_run(5, spmv_events=True)
+            assert ms > 0 and 0 < sp < ms
+            ms2, _ = d.bench_run(32, graph=graph)
+            assert ms2 > 0
+        finally:
+            d.close()
+        res[graph] = (its, x, h)
+    assert res[True][0] == res[False][0]
+    assert H.same_bits_or_both_nan(res[True][1], res[False][1])
+    assert H.same_bits_or_both_nan(res[True][2], res[False][2])
+    its, x, _ = res[True]
     x1, its1, _, _ = solve_local(rp, col, val, b, 1, 500, 1e-10, alg=alg)
     assert its == its1
     assert H.same_bits_or_both_nan(x, x1)
     x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=alg == cgx.CGX_ALG_CG1)
     assert abs(its - its_ref) <= 1
     assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
+
+
+def test_local_group_sums_match_solver_bit_exact():
+    """One in-process partition WITH the transport phases: the local sums are
+    the SpMV's / k_update_rf's last-arriver canonical sums (cgx_kernels.hip
+    canon_sum), fed to the same folded kernels through a one-value
+    all-reduce.  x and the history are bit-identical to cgx.Solver, whose
+    folded kernels sum the partials directly (sum_parts<1024>): the in-kernel
+    local sums reproduce the finalize order exactly, in every layout."""
+    rp, col, val, b = system("lap3d")
+    for layout in ("csr", "dc", "vi"):
+        x, its, hist, _ = solve_local(rp, col, val, b, 1, 40, 0.0, alg=cgx.CGX_ALG_HS,
+                                      layout=layout)
+        with cgx.Solver(0, layout=layout) as s:
+            s.set_matrix(rp, col, val)
+            s.set_rhs(b)
+            assert s.run(40) == its == 41
+            assert H.same_bits_or_both_nan(x, s.x()), layout
+            assert H.same_bits_or_both_nan(hist, s.history(41)), layout

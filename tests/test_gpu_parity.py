@@ -2,14 +2,17 @@
 the golden vectors of the compiled reference and against the pinned oracle.
 
 Bars (stated here, checked below):
-  * SpMV (mv_mult), sv_mult, vec_add, vec_sub: bit-exact.
+  * SpMV (mv_mult), sv_mult, vec_add, vec_sub: bit-exact, in every device
+    layout (CSR, CSR-DC, CSR-VI, column panels, matrix-free stencil).
   * conj_grad / solve in CGX_MODE_EXACT: bit-exact x at every golden max_iter
     (including the all-NaN breakdown of the n = 10 KAT at max_iter 5).
   * default (parallel-reduction) mode: ||x - x_ref||_2 <= FAST_RTOL ||x_ref||_2
     with FAST_RTOL = 1e-12 (the only difference is dot-product summation
-    order; simulated worst case on the fixtures is ~1e-14).
-  * full-size configs: size-independent properties (bit-exact SpMV against the
-    oracle, true relative residual ||b - A x|| / ||b|| <= tol after solve).
+    order; simulated worst case on the fixtures is ~1e-14), bit-reproducible
+    run to run.
+  * full-size configs (C2, C3, C4, C5): size-independent properties
+    (bit-exact SpMV against the oracle or the stencil, true relative residual
+    ||b - A x|| / ||b|| <= tol after solve).
 """
 import ctypes
 import os
@@ -25,6 +28,7 @@ pytestmark = pytest.mark.gpu
 FAST_RTOL = 1e-12
 NAMES = H.golden_names()
 CHAINED = [n for n in NAMES if H.load_golden(n)["chained"]]
+LAYOUTS = ["auto", "csr", "dc", "vi", "panel"]
 
 
 @pytest.fixture(scope="module")
@@ -50,171 +54,65 @@ def rel(x, ref):
     return np.linalg.norm(x - ref) / (d if d > 0 else 1.0)
 
 
+def same32(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32),
+                          np.asarray(b, np.float32).view(np.uint32))
+
+
+def expect_layout(rp, col, val, want="auto"):
+    """The layout libcgx must pick (cgx_matrix.h): VI when <= 255 distinct
+    (col - row, value-bits) pairs and the 512-row slices' padded code rows
+    stay within 2x the compact codes; else DC when <= 256 distinct offsets and
+    rows <= 255 entries; else CSR.  A forced layout falls back VI -> DC -> CSR."""
+    rp, col = np.asarray(rp), np.asarray(col)
+    n = len(rp) - 1
+    if want == "panel":  # column panels need x wider than one 2 MiB panel
+        pcols = max(1024, 2 * 2**20 // np.asarray(val).itemsize)
+        return "panel" if len(col) and n > pcols else "csr"
+    if want == "csr" or len(col) == 0:
+        return "csr"
+    lens = np.diff(rp)
+    off = col.astype(np.int64) - np.repeat(np.arange(n), lens)
+    v = np.asarray(val)
+    bits = v.view(np.uint64 if v.dtype == np.float64 else np.uint32).astype(np.uint64)
+    npair = len(np.unique(np.stack([off, bits.view(np.int64)]), axis=1).T)
+    words = 0
+    for s in range(0, n, 512):
+        m = int(lens[s:s + 512].max())
+        wd = max(1, (m + 3) // 4)
+        wd = 4 if wd == 3 else (wd if wd <= 4 else (wd + 3) // 4 * 4)
+        words += wd * 512
+        words = (words + 3) & ~3
+    vi_ok = npair <= 255 and 4 * words <= 2 * (len(col) + n) + 4096
+    dc_ok = len(np.unique(off)) <= 256 and lens.max() <= 255
+    if want in ("auto", "vi") and vi_ok:
+        return "vi"
+    if want in ("auto", "vi", "dc") and dc_ok:
+        return "dc"
+    return "csr"
+
+
 def test_device_visible():
     assert cgx.lib().cgx_device_count() > 0
 
 
 # ------------------------------------------------------------------ SpMV
 
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("name", CHAINED)
-def test_spmv_bit_exact_vs_reference(solver, name):
+def test_spmv_bit_exact_vs_reference(name, layout):
+    """mv_mult's golden output (the compiled reference, mv_ops.c:160-201) in
+    every layout; the layout picked is the documented one."""
     g = H.load_golden(name)
-    solver.set_mode(cgx.CGX_MODE_FAST)
-    solver.set_matrix(g["row_ptr"], g["col"], g["val"])
-    y = solver.spmv(g["b"])
-    assert H.same_bits_or_both_nan(y, g["ops"]["mv_mult"])
-
-
-@pytest.mark.parametrize("bs", ["64", "256", "512", "dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512", "dmalast", "eng", "eng0", "eng1", "eng3", "eng4", "eng5", "eng6", "eng7", "notg", "pipe", "pipe1", "pipe63"])
-@pytest.mark.parametrize("vec", ["1", "2", "4"])
-def test_spmv_variants_bit_exact(vec, bs, monkeypatch):
-    """Every SpMV variant (wave / workgroup row blocks, load widths, LDS-DMA,
-    pipelined persistent waves with 1/8/63 blocks each) keeps the sequential
-    per-row order, fp64 and fp32, including long rows."""
-    monkeypatch.setenv("CGX_SPMV_VEC", vec)
-    monkeypatch.setenv("CGX_SPMV_DMA", "0")  # register-staged kernels unless named
-    if bs in ("dma", "dma8", "dma32", "dmaw8", "dmaxcd", "dma456", "dma328", "dma512",
-              "dmalast"):
-        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4", "dmaw8": "1",
-                                            "dmaxcd": "1", "dma456": "1", "dma328": "1",
-                                            "dma512": "1", "dmalast": "1"}[bs])
-        if bs == "dmalast":
-            monkeypatch.setenv("CGX_SPMV_EPI_LAST", "1")
-        if bs in ("dma456", "dma328", "dma512"):
-            monkeypatch.setenv("CGX_SPMV_CAPW", bs[3:])
-        if bs == "dmaw8":
-            monkeypatch.setenv("CGX_SPMV_WPB", "8")
-        if bs == "dmaxcd":
-            monkeypatch.setenv("CGX_SPMV_XCD", "1")
-    elif bs.startswith("pipe"):
-        monkeypatch.setenv("CGX_SPMV_DMA", "2")
-        if bs != "pipe":
-            monkeypatch.setenv("CGX_SPMV_RBW", bs[4:])
-    elif bs.startswith("eng"):
-        monkeypatch.setenv("CGX_SPMV_DMA", "5")
-        if bs != "eng":
-            monkeypatch.setenv("CGX_ENG_SHAPE", bs[3:])
-    elif bs == "notg":
-        monkeypatch.setenv("CGX_SPMV_TG", "0")
-    else:
-        monkeypatch.setenv("CGX_SPMV_BS", bs)
-    rp, col, val, b = H.random_spd(4000, 9, seed=3)
-    g = H.load_golden("dense128")
-    with cgx.Solver(0) as s:
-        s.set_matrix(rp, col, val)
-        assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
+    with cgx.Solver(0, layout=layout) as s:
         s.set_matrix(g["row_ptr"], g["col"], g["val"])
-        assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"])
-        rp32, col32, v32 = cgx.random_spd(5000, 40, 9, f32=True)
-        x32 = np.random.default_rng(2).standard_normal(5000).astype(np.float32)
-        s.set_matrix(rp32, col32, v32)
-        assert np.array_equal(s.spmv(x32).view(np.uint32),
-                              H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
-        # a CG run through the fused-epilogue path
-        g = H.load_golden("lap3d_12")
-        s.set_matrix(g["row_ptr"], g["col"], g["val"])
-        s.set_rhs(g["b"])
-        s.run(20)
-        x_ref, _ = H.o_conj_grad(20, g["row_ptr"], g["col"], g["val"], g["b"])
-        assert rel(s.x(), x_ref) <= FAST_RTOL
-
-
-@pytest.mark.parametrize("bs", ["64", "256", "dma", "dma8", "dma32", "pipe", "eng", "eng4"])
-def test_spmv_long_rows_variants(bs, monkeypatch):
-    monkeypatch.setenv("CGX_SPMV_DMA", "0")
-    if bs in ("dma", "dma8", "dma32"):
-        monkeypatch.setenv("CGX_SPMV_DMA", {"dma": "1", "dma8": "8", "dma32": "4"}[bs])
-    elif bs == "pipe":
-        monkeypatch.setenv("CGX_SPMV_DMA", "2")
-    elif bs.startswith("eng"):
-        monkeypatch.setenv("CGX_SPMV_DMA", "5")
-        if bs != "eng":
-            monkeypatch.setenv("CGX_ENG_SHAPE", bs[3:])
-    else:
-        monkeypatch.setenv("CGX_SPMV_BS", bs)
-    n = 3000
-    rng = np.random.default_rng(8)
-    rows = [np.arange(n) if i in (0, 7, n - 1) else
-            np.unique(np.concatenate([[max(i - 1, 0), i, min(i + 1, n - 1)], rng.integers(0, n, 3)]))
-            for i in range(n)]
-    rp = np.zeros(n + 1, np.int32)
-    rp[1:] = np.cumsum([len(c) for c in rows])
-    col = np.concatenate(rows).astype(np.int32)
-    val = rng.standard_normal(len(col))
-    x = rng.standard_normal(n)
-    with cgx.Solver(0) as s:
-        s.set_matrix(rp, col, val)
-        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
-
-
-def test_spmv_long_rows_bit_exact(solver):
-    """Rows longer than one LDS row block (2048 products) take the chunked
-    path; row sums must still be sequential."""
-    n = 6000
-    rows = []
-    rng = np.random.default_rng(5)
-    for i in range(n):
-        if i in (0, 1, 2500, n - 1):
-            cols = np.arange(n)  # dense rows
+        got = s.info()["layout_name"]
+        want = expect_layout(g["row_ptr"], g["col"], g["val"], layout)
+        if layout == "panel":
+            assert got in ("panel", "csr")  # tiny matrices need no panels
         else:
-            cols = np.unique(np.concatenate([[max(i - 1, 0), i, min(i + 1, n - 1)],
-                                             rng.integers(0, n, 4)]))
-        rows.append(cols)
-    rp = np.zeros(n + 1, np.int32)
-    rp[1:] = np.cumsum([len(c) for c in rows])
-    col = np.concatenate(rows).astype(np.int32)
-    val = rng.standard_normal(len(col))
-    x = rng.standard_normal(n)
-    solver.set_matrix(rp, col, val)
-    assert H.same_bits_or_both_nan(solver.spmv(x), H.o_spmv(rp, col, val, x))
-
-
-def test_spmv_empty_rows_and_tiny(solver):
-    rp = np.array([0, 0, 2, 2, 3], np.int32)
-    col = np.array([0, 3, 1], np.int32)
-    val = np.array([2.0, -1.0, 5.0])
-    x = np.array([1.0, 2.0, 3.0, 4.0])
-    solver.set_matrix(rp, col, val)
-    assert H.same_bits_or_both_nan(solver.spmv(x), H.o_spmv(rp, col, val, x))
-
-
-def test_spmv_f32_bit_exact(solver):
-    rp, col, val = cgx.random_spd(20000, 16, 11, f32=True)
-    x = np.random.default_rng(1).standard_normal(20000).astype(np.float32)
-    solver.set_matrix(rp, col, val)
-    y = solver.spmv(x)
-    assert np.array_equal(y.view(np.uint32), H.o_spmv_f32(rp, col, val, x).view(np.uint32))
-
-
-@pytest.mark.parametrize("dma", ["0", "1", "2", "4", "5", "8", "1x", "1w", "1c", "1r0", "1b4", "1w8", "1v0", "1v2", "1v4"])
-def test_spmv_c3_full_size_bit_exact(dma, monkeypatch):
-    """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
-    bit-exact against the oracle at full size (default and pipelined kernels)."""
-    monkeypatch.setenv("CGX_SPMV_DMA", dma[0])
-    if dma.endswith("c"):
-        monkeypatch.setenv("CGX_LAYOUT", "csr")
-    if dma.endswith("r0"):
-        monkeypatch.setenv("CGX_DC_RLEN", "0")
-    if dma.endswith("b4"):
-        monkeypatch.setenv("CGX_DC_BITS", "4")
-    if dma.endswith("v0"):
-        monkeypatch.setenv("CGX_DC_VALS", "0")
-    if dma.endswith("v2") or dma.endswith("v4"):
-        monkeypatch.setenv("CGX_VI_BPW", dma[-1])
-    if dma.endswith("w8"):
-        monkeypatch.setenv("CGX_SPMV_WPB", "8")
-    if dma.endswith("x"):
-        monkeypatch.setenv("CGX_SPMV_XCD", "1")
-    if dma.endswith("w"):
-        monkeypatch.setenv("CGX_SPMV_CAPW", "456")
-    rp, col, val = cgx.laplacian3d(216, 216, 216)
-    x = np.random.default_rng(2).standard_normal(len(rp) - 1)
-    with cgx.Solver(0) as s:
-        s.set_matrix(rp, col, val)
-        # dictionary-coded columns on the default kernel (7 offsets), CSR otherwise
-        assert s.info()["n_dict"] == (7 if dma in ("1", "1x", "1r0", "1b4", "1w8", "1v0", "1v2", "1v4") else 0)
-        assert s.info()["dict_vals"] == (1 if dma in ("1", "1x", "1b4", "1v2", "1v4") else 0)
-        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+            assert got == want, (got, want)
+        assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"])
 
 
 def banded_spd(n, offsets, seed, f32=False):
@@ -248,93 +146,9 @@ def banded_spd(n, offsets, seed, f32=False):
     return rp, c.astype(np.int32), v
 
 
-def expect_dict(rp, col, val, vi_ok=True):
-    """(n_dict, dict_vals) the solver should pick for a CSR matrix: coded
-    columns for <= 256 distinct col - row offsets; value-indexed pairs when
-    also <= 64 distinct (offset, value bit pattern) pairs and every row has
-    <= 255 entries (the byte row lengths the pair kernel needs)."""
-    rp, col = np.asarray(rp), np.asarray(col)
-    n = len(rp) - 1
-    if len(col) == 0:
-        return 0, 0
-    off = col.astype(np.int64) - np.repeat(np.arange(n), np.diff(rp))
-    noff = len(np.unique(off))
-    if noff > 256:
-        return 0, 0
-    bits = np.asarray(val).view(np.uint64 if np.asarray(val).dtype == np.float64 else np.uint32)
-    npair = np.unique(np.stack([off, bits.astype(np.int64)]), axis=1).shape[1]
-    if vi_ok and npair <= 64 and np.diff(rp).max() <= 255:
-        return npair, 1
-    return noff, 0
-
-
-@pytest.mark.parametrize("bits", ["4", "8"])
-@pytest.mark.parametrize("rlen", ["1", "0"])
-@pytest.mark.parametrize("capw", ["", "328", "456"])
-def test_dictionary_coded_columns_bit_exact(capw, rlen, bits, monkeypatch):
-    """CSR-DC (k_spmv_dc): selected exactly when the matrix has <= 256
-    distinct column offsets col - row, and bit-identical to the oracle's
-    sequential row sums (fp64 and fp32, 64- and 256-entry dictionaries,
-    adaptive 328/512 windows; 456 keeps plain CSR; row bounds from byte row
-    lengths or from row_ptr; nibble codes for <= 16 offsets or bytes)."""
-    monkeypatch.setenv("CGX_DC_BITS", bits)
-    monkeypatch.setenv("CGX_DC_RLEN", rlen)
-    if capw:
-        monkeypatch.setenv("CGX_SPMV_CAPW", capw)
-    rng = np.random.default_rng(5)
-    cases = [("lap3d_12", None), ("lap2d_32", None), ("dense128", None)]
-    with cgx.Solver(0) as s:
-        for name, _ in cases:
-            g = H.load_golden(name)
-            s.set_matrix(g["row_ptr"], g["col"], g["val"])
-            nd, vi = s.info()["n_dict"], s.info()["dict_vals"]
-            want, want_vi = expect_dict(g["row_ptr"], g["col"], g["val"],
-                                        vi_ok=rlen == "1")
-            assert (nd, vi) == ((0, 0) if capw == "456" else (want, want_vi)), name
-            x = rng.standard_normal(len(g["row_ptr"]) - 1)
-            assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(g["row_ptr"], g["col"], g["val"], x))
-            assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"])
-        # 127 positive offsets -> 255 distinct: the 256-entry dictionary
-        offs = sorted(rng.choice(np.arange(1, 3000), 127, replace=False).tolist())
-        rp, col, val = banded_spd(5000, offs, 7)
-        s.set_matrix(rp, col, val)
-        assert s.info()["n_dict"] == (0 if capw == "456" else 255)
-        x = rng.standard_normal(5000)
-        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
-        # 257 distinct offsets: stays plain CSR, still bit-exact
-        rp, col, val = banded_spd(3000, list(range(1, 129)), 8)
-        s.set_matrix(rp, col, val)
-        assert s.info()["n_dict"] == 0
-        x = rng.standard_normal(3000)
-        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
-        # 256 distinct offsets, one row of 256 entries (> 255: row_ptr bounds),
-        # empty rows, non-symmetric
-        n = 700
-        rows = [list(range(0, 256))] + [[] if r % 5 == 0 else [r] for r in range(1, n)]
-        rp = np.zeros(n + 1, dtype=np.int32)
-        rp[1:] = np.cumsum([len(c) for c in rows])
-        col = np.array([c for cs in rows for c in cs], dtype=np.int32)
-        val = rng.standard_normal(len(col))
-        s.set_matrix(rp, col, val)
-        assert s.info()["n_dict"] == (0 if capw == "456" else 256)
-        x = rng.standard_normal(n)
-        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
-        # fp32 banded
-        rp, col, v32 = banded_spd(6000, [1, 77, 500], 9, f32=True)
-        s.set_matrix(rp, col, v32)
-        assert s.info()["n_dict"] == 7  # fp32 windows are not resized: CGX_SPMV_CAPW is fp64-only
-        x32 = rng.standard_normal(6000).astype(np.float32)
-        assert np.array_equal(s.spmv(x32).view(np.uint32),
-                              H.o_spmv_f32(rp, col, v32, x32).view(np.uint32))
-
-
-@pytest.mark.parametrize("seed", range(8))
-def test_dictionary_coded_random_patterns(seed):
-    """Randomised sparsity patterns for the coded-column encoder and kernel:
-    n not a multiple of 64, empty and ragged rows (0-40 entries), 1-256
-    distinct offsets drawn from a random band, unsorted offset draws (the
-    CSR columns are sorted per row); the SpMV is bit-identical to the oracle,
-    and a pattern with 257 offsets stays plain CSR."""
+def random_pattern(seed, small_values):
+    """n not a multiple of 64 or 512, empty and ragged rows (0-40 entries),
+    1-257 distinct offsets from a random band, columns sorted per row."""
     rng = np.random.default_rng(100 + seed)
     n = int(rng.integers(1, 9000))
     nd = int(rng.integers(1, 258))
@@ -348,90 +162,162 @@ def test_dictionary_coded_random_patterns(seed):
     rp = np.zeros(n + 1, dtype=np.int32)
     rp[1:] = np.cumsum([len(c) for c in rows])
     col = np.concatenate(rows).astype(np.int32) if rp[-1] else np.zeros(0, np.int32)
-    # odd seeds: values from a small set (value-indexed pairs when <= 64
-    # (offset, value) pairs), even seeds: all distinct
-    if seed % 2:
+    if small_values:  # value-indexed pairs when <= 255 (offset, value) pairs
         val = rng.choice(np.array([-1.0, 2.5, -0.0, 0.0, 1e-300, -3.25]), size=len(col))
     else:
         val = rng.standard_normal(len(col))
-    x = rng.standard_normal(n)
-    with cgx.Solver(0) as s:
+    return rp, col, val, rng.standard_normal(n)
+
+
+@pytest.mark.parametrize("layout", ["auto", "csr", "dc", "vi"])
+@pytest.mark.parametrize("seed", range(8))
+def test_spmv_random_patterns(seed, layout):
+    """Randomised patterns through each layout's encoder and kernel: the
+    documented layout is picked and y is bit-identical to the oracle (signed
+    zeros and a denormal-range value keep their bit patterns)."""
+    rp, col, val, x = random_pattern(seed, small_values=seed % 2 == 1)
+    with cgx.Solver(0, layout=layout) as s:
         s.set_matrix(rp, col, val)
-        assert (s.info()["n_dict"], s.info()["dict_vals"]) == expect_dict(rp, col, val)
+        assert s.info()["layout_name"] == expect_layout(rp, col, val, layout)
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
 
 
-@pytest.mark.parametrize("bits,bpw", [("8", "1"), ("8", "2"), ("8", "4"), ("4", "1")])
-@pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_value_indexed_pairs_bit_exact(bits, bpw, dtype, monkeypatch):
-    """CSR-VI: (offset, value) pair codes -- the SpMV reads no val stream.
-    Selected for constant-coefficient stencils and small value sets, off with
-    CGX_DC_VALS=0 or > 64 pairs; y bit-identical to the oracle in every case
-    (signed zeros and a denormal-range value keep their bit patterns; nibble
-    codes for <= 16 pairs)."""
-    monkeypatch.setenv("CGX_DC_BITS", bits)
-    monkeypatch.setenv("CGX_VI_BPW", bpw)
-    rng = np.random.default_rng(77)
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_spmv_long_and_empty_rows(layout):
+    """Rows longer than one LDS window (dense rows: the chunked path; in VI
+    the wide-row slices), empty rows, a 4-row matrix: bit-exact."""
+    n = 6000
+    rng = np.random.default_rng(5)
+    rows = [np.arange(n) if i in (0, 1, 2500, n - 1) else
+            np.unique(np.concatenate([[max(i - 1, 0), i, min(i + 1, n - 1)], rng.integers(0, n, 4)]))
+            for i in range(n)]
+    rp = np.zeros(n + 1, np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    x = rng.standard_normal(n)
+    with cgx.Solver(0, layout=layout) as s:
+        for val in (rng.standard_normal(len(col)),
+                    rng.choice(np.array([-1.0, 4.0]), size=len(col))):  # pairs: VI wide rows
+            s.set_matrix(rp, col, val)
+            assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        rp = np.array([0, 0, 2, 2, 3], np.int32)
+        col = np.array([0, 3, 1], np.int32)
+        val = np.array([2.0, -1.0, 5.0])
+        x = np.array([1.0, 2.0, 3.0, 4.0])
+        s.set_matrix(rp, col, val)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_spmv_f32_bit_exact(layout):
+    rng = np.random.default_rng(1)
+    with cgx.Solver(0, layout=layout) as s:
+        rp, col, val = cgx.random_spd(20000, 16, 11, f32=True)
+        x = rng.standard_normal(20000).astype(np.float32)
+        s.set_matrix(rp, col, val)
+        assert same32(s.spmv(x), H.o_spmv_f32(rp, col, val, x))
+        g = H.load_golden("lap3d_12")
+        v = g["val"].astype(np.float32)
+        s.set_matrix(g["row_ptr"], g["col"], v)
+        assert s.info()["layout_name"] == expect_layout(g["row_ptr"], g["col"], v, layout)
+        x = rng.standard_normal(len(g["row_ptr"]) - 1).astype(np.float32)
+        assert same32(s.spmv(x), H.o_spmv_f32(g["row_ptr"], g["col"], v, x))
+        rp, col, v32 = banded_spd(6000, [1, 77, 500], 9, f32=True)
+        s.set_matrix(rp, col, v32)
+        x = rng.standard_normal(6000).astype(np.float32)
+        assert same32(s.spmv(x), H.o_spmv_f32(rp, col, v32, x))
+
+
+def test_layout_selection_limits():
+    """The documented limits of each layout: 255 offsets -> DC (256-entry
+    dictionary); 257 offsets -> CSR; 255 pairs -> VI, 256 pairs -> DC; a row
+    of 256 entries -> CSR (DC's byte row lengths), bit-exact throughout."""
+    rng = np.random.default_rng(5)
     with cgx.Solver(0) as s:
-        for name in ("lap3d_12", "lap2d_32"):
-            g = H.load_golden(name)
-            v = g["val"].astype(np.float32) if dtype == "f32" else g["val"]
-            s.set_matrix(g["row_ptr"], g["col"], v)
-            assert (s.info()["n_dict"], s.info()["dict_vals"]) == expect_dict(g["row_ptr"], g["col"], v)
-            assert s.info()["dict_vals"] == 1
-            x = rng.standard_normal(len(g["row_ptr"]) - 1)
-            if dtype == "f32":
-                x = x.astype(np.float32)
-                assert np.array_equal(s.spmv(x).view(np.uint32),
-                                      H.o_spmv_f32(g["row_ptr"], g["col"], v, x).view(np.uint32))
-            else:
-                assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(g["row_ptr"], g["col"], v, x))
-        # a banded matrix whose values per offset take a few values: 5 offsets
-        # x 12 values = 60 pairs (VI), then 65 pairs (offset codes only)
-        for nv, want_vi in ((12, 1), (13, 0)):
-            n = 5000
+        offs = sorted(rng.choice(np.arange(1, 3000), 127, replace=False).tolist())
+        rp, col, val = banded_spd(5000, offs, 7)
+        s.set_matrix(rp, col, val)
+        assert (s.info()["layout_name"], s.info()["n_dict"]) == ("dc", 255)
+        x = rng.standard_normal(5000)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        rp, col, val = banded_spd(3000, list(range(1, 129)), 8)
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == "csr"
+        x = rng.standard_normal(3000)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        # 5 offsets x 51 values = 255 pairs (VI), 5 x 52 = 260 (DC)
+        for nv, want in ((51, "vi"), (52, "dc")):
+            n = 20000
             rp, col, _ = banded_spd(n, [1, 300], 3)
             vals = np.linspace(-2, 2, nv)
             off = col - np.repeat(np.arange(n), np.diff(rp))
             val = vals[(np.arange(len(col)) * 7 + off) % nv]
-            if dtype == "f32":
-                val = val.astype(np.float32)
             s.set_matrix(rp, col, val)
-            nd, vi = s.info()["n_dict"], s.info()["dict_vals"]
-            assert (nd, vi) == expect_dict(rp, col, val)
-            assert vi == want_vi
+            assert s.info()["layout_name"] == want
             x = rng.standard_normal(n)
-            if dtype == "f32":
-                x = x.astype(np.float32)
-                assert np.array_equal(s.spmv(x).view(np.uint32),
-                                      H.o_spmv_f32(rp, col, val, x).view(np.uint32))
-            else:
-                assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
-    monkeypatch.setenv("CGX_DC_VALS", "0")
-    g = H.load_golden("lap3d_12")
+            assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        n = 700
+        rows = [list(range(0, 256))] + [[] if r % 5 == 0 else [r] for r in range(1, n)]
+        rp = np.zeros(n + 1, dtype=np.int32)
+        rp[1:] = np.cumsum([len(c) for c in rows])
+        col = np.array([c for cs in rows for c in cs], dtype=np.int32)
+        val = rng.standard_normal(len(col))
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == "csr"
+        x = rng.standard_normal(n)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+
+
+def test_bad_column_rejected():
+    """A column outside [0, n) would be an out-of-bounds device gather: the
+    upload refuses it on the host."""
     with cgx.Solver(0) as s:
-        s.set_matrix(g["row_ptr"], g["col"], g["val"])
-        assert (s.info()["n_dict"], s.info()["dict_vals"]) == (7, 0)
+        with pytest.raises(cgx.CgxError):
+            s.set_matrix(np.array([0, 1, 2], np.int32), np.array([0, 2], np.int32), np.ones(2))
+        with pytest.raises(cgx.CgxError):
+            s.set_matrix(np.array([0, 2, 1], np.int32), np.array([0, 1], np.int32), np.ones(2))
 
 
-def test_dictionary_coded_cg_identical_to_csr(monkeypatch):
-    """The coded layout changes only how columns are stored: a CG run is
-    bit-identical to the plain-CSR run (x and the r.r history)."""
-    g = H.load_golden("lap3d_12")
-    out = {}
-    for layout in ("csr", "auto"):
-        if layout == "csr":
-            monkeypatch.setenv("CGX_LAYOUT", "csr")
-        else:
-            monkeypatch.delenv("CGX_LAYOUT", raising=False)
-        with cgx.Solver(0) as s:
-            s.set_matrix(g["row_ptr"], g["col"], g["val"])
-            assert (s.info()["n_dict"] > 0) == (layout == "auto")
-            s.set_rhs(g["b"])
-            s.run(40)
-            out[layout] = (s.x(), s.history(41))
-    assert H.same_bits_or_both_nan(out["csr"][0], out["auto"][0])
-    assert H.same_bits_or_both_nan(out["csr"][1], out["auto"][1])
+@pytest.mark.parametrize("layout", ["auto", "csr", "dc", "vi"])
+def test_spmv_c3_full_size_bit_exact(layout):
+    """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
+    bit-exact against the oracle at full size in every layout; the automatic
+    choice is VI (7 pairs, 8 codes per row), found from the sampled rows
+    without an exact host scan."""
+    rp, col, val = cgx.laplacian3d(216, 216, 216)
+    x = np.random.default_rng(2).standard_normal(len(rp) - 1)
+    with cgx.Solver(0, layout=layout) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["layout_name"] == {"auto": "vi"}.get(layout, layout)
+        assert i["encode_fallback"] == 0 and i["nt"] == 1
+        if i["layout_name"] == "vi":
+            assert i["n_dict"] == 7 and i["row_width"] == 8
+            assert i["spmv_grid"] == -(-(len(rp) - 1) // 512)
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+
+
+@pytest.mark.parametrize("layout", ["auto", "csr", "dc"])
+def test_c2_full_size(layout):
+    """BASELINE config C2 (2-D 5-pt 1000^2, the cache-resident 328-entry
+    window case): bit-exact SpMV at full size and solve(1e-8) reaches a true
+    relative residual below tol."""
+    rp, col, val = cgx.laplacian2d(1000, 1000)
+    n = len(rp) - 1
+    x = np.random.default_rng(7).standard_normal(n)
+    with cgx.Solver(0, layout=layout) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["layout_name"] == {"auto": "vi"}.get(layout, layout)
+        assert i["nt"] == 0  # the whole iteration fits the Infinity Cache
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        b = np.ones(n)
+        s.set_rhs(b)
+        its = s.run(6000, 1e-8)
+        xs = s.x()
+    r = b - H.o_spmv(rp, col, val, xs)
+    assert np.linalg.norm(r) <= 1.5e-8 * np.linalg.norm(b)
+    assert its < 6000
 
 
 # -------------------------------------------------------- mv_ops.h op list
@@ -461,6 +347,35 @@ def test_mv_ops_reference_op_list(name, exact_env):
     assert H.same_bits_or_both_nan(cgx.mv_values(out), g["ops"]["vec_sub"])
     assert out.contents.size == g["n"] and out.contents.nnz == g["n"]
     L.cgx_free_mv_deep(out)
+
+
+def test_mv_mult_matrix_residency():
+    """the op-level drop-in keeps A on the device.  The
+    reference's conj_grad calls mv_mult once per iteration on the same A
+    (cg.c:111): the second call reuses the upload; changing a value in place
+    (same pointers) or passing another matrix uploads again; y stays
+    bit-exact throughout."""
+    rp, col, val = cgx.laplacian3d(40, 30, 20)
+    x = np.random.default_rng(3).standard_normal(len(rp) - 1)
+    A = cgx.Mv(val, col, rp)
+    b = cgx.Mv(x)
+    u0, r0 = cgx.ops_counters()
+    y1 = cgx.mv_mult(A, b)
+    y2 = cgx.mv_mult(A, b)
+    u1, r1 = cgx.ops_counters()
+    assert (u1 - u0, r1 - r0) == (1, 1)
+    assert H.same_bits_or_both_nan(y1, H.o_spmv(rp, col, val, x))
+    assert H.same_bits_or_both_nan(y2, y1)
+    A.values[17] = 2.5  # in place: same pointers, new contents
+    y3 = cgx.mv_mult(A, b)
+    u2, r2 = cgx.ops_counters()
+    assert (u2 - u1, r2 - r1) == (1, 0)
+    assert H.same_bits_or_both_nan(y3, H.o_spmv(rp, col, A.values, x))
+    # conj_grad after mv_mult on the same A: no second upload
+    x_cg = cgx.conj_grad(5, A, b)
+    u3, r3 = cgx.ops_counters()
+    assert (u3 - u2, r3 - r2) == (0, 1)
+    assert np.all(np.isfinite(x_cg))
 
 
 def test_vec_sub_in_place_alias():
@@ -547,29 +462,69 @@ def test_solve_tolerance_matches_oracle(name, exact_env):
         assert H.same_bits_or_both_nan(x, x_o)
 
 
-def test_solver_history_exact(solver):
+@pytest.mark.parametrize("layout", ["csr", "dc", "vi", "panel"])
+def test_exact_mode_history_identical_across_layouts(layout):
+    """Exact mode (sequential dots): x and the r.r history equal the oracle's
+    bit for bit in every layout -- the layouts differ only in how A is
+    stored."""
     g = H.load_golden("lap3d_12")
-    solver.set_mode(cgx.CGX_MODE_EXACT)
-    solver.set_matrix(g["row_ptr"], g["col"], g["val"])
-    solver.set_rhs(g["b"])
-    its = solver.run(40)
-    assert its == 41
-    _, hist = H.o_conj_grad(40, g["row_ptr"], g["col"], g["val"], g["b"])
-    assert H.same_bits_or_both_nan(solver.history(41), hist)
-    solver.set_mode(cgx.CGX_MODE_FAST)
-
-
-@pytest.mark.parametrize("graph", ["0", "1"])
-def test_graph_and_eager_agree(graph, monkeypatch):
-    monkeypatch.setenv("CGX_GRAPH", graph)
-    g = H.load_golden("lap2d_32")
-    with cgx.Solver(0) as s:
+    with cgx.Solver(0, mode=cgx.CGX_MODE_EXACT, layout=layout) as s:
         s.set_matrix(g["row_ptr"], g["col"], g["val"])
         s.set_rhs(g["b"])
-        assert s.run(50) == 51
-        x = s.x()
-    x_ref, _ = H.o_conj_grad(50, g["row_ptr"], g["col"], g["val"], g["b"])
-    assert rel(x, x_ref) <= FAST_RTOL
+        assert s.run(40) == 41
+        x, h = s.x(), s.history(41)
+    x_ref, hist = H.o_conj_grad(40, g["row_ptr"], g["col"], g["val"], g["b"])
+    assert H.same_bits_or_both_nan(h, hist)
+    assert H.same_bits_or_both_nan(x, x_ref)
+
+
+@pytest.mark.parametrize("layout", ["auto", "csr", "dc", "vi"])
+def test_fast_mode_reproducible_and_stops(layout):
+    """Fast mode in each layout: within FAST_RTOL of the reference order,
+    bit-reproducible run to run (fixed-order reductions, no fp64 atomics),
+    the tolerance stop within one iteration of the oracle's, the stop
+    iteration's x update applied once (maxit 0, 1, 37 and tol stops that
+    land inside a replayed batch)."""
+    cases = [H.random_spd(30000, 9, seed=21)]
+    g = H.load_golden("lap3d_12")
+    cases.append((g["row_ptr"], g["col"], g["val"], g["b"]))
+    for rp, col, val, b in cases:
+        with cgx.Solver(0, layout=layout) as s:
+            s.set_matrix(rp, col, val)
+            for maxit, tol in [(0, 0.0), (1, 0.0), (37, 0.0), (2000, 1e-9), (2000, 1e-6)]:
+                runs = []
+                for _ in range(2):
+                    s.set_rhs(b)
+                    its = s.run(maxit, tol)
+                    runs.append((its, s.x(), s.history(its)))
+                assert runs[0][0] == runs[1][0]
+                assert H.same_bits_or_both_nan(runs[0][1], runs[1][1])
+                assert H.same_bits_or_both_nan(runs[0][2], runs[1][2])
+                if tol == 0.0:
+                    assert runs[0][0] == maxit + 1
+                    x_ref, _ = H.o_conj_grad(maxit, rp, col, val, b)
+                    assert rel(runs[0][1], x_ref) <= FAST_RTOL
+                else:
+                    _, its_o, _ = H.o_solve(maxit, tol, rp, col, val, b)
+                    assert abs(runs[0][0] - its_o) <= 1
+                    r = b - H.o_spmv(rp, col, val, runs[0][1])
+                    assert np.linalg.norm(r) <= 1.01 * tol * np.linalg.norm(b)
+
+
+def test_graph_and_eager_agree():
+    """The hipGraph-replayed iterations and the eager launches are the same
+    kernels in the same order: bit-identical x and history."""
+    g = H.load_golden("lap2d_32")
+    out = []
+    for graph in (True, False):
+        with cgx.Solver(0) as s:
+            s.set_matrix(g["row_ptr"], g["col"], g["val"])
+            s.set_rhs(g["b"])
+            s.bench_prepare(0)
+            s.bench_run(32, graph=graph)
+            out.append(s.x())
+    assert H.same_bits_or_both_nan(out[0], out[1])
+    assert np.all(np.isfinite(out[0]))
 
 
 @pytest.mark.parametrize("name", ["lap2d_32", "lap3d_12", "rand_spd_2000", "dense128"])
@@ -626,133 +581,9 @@ def test_empty_system():
     L.cgx_free_mv_deep(out)
 
 
-@pytest.mark.parametrize("ticket", ["0", "1"])
-@pytest.mark.parametrize("fuse", ["0", "1"])
-@pytest.mark.parametrize("dma", ["0", "1"])
-def test_reduction_paths_match_oracle_and_reproduce(ticket, fuse, dma, monkeypatch):
-    """Finalize kernels vs the in-kernel ticket reduction (register-staged
-    SpMV only), with and without the fused p-update, on both SpMV kernels:
-    all within FAST_RTOL of the reference order, and each bit-reproducible
-    run to run (deterministic reductions, no fp64 atomics)."""
-    if ticket == "1" and dma == "1":
-        pytest.skip("the LDS-DMA SpMV has no ticket epilogue (solver ignores CGX_TICKET)")
-    monkeypatch.setenv("CGX_TICKET", ticket)
-    monkeypatch.setenv("CGX_FUSE_XPAY", fuse)
-    monkeypatch.setenv("CGX_SPMV_DMA", dma)
-    rp, col, val, b = H.random_spd(30000, 9, seed=12)
-    x_ref, _ = H.o_conj_grad(60, rp, col, val, b)
-    xs, hs = [], []
-    with cgx.Solver(0) as s:
-        s.set_matrix(rp, col, val)
-        for _ in range(2):
-            s.set_rhs(b)
-            assert s.run(60) == 61
-            xs.append(s.x())
-            hs.append(s.history(61))
-        its = s.run(1000, 1e-9)
-        x_tol = s.x()
-    assert rel(xs[0], x_ref) <= FAST_RTOL
-    assert H.same_bits_or_both_nan(xs[0], xs[1]) and H.same_bits_or_both_nan(hs[0], hs[1])
-    _, its_o, _ = H.o_solve(1000, 1e-9, rp, col, val, b)
-    assert abs(its - its_o) <= 1
-    r = b - H.o_spmv(rp, col, val, x_tol)
-    assert np.linalg.norm(r) <= 1.01e-9 * np.linalg.norm(b)
-
-
-def test_ticket_large_grid_and_tiny(monkeypatch):
-    """Ticket reduction across > kTicketGroup^2 workgroups (two full levels)
-    and with a single workgroup."""
-    monkeypatch.setenv("CGX_TICKET", "1")
-    monkeypatch.setenv("CGX_SPMV_DMA", "0")
-    rp, col, val = cgx.laplacian3d(160, 160, 160)   # 4.1 M rows, 64 K SpMV workgroups
-    b = np.random.default_rng(3).standard_normal(len(rp) - 1)
-    with cgx.Solver(0) as s:
-        s.set_matrix(rp, col, val)
-        s.set_rhs(b)
-        s.run(5)
-        x = s.x()
-    x_ref, _ = H.o_conj_grad(5, rp, col, val, b)
-    assert rel(x, x_ref) <= FAST_RTOL
-    g = H.load_golden("kat_tridiag10")
-    with cgx.Solver(0) as s:
-        s.set_matrix(g["row_ptr"], g["col"], g["val"])
-        s.set_rhs(g["b"])
-        s.run(3)
-        assert rel(s.x(), g["iters"][3]) <= FAST_RTOL
-
-
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_sell_layout_bit_exact(fuse, monkeypatch):
-    """SELL-64 internal layout: SpMV bit-exact (padding after each row's
-    entries), CG within tolerance; irregular matrices fall back to CSR."""
-    monkeypatch.setenv("CGX_LAYOUT", "sell")
-    monkeypatch.setenv("CGX_FUSE_XPAY", fuse)
-    with cgx.Solver(0) as s:
-        for name in ["lap3d_12", "lap2d_32", "dense128", "rand_spd_2000", "kat_tridiag10"]:
-            g = H.load_golden(name)
-            s.set_matrix(g["row_ptr"], g["col"], g["val"])
-            assert H.same_bits_or_both_nan(s.spmv(g["b"]), g["ops"]["mv_mult"]), name
-            s.set_rhs(g["b"])
-            it = max(k for k in g["iters"] if not np.any(np.isnan(g["iters"][k])))
-            s.run(it)
-            assert rel(s.x(), g["iters"][it]) <= FAST_RTOL, name
-        rp, col, val = cgx.laplacian3d(70, 60, 50)
-        x = np.random.default_rng(6).standard_normal(len(rp) - 1)
-        s.set_matrix(rp, col, val)
-        assert s.info()["spmv_iter_bytes"] < s.info()["spmv_bytes"] + 4 * len(x) * 8
-        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
-        rp32, col32, v32 = cgx.random_spd(5000, 40, 9, f32=True)
-        x32 = np.random.default_rng(2).standard_normal(5000).astype(np.float32)
-        s.set_matrix(rp32, col32, v32)
-        assert np.array_equal(s.spmv(x32).view(np.uint32),
-                              H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
-
-
-@pytest.mark.parametrize("dma", ["0", "1"])
-def test_deferred_x_bit_identical(dma, monkeypatch):
-    """CGX_XDEFER folds x += alpha p into the p-update (one read of p less per
-    iteration).  Same per-element roundings and reductions, so x, the r.r
-    history and the stop iteration are bit-identical to the standard HS path,
-    for fixed iteration counts (max_iter stop) and for tolerance stops that
-    land inside a replayed batch (the stop iteration's x update must still
-    happen, later ones must not)."""
-    monkeypatch.setenv("CGX_SPMV_DMA", dma)
-    cases = [H.random_spd(30000, 9, seed=21), None]
-    g = H.load_golden("lap3d_12")
-    cases[1] = (g["row_ptr"], g["col"], g["val"], g["b"])
-    for rp, col, val, b in cases:
-        out = {}
-        for xd in ("0", "1", "fold", "foldpf"):
-            # "fold": CGX_FOLD, the alpha/beta/stop steps inside the vector
-            # kernels (no finalize launches) -- same scalars bit for bit;
-            # "foldpf": the same with the first loads issued before the
-            # partial sums (CGX_VEC_PF)
-            monkeypatch.setenv("CGX_XDEFER", "0" if xd == "0" else "1")
-            monkeypatch.setenv("CGX_FOLD", "1" if xd.startswith("fold") else "0")
-            monkeypatch.setenv("CGX_VEC_PF", "1" if xd == "foldpf" else "0")
-            with cgx.Solver(0) as s:
-                s.set_matrix(rp, col, val)
-                res = []
-                for maxit, tol in [(0, 0.0), (1, 0.0), (37, 0.0), (2000, 1e-9), (2000, 1e-6)]:
-                    s.set_rhs(b)
-                    its = s.run(maxit, tol)
-                    res.append((its, s.x(), s.history(its)))
-                out[xd] = res
-        for other in ("1", "fold", "foldpf"):
-            for (i0, x0, h0), (i1, x1, h1) in zip(out["0"], out[other]):
-                assert i0 == i1, other
-                assert H.same_bits_or_both_nan(x0, x1), other
-                assert H.same_bits_or_both_nan(h0, h1), other
-    x_ref, _ = H.o_conj_grad(37, g["row_ptr"], g["col"], g["val"], g["b"])
-    assert rel(out["1"][2][1], x_ref) <= FAST_RTOL
-
-
-@pytest.mark.parametrize("xd", ["0", "1", "fold"])
-def test_history_after_buffer_growth(xd, monkeypatch):
+def test_history_after_buffer_growth():
     """Cached hipGraphs are dropped when a longer run reallocates the r.r
     history buffer (regression: r01, the graph kept the freed pointer)."""
-    monkeypatch.setenv("CGX_XDEFER", "0" if xd == "0" else "1")
-    monkeypatch.setenv("CGX_FOLD", "1" if xd == "fold" else "0")
     rp, col, val, b = H.random_spd(30000, 9, seed=21)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
@@ -772,72 +603,88 @@ def test_history_after_buffer_growth(xd, monkeypatch):
 
 def test_stream_ceilings():
     """The on-box ceilings bench.py reports beside the SpMV roofline: sane
-    fractions of the 8 TB/s spec, reads faster than the triad's mix."""
+    fractions of the 8 TB/s spec."""
     t = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_TRIAD)
     r = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_READ)
     assert 2000.0 < t < 8000.0 and 2000.0 < r < 8000.0
 
 
-@pytest.mark.parametrize("kb", ["8", "64", "64w"])
-def test_column_panels_bit_exact(kb, monkeypatch):
-    """Column-panel layout (CGX_LAYOUT=panel): rows continue their sequential
-    sums panel after panel, so SpMV stays bit-exact in fp64 and fp32, rows
-    longer than a window (dense rows crossing every panel) and rows with no
-    entry in a panel included; CG matches the oracle."""
-    monkeypatch.setenv("CGX_LAYOUT", "panel")
-    monkeypatch.setenv("CGX_PANEL_KB", kb.rstrip("w"))
-    if kb.endswith("w"):
-        monkeypatch.setenv("CGX_PANEL_WIN512", "1")
-    rp, col, val, b = H.random_spd(30000, 9, seed=31)
+def test_spmv_only_bench():
+    """CGX_BENCH_SPMV_ONLY: back-to-back SpMVs, the iteration state untouched."""
+    rp, col, val = cgx.laplacian3d(64, 64, 64)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
-        assert s.info()["n_panels"] > 1
+        s.set_rhs(np.ones(len(rp) - 1))
+        s.bench_prepare(2)
+        ms, sp = s.bench_run(10, graph=False, spmv_events=True, spmv_only=True)
+        assert ms > 0 and 0 < sp <= ms / 10 * 1.01
+        ms2, _ = s.bench_run(10)
+        assert ms2 > 0
+
+
+# ------------------------------------------------------------ column panels
+
+def rows_with_dense(n, dense, seed):
+    """Tridiagonal band + 4 random columns per row, plus fully dense rows."""
+    rng = np.random.default_rng(seed)
+    r = np.repeat(np.arange(n, dtype=np.int64), 7)
+    c = np.stack([np.arange(n) - 1, np.arange(n), np.arange(n) + 1] +
+                 [rng.integers(0, n, n) for _ in range(4)], axis=1).reshape(-1)
+    keep = (c >= 0) & (c < n)
+    r, c = r[keep], c[keep]
+    for d in dense:
+        r = np.concatenate([r, np.full(n, d)])
+        c = np.concatenate([c, np.arange(n)])
+    key = np.unique(r * n + c)
+    r, c = key // n, key % n
+    rp = np.zeros(n + 1, np.int32)
+    np.add.at(rp, r + 1, 1)
+    rp = np.cumsum(rp).astype(np.int32)
+    return rp, c.astype(np.int32), rng.standard_normal(len(c)), rng.standard_normal(n)
+
+
+def test_column_panels_bit_exact():
+    """Column-panel layout: rows continue their sequential sums panel after
+    panel, so SpMV stays bit-exact in fp64 and fp32, rows longer than a window
+    (dense rows crossing every panel) included; CG matches the oracle."""
+    rp, col, val = cgx.random_spd(300000, 9, 31)
+    b = np.random.default_rng(31).standard_normal(300000)
+    with cgx.Solver(0, layout="panel") as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == "panel" and s.info()["n_panels"] > 1
         assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
         s.set_rhs(b)
         s.run(40)
         x_ref, _ = H.o_conj_grad(40, rp, col, val, b)
         assert rel(s.x(), x_ref) <= FAST_RTOL
-        s.set_rhs(b)
-        its = s.run(2000, 1e-9)
-        _, its_o, _ = H.o_solve(2000, 1e-9, rp, col, val, b)
-        assert abs(its - its_o) <= 1
-        # dense rows (long-row path) crossing all panels
-        n = 6000
-        rng = np.random.default_rng(9)
-        rows = [np.arange(n) if i in (0, 17, n - 1) else
-                np.unique(np.concatenate([[max(i - 1, 0), i, min(i + 1, n - 1)],
-                                          rng.integers(0, n, 4)])) for i in range(n)]
-        rp2 = np.zeros(n + 1, np.int32)
-        rp2[1:] = np.cumsum([len(c) for c in rows])
-        col2 = np.concatenate(rows).astype(np.int32)
-        val2 = rng.standard_normal(len(col2))
-        x2 = rng.standard_normal(n)
+        rp2, col2, val2, x2 = rows_with_dense(600000, (0, 17, 599999), 9)
         s.set_matrix(rp2, col2, val2)
+        assert s.info()["n_panels"] > 1
         assert H.same_bits_or_both_nan(s.spmv(x2), H.o_spmv(rp2, col2, val2, x2))
-        rp32, col32, v32 = cgx.random_spd(20000, 40, 9, f32=True)
-        x32 = np.random.default_rng(2).standard_normal(20000).astype(np.float32)
+        rp32, col32, v32 = cgx.random_spd(600000, 40, 9, f32=True)
+        x32 = np.random.default_rng(2).standard_normal(600000).astype(np.float32)
         s.set_matrix(rp32, col32, v32)
         assert s.info()["n_panels"] > 1
-        assert np.array_equal(s.spmv(x32).view(np.uint32),
-                              H.o_spmv_f32(rp32, col32, v32, x32).view(np.uint32))
+        assert same32(s.spmv(x32), H.o_spmv_f32(rp32, col32, v32, x32))
 
 
 def test_column_panels_auto_c5():
     """C5 (random SPD, 5 M rows, fp32) selects column panels by itself and is
-    bit-exact at full size; a large Laplacian keeps plain CSR."""
+    bit-exact at full size; a large Laplacian does not."""
     rp, col, val = cgx.random_spd(5_000_000, 32, 42, f32=True)
     x = np.random.default_rng(3).standard_normal(len(rp) - 1).astype(np.float32)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
-        assert s.info()["n_panels"] == 10
-        assert np.array_equal(s.spmv(x).view(np.uint32),
-                              H.o_spmv_f32(rp, col, val, x).view(np.uint32))
+        assert s.info()["layout_name"] == "panel" and s.info()["n_panels"] == 10
+        assert same32(s.spmv(x), H.o_spmv_f32(rp, col, val, x))
     del rp, col, val
     rp, col, val = cgx.laplacian3d(128, 128, 128)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
         assert s.info()["n_panels"] == 1
 
+
+# ------------------------------------------- generators, stencil, big configs
 
 def lap_dict(dim, nx, ny, nz):
     d = {0}
@@ -854,7 +701,8 @@ def lap_dict(dim, nx, ny, nz):
                                        (2, (32, 32, 1)), (2, (17, 9, 1)), (3, (216, 216, 216))])
 def test_device_generated_laplacian_bit_exact(dim, shape):
     """the Laplacian generated in device memory is the host
-    generator's CSR bit for bit (C3 at full size included), and solves alike."""
+    generator's CSR bit for bit (C3 at full size included), encoded to
+    CSR-VI on the device against the stencil's pairs, and solves alike."""
     nx, ny, nz = shape
     host = cgx.laplacian3d(nx, ny, nz) if dim == 3 else cgx.laplacian2d(nx, ny)
     with cgx.Solver(0) as s:
@@ -862,16 +710,14 @@ def test_device_generated_laplacian_bit_exact(dim, shape):
         rp, col, val = s.matrix()
         assert np.array_equal(rp, host[0]) and np.array_equal(col, host[1])
         assert H.same_bits_or_both_nan(val, host[2])
-        # coded columns encoded on the device against the stencil's offsets
-        n = len(rp) - 1
-        offs = np.unique(col - np.repeat(np.arange(n), np.diff(rp)))
+        assert s.info()["layout_name"] == "vi"
         assert s.info()["n_dict"] == len(lap_dict(dim, nx, ny, nz))
-        assert set(offs.tolist()) <= set(lap_dict(dim, nx, ny, nz))
+        n = len(rp) - 1
         x = np.random.default_rng(6).standard_normal(n)
         if n <= 200_000:
             assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(*host, x))
-        if len(rp) - 1 <= 2000:
-            b = np.random.default_rng(4).standard_normal(len(rp) - 1)
+        if n <= 2000:
+            b = np.random.default_rng(4).standard_normal(n)
             s.set_rhs(b)
             s.run(25)
             x_ref, _ = H.o_conj_grad(25, *host, b)
@@ -890,7 +736,7 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
     x = np.random.default_rng(5).standard_normal(n)
     with cgx.Solver(0) as s:
         s.set_stencil(dim, nx, ny, nz)
-        assert s.info()["nnz"] == len(col)
+        assert s.info()["nnz"] == len(col) and s.info()["layout_name"] == "stencil"
         y = s.spmv(x)
     assert H.same_bits_or_both_nan(y, H.o_spmv(rp, col, val, x))
     if n <= 2000:
@@ -907,92 +753,36 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
         assert abs(its - its_o) <= 1
 
 
-@pytest.mark.parametrize("bpw", ["1", "2", "4"])
-def test_value_indexed_cg(bpw, monkeypatch):
-    """CG on value-indexed pairs: with one row block per wave the SpMV
-    partials group exactly as the offset-coded kernel's, so the run is
-    bit-identical to CGX_DC_VALS=0; 2 and 4 blocks per wave regroup p.s
-    (fast-mode tolerance against the oracle, reproducible)."""
-    monkeypatch.setenv("CGX_VI_BPW", bpw)
-    rp, col, val = cgx.laplacian3d(60, 50, 40)
-    b = np.random.default_rng(13).standard_normal(len(rp) - 1)
-    out = {}
-    for vals in ("1", "0", "1"):
-        monkeypatch.setenv("CGX_DC_VALS", vals)
-        with cgx.Solver(0) as s:
-            s.set_matrix(rp, col, val)
-            assert s.info()["dict_vals"] == int(vals)
-            s.set_rhs(b)
-            s.run(30)
-            out.setdefault(vals, []).append((s.x(), s.history(31)))
-    x_ref, _ = H.o_conj_grad(30, rp, col, val, b)
-    assert rel(out["1"][0][0], x_ref) <= FAST_RTOL
-    assert H.same_bits_or_both_nan(out["1"][0][0], out["1"][1][0])
-    with cgx.Solver(0) as s:
-        s.set_matrix(rp, col, val)
-        want = -(-s.info()["n_rowblocks"] // (int(bpw) * 4))
-        assert s.info()["spmv_grid"] == want
-        y = s.spmv(b)
-        assert H.same_bits_or_both_nan(y, H.o_spmv(rp, col, val, b))
-    if bpw == "1":
-        assert H.same_bits_or_both_nan(out["1"][0][0], out["0"][0][0])
-        assert H.same_bits_or_both_nan(out["1"][0][1], out["0"][0][1])
-
-
-@pytest.mark.parametrize("wpb", ["8"])
-def test_coded_wide_workgroups_cg(wpb, monkeypatch):
-    """The 8-wave coded-column kernel (half the epilogue partials) inside
-    the HS iteration: x within the fast-mode tolerance, runs reproducible."""
-    monkeypatch.setenv("CGX_SPMV_WPB", wpb)
-    rp, col, val = cgx.laplacian3d(60, 50, 40)
-    b = np.random.default_rng(12).standard_normal(len(rp) - 1)
-    xs = []
-    for _ in range(2):
-        with cgx.Solver(0) as s:
-            s.set_matrix(rp, col, val)
-            assert s.info()["n_dict"] == 7
-            assert s.info()["spmv_grid"] == -(-s.info()["n_rowblocks"] // int(wpb))
-            s.set_rhs(b)
-            s.run(30)
-            xs.append(s.x())
-    x_ref, _ = H.o_conj_grad(30, rp, col, val, b)
-    assert rel(xs[0], x_ref) <= FAST_RTOL
-    assert H.same_bits_or_both_nan(xs[0], xs[1])
-
-
-@pytest.mark.parametrize("kb", ["", "64", "0"])
-def test_tiled_block_order_bit_exact(kb, monkeypatch):
-    """L2-tiled row-block order (CGX_DC_TILE_KB budget; 0 = off): the SpMV
-    is bit-identical to the oracle whatever the order, and a CG run stays
-    within the fast-mode tolerance."""
-    if kb == "0":
-        monkeypatch.setenv("CGX_DC_TILE", "0")
-    elif kb:
-        monkeypatch.setenv("CGX_DC_TILE_KB", kb)
-    rp, col, val = cgx.laplacian3d(120, 100, 20)  # plane 12000 rows: 288 KB of x per 3 planes
+@pytest.mark.parametrize("layout", ["vi", "dc"])
+def test_tiled_item_order_bit_exact(layout):
+    """L2-tiled work-item order for a stencil whose plane exceeds the L2
+    budget (600 x 600 planes: 3 planes of x = 8.6 MB > 1.5 MiB per XCD): only
+    the order changes, so the SpMV is bit-identical to the oracle and a CG run
+    stays within the fast-mode tolerance."""
+    rp, col, val = cgx.laplacian3d(600, 600, 5)
     n = len(rp) - 1
     x = np.random.default_rng(8).standard_normal(n)
-    with cgx.Solver(0) as s:
+    with cgx.Solver(0, layout=layout) as s:
         s.set_matrix(rp, col, val)
-        assert s.info()["n_dict"] == 7
-        assert s.info()["tile_bands"] == {"": 0, "64": 5, "0": 0}[kb]
+        assert s.info()["layout_name"] == layout
+        assert s.info()["tile_bands"] == 6
         assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
         s.set_rhs(x)
-        s.run(30)
-        x_ref, _ = H.o_conj_grad(30, rp, col, val, x)
+        s.run(10)
+        x_ref, _ = H.o_conj_grad(10, rp, col, val, x)
         assert rel(s.x(), x_ref) <= FAST_RTOL
 
 
 def test_c4_full_size_spmv_device_generated():
     """C4 at full size (400^3: 64,000,000 rows, 447,040,000 nnz -- the largest
-    BASELINE config, int32 offsets up to 2^28.7): the device-generated CSR
-    SpMV equals the matrix-free stencil bit for bit (the stencil is pinned to
-    the oracle's CSR SpMV at small sizes by test_matrix_free_stencil_bit_exact)."""
+    BASELINE config): the device-generated CSR-VI SpMV equals the matrix-free
+    stencil bit for bit (the stencil is pinned to the oracle's CSR SpMV at
+    small sizes by test_matrix_free_stencil_bit_exact)."""
     x = np.random.default_rng(11).standard_normal(400 ** 3)
     with cgx.Solver(0) as s:
         s.gen_laplacian(3, 400, 400, 400)
         assert s.info()["nnz"] == 447_040_000
-        assert s.info()["n_dict"] == 7  # coded columns, encoded on the device
+        assert s.info()["layout_name"] == "vi" and s.info()["tile_bands"] > 0
         y = s.spmv(x)
     with cgx.Solver(0) as s:
         s.set_stencil(3, 400, 400, 400)

@@ -1,0 +1,641 @@
+// spmv_lab.hip -- kernel lab for the C3 SpMV (tools only, not the product).
+//
+// C3 = 7-point 3-D Laplacian 216^3 (10,077,696 rows, 70,263,936 nnz, fp64).
+// Every variant computes y = A x AND the x.y epilogue partials (what the CG
+// iteration's SpMV does), is checked bit-for-bit against a host sequential
+// row sum (the reference's order, mv_ops.c:190-194), and is timed with HIP
+// events over order-rotated rounds.  Variants:
+//   csr      k_spmv_dma as in libcgx r01 (LDS-DMA val/col window per 64-row
+//            block, nt stream, XCD-contiguous, 4 gathers in flight)
+//   csr_nty  + non-temporal y store
+//   csr_u8   + 8 gathers in flight (nt y)
+//   csr_w456 456-entry windows (7 workgroups per CU) (nt y)
+//   vi       k_spmv_vi as in libcgx r01 (compact codes + byte row lengths)
+//   ell1/2   ELL-VI: one 8-byte code row per matrix row (pad code 255 =
+//            no entry), thread per row (1 or 2 rows per thread), no block
+//            descriptor, no LDS window, no prefix sum
+//   sten_old k_stencil as in libcgx r01
+//   sten     7 loads issued before the first add, no divisions in the loop
+//   read     a read-only stream of the CSR val+col bytes (843 MB)
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o spmv_lab spmv_lab.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+#define CK(x)                                                                     \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      printf("HIP %s at line %d\n", hipGetErrorString(e_), __LINE__);             \
+      exit(1);                                                                    \
+    }                                                                             \
+  } while (0)
+
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int kWave = 64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ int xcd_block() {
+  const int b = blockIdx.x, G = gridDim.x;
+  if (G < 16) return b;
+  const int x = b & 7, i = b >> 3, q = G >> 3, rem = G & 7;
+  return x * q + min(x, rem) + i;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int WPB>
+__device__ __forceinline__ void epi_store(double dot, double *part) {
+  __shared__ double red[WPB];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  dot = wave_sum(dot);
+  if (lane == 0) red[wid] = dot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = red[0];
+#pragma unroll
+    for (int w = 1; w < WPB; ++w) s = s + red[w];
+    part[blockIdx.x] = s;
+  }
+}
+
+struct Csr {
+  const int *rp, *col, *blkrk;
+  const double *val, *x;
+  double *y, *part;
+  int nblk;
+};
+
+// ------------------------------------------------------------------ CSR
+template <int CAPW, int U, bool NTY, int WPB = 4, bool PRIO = false>
+__global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
+  __shared__ __attribute__((aligned(16))) double lval_all[WPB * CAPW];
+  __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double *lval = lval_all + wid * CAPW;
+  int *lcol = lcol_all + wid * CAPW;
+  const int wb = __builtin_amdgcn_readfirstlane(xcd_block() * WPB + wid);
+  double dot = 0.0;
+  if (wb < a.nblk) {
+    const int *d = a.blkrk + 2 * wb;
+    const int r0 = d[0], k0 = d[1], nr = d[2] - d[0], k1 = d[3];
+    const int kb = k0 & ~3;
+    const int m = k1 - kb;
+#pragma unroll
+    for (int i = 0; i < (CAPW * 8 + 1023) / 1024; ++i)
+      if ((i * 64 + lane) * 2 < m)
+        __builtin_amdgcn_global_load_lds((const void *)(a.val + kb + i * 128 + lane * 2),
+                                         (lds_void *)(lval + i * 128), 16, 0, 2);
+#pragma unroll
+    for (int i = 0; i < (CAPW * 4 + 1023) / 1024; ++i)
+      if ((i * 64 + lane) * 4 < m)
+        __builtin_amdgcn_global_load_lds((const void *)(a.col + kb + i * 256 + lane * 4),
+                                         (lds_void *)(lcol + i * 256), 16, 0, 2);
+    int j0 = 0, j1 = 0;
+    double xrow = 0.0, acc = 0.0;
+    if (lane < nr) {
+      j0 = a.rp[r0 + lane];
+      j1 = a.rp[r0 + lane + 1];
+      xrow = a.x[r0 + lane];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_lds_sync();
+    if (PRIO) __builtin_amdgcn_s_setprio(2);
+    if (lane < nr) {
+      for (int j = j0 - kb; j < j1 - kb; j += U) {
+        const int cnt = min(U, j1 - kb - j);
+        int cc[U];
+        double vv[U], xx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int idx = u < cnt ? j + u : j;
+          cc[u] = u < cnt ? lcol[idx] : 0;
+          vv[u] = lval[idx];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xx[u] = a.x[cc[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const double pr = vv[u] * xx[u];
+          acc = acc + (u < cnt ? pr : 0.0);
+        }
+      }
+      if (NTY) __builtin_nontemporal_store(acc, a.y + r0 + lane);
+      else a.y[r0 + lane] = acc;
+      dot = xrow * acc;
+    }
+  }
+  epi_store<WPB>(dot, a.part);
+}
+
+// ------------------------------------------------------- compact CSR-VI
+struct Vi {
+  const unsigned char *code, *rlen;
+  const int *blkrk, *dict;
+  const double *dval, *x;
+  double *y, *part;
+  int nblk;
+};
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(v, off, 64);
+    v += lane >= off ? t : 0;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_vi(Vi a) {
+  constexpr int WPB = 4, CAPC = 528, U = 8;
+  __shared__ __attribute__((aligned(16))) unsigned char lcode_all[WPB * CAPC];
+  __shared__ int ldict_all[WPB * 64];
+  __shared__ double ldv_all[WPB * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned char *lcode = lcode_all + wid * CAPC;
+  int *ldict = ldict_all + wid * 64;
+  double *ldv = ldv_all + wid * 64;
+  const int wb = __builtin_amdgcn_readfirstlane(xcd_block() * WPB + wid);
+  double dot = 0.0;
+  if (wb < a.nblk) {
+    const int *d = a.blkrk + 2 * wb;
+    const int r0 = d[0], k0 = d[1], nr = d[2] - d[0], k1 = d[3];
+    const int kc = k0 & ~15;
+    const int mc = k1 - kc;
+    const unsigned char *cb = a.code + kc;
+    if (lane * 16 < mc)
+      __builtin_amdgcn_global_load_lds((const void *)(cb + lane * 16), (lds_void *)lcode, 16, 0, 2);
+    const int len = lane < nr ? a.rlen[r0 + lane] : 0;
+    const double xrow = lane < nr ? a.x[r0 + lane] : 0.0;
+    const int dv = a.dict[lane];
+    const double dvv = a.dval[lane];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ldict[lane] = dv;
+    ldv[lane] = dvv;
+    const int jb = k0 + wave_incl_scan(len, lane) - len - kc;
+    wave_lds_sync();
+    double acc = 0.0;
+    for (int j = 0; j < len; j += U) {
+      int code[U];
+      double xx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) code[u] = lcode[j + u < len ? jb + j + u : 0];
+#pragma unroll
+      for (int u = 0; u < U; ++u) xx[u] = a.x[j + u < len ? r0 + lane + ldict[code[u]] : 0];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double pr = ldv[code[u]] * xx[u];
+        acc = acc + (j + u < len ? pr : 0.0);
+      }
+    }
+    if (lane < nr) {
+      __builtin_nontemporal_store(acc, a.y + r0 + lane);
+      dot = xrow * acc;
+    }
+  }
+  epi_store<WPB>(dot, a.part);
+}
+
+// ------------------------------------------------------------- ELL-VI
+// code8[row]: the row's pair codes in CSR order, bytes 0..7, 255 = no entry.
+struct Ell {
+  const unsigned long long *code8;
+  const int *dict;
+  const double *dval, *x;
+  double *y, *part;
+  int n;
+};
+
+template <int RPT, bool NTC>
+__global__ __launch_bounds__(256) void k_ell(Ell a) {
+  __shared__ int ldict[64];
+  __shared__ double ldv[64];
+  const int t = threadIdx.x;
+  const int base = xcd_block() * 256 * RPT + t;
+  unsigned long long cw[RPT];
+  double xr[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int row = base + q * 256;
+    cw[q] = row < a.n ? (NTC ? __builtin_nontemporal_load(a.code8 + row) : a.code8[row])
+                      : ~0ull;
+    xr[q] = row < a.n ? a.x[row] : 0.0;
+  }
+  if (t < 64) {
+    ldict[t] = a.dict[t];
+    ldv[t] = a.dval[t];
+  }
+  __syncthreads();
+  double dot = 0.0;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int row = base + q * 256;
+    double xx[8];
+    int c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      c[u] = (int)((cw[q] >> (8 * u)) & 255);
+      const int ci = c[u] & 63;
+      xx[u] = a.x[c[u] != 255 ? row + ldict[ci] : 0];
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double pr = ldv[c[u] & 63] * xx[u];
+      acc = c[u] != 255 ? acc + pr : acc;
+    }
+    if (row < a.n) {
+      __builtin_nontemporal_store(acc, a.y + row);
+      dot = dot + xr[q] * acc;
+    }
+  }
+  epi_store<4>(dot, a.part);
+}
+
+// chunked grid: workgroup g (XCD-contiguous) owns slices [lo, hi) of 256*RPT
+// rows; the next slice's codes and x[row] are loaded before this slice's
+// gathers (one slice of prefetch), so the wave never waits on a code load
+template <int RPT>
+__global__ __launch_bounds__(256) void k_ellg(Ell a) {
+  __shared__ int ldict[64];
+  __shared__ double ldv[64];
+  const int t = threadIdx.x;
+  const int G = gridDim.x, g = xcd_block();
+  const int ns = (a.n + 256 * RPT - 1) / (256 * RPT);
+  const int lo = (int)((long long)ns * g / G), hi = (int)((long long)ns * (g + 1) / G);
+  if (t < 64) {
+    ldict[t] = a.dict[t];
+    ldv[t] = a.dval[t];
+  }
+  unsigned long long cw[RPT];
+  double xr[RPT];
+  auto load = [&](int sl) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int row = sl * 256 * RPT + q * 256 + t;
+      cw[q] = sl < hi && row < a.n ? __builtin_nontemporal_load(a.code8 + row) : ~0ull;
+      xr[q] = sl < hi && row < a.n ? a.x[row] : 0.0;
+    }
+  };
+  load(lo);
+  __syncthreads();
+  double dot = 0.0;
+  for (int sl = lo; sl < hi; ++sl) {
+    unsigned long long cc[RPT];
+    double xc[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      cc[q] = cw[q];
+      xc[q] = xr[q];
+    }
+    load(sl + 1);
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int row = sl * 256 * RPT + q * 256 + t;
+      double xx[8];
+      int c[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        c[u] = (int)((cc[q] >> (8 * u)) & 255);
+        xx[u] = a.x[c[u] != 255 ? row + ldict[c[u] & 63] : 0];
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double pr = ldv[c[u] & 63] * xx[u];
+        acc = c[u] != 255 ? acc + pr : acc;
+      }
+      if (row < a.n) {
+        __builtin_nontemporal_store(acc, a.y + row);
+        dot = dot + xc[q] * acc;
+      }
+    }
+  }
+  epi_store<4>(dot, a.part);
+}
+
+// ------------------------------------------------------------ stencils
+struct Sten {
+  int nx, ny, nz;
+  double inv_nx, inv_pl;
+  const double *x;
+  double *y, *part;
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_sten_old(Sten g) {
+  const int nx = g.nx, ny = g.ny, pl = g.nx * g.ny, n = g.n;
+  double dot = 0.0;
+  const int r = xcd_block() * 256 + threadIdx.x;
+  if (r < n) {
+    const int i = r % nx, j = (r / nx) % ny, l = r / pl;
+    const double *x = g.x;
+    double acc = 0.0;
+    if (l > 0) acc = acc + -1.0 * x[r - pl];
+    if (j > 0) acc = acc + -1.0 * x[r - nx];
+    if (i > 0) acc = acc + -1.0 * x[r - 1];
+    const double xr = x[r];
+    acc = acc + 6.0 * xr;
+    if (i < nx - 1) acc = acc + -1.0 * x[r + 1];
+    if (j < ny - 1) acc = acc + -1.0 * x[r + nx];
+    if (l < g.nz - 1) acc = acc + -1.0 * x[r + pl];
+    g.y[r] = acc;
+    dot = xr * acc;
+  }
+  epi_store<4>(dot, g.part);
+}
+
+// exact floor(a / d) for 0 <= a < 2^31 from a double reciprocal
+__device__ __forceinline__ int fdiv(int a, int d, double inv) {
+  int q = (int)((double)a * inv);
+  q -= q * d > a;
+  q += (q + 1) * d <= a;
+  return q;
+}
+
+template <bool NTY>
+__global__ __launch_bounds__(256) void k_sten(Sten g) {
+  const int nx = g.nx, ny = g.ny, pl = g.nx * g.ny, n = g.n;
+  double dot = 0.0;
+  const int r = xcd_block() * 256 + threadIdx.x;
+  if (r < n) {
+    const int l = fdiv(r, pl, g.inv_pl);
+    const int rem = r - l * pl;
+    const int j = fdiv(rem, nx, g.inv_nx);
+    const int i = rem - j * nx;
+    const bool ml = l > 0, mj = j > 0, mi = i > 0, pi = i < nx - 1, pj = j < ny - 1,
+               pL = l < g.nz - 1;
+    const double *x = g.x;
+    // all seven loads in flight at once (clamped addresses), then the adds in
+    // the CSR row's order; a missing neighbour adds nothing
+    const double v0 = x[ml ? r - pl : r], v1 = x[mj ? r - nx : r], v2 = x[mi ? r - 1 : r];
+    const double xr = x[r];
+    const double v4 = x[pi ? r + 1 : r], v5 = x[pj ? r + nx : r], v6 = x[pL ? r + pl : r];
+    double acc = 0.0;
+    acc = ml ? acc + -1.0 * v0 : acc;
+    acc = mj ? acc + -1.0 * v1 : acc;
+    acc = mi ? acc + -1.0 * v2 : acc;
+    acc = acc + 6.0 * xr;
+    acc = pi ? acc + -1.0 * v4 : acc;
+    acc = pj ? acc + -1.0 * v5 : acc;
+    acc = pL ? acc + -1.0 * v6 : acc;
+    if (NTY) __builtin_nontemporal_store(acc, g.y + r);
+    else g.y[r] = acc;
+    dot = xr * acc;
+  }
+  epi_store<4>(dot, g.part);
+}
+
+// --------------------------------------------------------------- ceilings
+typedef double d2v __attribute__((ext_vector_type(2)));
+// reads val (n2v double2) and col (n2c int4): the CSR stream's bytes
+__global__ __launch_bounds__(256) void k_read(const d2v *__restrict__ v, long long n2v,
+                                              const int4 *__restrict__ c, long long n2c,
+                                              double *sink) {
+  double acc = 0.0;
+  const long long G = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2v; i += G) {
+    const d2v w = __builtin_nontemporal_load(v + i);
+    acc += w.x + w.y;
+  }
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2c; i += G) {
+    const int4 w = c[i];
+    acc += (double)(w.x + w.w);
+  }
+  if (acc == 1.2345e300) sink[0] = acc;
+}
+
+// in-situ cache state: what the CG iteration's vector kernels do between
+// two SpMVs (read r, s; write r; read x, p, r; write x, p) -- here x is
+// rewritten with its own values, two scratch vectors read and written
+__global__ __launch_bounds__(256) void k_pollute(double *x, double *a, double *b, int n) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const double xv = x[i], av = a[i], bv = b[i];
+    a[i] = av + bv;
+    b[i] = bv - av;
+    x[i] = xv;
+  }
+}
+
+// ------------------------------------------------------------------- host
+int main(int argc, char **argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 216;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+  const bool insitu = argc > 3 && atoi(argv[3]) != 0;
+  const int reps = 20;
+  const int nx = N, ny = N, nz = N, pl = nx * ny, n = nx * ny * nz;
+  std::vector<int> rp(n + 1), col;
+  std::vector<double> val;
+  col.reserve((size_t)n * 7);
+  val.reserve((size_t)n * 7);
+  std::vector<unsigned long long> code8(n, ~0ull);
+  std::vector<unsigned char> code, rlen(n);
+  const int offs[7] = {-pl, -nx, -1, 0, 1, nx, pl};  // sorted: code = position
+  for (int r = 0; r < n; ++r) {
+    rp[r] = (int)col.size();
+    const int i = r % nx, j = (r / nx) % ny, l = r / pl;
+    const bool has[7] = {l > 0, j > 0, i > 0, true, i < nx - 1, j < ny - 1, l < nz - 1};
+    int u = 0;
+    for (int q = 0; q < 7; ++q)
+      if (has[q]) {
+        col.push_back(r + offs[q]);
+        val.push_back(q == 3 ? 6.0 : -1.0);
+        code.push_back((unsigned char)q);
+        code8[r] = (code8[r] & ~(0xffull << (8 * u))) | ((unsigned long long)q << (8 * u));
+        ++u;
+      }
+    rlen[r] = (unsigned char)u;
+  }
+  rp[n] = (int)col.size();
+  const int nnz = rp[n];
+  std::vector<int> blkrk;
+  for (int r = 0; r < n; r += 64) {
+    blkrk.push_back(r);
+    blkrk.push_back(rp[r]);
+  }
+  blkrk.push_back(n);
+  blkrk.push_back(nnz);
+  const int nblk = (int)blkrk.size() / 2 - 1;
+  std::vector<double> x(n);
+  unsigned long long s = 12345;
+  for (int i = 0; i < n; ++i) {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    x[i] = (double)(s >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+  }
+  std::vector<double> yref(n);
+  for (int r = 0; r < n; ++r) {
+    double acc = 0.0;
+    for (int k = rp[r]; k < rp[r + 1]; ++k) acc = acc + val[k] * x[col[k]];
+    yref[r] = acc;
+  }
+  printf("C3 lab: n %d nnz %d blocks %d\n", n, nnz, nblk);
+
+  const size_t pad = 4096;
+  int *d_rp, *d_col, *d_blkrk, *d_dict;
+  double *d_val, *d_x, *d_y, *d_part, *d_dval, *d_sink;
+  unsigned char *d_code, *d_rlen;
+  unsigned long long *d_code8;
+  CK(hipMalloc(&d_rp, (n + 1) * 4 + pad));
+  CK(hipMalloc(&d_col, (size_t)nnz * 4 + pad));
+  CK(hipMalloc(&d_val, (size_t)nnz * 8 + pad));
+  CK(hipMalloc(&d_blkrk, blkrk.size() * 4 + pad));
+  CK(hipMalloc(&d_x, (size_t)n * 8 + pad));
+  CK(hipMalloc(&d_y, (size_t)n * 8 + pad));
+  CK(hipMalloc(&d_part, (size_t)n / 8 + pad));
+  CK(hipMalloc(&d_code, (size_t)nnz + pad));
+  CK(hipMalloc(&d_rlen, (size_t)n + pad));
+  CK(hipMalloc(&d_code8, (size_t)n * 8 + pad));
+  CK(hipMalloc(&d_dict, 64 * 4));
+  CK(hipMalloc(&d_dval, 64 * 8));
+  CK(hipMalloc(&d_sink, 64));
+  double *d_s1, *d_s2;
+  CK(hipMalloc(&d_s1, (size_t)n * 8));
+  CK(hipMalloc(&d_s2, (size_t)n * 8));
+  CK(hipMemset(d_s1, 0, (size_t)n * 8));
+  CK(hipMemset(d_s2, 0, (size_t)n * 8));
+  CK(hipMemset(d_col, 0, (size_t)nnz * 4 + pad));
+  CK(hipMemset(d_val, 0, (size_t)nnz * 8 + pad));
+  CK(hipMemset(d_code, 0, (size_t)nnz + pad));
+  CK(hipMemcpy(d_rp, rp.data(), (n + 1) * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_col, col.data(), (size_t)nnz * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_val, val.data(), (size_t)nnz * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_blkrk, blkrk.data(), blkrk.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_x, x.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_code, code.data(), (size_t)nnz, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_rlen, rlen.data(), (size_t)n, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_code8, code8.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  std::vector<int> dict(64, 0);
+  std::vector<double> dval(64, 0.0);
+  for (int q = 0; q < 7; ++q) {
+    dict[q] = offs[q];
+    dval[q] = q == 3 ? 6.0 : -1.0;
+  }
+  CK(hipMemcpy(d_dict, dict.data(), 64 * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_dval, dval.data(), 64 * 8, hipMemcpyHostToDevice));
+
+  Csr c{d_rp, d_col, d_blkrk, d_val, d_x, d_y, d_part, nblk};
+  Vi v{d_code, d_rlen, d_blkrk, d_dict, d_dval, d_x, d_y, d_part, nblk};
+  Ell e{d_code8, d_dict, d_dval, d_x, d_y, d_part, n};
+  Sten st{nx, ny, nz, 1.0 / nx, 1.0 / pl, d_x, d_y, d_part, n};
+  const int g4 = (nblk + 3) / 4, gr = (n + 255) / 256;
+  const long long csr_bytes = (long long)nnz * 12 + 4LL * (n + 1) + 16LL * n;
+  struct Var {
+    std::string name;
+    std::function<void()> run;
+    double bytes;  // the variant's own algorithmic bytes
+    bool check;
+  };
+  std::vector<Var> vars = {
+      {"csr", [&] { hipLaunchKernelGGL((k_csr<512, 4, false>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_nty", [&] { hipLaunchKernelGGL((k_csr<512, 4, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u8", [&] { hipLaunchKernelGGL((k_csr<512, 8, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_w456", [&] { hipLaunchKernelGGL((k_csr<456, 4, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u8w456", [&] { hipLaunchKernelGGL((k_csr<456, 8, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_prio", [&] { hipLaunchKernelGGL((k_csr<456, 8, true, 4, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_wpb8", [&] { hipLaunchKernelGGL((k_csr<456, 8, true, 8>), dim3((nblk + 7) / 8), dim3(512), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"vi", [&] { hipLaunchKernelGGL(k_vi, dim3(g4), dim3(256), 0, 0, v); },
+       (double)nnz + 17.0 * n, true},
+      {"ell1", [&] { hipLaunchKernelGGL((k_ell<1, true>), dim3(gr), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ell1c", [&] { hipLaunchKernelGGL((k_ell<1, false>), dim3(gr), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ell2", [&] { hipLaunchKernelGGL((k_ell<2, true>), dim3((n + 511) / 512), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ellg2_2k", [&] { hipLaunchKernelGGL((k_ellg<2>), dim3(2048), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ellg2_4k", [&] { hipLaunchKernelGGL((k_ellg<2>), dim3(4096), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ellg1_4k", [&] { hipLaunchKernelGGL((k_ellg<1>), dim3(4096), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ellg2_8k", [&] { hipLaunchKernelGGL((k_ellg<2>), dim3(8192), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"ell2c", [&] { hipLaunchKernelGGL((k_ell<2, false>), dim3((n + 511) / 512), dim3(256), 0, 0, e); },
+       24.0 * n, true},
+      {"sten_old", [&] { hipLaunchKernelGGL(k_sten_old, dim3(gr), dim3(256), 0, 0, st); },
+       16.0 * n, true},
+      {"sten", [&] { hipLaunchKernelGGL((k_sten<false>), dim3(gr), dim3(256), 0, 0, st); },
+       16.0 * n, true},
+      {"sten_nty", [&] { hipLaunchKernelGGL((k_sten<true>), dim3(gr), dim3(256), 0, 0, st); },
+       16.0 * n, true},
+      {"read843", [&] {
+         hipLaunchKernelGGL(k_read, dim3(256 * 16), dim3(256), 0, 0, (const d2v *)d_val,
+                            (long long)nnz / 2, (const int4 *)d_col, (long long)nnz / 4, d_sink);
+       },
+       (double)nnz * 12, false},
+  };
+  std::vector<double> y(n);
+  for (auto &vr : vars) {
+    if (!vr.check) continue;
+    CK(hipMemset(d_y, 0xff, (size_t)n * 8));
+    vr.run();
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(y.data(), d_y, (size_t)n * 8, hipMemcpyDeviceToHost));
+    long bad = 0;
+    for (int i = 0; i < n; ++i) bad += memcmp(&y[i], &yref[i], 8) != 0;
+    printf("check %-9s %s (%ld rows differ)\n", vr.name.c_str(), bad ? "FAIL" : "bit-exact", bad);
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<double>> t(vars.size());
+  for (int rd = 0; rd < rounds; ++rd) {
+    for (size_t q = 0; q < vars.size(); ++q) {
+      const size_t i = (q + rd) % vars.size();  // order-rotated
+      vars[i].run();
+      if (insitu) {  // pollute, then time the SpMV alone, reps times
+        double sum = 0;
+        for (int k = 0; k < reps; ++k) {
+          hipLaunchKernelGGL(k_pollute, dim3(4096), dim3(256), 0, 0, d_x, d_s1, d_s2, n);
+          CK(hipEventRecord(e0, 0));
+          vars[i].run();
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          sum += ms;
+        }
+        t[i].push_back(1e3 * sum / reps);
+        continue;
+      }
+      CK(hipEventRecord(e0, 0));
+      for (int k = 0; k < reps; ++k) vars[i].run();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[i].push_back(1e3 * ms / reps);
+    }
+  }
+  printf("%-10s %9s %9s %9s %8s\n", "variant", "min_us", "med_us", "GB/s", "CSR-frac");
+  for (size_t i = 0; i < vars.size(); ++i) {
+    std::sort(t[i].begin(), t[i].end());
+    const double mn = t[i].front(), md = t[i][t[i].size() / 2];
+    printf("%-10s %9.2f %9.2f %9.1f %8.3f\n", vars[i].name.c_str(), mn, md,
+           vars[i].bytes / (md * 1e-6) / 1e9, csr_bytes / (md * 1e-6) / 1e9 / 8000.0);
+  }
+  return 0;
+}
