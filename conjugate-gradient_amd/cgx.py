@@ -22,10 +22,10 @@ CGX_MODE_FAST, CGX_MODE_EXACT = 0, 1
 CGX_ALG_HS, CGX_ALG_CG1 = 0, 1
 CGX_F64, CGX_F32 = 0, 1
 CGX_BENCH_GRAPH, CGX_BENCH_SPMV_EVENTS, CGX_BENCH_SPMV_ONLY = 1, 2, 4
-(CGX_LAYOUT_AUTO, CGX_LAYOUT_CSR, CGX_LAYOUT_DC, CGX_LAYOUT_VI, CGX_LAYOUT_PANEL,
+(CGX_LAYOUT_AUTO, CGX_LAYOUT_CSR, CGX_LAYOUT_DC, CGX_LAYOUT_DIA, CGX_LAYOUT_PANEL,
  CGX_LAYOUT_STENCIL) = range(6)
 LAYOUT_NAMES = {CGX_LAYOUT_AUTO: "auto", CGX_LAYOUT_CSR: "csr", CGX_LAYOUT_DC: "dc",
-                CGX_LAYOUT_VI: "vi", CGX_LAYOUT_PANEL: "panel", CGX_LAYOUT_STENCIL: "stencil"}
+                CGX_LAYOUT_DIA: "dia", CGX_LAYOUT_PANEL: "panel", CGX_LAYOUT_STENCIL: "stencil"}
 LAYOUTS = {v: k for k, v in LAYOUT_NAMES.items()}
 
 _i32p = ctypes.POINTER(ctypes.c_int)
@@ -52,8 +52,9 @@ class CgxInfo(ctypes.Structure):
                 ("iter_bytes", ctypes.c_double), ("spmv_iter_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("n_panels", ctypes.c_int),
                 ("n_dict", ctypes.c_int), ("tile_bands", ctypes.c_int), ("nt", ctypes.c_int),
-                ("row_width", ctypes.c_int), ("encode_fallback", ctypes.c_int),
-                ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double)]
+                ("code_bytes_per_row", ctypes.c_int), ("encode_fallback", ctypes.c_int),
+                ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double),
+                ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):

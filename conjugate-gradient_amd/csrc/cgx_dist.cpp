@@ -896,7 +896,7 @@ void cgx_dist_destroy(cgx_dist *d) {
 }
 
 int cgx_dist_set_layout(cgx_dist *d, int layout) {
-  if (!d || layout < CGX_LAYOUT_AUTO || layout > CGX_LAYOUT_VI) return CGX_EINVAL;
+  if (!d || layout < CGX_LAYOUT_AUTO || layout > CGX_LAYOUT_DIA) return CGX_EINVAL;
   d->want_layout = layout;
   return 0;
 }
@@ -988,7 +988,7 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   s->device_bytes = d->A.dev_bytes + d->vec_bytes;
   s->spmv_iter_bytes = d->have_matrix ? d->A.layout_bytes() : 0.0;
   s->layout = d->have_matrix ? cgx::public_layout(d->A) : CGX_LAYOUT_AUTO;
-  s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_VI ? d->A.npair : 0;
+  s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_DIA ? d->A.dia.ndiag : 0;
   s->graph = d->graph_state;
   s->alg = d->alg;
   return 0;

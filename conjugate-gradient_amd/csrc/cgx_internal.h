@@ -29,16 +29,21 @@ void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 // Checks that `device` exists and is a gfx950 (MI355X); CGX_ENODEV otherwise.
 int check_device(int device, int *cus = nullptr);
 // Device allocation (physically contiguous when the driver allows it: -1 to
-// -2% per C3 iteration, r01), zero-size requests get 16 bytes.  Adds the
-// size to *counter.  CGX_ENOMEM (with cgx_last_error set) on failure.
+// -2% per C3 iteration, r01), zero-size requests get 16 bytes.  Every
+// buffer starts kGuardBytes (zeroed) after its allocation, so a pair load
+// of x[-1], x[0] (DIA / stencil SpMV, an edge row without that neighbour)
+// stays inside it.  Adds the size to *counter.  CGX_ENOMEM (with
+// cgx_last_error set) on failure.  Free with dev_free only.
+constexpr size_t kGuardBytes = 256;
 int dev_alloc(void **p, size_t bytes, size_t *counter);
+void dev_free_raw(void *p);
 template <typename P>
 inline int dev_alloc(P **p, size_t bytes, size_t *counter) {
   return dev_alloc((void **)p, bytes, counter);
 }
 template <typename P>
 inline void dev_free(P **p) {
-  if (*p) (void)hipFree((void *)*p);
+  dev_free_raw((void *)*p);
   *p = nullptr;
 }
 
@@ -86,8 +91,9 @@ constexpr int kFinBS = 1024;
 constexpr int kFoldBS = 1024;
 constexpr int kPad = 8;            // val/col/vectors padded by this many entries
 constexpr int kWindowPad = 1024;   // + one SpMV window (LDS-DMA reads 16-B pieces)
-constexpr int kViSliceRows = 512;  // CSR-VI slice: one workgroup, 2 rows per thread
-constexpr int kViPad = 255;        // CSR-VI pad code: no entry
+constexpr int kDiaSliceRows = 512; // DIA-VI work item: one workgroup, 2 rows per thread
+constexpr int kDiaMax = 16;        // DIA-VI: diagonals (nibbles in a 64-bit row word)
+constexpr int kDiaVals = 15;       // DIA-VI: values per diagonal (nibble 15 = no entry)
 constexpr double kMallBytes = 256.0 * 1024 * 1024;  // Infinity Cache
 
 // ---------------------------------------------------- Laplacian operators
@@ -126,16 +132,17 @@ std::vector<int> lap_offsets(const LapSpec &g);
 //   L_DC       dictionary-coded columns: col = row + dict[code], one code
 //              byte per nonzero + byte row lengths, value stream kept
 //                                                            (k_spmv_dc)
-//   L_VI       value-indexed pairs in 512-row slices: one code per nonzero
-//              names (offset, value), rows padded to the slice width with
-//              code 255, thread per row, no value stream      (k_spmv_vi)
+//   L_DIA      value-indexed diagonal codes (DIA-VI): <= 16 diagonals
+//              (col - row), <= 15 values each; per row one nibble per
+//              diagonal (value index, 15 = no entry), no column or value
+//              stream; two rows per thread, pair loads of x   (k_spmv_dia)
 //   L_STENCIL  matrix-free 5/7-point Laplacian                (k_stencil)
 // Every kernel sums each row sequentially in column order from 0.0 with
 // separately rounded products: y is bit-identical across layouts and to the
 // reference's mv_mult on chained matrices (mv_ops.c:187-197).
-enum Layout : int { L_CSR = 0, L_DC = 1, L_VI = 2, L_STENCIL = 3 };
+enum Layout : int { L_CSR = 0, L_DC = 1, L_DIA = 2, L_STENCIL = 3 };
 
-// Work items of one launch (CSR/DC: row blocks; VI: slices): list[0, count)
+// Work items of one launch (CSR/DC: row blocks; DIA: 512-row slices): list[0, count)
 // when list != nullptr, else first, first+1, ..., first+count-1.
 struct Items {
   const int *list;
@@ -156,6 +163,14 @@ struct FinArgs {
   const double *pb;
   int nb;
   double *out;
+};
+
+// DIA-VI candidates for the device encoder: diagonal offsets and the number
+// of values in each diagonal's table.
+struct DiaCand {
+  int ndiag;
+  int doff[kDiaMax];
+  int nval[kDiaMax];
 };
 
 template <typename T>
@@ -179,16 +194,18 @@ struct SpmvArgs {
   const unsigned char *code, *rlen;
   const int *dict;  // 64 or 256 entries (ndict_cap)
   int ndict_cap;
-  // VI
-  const unsigned *vcode;  // slice-major code rows (4 codes per dword)
-  const int2 *sdesc;      // per slice: {dword offset, row width in dwords}
-  const int *vdict;       // pair offsets col - row
-  const T *vval;          // pair values
-  int npair;
-  int wdmax;              // widest slice (dwords): 1, 2, 4, or 0 = wider
-  int n;                  // rows (VI, stencil)
+  int gath;               // CSR / DC: x gathers per row chunk (7 or 8)
+  // DIA
+  const unsigned *dcode;  // row r: dword r (<= 8 diagonals) or dwords 2r, 2r+1
+  const T *vtab;          // [16][16] values, vtab[16 k + v]
+  int ndiag;              // diagonals
+  int kdiag;              // index of the main diagonal (offset 0), -1: none
+  int doff[kDiaMax];      // diagonal offsets col - row, ascending
+  int n;                  // rows (DIA, stencil)
+  int ncols;              // entries of x (DIA pair loads stay inside)
   // stencil
   LapSpec lap;
+  double inv_nx, inv_pl;  // 1 / nx, 1 / (nx ny): exact floor divisions (fdiv)
 };
 
 // Workgroups of one launch (= epilogue partials it writes).
@@ -258,14 +275,13 @@ hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
 hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dict, int nd,
                             unsigned char *code, int *err, hipStream_t st,
                             const double *val = nullptr, const double *dval = nullptr);
-// CSR-VI code rows of a device CSR (slice s at sdesc[s], rows of <= 4 wd_s
-// entries): entry k of row r gets the index of (col - r, val bits) among the
-// np sorted pairs (offset ascending, ties by value bits), pads get 255;
-// err |= 1 when a nonzero matches no pair.
+// DIA-VI codes of a device CSR (rows [0, npad), rows >= n all "no entry"):
+// err |= 1 when an entry's diagonal or value is not a candidate or a row's
+// columns do not strictly ascend.
 template <typename T>
-hipError_t launch_vi_encode(int n, const int *rp, const int *col, const T *val,
-                            const int2 *sdesc, const int *pair_off, const T *pair_val, int np,
-                            unsigned *vcode, int *err, hipStream_t st);
+hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, const T *val,
+                             const DiaCand &c, const T *vtab, unsigned *code, int *err,
+                             hipStream_t st);
 
 int vec_grid_for(int n, int cus);
 

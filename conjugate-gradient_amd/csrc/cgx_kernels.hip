@@ -315,9 +315,9 @@ __device__ __forceinline__ bool load_block(const SpmvArgs<T> &a, int wi, Blk &B,
 // A row longer than the window gets a block of its own and is streamed in
 // window-sized chunks by lane 0.  NT: the once-per-iteration matrix stream
 // and the y store bypass the caches (the CG vectors stay resident).
-template <typename T, int CAPW, bool EPI, bool NT, bool LIST>
+template <typename T, int CAPW, int U, bool EPI, bool NT, bool LIST>
 __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
-  constexpr int WPB = 4, U = 8, AUX = NT ? 2 : 0;
+  constexpr int WPB = 4, AUX = NT ? 2 : 0;
   static_assert(CAPW % 4 == 0, "window");
   __shared__ __attribute__((aligned(16))) T lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
@@ -404,9 +404,9 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
 // land in the wave's LDS slice by LDS-DMA, row bounds come from a wave prefix
 // sum of the lengths, lane t decodes and sums row t sequentially (bit-
 // identical y).  The dictionary is copied into each wave's LDS slice.
-template <typename T, int CAPW, int ND, bool EPI, bool NT, bool LIST>
+template <typename T, int CAPW, int ND, int U, bool EPI, bool NT, bool LIST>
 __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
-  constexpr int WPB = 4, U = 8, AUX = NT ? 2 : 0;
+  constexpr int WPB = 4, AUX = NT ? 2 : 0;
   static_assert(CAPW % 4 == 0 && ND % kWave == 0, "window / dictionary");
   // code window: starts at the 16-B granule holding entry k0, so up to 15
   // more entries than the val window in front
@@ -501,109 +501,117 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
   if (EPI) epi_store<WPB>(dot, a.part, a.fin);
 }
 
-// ------------------------------------------------------------- k_spmv_vi
-// Value-indexed pairs (CSR-VI) in 512-row slices.  A matrix whose nonzeros
-// use at most 255 distinct (col - row, value) pairs -- constant-coefficient
-// stencils, small value sets -- stores one code byte per nonzero naming both
-// (col = row + vdict[code], val = vval[code] bit for bit) and no value
-// stream.  The codes of a slice are row-major with a fixed row width of wd
-// dwords (4 codes each; 1, 2 or a multiple of 4), rows padded with code 255,
-// so row r's codes sit at sdesc[s].x + (r - 512 s) * wd: one thread per row
-// loads them with ONE coalesced load (8 B per lane for 8 codes), with no
-// block descriptor, LDS window, or prefix sum in front of the gathers -- two
-// dependent memory round trips per row (codes, then x), the minimum.  Each
-// thread takes rows t and t + 256 of the slice (16 gathers in flight at 8
-// codes per row).  Products and sums are the CSR row's, in its order: y is
-// bit-identical to k_spmv_csr.
+// ------------------------------------------------------------ k_spmv_dia
+// Value-indexed diagonal codes (DIA-VI).  A matrix whose nonzeros lie on at
+// most 16 diagonals d_0 < ... < d_{K-1} (col - row), with at most 15
+// distinct values (bit patterns) per diagonal -- stencils, banded matrices
+// with few coefficients -- stores per row one nibble per diagonal: the index
+// of the entry's value in that diagonal's value table, 15 = no entry
+// (4 bytes per row for K <= 8, 8 for K <= 16), and no column or value
+// stream.  A row's entries ascend in column, i.e. in diagonal (checked by the
+// encoder), so summing k = 0..K-1 adds the CSR row's products in its order:
+// y is bit-identical to k_spmv_csr.  Two rows per thread, r even: the
+// neighbours x[r + d_k], x[r + 1 + d_k] of both rows are ONE 16-byte (fp64)
+// load, issued only by lanes whose rows hold diagonal k (a wave skips a
+// diagonal none of its rows hold, e.g. a partition's ghost diagonals) -- half
+// the vector-memory instructions of a row-per-thread gather, the lesson of
+// the lab (tools/mb/spmv_lab.hip: 82 -> 38 us at C3).  The codes of the two
+// rows are one load; the only dependent round trip is codes -> x.
+template <typename T> struct Pair;
+template <> struct Pair<double> {
+  typedef double type __attribute__((ext_vector_type(2), aligned(8)));
+};
+template <> struct Pair<float> {
+  typedef float type __attribute__((ext_vector_type(2), aligned(4)));
+};
+
+// (x[b], x[b+1]) as one load, for -1 <= b <= ncols - 1: a pair reaches
+// past x only where one of its two rows holds no entry there, and the
+// product of that half is selected away.  x[-1] is the allocation's front
+// guard (dev_alloc), x[ncols] the first padding entry (vectors carry kPad).
 template <typename T>
-__device__ __forceinline__ void vi_row_codes(const unsigned *p, int wd, int c0, unsigned (&w)[4],
-                                             bool ok) {
-  // dwords [c0, c0 + min(4, wd - c0)) of a row; missing ones are all pads
-#pragma unroll
-  for (int d = 0; d < 4; ++d) w[d] = 0xffffffffu;
-  if (!ok) return;
-  const int nd = min(4, wd - c0);
-  if (nd == 4) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(p + c0);
-    w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-  } else if (nd == 2) {
-    const uint2 v = *reinterpret_cast<const uint2 *>(p + c0);
-    w[0] = v.x, w[1] = v.y;
-  } else {
-    w[0] = p[c0];
+__device__ __forceinline__ typename Pair<T>::type ld_pair(const T *x, int b) {
+  return *reinterpret_cast<const typename Pair<T>::type *>(x + b);
+}
+
+template <typename T>
+__device__ __forceinline__ void st_pair(T *y, int r, int n, T a0, T a1, bool nt) {
+  typedef typename Pair<T>::type P;
+  if (r + 1 < n) {
+    P o;
+    o.x = a0;
+    o.y = a1;
+    if (nt) __builtin_nontemporal_store(o, reinterpret_cast<P *>(y + r));
+    else *reinterpret_cast<P *>(y + r) = o;
+  } else if (r < n) {
+    st_y(y + r, a0, nt);
   }
 }
 
-template <typename T, int WD, bool EPI, bool NT, bool LIST>
-__global__ __launch_bounds__(256) void k_spmv_vi(SpmvArgs<T> a) {
-  constexpr int RPT = 2, NC = (WD == 0 ? 4 : WD) * 4;  // codes per chunk
-  __shared__ int ldict[256];
-  __shared__ T lval[256];
+template <typename T, int KW, bool EPI, bool NT, bool LIST>
+__global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
+  constexpr int KM = 8 * KW;  // diagonals a code word holds
+  __shared__ T lv[KM * 16];
+  typedef typename Pair<T>::type P;
   const int t = threadIdx.x;
   const int wi = xcd_block();
   const int stop = a.done ? *a.done : 0;
   const int s = LIST ? a.items.list[wi] : a.items.first + wi;
-  const int2 sd = a.sdesc[s];
-  if (stop) return;
-  const int r0 = s * kViSliceRows, wd = sd.y;
-  const unsigned *base = a.vcode + sd.x;
-  int row[RPT];
-  unsigned w[RPT][4];
-  T xrow[RPT];
+  if (stop) return;  // uniform: every thread of the grid reads the same flag
+  const int r = s * kDiaSliceRows + 2 * t;
+  const int rs = r < a.n ? r : 0;  // a row pair past the end (codes all 15) reloads x[0]
+  unsigned long long c0, c1;  // nibble k of row r / r + 1
+  if (KW == 1) {
+    const uint2 w = *reinterpret_cast<const uint2 *>(a.dcode + r);
+    c0 = w.x;
+    c1 = w.y;
+  } else {
+    const uint4 w = *reinterpret_cast<const uint4 *>(a.dcode + 2 * r);
+    c0 = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
+    c1 = (unsigned long long)w.z | ((unsigned long long)w.w << 32);
+  }
+  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
+  P xv[KM];
 #pragma unroll
-  for (int q = 0; q < RPT; ++q) {
-    row[q] = r0 + q * 256 + t;
-    const bool ok = row[q] < a.n;
-    vi_row_codes<T>(base + (q * 256 + t) * wd, wd, 0, w[q], ok);
-    xrow[q] = EPI && ok ? a.x[row[q]] : T(0);
+  for (int k = 0; k < KM; ++k) {
+    // unconditional (a lane whose rows hold no entry on diagonal k reloads
+    // its own x[r]): a conditional load makes the compiler wait on it
+    const unsigned n0 = (unsigned)(c0 >> (4 * k)) & 15u, n1 = (unsigned)(c1 >> (4 * k)) & 15u;
+    xv[k] = ld_pair(a.x, k < a.ndiag && (n0 != 15u || n1 != 15u) ? r + a.doff[k] : rs);
   }
-  if (t < a.npair) {
-    ldict[t] = a.vdict[t];
-    lval[t] = a.vval[t];
-  }
+  // x[r], x[r+1] for the epilogue: a pair load of its own (picking the main
+  // diagonal's registers costs the compiler 4x the VGPRs)
+  P xr = P{T(0), T(0)};
+  if (EPI && r < a.n) xr = ld_pair(a.x, r);
+  if (t < a.ndiag * 16) lv[t] = tv;
   __syncthreads();
-  T acc[RPT] = {};
-  for (int c0 = 0;;) {
-    T xx[RPT][NC];
-    int code[RPT][NC];
+  T a0 = T(0), a1 = T(0);
 #pragma unroll
-    for (int q = 0; q < RPT; ++q)
-#pragma unroll
-      for (int u = 0; u < NC; ++u) {
-        code[q][u] = (w[q][u >> 2] >> ((u & 3) * 8)) & 255;
-        xx[q][u] = a.x[code[q][u] != kViPad ? row[q] + ldict[code[q][u]] : (row[q] < a.n ? row[q] : 0)];
-      }
-#pragma unroll
-    for (int q = 0; q < RPT; ++q)
-#pragma unroll
-      for (int u = 0; u < NC; ++u) {
-        const T pr = lval[code[q][u]] * xx[q][u];
-        acc[q] = code[q][u] != kViPad ? acc[q] + pr : acc[q];
-      }
-    c0 += NC / 4;
-    if (WD != 0 || c0 >= wd) break;
-#pragma unroll
-    for (int q = 0; q < RPT; ++q)
-      vi_row_codes<T>(base + (q * 256 + t) * wd, wd, c0, w[q], row[q] < a.n);
-  }
-  double dot = 0.0;
-#pragma unroll
-  for (int q = 0; q < RPT; ++q)
-    if (row[q] < a.n) {
-      st_y(a.y + row[q], acc[q], NT);
-      if (EPI) dot = dot + (double)xrow[q] * (double)acc[q];
+  for (int k = 0; k < KM; ++k) {
+    if (k < a.ndiag) {
+      const unsigned n0 = (unsigned)(c0 >> (4 * k)) & 15u, n1 = (unsigned)(c1 >> (4 * k)) & 15u;
+      const T p0 = lv[k * 16 + n0] * xv[k].x, p1 = lv[k * 16 + n1] * xv[k].y;
+      a0 = n0 != 15u ? a0 + p0 : a0;
+      a1 = n1 != 15u ? a1 + p1 : a1;
     }
+  }
+  st_pair(a.y, r, a.n, a0, a1, NT);
+  double dot = 0.0;
+  if (EPI) {
+    if (r < a.n) dot = (double)xr.x * (double)a0;
+    if (r + 1 < a.n) dot = dot + (double)xr.y * (double)a1;
+  }
   if (EPI) epi_store<4>(dot, a.part, a.fin);
 }
 
 // -------------------------------------------------------------- k_stencil
 // Matrix-free SpMV of the same Laplacian: row r sums its products in the CSR
 // row's column order from 0 with the same values, so y is bit-identical to
-// the CSR SpMV.  Only x (once, coalesced along rows) and y move: the upper
-// bound SURVEY.md 8f asks for beside the CSR runs.  All seven x loads are
-// issued before the first add (clamped addresses; a missing neighbour adds
-// nothing), and the grid coordinates come from two exact reciprocal
-// divisions instead of three integer divisions.
+// the CSR SpMV.  Only x (once) and y move: the upper bound SURVEY.md 8f asks
+// for beside the stored-matrix runs.  Two rows per thread (r even), as in
+// k_spmv_dia: x[r +- nx], x[r +- nx*ny] and x[r], x[r+1] are pair loads,
+// x[r-1] / x[r+2] the neighbouring lanes' centre pair (one extra load at the
+// wave edges); grid coordinates from exact reciprocal divisions.
 __device__ __forceinline__ int fdiv(int a, int d, double inv) {
   int q = (int)((double)a * inv);  // exact floor(a / d) for 0 <= a < 2^31
   q -= q * d > a;
@@ -611,36 +619,72 @@ __device__ __forceinline__ int fdiv(int a, int d, double inv) {
   return q;
 }
 
+struct LapFlags {
+  bool ml, mj, mi, pi, pj, pL;  // neighbour present: -pl, -nx, -1, +1, +nx, +pl
+};
+
+__device__ __forceinline__ LapFlags lap_flags(int r, const LapSpec &g, double inv_pl,
+                                              double inv_nx) {
+  const int pl = g.nx * g.ny;
+  const int l = g.dim == 3 ? fdiv(r, pl, inv_pl) : 0;
+  const int rem = r - l * pl;
+  const int j = fdiv(rem, g.nx, inv_nx);
+  const int i = rem - j * g.nx;
+  return LapFlags{g.dim == 3 && l > 0, j > 0,           i > 0,
+                  i < g.nx - 1,        j < g.ny - 1,    g.dim == 3 && l < g.nz - 1};
+}
+
 template <typename T, bool EPI, bool NT>
 __global__ __launch_bounds__(256) void k_stencil(SpmvArgs<T> a) {
+  typedef typename Pair<T>::type P;
   const LapSpec g = a.lap;
-  const int nx = g.nx, ny = g.ny, pl = g.nx * g.ny, n = a.n;
+  const int nx = g.nx, pl = g.nx * g.ny, n = a.n;
   const int stop = a.done ? *a.done : 0;
   if (stop) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int r = (xcd_block() * 256 + threadIdx.x) * 2;
+  const int rr = r < n ? r : 0;
+  const double inv_pl = a.inv_pl, inv_nx = a.inv_nx;
+  const LapFlags f0 = lap_flags(rr, g, inv_pl, inv_nx);
+  const bool v1 = rr + 1 < n;
+  const LapFlags f1 = lap_flags(v1 ? rr + 1 : rr, g, inv_pl, inv_nx);
+  const T *x = a.x;
+  // every load goes out before the first use, unconditionally (a missing
+  // neighbour pair reloads x[r]: a conditional load makes the compiler wait)
+  const T eL = x[lane == 0 && f0.mi ? rr - 1 : rr];
+  const T eR = x[lane == kWave - 1 && v1 && f1.pi ? rr + 2 : rr];
+  const P zm = ld_pair(x, f0.ml || (v1 && f1.ml) ? rr - pl : rr);
+  const P ym = ld_pair(x, f0.mj || (v1 && f1.mj) ? rr - nx : rr);
+  const P c = ld_pair(x, rr);
+  const P yp = ld_pair(x, f0.pj || (v1 && f1.pj) ? rr + nx : rr);
+  const P zp = ld_pair(x, f0.pL || (v1 && f1.pL) ? rr + pl : rr);
+  __builtin_amdgcn_sched_barrier(0);  // no use of a load is scheduled above the last load
+  T left = __shfl_up(c.y, 1, kWave), right = __shfl_down(c.x, 1, kWave);
+  if (lane == 0) left = eL;
+  if (lane == kWave - 1) right = eR;
   const T m1 = T(-1), dg = T(g.dim == 3 ? 6 : 4);
+  T a0 = T(0), a1 = T(0);
+  a0 = f0.ml ? a0 + m1 * zm.x : a0;
+  a0 = f0.mj ? a0 + m1 * ym.x : a0;
+  a0 = f0.mi ? a0 + m1 * left : a0;
+  a0 = a0 + dg * c.x;
+  a0 = f0.pi ? a0 + m1 * c.y : a0;
+  a0 = f0.pj ? a0 + m1 * yp.x : a0;
+  a0 = f0.pL ? a0 + m1 * zp.x : a0;
+  a1 = f1.ml ? a1 + m1 * zm.y : a1;
+  a1 = f1.mj ? a1 + m1 * ym.y : a1;
+  a1 = f1.mi ? a1 + m1 * c.x : a1;
+  a1 = a1 + dg * c.y;
+  a1 = f1.pi ? a1 + m1 * right : a1;
+  a1 = f1.pj ? a1 + m1 * yp.y : a1;
+  a1 = f1.pL ? a1 + m1 * zp.y : a1;
   double dot = 0.0;
-  const int r = xcd_block() * 256 + threadIdx.x;
   if (r < n) {
-    const int l = g.dim == 3 ? fdiv(r, pl, 1.0 / pl) : 0;
-    const int rem = r - l * pl;
-    const int j = fdiv(rem, nx, 1.0 / nx);
-    const int i = rem - j * nx;
-    const bool ml = g.dim == 3 && l > 0, mj = j > 0, mi = i > 0, pi = i < nx - 1,
-               pj = j < ny - 1, pL = g.dim == 3 && l < g.nz - 1;
-    const T *x = a.x;
-    const T v0 = x[ml ? r - pl : r], v1 = x[mj ? r - nx : r], v2 = x[mi ? r - 1 : r];
-    const T xr = x[r];
-    const T v4 = x[pi ? r + 1 : r], v5 = x[pj ? r + nx : r], v6 = x[pL ? r + pl : r];
-    T acc = T(0);
-    acc = ml ? acc + m1 * v0 : acc;
-    acc = mj ? acc + m1 * v1 : acc;
-    acc = mi ? acc + m1 * v2 : acc;
-    acc = acc + dg * xr;
-    acc = pi ? acc + m1 * v4 : acc;
-    acc = pj ? acc + m1 * v5 : acc;
-    acc = pL ? acc + m1 * v6 : acc;
-    st_y(a.y + r, acc, NT);
-    if (EPI) dot = (double)xr * (double)acc;
+    st_pair(a.y, r, n, a0, a1, NT);
+    if (EPI) {
+      dot = (double)c.x * (double)a0;
+      if (v1) dot = dot + (double)c.y * (double)a1;
+    }
   }
   if (EPI) epi_store<4>(dot, a.part, a.fin);
 }
@@ -1278,11 +1322,14 @@ __global__ __launch_bounds__(256) void k_dc_encode(int n, const int *__restrict_
   }
 }
 
-// CSR-VI code rows of a device-resident CSR (host: the candidate pairs, the
-// slice widths; device: one pass over col/val).  Pairs are sorted by offset,
-// ties by the value's bit pattern (so -0.0, +0.0 and every NaN payload stay
-// distinct); a nonzero that matches no pair raises the error flag and the
-// host keeps another layout.
+// DIA-VI codes of a device-resident CSR (host: the candidate diagonals and
+// their value tables; device: one pass over col/val).  Row r gets nibble k =
+// the index of its entry's value in diagonal k's table (bit patterns, so
+// -0.0, +0.0 and every NaN payload stay distinct), 15 where it has no entry;
+// rows [n, npad) are all 15.  err |= 1 when an entry's diagonal or value is
+// not among the candidates, or a row's columns do not strictly ascend (the
+// diagonal order would then not be the row's order); the host then keeps
+// another layout.
 template <typename T>
 struct Bits;
 template <>
@@ -1297,40 +1344,42 @@ struct Bits<float> {
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_vi_encode(int n, const int *__restrict__ rp,
-                                                   const int *__restrict__ col,
-                                                   const T *__restrict__ val,
-                                                   const int2 *__restrict__ sdesc,
-                                                   const int *__restrict__ poff,
-                                                   const T *__restrict__ pval, int np,
-                                                   unsigned *__restrict__ vcode,
-                                                   int *__restrict__ err) {
+__global__ __launch_bounds__(256) void k_dia_encode(int n, int npad, const int *__restrict__ rp,
+                                                    const int *__restrict__ col,
+                                                    const T *__restrict__ val, DiaCand c,
+                                                    const T *__restrict__ vtab, int kw,
+                                                    unsigned *__restrict__ code,
+                                                    int *__restrict__ err) {
   typedef typename Bits<T>::U U;
-  for (int r = blockIdx.x * 256 + threadIdx.x; r < n; r += gridDim.x * 256) {
-    const int2 sd = sdesc[r / kViSliceRows];
-    const int wd = sd.y;
-    unsigned *out = vcode + sd.x + (long long)(r % kViSliceRows) * wd;
-    const int k0 = rp[r], k1 = rp[r + 1];
-    if (k1 - k0 > 4 * wd) atomicOr(err, 1);
-    for (int d = 0; d < wd; ++d) {
-      unsigned word = 0xffffffffu;
-      for (int b = 0; b < 4; ++b) {
-        const int k = k0 + 4 * d + b;
-        if (k >= k1) break;
+  for (int r = blockIdx.x * 256 + threadIdx.x; r < npad; r += gridDim.x * 256) {
+    unsigned long long w = ~0ull;
+    if (r < n) {
+      int prev = -1;
+      for (int k = rp[r]; k < rp[r + 1]; ++k) {
         const int off = col[k] - r;
-        const U vb = Bits<T>::of(val[k]);
-        int lo = 0, hi = np - 1;  // first pair >= (off, vb)
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          const int mo = poff[mid];
-          const U mb = Bits<T>::of(pval[mid]);
-          if (mo < off || (mo == off && mb < vb)) lo = mid + 1;
-          else hi = mid;
+        int q = 0;
+        while (q < c.ndiag && c.doff[q] != off) ++q;
+        if (q == c.ndiag || q <= prev) {
+          atomicOr(err, 1);
+          break;
         }
-        if (poff[lo] != off || Bits<T>::of(pval[lo]) != vb) atomicOr(err, 1);
-        word = (word & ~(0xffu << (8 * b))) | ((unsigned)lo << (8 * b));
+        prev = q;
+        const U vb = Bits<T>::of(val[k]);
+        int v = 0;
+        while (v < c.nval[q] && Bits<T>::of(vtab[q * 16 + v]) != vb) ++v;
+        if (v == c.nval[q]) {
+          atomicOr(err, 1);
+          break;
+        }
+        w &= ~(15ull << (4 * q));
+        w |= (unsigned long long)v << (4 * q);
       }
-      out[d] = word;
+    }
+    if (kw == 1) {
+      code[r] = (unsigned)w;
+    } else {
+      code[2 * (long long)r] = (unsigned)w;
+      code[2 * (long long)r + 1] = (unsigned)(w >> 32);
     }
   }
 }
@@ -1342,34 +1391,44 @@ __global__ __launch_bounds__(256) void k_vi_encode(int n, const int *__restrict_
 template <typename T>
 int spmv_grid(const SpmvArgs<T> &a) {
   switch (a.layout) {
-    case L_VI: return a.items.count;
-    case L_STENCIL: return (a.n + 255) / 256;
+    case L_DIA: return a.items.count;
+    case L_STENCIL: return (a.n + 511) / 512;
     default: return (a.items.count + 3) / 4;
   }
 }
 
+// U: x gathers issued per row chunk -- 7 when the rows are short (a 7-point
+// row is then exactly one chunk: -4% at C3, tools/mb/spmv_lab.hip), else 8
 template <typename T, int CAPW, bool EPI, bool NT>
 static void launch_csr_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
-  if (a.items.list)
-    hipLaunchKernelGGL((k_spmv_csr<T, CAPW, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_spmv_csr<T, CAPW, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+  const bool l = a.items.list != nullptr;
+  if (a.gath == 7) {
+    if (l) hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 7, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 7, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+  } else {
+    if (l) hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 8, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 8, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+  }
 }
 
 template <typename T, int CAPW, int ND, bool EPI, bool NT>
 static void launch_dc_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
-  if (a.items.list)
-    hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+  const bool l = a.items.list != nullptr;
+  if (a.gath == 7) {
+    if (l) hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 7, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 7, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+  } else {
+    if (l) hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 8, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 8, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+  }
 }
 
-template <typename T, int WD, bool EPI, bool NT>
-static void launch_vi_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
+template <typename T, int KW, bool EPI, bool NT>
+static void launch_dia_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
   if (a.items.list)
-    hipLaunchKernelGGL((k_spmv_vi<T, WD, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_spmv_dia<T, KW, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((k_spmv_vi<T, WD, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_spmv_dia<T, KW, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
 }
 
 template <typename T, bool EPI, bool NT>
@@ -1400,13 +1459,9 @@ static hipError_t launch_spmv_en(const SpmvArgs<T> &a, int g, hipStream_t st) {
       }
       break;
     }
-    case L_VI:
-      switch (a.wdmax) {
-        case 1: launch_vi_w<T, 1, EPI, NT>(a, g, st); break;
-        case 2: launch_vi_w<T, 2, EPI, NT>(a, g, st); break;
-        case 4: launch_vi_w<T, 4, EPI, NT>(a, g, st); break;
-        default: launch_vi_w<T, 0, EPI, NT>(a, g, st); break;
-      }
+    case L_DIA:
+      if (a.ndiag <= 8) launch_dia_w<T, 1, EPI, NT>(a, g, st);
+      else launch_dia_w<T, 2, EPI, NT>(a, g, st);
       break;
     case L_STENCIL:
       hipLaunchKernelGGL((k_stencil<T, EPI, NT>), dim3(g), dim3(256), 0, st, a);
@@ -1554,13 +1609,13 @@ hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dic
 }
 
 template <typename T>
-hipError_t launch_vi_encode(int n, const int *rp, const int *col, const T *val,
-                            const int2 *sdesc, const int *pair_off, const T *pair_val, int np,
-                            unsigned *vcode, int *err, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  const int grid = std::max(1, std::min((n + 255) / 256, 16384));
-  hipLaunchKernelGGL((k_vi_encode<T>), dim3(grid), dim3(256), 0, st, n, rp, col, val, sdesc,
-                     pair_off, pair_val, np, vcode, err);
+hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, const T *val,
+                             const DiaCand &c, const T *vtab, unsigned *code, int *err,
+                             hipStream_t st) {
+  if (npad <= 0) return hipSuccess;
+  const int grid = std::max(1, std::min((npad + 255) / 256, 16384));
+  hipLaunchKernelGGL((k_dia_encode<T>), dim3(grid), dim3(256), 0, st, n, npad, rp, col, val, c,
+                     vtab, c.ndiag <= 8 ? 1 : 2, code, err);
   return hipGetLastError();
 }
 
@@ -1586,9 +1641,9 @@ hipError_t launch_vi_encode(int n, const int *rp, const int *col, const T *val,
   template hipError_t launch_axpby<T>(int, int, double, const T *, const T *, T *, int,          \
                                       hipStream_t);                                              \
   template hipError_t launch_gather<T>(int, const int *, const T *, T *, hipStream_t);           \
-  template hipError_t launch_vi_encode<T>(int, const int *, const int *, const T *,              \
-                                          const int2 *, const int *, const T *, int,             \
-                                          unsigned *, int *, hipStream_t);
+  template hipError_t launch_dia_encode<T>(int, int, const int *, const int *, const T *,       \
+                                           const DiaCand &, const T *, unsigned *, int *,       \
+                                           hipStream_t);
 
 CGX_INSTANTIATE(double)
 CGX_INSTANTIATE(float)

@@ -3,6 +3,7 @@
 #include "cgx_matrix.h"
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -189,33 +190,84 @@ void build_panels(int n, int ncols, const int *rp, const int *col, const T *val,
   }
 }
 
-// CSR-VI slice widths: the widest row of each 512-row slice in dwords (4
-// codes each), rounded to 1, 2 or a multiple of 4; dword offsets 16-B
-// aligned.  False when the padded codes would exceed 2x the compact bytes
-// (nnz + n) -- irregular row lengths, where CSR-DC's compact codes win.
-bool plan_slices(int n, const int *rp, std::vector<int2> &sd, int &wdmax, double &bytes) {
-  const int ns = (n + kViSliceRows - 1) / kViSliceRows;
-  sd.resize((size_t)ns + 1);
-  long long off = 0;
-  wdmax = 0;
-  for (int s = 0; s < ns; ++s) {
-    const int r0 = s * kViSliceRows, r1 = std::min(n, r0 + kViSliceRows);
-    int m = 0;
-    for (int r = r0; r < r1; ++r) m = std::max(m, rp[r + 1] - rp[r]);
-    int wd = (m + 3) / 4;
-    if (wd == 0) wd = 1;
-    if (wd == 3) wd = 4;
-    if (wd > 4) wd = (wd + 3) / 4 * 4;
-    sd[(size_t)s] = make_int2((int)off, wd);
-    off += (long long)wd * kViSliceRows;
-    off = (off + 3) & ~3LL;
-    wdmax = std::max(wdmax, wd);
-    if (off > INT32_MAX) return false;
+// DIA-VI codes cover whole 512-row slices (two rows per thread).
+int padded_rows_for(int n) {
+  return (int)(((long long)n + kDiaSliceRows - 1) / kDiaSliceRows * kDiaSliceRows);
+}
+
+// DIA-VI candidates from the sorted (offset, value bits) keys: <= 16
+// diagonals, <= 15 values each, in an order every row's entries follow.
+// The order is a topological sort (ties by offset) of "offset a comes
+// before offset b in some row", from the same rows the keys came from
+// (sample: every step-th row plus the first and last 4096; else all): a
+// stored row in ascending columns gives ascending offsets, but a partition's
+// ghost columns (local n_loc + position, after the owned ones) come first
+// in the rows of its first plane -- the diagonal order is then [ghost below,
+// -pl, ..., +pl, ghost above] and the sums stay in the rows' order.  The
+// device encoder checks every row against it.  vt[16 k + v] = value v of
+// diagonal k.
+template <typename T>
+bool group_dia(int n, const int *rp, const int *col, bool sample, const std::vector<int> &poff,
+               const std::vector<T> &pval, DiaCand &c, std::vector<T> &vt) {
+  memset(&c, 0, sizeof c);
+  vt.assign(kDiaMax * 16, T(0));
+  std::vector<int> offs;
+  for (size_t i = 0; i < poff.size(); ++i)
+    if (i == 0 || poff[i] != poff[i - 1]) offs.push_back(poff[i]);
+  const int K = (int)offs.size();
+  if (K == 0 || K > kDiaMax) return false;
+  auto idx = [&](int o) {  // K when o is not a candidate
+    const int i = (int)(std::lower_bound(offs.begin(), offs.end(), o) - offs.begin());
+    return i < K && offs[(size_t)i] == o ? i : K;
+  };
+  // before[a] bit b: offset a precedes offset b in some scanned row
+  const int nt = sample ? 1 : host_threads(rp[n]);
+  std::vector<std::array<unsigned, kDiaMax>> before((size_t)nt);
+  for (auto &b : before) b.fill(0u);
+  auto scan = [&](std::array<unsigned, kDiaMax> &b, long long lo, long long hi, long long step) {
+    for (long long r = lo; r < hi; r += step)
+      for (int k = rp[r] + 1; k < rp[r + 1]; ++k) {
+        const int a = idx(col[k - 1] - (int)r), z = idx(col[k] - (int)r);
+        if (a < K && z < K) b[(size_t)a] |= 1u << z;
+      }
+  };
+  if (!col) {
+    // generated Laplacian: its rows ascend in column, i.e. in offset
+  } else if (sample) {
+    const long long step = std::max<long long>(1, n / 65536);
+    scan(before[0], 0, std::min(n, 4096), 1);
+    scan(before[0], 0, n, step);
+    scan(before[0], std::max(0, n - 4096), n, 1);
+  } else {
+    parallel_rows(n, rp[n], [&](int t, long long lo, long long hi) { scan(before[(size_t)t], lo, hi, 1); });
   }
-  sd[(size_t)ns] = make_int2((int)off, 0);
-  bytes = 4.0 * (double)off;
-  const double compact = (double)rp[n] + (double)n;
-  return bytes <= 2.0 * compact + 4096.0;
+  std::array<unsigned, kDiaMax> pred{};  // pred[b] bit a: a must come before b
+  for (auto &b : before)
+    for (int a = 0; a < K; ++a)
+      for (int z = 0; z < K; ++z)
+        if (b[(size_t)a] >> z & 1u) pred[(size_t)z] |= 1u << a;
+  std::vector<int> order;
+  unsigned placed = 0;
+  while ((int)order.size() < K) {
+    int pick = -1;
+    for (int q = 0; q < K && pick < 0; ++q)  // smallest offset whose predecessors are placed
+      if (!(placed >> q & 1u) && (pred[(size_t)q] & ~placed) == 0) pick = q;
+    if (pick < 0) return false;  // the rows disagree on the order: no DIA
+    order.push_back(pick);
+    placed |= 1u << pick;
+  }
+  std::vector<int> pos((size_t)K);
+  for (int k = 0; k < K; ++k) {
+    pos[(size_t)order[(size_t)k]] = k;
+    c.doff[k] = offs[(size_t)order[(size_t)k]];
+  }
+  c.ndiag = K;
+  for (size_t i = 0; i < poff.size(); ++i) {
+    const int k = pos[(size_t)idx(poff[i])];
+    if (c.nval[k] == kDiaVals) return false;
+    vt[(size_t)k * 16 + c.nval[k]++] = pval[i];
+  }
+  return true;
 }
 
 // L2 tiling of the item order for a wide stencil: the x lines a row needs sit
@@ -284,21 +336,21 @@ void DevMatrix::release() {
   dev_free(&d_code);
   dev_free(&d_rlen);
   dev_free(&d_dict);
-  dev_free(&d_vcode);
-  dev_free(&d_sdesc);
-  dev_free(&d_vdict);
-  dev_free(&d_vval);
+  dev_free(&d_dcode);
+  dev_free(&d_vtab);
   dev_free(&d_order);
   order.clear();
   blk_row.clear();
   panel_first.clear();
   panel_count.clear();
-  n = nnz = ncols = nblk = ndict = npair = nslice = wdmax = tile_bands = 0;
+  n = nnz = ncols = nblk = ndict = tile_bands = 0;
+  memset(&dia, 0, sizeof dia);
+  kdiag = -1;
+  gath = 8;
   npanel = 1;
   layout = L_CSR;
   nt = false;
   dev_bytes = 0;
-  vcode_bytes = 0;
   encode_fallback = 0;
   setup_host_ms = setup_dev_ms = 0;
 }
@@ -365,31 +417,25 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   int rc;
 
   // ---- which layout: candidates from a sample (or the generator's stencil)
-  const bool want_vi = want == CGX_LAYOUT_AUTO || want == CGX_LAYOUT_VI;
-  const bool want_dc = want_vi || want == CGX_LAYOUT_DC;
-  std::vector<int> poff;  // VI pair offsets / DC offsets, sorted
-  std::vector<T> pval;
-  std::vector<int2> sd;
+  const bool want_dia = want == CGX_LAYOUT_AUTO || want == CGX_LAYOUT_DIA;
+  const bool want_dc = want_dia || want == CGX_LAYOUT_DC;
+  std::vector<int> poff;  // (offset, value) keys, sorted
+  std::vector<T> pval, vt;
   int maxlen = 0;
   for (int r = 0; r < n; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
-  bool vi_ok = false, dc_ok = false;
-  if (n > 0 && nnz > 0 && want_vi) {
-    int wdm = 0;
-    double vb = 0;
-    if (plan_slices(n, rp, sd, wdm, vb)) {
-      if (gen) {  // one value per offset: 2 dim on the diagonal, -1 off it
-        poff = lap_offsets(*gen);
-        for (int o : poff) pval.push_back(o == 0 ? T(2 * gen->dim) : T(-1));
-        vi_ok = true;
-      } else {
-        vi_ok = find_pairs(n, rp, col, val, true, 255, true, poff, pval);
-      }
-      wdmax = wdm;
-      vcode_bytes = vb;
+  bool dia_ok = false, dc_ok = false;
+  if (n > 0 && nnz > 0 && want_dia) {
+    if (gen) {  // one value per offset: 2 dim on the diagonal, -1 off it
+      poff = lap_offsets(*gen);
+      for (int o : poff) pval.push_back(o == 0 ? T(2 * gen->dim) : T(-1));
+      dia_ok = group_dia<T>(n, rp, nullptr, true, poff, pval, dia, vt);
+    } else if (maxlen <= kDiaMax) {
+      dia_ok = find_pairs(n, rp, col, val, true, kDiaMax * kDiaVals, true, poff, pval) &&
+               group_dia(n, rp, col, true, poff, pval, dia, vt);
     }
   }
   std::vector<int> doff;
-  if (!vi_ok && n > 0 && nnz > 0 && want_dc && maxlen <= 255) {
+  if (!dia_ok && n > 0 && nnz > 0 && want_dc && maxlen <= 255) {
     std::vector<T> dummy;
     if (gen) {
       doff = lap_offsets(*gen);
@@ -404,7 +450,7 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   std::vector<T> pval_panel;
   const bool want_panel = want == CGX_LAYOUT_PANEL;
   npanel = 1;
-  if (!vi_ok && !dc_ok && !gen && n > 0 && nnz > 0 && allow_panels &&
+  if (!dia_ok && !dc_ok && !gen && n > 0 && nnz > 0 && allow_panels &&
       (want == CGX_LAYOUT_AUTO || want_panel))
     npanel = choose_panels(n, rp, col, ts, want_panel);
   if (npanel > 1) {
@@ -445,45 +491,40 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     return code;
   };
 
-  // ---- CSR-VI: device encode against the candidates, exact host scan on a miss
-  if (vi_ok) {
-    nslice = (int)sd.size() - 1;
-    const size_t words = (size_t)sd.back().x + 4;
-    if ((rc = dev_alloc(&d_vcode, words * 4, &dev_bytes)) ||
-        (rc = dev_alloc(&d_sdesc, sd.size() * sizeof(int2), &dev_bytes)) ||
-        (rc = dev_alloc(&d_vdict, 256 * 4, &dev_bytes)) ||
-        (rc = dev_alloc(&d_vval, 256 * ts, &dev_bytes)))
-      return fail(rc);
-    CGX_HIP(hipMemcpyAsync(d_sdesc, sd.data(), sd.size() * sizeof(int2), hipMemcpyHostToDevice, st));
-    for (int attempt = 0; attempt < 2 && vi_ok; ++attempt) {
-      std::vector<int> po = poff;
-      std::vector<T> pv = pval;
-      po.resize(256, 0);
-      pv.resize(256, T(0));
-      CGX_HIP(hipMemcpyAsync(d_vdict, po.data(), 256 * 4, hipMemcpyHostToDevice, st));
-      CGX_HIP(hipMemcpyAsync(d_vval, pv.data(), 256 * ts, hipMemcpyHostToDevice, st));
+  // ---- DIA-VI: device encode against the candidates, exact host scan on a miss
+  if (dia_ok) {
+    const int npad = padded_rows_for(n);
+    for (int attempt = 0; attempt < 2 && dia_ok; ++attempt) {
+      const int kw = dia.ndiag <= 8 ? 1 : 2;
+      dev_free(&d_dcode);
+      dev_free(&d_vtab);
+      if ((rc = dev_alloc(&d_dcode, ((size_t)npad * kw + 4) * 4, &dev_bytes)) ||
+          (rc = dev_alloc(&d_vtab, (size_t)kDiaMax * 16 * ts, &dev_bytes)))
+        return fail(rc);
+      CGX_HIP(hipMemcpyAsync(d_vtab, vt.data(), (size_t)kDiaMax * 16 * ts, hipMemcpyHostToDevice, st));
       CGX_HIP(hipMemsetAsync(d_err, 0, 4, st));
-      CGX_HIP(launch_vi_encode<T>(n, d_rp, d_col, (const T *)d_val, d_sdesc, d_vdict,
-                                  (const T *)d_vval, (int)poff.size(), d_vcode, d_err, st));
+      CGX_HIP(launch_dia_encode<T>(n, npad, d_rp, d_col, (const T *)d_val, dia, (const T *)d_vtab,
+                                   d_dcode, d_err, st));
       int err = 0;
       if ((rc = read_err(&err))) return fail(rc);
       if (!err) break;
-      if (attempt == 0 && !gen) {  // the sample missed a pair: exact scan
+      if (attempt == 0 && !gen) {  // the sample missed a diagonal or a value: exact scan
         encode_fallback = 1;
-        vi_ok = find_pairs(n, rp, col, val, true, 255, false, poff, pval);
+        dia_ok = find_pairs(n, rp, col, val, true, kDiaMax * kDiaVals, false, poff, pval) &&
+                 group_dia(n, rp, col, false, poff, pval, dia, vt);
       } else {
-        vi_ok = false;
+        dia_ok = false;  // e.g. a row whose columns do not ascend
       }
     }
-    if (vi_ok) {
-      npair = (int)poff.size();
-      layout = L_VI;
+    if (dia_ok) {
+      layout = L_DIA;
+      kdiag = -1;
+      for (int k = 0; k < dia.ndiag; ++k)
+        if (dia.doff[k] == 0) kdiag = k;
     } else {
-      dev_free(&d_vcode);
-      dev_free(&d_sdesc);
-      dev_free(&d_vdict);
-      dev_free(&d_vval);
-      nslice = 0;
+      dev_free(&d_dcode);
+      dev_free(&d_vtab);
+      memset(&dia, 0, sizeof dia);
       if (want_dc && maxlen <= 255 && !dc_ok) {
         std::vector<T> dummy;
         if (gen) {
@@ -497,7 +538,8 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   }
 
   // ---- row blocks (CSR / DC)
-  if (layout != L_VI) {
+  gath = nnz <= 7LL * n ? 7 : 8;
+  if (layout != L_DIA) {
     capw = ts == 4 ? 1024 : 512;
     if (ts == 8 && npanel == 1 && n > 0) {
       // LDS window sized to the matrix: 328 entries when every 64-row block
@@ -528,7 +570,7 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   }
 
   // ---- CSR-DC
-  if (layout != L_VI && dc_ok && npanel == 1) {
+  if (layout != L_DIA && dc_ok && npanel == 1) {
     if ((rc = dev_alloc(&d_code, nnz_pad, &dev_bytes)) ||
         (rc = dev_alloc(&d_dict, 256 * 4, &dev_bytes)) ||
         (rc = dev_alloc(&d_rlen, (size_t)n + 64, &dev_bytes)))
@@ -566,10 +608,13 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   }
   (void)hipFree(d_err);
 
-  // ---- L2-tiled item order for wide stencils (DC / VI)
-  if (layout == L_DC || layout == L_VI) {
+  // ---- L2-tiled item order for wide stencils (DC / DIA)
+  if (layout == L_DC || layout == L_DIA) {
     long long P = 0;
-    for (int v : (layout == L_VI ? poff : doff)) P = std::max(P, (long long)std::abs(v));
+    if (layout == L_DIA)
+      for (int k = 0; k < dia.ndiag; ++k) P = std::max(P, (long long)std::abs(dia.doff[k]));
+    else
+      for (int v : doff) P = std::max(P, (long long)std::abs(v));
     const std::vector<int> ir = item_rows();
     order = tile_order(ir, P, ts, tile_bands);
     if (!order.empty()) {
@@ -599,17 +644,18 @@ template int DevMatrix::upload<float>(int, int, int, const int *, const int *, c
 
 int DevMatrix::items() const {
   switch (layout) {
-    case L_VI: return nslice;
-    case L_STENCIL: return (n + 255) / 256;
+    case L_DIA:
+    case L_STENCIL: return (n + kDiaSliceRows - 1) / kDiaSliceRows;
     default: return nblk;
   }
 }
 
+int DevMatrix::padded_rows() const { return padded_rows_for(n); }
+
 std::vector<int> DevMatrix::item_rows() const {
   if (layout == L_CSR || layout == L_DC) return blk_row;
   std::vector<int> r;
-  const int step = layout == L_VI ? kViSliceRows : 256;
-  for (int i = 0; i < n; i += step) r.push_back(i);
+  for (int i = 0; i < n; i += kDiaSliceRows) r.push_back(i);
   r.push_back(n);
   return r;
 }
@@ -622,7 +668,7 @@ double DevMatrix::csr_bytes() const {
 double DevMatrix::layout_bytes() const {
   const double sv = dtype == CGX_F32 ? 4.0 : 8.0;
   switch (layout) {
-    case L_VI: return vcode_bytes + 2.0 * n * sv + (4.0 + sv) * npair;
+    case L_DIA: return (dia.ndiag <= 8 ? 4.0 : 8.0) * n + 2.0 * n * sv;
     case L_DC: return (double)nnz * (sv + 1) + 1.0 * n + 2.0 * n * sv + 4.0 * ndict;
     case L_STENCIL: return 2.0 * n * sv;
     default:
@@ -652,21 +698,26 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
   a.rlen = d_rlen;
   a.dict = d_dict;
   a.ndict_cap = ndict <= 64 ? 64 : 256;
-  a.vcode = d_vcode;
-  a.sdesc = d_sdesc;
-  a.vdict = d_vdict;
-  a.vval = (const T *)d_vval;
-  a.npair = npair;
-  a.wdmax = wdmax <= 4 ? wdmax : 0;
+  a.gath = gath;
+  a.dcode = d_dcode;
+  a.vtab = (const T *)d_vtab;
+  a.ndiag = dia.ndiag;
+  a.kdiag = kdiag;
+  for (int k = 0; k < kDiaMax; ++k) a.doff[k] = dia.doff[k];
+  a.ncols = ncols;
   a.n = n;
   a.lap = lap;
+  if (layout == L_STENCIL) {
+    a.inv_nx = 1.0 / lap.nx;
+    a.inv_pl = 1.0 / ((double)lap.nx * lap.ny);
+  }
   return a;
 }
 
 int DevMatrix::partials(Items it) const {
   switch (layout) {
-    case L_VI: return it.count;
-    case L_STENCIL: return (n + 255) / 256;
+    case L_DIA: return it.count;
+    case L_STENCIL: return (n + kDiaSliceRows - 1) / kDiaSliceRows;
     default:
       if (npanel > 1) return (panel_count.back() + 3) / 4;
       return (it.count + 3) / 4;
@@ -677,7 +728,7 @@ template <typename T>
 hipError_t DevMatrix::spmv(const T *x, T *y, double *part, const int *done, Items it,
                            hipStream_t s, int *nparts) const {
   if (nparts) *nparts = partials(it);
-  if (layout == L_STENCIL) it = Items{nullptr, 0, (n + 255) / 256};
+  if (layout == L_STENCIL) it = Items{nullptr, 0, (n + kDiaSliceRows - 1) / kDiaSliceRows};
   if (npanel <= 1) return launch_spmv<T>(args<T>(x, y, part, done, it), s);
   for (int q = 0; q < npanel; ++q) {
     SpmvArgs<T> a = args<T>(x, y, q + 1 == npanel ? part : nullptr, done,

@@ -6,10 +6,11 @@
 // col_indices, fp64 values; fp32 for SURVEY.md C5).  The CSR arrays always
 // stay resident; on top of them the matrix picks, once per upload, the
 // layout the SpMV streams (cgx_internal.h, Layout):
-//   auto: CSR-VI when the nonzeros use <= 255 distinct (col - row, value)
-//         pairs and the row widths are regular; else CSR-DC when they use
-//         <= 256 distinct offsets (rows <= 255 entries); else plain CSR,
-//         with column panels when the gathers have no locality (C5).
+//   auto: DIA-VI when the nonzeros lie on <= 16 diagonals (col - row) with
+//         <= 15 distinct values each and every row's columns ascend; else
+//         CSR-DC when they use <= 256 distinct offsets (rows <= 255
+//         entries); else plain CSR, with column panels when the gathers
+//         have no locality (C5).
 // Candidates (pairs / offsets) come from a sample of rows on the host; the
 // device encoder then checks every nonzero against them, and a miss falls
 // back to an exact host scan -- so the setup of a 10 M-row stencil is one
@@ -44,13 +45,12 @@ struct DevMatrix {
   unsigned char *d_code = nullptr, *d_rlen = nullptr;
   int *d_dict = nullptr;
   int ndict = 0;
-  // VI
-  unsigned *d_vcode = nullptr;
-  int2 *d_sdesc = nullptr;
-  int *d_vdict = nullptr;
-  void *d_vval = nullptr;
-  int npair = 0, nslice = 0, wdmax = 0;
-  double vcode_bytes = 0;
+  // DIA
+  unsigned *d_dcode = nullptr;  // per row 1 (<= 8 diagonals) or 2 dwords of nibbles
+  void *d_vtab = nullptr;       // [16][16] values
+  DiaCand dia{};
+  int kdiag = -1;               // main diagonal's index, -1: none
+  int gath = 8;                 // CSR / DC: gathers per row chunk
   // L2-tiled order of the work items (DC / VI, wide stencils; nullptr: natural)
   int *d_order = nullptr;
   std::vector<int> order;    // host copy of the tiled order (empty: natural)
@@ -74,6 +74,8 @@ struct DevMatrix {
   int items() const;  // work items of the layout (blocks or slices)
   // host: first row of each item, items() + 1 entries
   std::vector<int> item_rows() const;
+  // rows covered by the items (DIA pads to whole 512-row slices)
+  int padded_rows() const;
   // algorithmic HBM bytes of one SpMV in the layout it runs on
   double layout_bytes() const;
   // CSR-basis algorithmic bytes (SURVEY.md 8d B_spmv)

@@ -65,18 +65,27 @@ int check_device(int device, int *cus) {
 
 int dev_alloc(void **p, size_t bytes, size_t *counter) {
   if (bytes == 0) bytes = 16;
-  hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+  void *raw = nullptr;
+  const size_t total = bytes + kGuardBytes;
+  hipError_t e = hipExtMallocWithFlags(&raw, total, hipDeviceMallocContiguous);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    e = hipMalloc(p, bytes);
+    e = hipMalloc(&raw, total);
   }
+  if (e == hipSuccess) e = hipMemset(raw, 0, kGuardBytes);  // the guard reads as 0.0
   if (e != hipSuccess) {
     set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    if (raw) (void)hipFree(raw);
     *p = nullptr;
     return CGX_ENOMEM;
   }
-  if (counter) *counter += bytes;
+  *p = (char *)raw + kGuardBytes;
+  if (counter) *counter += total;
   return 0;
+}
+
+void dev_free_raw(void *p) {
+  if (p) (void)hipFree((char *)p - kGuardBytes);
 }
 
 int vec_grid_for(int n, int cus) {
@@ -90,7 +99,7 @@ int vec_grid_for(int n, int cus) {
 
 int public_layout(const DevMatrix &m) {
   switch (m.layout) {
-    case L_VI: return CGX_LAYOUT_VI;
+    case L_DIA: return CGX_LAYOUT_DIA;
     case L_DC: return CGX_LAYOUT_DC;
     case L_STENCIL: return CGX_LAYOUT_STENCIL;
     default: return m.npanel > 1 ? CGX_LAYOUT_PANEL : CGX_LAYOUT_CSR;
@@ -694,10 +703,12 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->spmv_iter_bytes = A.layout_bytes();
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
-  info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_VI ? A.npair : 0;
+  info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;
   info->tile_bands = A.tile_bands;
   info->nt = A.nt ? 1 : 0;
-  info->row_width = A.layout == L_VI ? 4 * A.wdmax : 0;
+  info->code_bytes_per_row = A.layout == L_DIA ? (A.dia.ndiag <= 8 ? 4 : 8) : 0;
+  for (int k = 0; k < A.dia.ndiag; ++k) info->n_values += A.dia.nval[k];
+  info->gathers_per_chunk = A.layout == L_CSR || A.layout == L_DC ? A.gath : 0;
   info->setup_host_ms = A.setup_host_ms;
   info->setup_device_ms = A.setup_dev_ms;
   info->encode_fallback = A.encode_fallback;

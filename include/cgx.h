@@ -84,48 +84,52 @@ enum { CGX_F64 = 0, CGX_F32 = 1 };
 
 /* Device layout of the matrix the SpMV streams (the C ABI always takes the
  * reference's CSR; the CSR arrays stay resident whatever the layout):
- *   AUTO     VI where it applies, else DC, else CSR (PANEL for gathers with
+ *   AUTO     DIA where it applies, else DC, else CSR (PANEL for gathers with
  *            no locality, e.g. random SPD)                       (default)
  *   CSR      plain CSR, int32 columns: SURVEY.md 8d's B_spmv layout
  *   DC       dictionary-coded columns: <= 256 distinct col - row offsets,
  *            one code byte per nonzero + the value stream, rows <= 255
- *   VI       value-indexed pairs: <= 255 distinct (col - row, value) pairs,
- *            one code byte per nonzero naming both, no value stream, rows
- *            in 512-row slices of fixed width (stencils, small value sets)
+ *   DIA      value-indexed diagonal codes: nonzeros on <= 16 diagonals
+ *            (col - row) with <= 15 distinct values each, every row's
+ *            columns ascending; one nibble per (row, diagonal) names the
+ *            entry's value or "no entry" -- no column or value stream
+ *            (stencils, banded matrices with few coefficients)
  *   PANEL    CSR split into column panels (one SpMV pass per panel)
  *   STENCIL  matrix-free Laplacian (cgx_solver_set_stencil; info only)
- * A requested layout that does not apply falls back VI -> DC -> CSR;
+ * A requested layout that does not apply falls back DIA -> DC -> CSR;
  * cgx_info.layout says which one runs.  Every layout sums each row in the
  * reference's order: y is bit-identical across layouts. */
-enum { CGX_LAYOUT_AUTO = 0, CGX_LAYOUT_CSR = 1, CGX_LAYOUT_DC = 2, CGX_LAYOUT_VI = 3,
+enum { CGX_LAYOUT_AUTO = 0, CGX_LAYOUT_CSR = 1, CGX_LAYOUT_DC = 2, CGX_LAYOUT_DIA = 3,
        CGX_LAYOUT_PANEL = 4, CGX_LAYOUT_STENCIL = 5 };
 
 typedef struct {
   int n, nnz, dtype, mode, alg;
   int layout;           /* CGX_LAYOUT_* the SpMV runs on                     */
   int n_items;          /* SpMV work items: 64-row blocks (CSR/DC/PANEL) or
-                           512-row slices (VI)                              */
+                           512-row slices (DIA, STENCIL)                     */
   int spmv_grid;        /* workgroups of one SpMV launch (= its partials)    */
   int vec_grid;         /* 256-thread units of the vector-update launches    */
   double spmv_bytes;    /* algorithmic HBM bytes per SpMV, CSR basis
                            (SURVEY.md 8d B_spmv)                             */
   double iter_bytes;    /* algorithmic HBM bytes per CG iteration (8d)       */
   double spmv_iter_bytes; /* algorithmic bytes of one SpMV in the layout it
-                             runs on (VI: padded code rows + x + y + pairs;
-                             DC: codes + values + row lengths + x + y;
-                             PANEL: + P row_ptrs and y round trips)         */
+                             runs on (DIA: codes + x + y; DC: codes + values
+                             + row lengths + x + y; PANEL: + P row_ptrs and
+                             y round trips)                                 */
   size_t device_bytes;  /* device memory held by the solver                  */
   int n_panels;         /* column panels of the SpMV (1: none)               */
-  int n_dict;           /* DC: distinct col - row offsets; VI: distinct
-                           (offset, value) pairs; 0 otherwise               */
+  int n_dict;           /* DC: distinct col - row offsets; DIA: diagonals;
+                           0 otherwise                                      */
   int tile_bands;       /* L2-tiled item order: bands of the widest offset's
                            period swept one after another (0: natural)      */
   int nt;               /* 1: matrix stream and y store non-temporal        */
-  int row_width;        /* VI: codes per row of the widest slice            */
-  int encode_fallback;  /* 1: the sampled pairs/offsets missed one; an exact
+  int code_bytes_per_row; /* DIA: 4 (<= 8 diagonals) or 8                   */
+  int encode_fallback;  /* 1: the sampled candidates missed one; an exact
                            host scan was needed                             */
   double setup_host_ms;   /* set_matrix: host time (checks, plan, submit)    */
   double setup_device_ms; /* set_matrix: device time after the last submit  */
+  int n_values;         /* DIA: values over all diagonal tables             */
+  int gathers_per_chunk; /* CSR / DC: x gathers issued per row chunk (7|8)  */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);

@@ -108,9 +108,9 @@ def test_local_group_bench_and_interior_split():
         parts[0].close()
     # z-slabs of 16 planes: one ghost plane per neighbour, boundary blocks
     # are the first and last plane's 64-row blocks
-    # VI slices of 512 rows: the first and last plane's 2 slices per face
+    # DIA slices of 512 rows: the first and last plane's 2 slices per face
     assert [s["n_ghost"] for s in st] == [1024, 2048, 2048, 1024]
-    assert [s["layout_name"] for s in st] == ["vi"] * 4
+    assert [s["layout_name"] for s in st] == ["dia"] * 4
     assert [s["boundary_items"] for s in st] == [2, 4, 4, 2]
     assert all(s["interior_items"] > 0 for s in st)
 
@@ -148,19 +148,19 @@ def test_history_after_buffer_growth():
 def test_layouts_partitions_identical_in_exact_sums(P):
     """Partitions of a Laplacian keep a small set of local column offsets
     (owned rows: the stencil's; ghost columns: one more constant offset per
-    face), so every part runs CSR-DC or CSR-VI like the single-GPU solver.
+    face), so every part runs CSR-DC or DIA-VI like the single-GPU solver.
     With tol = 0 the layouts only change how A is stored and how the SpMV
-    partials are grouped: x agrees to rounding (1e-12) across CSR, DC, VI."""
+    partials are grouped: x agrees to rounding (1e-12) across CSR, DC, DIA."""
     rp, col, val, b = system("lap3d")
     out = {}
-    for layout in ("csr", "dc", "vi"):
+    for layout in ("csr", "dc", "dia"):
         x, its, hist, stats = solve_local(rp, col, val, b, P, 50, 0.0, layout=layout)
         assert all(s["layout_name"] == layout for s in stats)
         if layout != "csr":
             assert all(0 < s["n_dict"] <= 21 for s in stats)  # <= 7 stencil + 7 per ghost face
             assert all(s["spmv_iter_bytes"] < s["spmv_bytes"] for s in stats)
         out[layout] = x
-    for layout in ("dc", "vi"):
+    for layout in ("dc", "dia"):
         assert np.linalg.norm(out[layout] - out["csr"]) <= 1e-12 * np.linalg.norm(out["csr"])
 
 
@@ -280,7 +280,7 @@ def test_local_group_sums_match_solver_bit_exact():
     folded kernels sum the partials directly (sum_parts<1024>): the in-kernel
     local sums reproduce the finalize order exactly, in every layout."""
     rp, col, val, b = system("lap3d")
-    for layout in ("csr", "dc", "vi"):
+    for layout in ("csr", "dc", "dia"):
         x, its, hist, _ = solve_local(rp, col, val, b, 1, 40, 0.0, alg=cgx.CGX_ALG_HS,
                                       layout=layout)
         with cgx.Solver(0, layout=layout) as s:

@@ -84,7 +84,7 @@ struct Csr {
 };
 
 // ------------------------------------------------------------------ CSR
-template <int CAPW, int U, bool NTY, int WPB = 4, bool PRIO = false>
+template <int CAPW, int U, bool NTY, int WPB = 4, bool PRIO = false, bool SHJ = false>
 __global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
   __shared__ __attribute__((aligned(16))) double lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
@@ -112,10 +112,14 @@ __global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
     double xrow = 0.0, acc = 0.0;
     if (lane < nr) {
       j0 = a.rp[r0 + lane];
-      j1 = a.rp[r0 + lane + 1];
+      if (!SHJ) j1 = a.rp[r0 + lane + 1];
       xrow = a.x[r0 + lane];
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (SHJ) {  // row end = the next lane's row start; the block's last row ends at k1
+      j1 = __shfl_down(j0, 1, 64);
+      if (lane == nr - 1) j1 = k1;
+    }
     wave_lds_sync();
     if (PRIO) __builtin_amdgcn_s_setprio(2);
     if (lane < nr) {
@@ -403,8 +407,124 @@ __global__ __launch_bounds__(256) void k_sten(Sten g) {
   epi_store<4>(dot, g.part);
 }
 
-// --------------------------------------------------------------- ceilings
 typedef double d2v __attribute__((ext_vector_type(2)));
+typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));  // 8-B aligned pair
+
+// two rows per thread (r even, nx even): every neighbour pair x[r+d], x[r+1+d]
+// with d = +-pl, +-nx, 0 is ONE 16-B load; x[r-1] / x[r+2] come from the
+// neighbouring lanes' centre pair (one extra load at the wave edges).  Half
+// the vector-memory instructions of k_sten, same products, same order.
+template <bool NTY>
+__global__ __launch_bounds__(256) void k_sten2(Sten g) {
+  const int nx = g.nx, ny = g.ny, pl = g.nx * g.ny, n = g.n;
+  const int lane = threadIdx.x & 63;
+  const int r = (xcd_block() * 256 + threadIdx.x) * 2;
+  const bool act = r < n;
+  const int rr = act ? r : 0;
+  const int l = fdiv(rr, pl, g.inv_pl);
+  const int rem = rr - l * pl;
+  const int j = fdiv(rem, nx, g.inv_nx);
+  const int i = rem - j * nx;
+  const bool ml = l > 0, mj = j > 0, pj = j < ny - 1, pL = l < g.nz - 1;
+  const d2v *X = (const d2v *)g.x;
+  const int h = rr >> 1;
+  // every load goes out before the first use (edge lanes' extra loads too)
+  double eL = 0.0, eR = 0.0;
+  if (lane == 0) eL = g.x[i > 0 ? rr - 1 : rr];
+  if (lane == 63) eR = g.x[i + 2 < nx ? rr + 2 : rr];
+  const d2v zm = X[ml ? h - pl / 2 : h], ym = X[mj ? h - nx / 2 : h];
+  const d2v c = X[h];
+  const d2v yp = X[pj ? h + nx / 2 : h], zp = X[pL ? h + pl / 2 : h];
+  double left = __shfl_up(c.y, 1, 64), right = __shfl_down(c.x, 1, 64);
+  if (lane == 0) left = eL;
+  if (lane == 63) right = eR;
+  double dot = 0.0;
+  if (act) {
+    double a0 = 0.0, a1 = 0.0;
+    a0 = ml ? a0 + -1.0 * zm.x : a0;
+    a0 = mj ? a0 + -1.0 * ym.x : a0;
+    a0 = i > 0 ? a0 + -1.0 * left : a0;
+    a0 = a0 + 6.0 * c.x;
+    a0 = a0 + -1.0 * c.y;
+    a0 = pj ? a0 + -1.0 * yp.x : a0;
+    a0 = pL ? a0 + -1.0 * zp.x : a0;
+    a1 = ml ? a1 + -1.0 * zm.y : a1;
+    a1 = mj ? a1 + -1.0 * ym.y : a1;
+    a1 = a1 + -1.0 * c.x;
+    a1 = a1 + 6.0 * c.y;
+    a1 = i + 2 < nx ? a1 + -1.0 * right : a1;
+    a1 = pj ? a1 + -1.0 * yp.y : a1;
+    a1 = pL ? a1 + -1.0 * zp.y : a1;
+    d2v o;
+    o.x = a0;
+    o.y = a1;
+    if (NTY) __builtin_nontemporal_store(o, (d2v *)g.y + h);
+    else ((d2v *)g.y)[h] = o;
+    dot = c.x * a0;
+    dot = dot + c.y * a1;
+  }
+  epi_store<4>(dot, g.part);
+}
+
+// ------------------------------------------------------------- DIA-VI
+// <= K distinct column offsets d_0 < ... < d_{K-1}; per row a word of K
+// nibbles, nibble k = index of the value of the row's entry at offset d_k in
+// a per-offset value table (15 = no entry).  A row's entries ascend in
+// column = ascend in offset, so summing k = 0..K-1 is the CSR order.  Two
+// rows per thread: x[r+d_k], x[r+1+d_k] is one (8-B aligned) 16-B load,
+// issued only by lanes whose rows hold offset k.
+struct Dia {
+  const unsigned *code;  // row r: code[r] (K <= 8)
+  const double *vtab;    // [K][16]
+  const double *x;
+  double *y, *part;
+  int n;
+  int d[8];
+};
+
+template <int K, bool NTY>
+__global__ __launch_bounds__(256) void k_dia2(Dia a) {
+  __shared__ double lv[K * 16];
+  const int t = threadIdx.x;
+  const double tv = t < K * 16 ? a.vtab[t] : 0.0;
+  const int r = (xcd_block() * 256 + t) * 2;
+  const bool act = r < a.n;
+  const uint2 cw = act ? reinterpret_cast<const uint2 *>(a.code)[r >> 1] : make_uint2(~0u, ~0u);
+  d2v xv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const unsigned n0 = (cw.x >> (4 * k)) & 15u, n1 = (cw.y >> (4 * k)) & 15u;
+    xv[k] = d2v{0.0, 0.0};
+    if (n0 != 15u || n1 != 15u) xv[k] = *(const d2u *)(a.x + r + a.d[k]);
+  }
+  if (t < K * 16) lv[t] = tv;
+  __syncthreads();
+  double a0 = 0.0, a1 = 0.0, xr0 = 0.0, xr1 = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const unsigned n0 = (cw.x >> (4 * k)) & 15u, n1 = (cw.y >> (4 * k)) & 15u;
+    const double p0 = lv[k * 16 + n0] * xv[k].x, p1 = lv[k * 16 + n1] * xv[k].y;
+    a0 = n0 != 15u ? a0 + p0 : a0;
+    a1 = n1 != 15u ? a1 + p1 : a1;
+    if (a.d[k] == 0) {
+      xr0 = xv[k].x;
+      xr1 = xv[k].y;
+    }
+  }
+  double dot = 0.0;
+  if (act) {
+    d2v o;
+    o.x = a0;
+    o.y = a1;
+    if (NTY) __builtin_nontemporal_store(o, (d2v *)(a.y + r));
+    else *(d2v *)(a.y + r) = o;
+    dot = xr0 * a0;
+    dot = dot + xr1 * a1;
+  }
+  epi_store<4>(dot, a.part);
+}
+
+// --------------------------------------------------------------- ceilings
 // reads val (n2v double2) and col (n2c int4): the CSR stream's bytes
 __global__ __launch_bounds__(256) void k_read(const d2v *__restrict__ v, long long n2v,
                                               const int4 *__restrict__ c, long long n2c,
@@ -425,12 +545,19 @@ __global__ __launch_bounds__(256) void k_read(const d2v *__restrict__ v, long lo
 // in-situ cache state: what the CG iteration's vector kernels do between
 // two SpMVs (read r, s; write r; read x, p, r; write x, p) -- here x is
 // rewritten with its own values, two scratch vectors read and written
+template <bool NT>
 __global__ __launch_bounds__(256) void k_pollute(double *x, double *a, double *b, int n) {
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const double xv = x[i], av = a[i], bv = b[i];
-    a[i] = av + bv;
-    b[i] = bv - av;
-    x[i] = xv;
+    if (NT) {
+      __builtin_nontemporal_store(av + bv, a + i);
+      __builtin_nontemporal_store(bv - av, b + i);
+      __builtin_nontemporal_store(xv, x + i);
+    } else {
+      a[i] = av + bv;
+      b[i] = bv - av;
+      x[i] = xv;
+    }
   }
 }
 
@@ -438,7 +565,9 @@ __global__ __launch_bounds__(256) void k_pollute(double *x, double *a, double *b
 int main(int argc, char **argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 216;
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
-  const bool insitu = argc > 3 && atoi(argv[3]) != 0;
+  const int insitu_mode = argc > 3 ? atoi(argv[3]) : 0;  // 1: pollute, 2: pollute with nt stores
+  const bool insitu = insitu_mode != 0;
+  const char *only = argc > 4 ? argv[4] : nullptr;       // comma list of variant names
   const int reps = 20;
   const int nx = N, ny = N, nz = N, pl = nx * ny, n = nx * ny * nz;
   std::vector<int> rp(n + 1), col;
@@ -534,6 +663,31 @@ int main(int argc, char **argv) {
   Vi v{d_code, d_rlen, d_blkrk, d_dict, d_dval, d_x, d_y, d_part, nblk};
   Ell e{d_code8, d_dict, d_dval, d_x, d_y, d_part, n};
   Sten st{nx, ny, nz, 1.0 / nx, 1.0 / pl, d_x, d_y, d_part, n};
+  // DIA-VI: one value per offset (index 0), nibble 15 = absent
+  std::vector<unsigned> code4((size_t)n + 64, ~0u);
+  for (int r = 0; r < n; ++r) {
+    const int i = r % nx, j = (r / nx) % ny, l = r / pl;
+    const bool has[7] = {l > 0, j > 0, i > 0, true, i < nx - 1, j < ny - 1, l < nz - 1};
+    unsigned w = ~0u;
+    for (int q = 0; q < 7; ++q)
+      if (has[q]) w &= ~(15u << (4 * q));  // nibble 0 = value index 0
+    code4[(size_t)r] = w;
+  }
+  unsigned *d_code4;
+  double *d_vtab, *d_xg;
+  CK(hipMalloc(&d_code4, code4.size() * 4));
+  CK(hipMemcpy(d_code4, code4.data(), code4.size() * 4, hipMemcpyHostToDevice));
+  std::vector<double> vtab(8 * 16, 0.0);
+  for (int q = 0; q < 7; ++q) vtab[q * 16] = q == 3 ? 6.0 : -1.0;
+  CK(hipMalloc(&d_vtab, vtab.size() * 8));
+  CK(hipMemcpy(d_vtab, vtab.data(), vtab.size() * 8, hipMemcpyHostToDevice));
+  // x with one guard element on each side (a paired load may touch x[-1] / x[n])
+  CK(hipMalloc(&d_xg, ((size_t)n + 8) * 8));
+  CK(hipMemset(d_xg, 0, ((size_t)n + 8) * 8));
+  CK(hipMemcpy(d_xg + 2, x.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  Dia dia{d_code4, d_vtab, d_xg + 2, d_y, d_part, n, {-pl, -nx, -1, 0, 1, nx, pl, 0}};
+  Sten st2 = st;
+  st2.x = d_xg + 2;
   const int g4 = (nblk + 3) / 4, gr = (n + 255) / 256;
   const long long csr_bytes = (long long)nnz * 12 + 4LL * (n + 1) + 16LL * n;
   struct Var {
@@ -581,12 +735,36 @@ int main(int argc, char **argv) {
        16.0 * n, true},
       {"sten_nty", [&] { hipLaunchKernelGGL((k_sten<true>), dim3(gr), dim3(256), 0, 0, st); },
        16.0 * n, true},
+      {"sten2", [&] { hipLaunchKernelGGL((k_sten2<false>), dim3((n / 2 + 255) / 256), dim3(256), 0, 0, st2); },
+       16.0 * n, true},
+      {"sten2_nty", [&] { hipLaunchKernelGGL((k_sten2<true>), dim3((n / 2 + 255) / 256), dim3(256), 0, 0, st2); },
+       16.0 * n, true},
+      {"dia2", [&] { hipLaunchKernelGGL((k_dia2<7, false>), dim3((n / 2 + 255) / 256), dim3(256), 0, 0, dia); },
+       20.0 * n, true},
+      {"dia2_nty", [&] { hipLaunchKernelGGL((k_dia2<7, true>), dim3((n / 2 + 255) / 256), dim3(256), 0, 0, dia); },
+       20.0 * n, true},
+      {"csr_u7w456", [&] { hipLaunchKernelGGL((k_csr<456, 7, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u7sh", [&] { hipLaunchKernelGGL((k_csr<512, 7, true, 4, false, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u7w456sh", [&] { hipLaunchKernelGGL((k_csr<456, 7, true, 4, false, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u7", [&] { hipLaunchKernelGGL((k_csr<512, 7, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
       {"read843", [&] {
          hipLaunchKernelGGL(k_read, dim3(256 * 16), dim3(256), 0, 0, (const d2v *)d_val,
                             (long long)nnz / 2, (const int4 *)d_col, (long long)nnz / 4, d_sink);
        },
        (double)nnz * 12, false},
   };
+  if (only) {
+    std::vector<Var> keep;
+    const std::string sel = std::string(",") + only + ",";
+    for (auto &v : vars)
+      if (sel.find("," + v.name + ",") != std::string::npos) keep.push_back(v);
+    vars = keep;
+  }
+  double *pol_x = d_x;  // the pollution rewrites the gathered vector (same values)
   std::vector<double> y(n);
   for (auto &vr : vars) {
     if (!vr.check) continue;
@@ -609,7 +787,10 @@ int main(int argc, char **argv) {
       if (insitu) {  // pollute, then time the SpMV alone, reps times
         double sum = 0;
         for (int k = 0; k < reps; ++k) {
-          hipLaunchKernelGGL(k_pollute, dim3(4096), dim3(256), 0, 0, d_x, d_s1, d_s2, n);
+          if (insitu_mode == 2)
+            hipLaunchKernelGGL(k_pollute<true>, dim3(4096), dim3(256), 0, 0, pol_x, d_s1, d_s2, n);
+          else
+            hipLaunchKernelGGL(k_pollute<false>, dim3(4096), dim3(256), 0, 0, pol_x, d_s1, d_s2, n);
           CK(hipEventRecord(e0, 0));
           vars[i].run();
           CK(hipEventRecord(e1, 0));
