@@ -3,16 +3,26 @@
 CPU baseline beside it (BASELINE.json metric).
 
 A "step" is one CG iteration of the device-resident solver (SpMV + dot
-products + vector updates) on a synthetic SPD system already resident in
-HBM.  Default workload (N = 1): C3, the 7-point 3-D Laplacian 216^3
-(10,077,696 rows, 70,263,936 nnz, fp64, b = 1) -- BASELINE.json's HBM
-roofline configuration.
+products + vector updates) on a synthetic SPD system already resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c4|c2|c5]
 
-N > 1 is launched by torch.distributed.run (one process per GPU); each rank
-owns a 216^3-row slab of a 216 x 216 x (216 N) Laplacian (weak scaling), the
-solver exchanges halo planes and all-reduces its dot products over RCCL.
+N = 1 (default workload C3): the 7-point 3-D Laplacian 216^3 (10,077,696 rows,
+70,263,936 nnz, fp64, b = 1) -- BASELINE.json's HBM roofline configuration --
+in the layout libcgx picks for it, plus, in the same run, the same solve with
+the reference's plain CSR (SURVEY.md 8d's B_spmv: the north-star roofline
+figure), with dictionary-coded columns and matrix-free; C4 (64M rows) on this
+one GPU (the N = 1 point of the C4 strong-scaling curve); the end-to-end
+drop-in call solve(A, b, &x, 1e-8, maxit) through the C ABI; the CPU baseline.
+
+N > 1 (default workload C4): one process per GPU.  Without WORLD_SIZE in the
+environment this script starts itself under torch.distributed.run as a child
+process (before touching the GPU) and forwards rank 0's line.  Each rank owns
+a contiguous row block of the 400^3 Laplacian (64,000,000 rows; strong
+scaling); halo planes go point to point and the dot products are all-reduced
+over RCCL.  Before the timed run a small 3-D Laplacian is solved across the N
+ranks to tol 1e-10 and checked against a single-GPU solve of the same system
+(the `parity` gate: the timed run happens only if it passes).
 
 Output: ONE JSON line on rank 0.
 """
@@ -21,6 +31,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -40,78 +52,110 @@ WORKLOADS = {
                kind="lap2d", dims=(1000, 1000), dtype="f64"),
     "c4": dict(desc="C4: 7-point 3-D Laplacian 400^3 (64,000,000 rows), fp64, b = 1, "
                     "row-partitioned over the ranks (strong scaling)",
-               kind="lap3d", dims=(400, 400, 400), dtype="f64", strong=True),
+               kind="lap3d", dims=(400, 400, 400), dtype="f64"),
     "c5": dict(desc="C5: random SPD 5,000,000 rows, 32 partners/row symmetrised "
                     "(~64 nnz/row), splitmix64 seed 42, fp32",
                kind="rand", n=5_000_000, partners=32, seed=42, dtype="f32"),
 }
 
 
+# ----------------------------------------------------------------- launcher
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(argv, nproc, port):
+    """The child command for N > 1 without WORLD_SIZE: this script under
+    torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            str(REPO / "bench.py"), *argv]
+
+
+def launch_ranks(argv, nproc):
+    """Runs the ranks as a child process (never exec: this process has not
+    touched the GPU and must not be replaced); rank 0 prints the line."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(launch_cmd(argv, nproc, free_port()), env=env).returncode
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: c3 at N = 1, c4 at N > 1")
+    ap.add_argument("--alg", default=None, choices=["hs", "cg1"],
+                    help="N > 1: recurrence (default: a timed trial of both)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="N = 1: only the headline solve (no CSR/DC/stencil/C4/e2e legs)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ systems
+
 def make_system(wl, rank=0, world=1):
+    """Host CSR of this rank's rows (the C boundary takes host CSR)."""
     import numpy as np
     import cgx
     if wl["kind"] == "lap3d":
         nx, ny, nz = wl["dims"]
-        nz_g = nz if wl.get("strong") else nz * world
-        n_g = nx * ny * nz_g
-        rb, re_ = n_g * rank // world, n_g * (rank + 1) // world
-        rp, col, val = cgx.laplacian3d(nx, ny, nz_g, rb, re_)
-        return dict(rp=rp, col=col, val=val, b=np.ones(re_ - rb), n_global=n_g,
-                    row_begin=rb, row_end=re_)
-    if wl["kind"] == "lap2d":
+        n_g = nx * ny * nz
+        rb, re_ = cgx.partition_rows(n_g, world, rank)
+        rp, col, val = cgx.laplacian3d(nx, ny, nz, rb, re_)
+    elif wl["kind"] == "lap2d":
         nx, ny = wl["dims"]
-        ny_g = ny * world
-        n_g = nx * ny_g
-        rb, re_ = n_g * rank // world, n_g * (rank + 1) // world
-        rp, col, val = cgx.laplacian2d(nx, ny_g, rb, re_)
-        return dict(rp=rp, col=col, val=val, b=np.ones(re_ - rb), n_global=n_g,
-                    row_begin=rb, row_end=re_)
-    n = wl["n"]
-    rp, col, val = cgx.random_spd(n, wl["partners"], wl["seed"], f32=True)
-    b = np.random.default_rng(1).standard_normal(n).astype(np.float32)
-    return dict(rp=rp, col=col, val=val, b=b, n_global=n, row_begin=0, row_end=n)
+        n_g = nx * ny
+        rb, re_ = cgx.partition_rows(n_g, world, rank)
+        rp, col, val = cgx.laplacian2d(nx, ny, rb, re_)
+    else:
+        n_g = wl["n"]
+        rb, re_ = 0, n_g
+        rp, col, val = cgx.random_spd(n_g, wl["partners"], wl["seed"], f32=True)
+        b = np.random.default_rng(1).standard_normal(n_g).astype(np.float32)
+        return dict(rp=rp, col=col, val=val, b=b, n_global=n_g, row_begin=rb, row_end=re_)
+    return dict(rp=rp, col=col, val=val, b=np.ones(re_ - rb), n_global=n_g, row_begin=rb,
+                row_end=re_)
 
 
-def load_traffic(workload, alg):
-    """HBM bytes per SpMV launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_<workload>.json, written by profiles/collect_pmc.py), or None."""
-    p = REPO / "profiles" / f"pmc_{workload}.json"
+def load_traffic(tag):
+    """L2->fabric bytes per SpMV launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_<tag>.json, tools/pmc_summary.py), or None."""
+    p = REPO / "profiles" / f"pmc_{tag}.json"
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text())
-        return d.get("spmv_hbm_bytes_per_launch")
+        return json.loads(p.read_text()).get("spmv_hbm_bytes_per_launch")
     except Exception:
         return None
 
 
-def spmv_layout_label(info, stream_bytes):
-    """Kernel label for the layout a solver picked (coded columns, pairs)."""
-    nd = info.get("n_dict", 0)
-    label = spmv_kernel_label(stream_bytes)
-    if nd and info.get("dict_vals", 0):
-        return (f"k_spmv_vi (LDS-DMA code stream, value-indexed (offset, value) pairs: "
-                f"{nd} pairs, 1 B/nnz, no value stream; one 64-row block per wave)")
-    if nd:
-        return label.replace("k_spmv_dma (LDS-DMA CSR-stream",
-                             f"k_spmv_dc (LDS-DMA CSR-stream, dictionary-coded columns: "
-                             f"{nd} offsets, 1 B/nnz")
-    return label
+KERNELS = {
+    "dia": "k_spmv_dia (DIA-VI: value-indexed diagonal codes, two rows per thread, pair loads of x)",
+    "dc": "k_spmv_dc (LDS-DMA code window + value window per 64-row block, dictionary-coded columns)",
+    "csr": "k_spmv_csr (LDS-DMA val/col window per 64-row block, lane-per-row sums from LDS)",
+    "panel": "k_spmv_csr over column panels",
+    "stencil": "k_stencil (matrix-free, two rows per thread)",
+}
 
 
-def spmv_kernel_label(stream_bytes):
-    """The SpMV kernel the solver selects (cgx_solver.cpp defaults, CGX_* knobs;
-    nt by default only above kNtStreamBytes = 160 MiB of val+col)."""
-    if os.environ.get("CGX_LAYOUT") == "sell":
-        return "k_spmv_sell (SELL-64)"
-    dma = os.environ.get("CGX_SPMV_DMA", "1")
-    nt_env = os.environ.get("CGX_SPMV_NT")
-    nt = (nt_env == "1") if nt_env is not None else (dma in ("1", "3") and stream_bytes > 160 * 2**20)
-    name = {"0": "k_spmv_wave (register-staged CSR-stream, LDS row sums)",
-            "1": "k_spmv_dma (LDS-DMA CSR-stream, LDS row sums)",
-            "2": "k_spmv_pipe (persistent waves, LDS-DMA prefetch)",
-            "8": "k_spmv_dma (LDS-DMA CSR-stream, 8 gathers per chunk)"}.get(dma, f"dma={dma}")
-    return name + (", nt stream" if nt else "")
+def layout_desc(info):
+    name = info["layout_name"]
+    if name == "dia":
+        return (f"DIA-VI: {info['n_dict']} diagonals, {info['n_values']} values, "
+                f"{info['code_bytes_per_row']} code bytes per row, no column or value stream")
+    if name == "dc":
+        return f"CSR-DC: {info['n_dict']} column offsets, 1 code byte per nonzero + values"
+    if name == "panel":
+        return f"CSR in {info['n_panels']} column panels"
+    return "CSR (int32 columns, fp64 values): the reference's struct"
 
 
 def cpu_model():
@@ -124,9 +168,34 @@ def cpu_model():
     return "unknown"
 
 
+# -------------------------------------------------------------- CPU legs
+
+def cpu_baseline(sysm, budget_s):
+    """The oracle's CSR-sequential HS-CG (bit-exact to the reference on chained
+    matrices) on ONE host core, on the same matrix, for as many iterations as
+    fit in ~budget_s seconds."""
+    import numpy as np
+    import helpers as H
+    rp, col, val, b = sysm["rp"], sysm["col"], sysm["val"], sysm["b"]
+    if val.dtype != np.float64:
+        val = val.astype(np.float64)
+        b = b.astype(np.float64)
+    t0 = time.perf_counter()
+    H.o_solve(0, 0.0, rp, col, val, b)          # 1 iteration (probe)
+    t1 = time.perf_counter() - t0
+    its = max(1, min(1000, int(budget_s / max(t1, 1e-6))))
+    t0 = time.perf_counter()
+    _, done, _ = H.o_solve(its - 1, 0.0, rp, col, val, b)
+    dt = time.perf_counter() - t0
+    return dict(value=done / dt, unit="it/s", cores=1, kind="port",
+                sample=f"{done} HS-CG iterations of the same system (oracle/cg_oracle.c "
+                       f"CSR-sequential restatement, bit-exact to the reference's "
+                       f"mv_mult on chained matrices), 1 host core, {dt:.1f} s")
+
+
 def cpu_baseline_mt(sysm, budget_s):
     """SURVEY.md 8d leg (c): the same CSR-sequential HS-CG with its row loops
-    split over all host cores this job may use (oracle_solve_mt, pthreads;
+    split over the host cores this job may use (oracle_solve_mt, pthreads;
     OMP_NUM_THREADS on the GPU box = the box's CPU share)."""
     import numpy as np
     import helpers as H
@@ -152,8 +221,7 @@ def reference_c1(budget_s=2.0):
     the reference's cg.c + mv_ops.c at its Makefile flags, built by
     `make -C oracle ref`) timing conj_grad on C1, the dense 128 SPD system --
     the one configuration where its O(n^2) dense-row SpMV is feasible.
-    Returns None when the binary was not built (no /root/reference)."""
-    import subprocess
+    None when the binary was not built (no /root/reference)."""
     import tempfile
     import helpers as H
     exe = REPO / "oracle" / "_ref" / "ref_harness"
@@ -175,255 +243,403 @@ def reference_c1(budget_s=2.0):
                        f"(oracle/_ref/ref_harness, the reference's own sources and flags)")
 
 
-def cpu_baseline(sysm, budget_s):
-    """The oracle's CSR-sequential HS-CG (bit-exact to the reference on chained
-    matrices) on ONE host core, on the same matrix, for as many iterations as
-    fit in ~budget_s seconds."""
-    import numpy as np
-    import helpers as H
-    rp, col, val, b = sysm["rp"], sysm["col"], sysm["val"], sysm["b"]
-    if val.dtype != np.float64:
-        val = val.astype(np.float64)
-        b = b.astype(np.float64)
-    t0 = time.perf_counter()
-    H.o_solve(0, 0.0, rp, col, val, b)          # 1 iteration (probe)
-    t1 = time.perf_counter() - t0
-    its = max(1, min(1000, int(budget_s / max(t1, 1e-6))))
-    t0 = time.perf_counter()
-    _, done, _ = H.o_solve(its - 1, 0.0, rp, col, val, b)
-    dt = time.perf_counter() - t0
-    return dict(value=done / dt, unit="it/s", cores=1, kind="port",
-                sample=f"{done} HS-CG iterations of the same system (oracle/cg_oracle.c "
-                       f"CSR-sequential restatement, bit-exact to the reference's "
-                       f"mv_mult on chained matrices), 1 host core, {dt:.1f} s")
+# ----------------------------------------------------------- single GPU
+
+def spmv_roofline(bytes_, ms, peak=HBM_PEAK_GBS):
+    gbs = bytes_ / (ms * 1e-3) / 1e9
+    return round(gbs, 1), round(gbs / peak, 4)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--alg", default=None, choices=["hs", "cg1", "cg1-dist", "hs-dist", "auto-dist"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-
-    import torch  # loads the HIP runtime libcgx then shares (same SONAME)
-    import torch.distributed as dist
-    import numpy as np
+def solver_leg(sysm, steps, warmup, layout, device=0, b2b=False):
+    """One solver on the system in `layout`: CG it/s (graph replay), the
+    average in-iteration SpMV time (HIP events around every SpMV launch on
+    the solver's stream) and, with b2b, back-to-back SpMVs y = A p (the
+    standard SpMV benchmark, the kernel without the p.s epilogue)."""
     import cgx
-
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    wl = WORKLOADS[args.workload]
-    if world > 1 and wl["kind"] == "rand":
-        raise SystemExit("bench: C5 (random SPD) is a single-GPU configuration (BASELINE.json)")
-    # N > 1: the partitioned solver; its recurrence is chosen by a short
-    # timed trial of both (below) unless --alg names one
-    alg = args.alg or ("auto-dist" if world > 1 else "hs")
-    sysm = make_system(wl, rank, world)
-
-    use_dist = world > 1 or alg.endswith("-dist")
-    torch.cuda.synchronize()
-    t_up = time.perf_counter()  # host -> HBM upload + row-block plan (outside `value`)
-    trial = None
-    if use_dist:
-        # one rank per GPU; RCCL communicator from an id rank 0 broadcasts
-        uid = [cgx.dist_unique_id() if (rank == 0 and world > 1) else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        s = cgx.DistSolver(local_rank, world, rank, uid[0])
-        s.set_matrix(sysm["n_global"], sysm["rp"], sysm["col"], sysm["val"])
-        s.set_rhs(sysm["b"])
-        dinfo = s.info()
-        if alg == "auto-dist":
-            # HS needs two all-reduces per iteration, CG1 one but 8 B/row more
-            # vector traffic: which wins depends on the node's all-reduce
-            # latency, so time both (max over ranks, same choice everywhere)
-            trial = {}
-            for name, a in (("hs-dist", cgx.CGX_ALG_HS), ("cg1-dist", cgx.CGX_ALG_CG1)):
-                s.set_alg(a)
-                s.bench_prepare(3)
-                barrier()
-                tms = s.bench_run(20)[0] / 20
-                if world > 1:
-                    t = torch.tensor([tms], device="cuda", dtype=torch.float64)
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                    tms = float(t.item())
-                trial[name] = round(tms, 4)
-            alg = min(trial, key=trial.get)
-        s.set_alg(cgx.CGX_ALG_HS if alg == "hs-dist" else cgx.CGX_ALG_CG1)
-        info = dict(spmv_bytes=dinfo["spmv_bytes"], iter_bytes=dinfo["iter_bytes"],
-                    spmv_iter_bytes=dinfo["spmv_iter_bytes"], n_dict=dinfo["n_dict"],
-                    dict_vals=dinfo["dict_vals"])
-    else:
-        s = cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS)
+    with cgx.Solver(device, layout=layout) as s:
+        t0 = time.perf_counter()
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
         s.set_rhs(sysm["b"])
-        info = s.info()
-        dinfo = None
+        setup_ms = 1e3 * (time.perf_counter() - t0)
+        s.bench_prepare(warmup)
+        dev_ms = s.bench_run(steps, graph=True)[0]
+        _, spmv_ms = s.bench_run(steps, graph=False, spmv_events=True)
+        out = dict(value=round(steps / (dev_ms * 1e-3), 2), unit="it/s",
+                   device_ms_per_step=round(dev_ms / steps, 4),
+                   spmv_us=round(spmv_ms * 1e3, 2), info=s.info(), setup_ms=round(setup_ms, 1))
+        if b2b:
+            _, b2b_ms = s.bench_run(steps, graph=False, spmv_events=True, spmv_only=True)
+            out["b2b_spmv_us"] = round(b2b_ms * 1e3, 2)
+    return out
 
+
+def solve_e2e(sysm, tol=1e-8, maxit=20000):
+    """What cg.c:71-75 times: the drop-in call solve(A, b, &x, tol, maxit)
+    through the C ABI on host structs -- content hash of A, upload + layout
+    encoding (first call), the device iterations, x back to the host -- cold
+    (A not yet resident) and warm (A resident, the second call on the same
+    struct).  The true residual is computed here on the host (scipy)."""
+    import numpy as np
+    import scipy.sparse as sp
+    import cgx
+    A = cgx.Mv(sysm["val"], sysm["col"], sysm["rp"])
+    b = cgx.Mv(sysm["b"])
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
+    out = {}
+    for leg in ("cold", "warm"):
+        t0 = time.perf_counter()
+        x, its = cgx.solve(A, b, tol, maxit)
+        wall = 1e3 * (time.perf_counter() - t0)
+        t = cgx.ops_last_timing()
+        n = len(sysm["b"])
+        Am = sp.csr_matrix((sysm["val"], sysm["col"], sysm["rp"]), shape=(n, n))
+        res = float(np.linalg.norm(sysm["b"] - Am @ x) / np.linalg.norm(sysm["b"]))
+        out[leg] = dict(wall_ms=round(wall, 1), iters=its, true_rel_residual=res,
+                        setup_ms=round(t["setup_ms"], 1), hash_ms=round(t["hash_ms"], 1),
+                        solve_ms=round(t["solve_ms"], 1), download_ms=round(t["download_ms"], 1),
+                        uploaded=bool(t["uploaded"]),
+                        setup_frac=round(t["setup_ms"] / max(wall, 1e-9), 3))
+    out["note"] = (f"solve(A,b,&x,{tol:g},{maxit}) through the C ABI on host structs "
+                   "(include/cgx.h), wall time incl. ctypes; cold = A uploaded and encoded, "
+                   "warm = A resident (op-level residency)")
+    return out
+
+
+def c4_one_gpu(steps, warmup, device=0):
+    """The N = 1 point of the C4 strong-scaling curve: 400^3 generated in
+    device memory (cgx_solver_gen_laplacian), the layout libcgx picks."""
+    import numpy as np
+    import cgx
+    nx = 400
+    with cgx.Solver(device) as s:
+        t0 = time.perf_counter()
+        s.gen_laplacian(3, nx, nx, nx)
+        s.set_rhs(np.ones(nx ** 3))
+        setup = 1e3 * (time.perf_counter() - t0)
+        s.bench_prepare(warmup)
+        ms = s.bench_run(steps, graph=True)[0]
+        _, spmv_ms = s.bench_run(min(steps, 30), graph=False, spmv_events=True)
+        i = s.info()
+    gbs, frac = spmv_roofline(i["spmv_iter_bytes"], spmv_ms)
+    return dict(value=round(steps / (ms * 1e-3), 2), unit="it/s", n=nx ** 3,
+                layout=i["layout_name"], spmv_us=round(spmv_ms * 1e3, 2), spmv_gbs=gbs,
+                spmv_frac=frac, setup_ms=round(setup, 1),
+                note="C4 (400^3) on ONE GPU, same code path as the N = 1 headline: the "
+                     "base of the C4 strong-scaling curve (N > 1 lines run C4 across N ranks)")
+
+
+def run_single(args, wl_name):
+    import numpy as np
+    import torch
+    import cgx
+
+    wl = WORKLOADS[wl_name]
+    torch.cuda.set_device(0)
+    sysm = make_system(wl)
     torch.cuda.synchronize()
+
+    # ---- headline: the layout libcgx picks (default path of the drop-in)
+    t_up = time.perf_counter()
+    s = cgx.Solver(0)
+    s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+    s.set_rhs(sysm["b"])
+    info = s.info()
     upload_ms = 1e3 * (time.perf_counter() - t_up)
 
-    # ---- timed region: exactly K steps, barrier + sync on both sides
+    # timed region: exactly K steps, sync on both sides
     s.bench_prepare(args.warmup)
-    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dev_ms = s.bench_run(args.steps)[0] if use_dist else s.bench_run(args.steps, graph=True)[0]
+    dev_ms = s.bench_run(args.steps, graph=True)[0]
     torch.cuda.synchronize()
-    barrier()
     wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
     ms_per_step = 1e3 * wall / args.steps
+    # the SpMV's average launch time inside the iteration (HIP events on the
+    # solver's stream), K more iterations
+    _, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
+    s.close()
+    head_gbs, head_frac = spmv_roofline(info["spmv_iter_bytes"], spmv_ms)
 
-    # ---- roofline of the dominant kernel (SpMV): HIP events around every
-    # SpMV launch on the solver's stream over K more iterations.
-    if use_dist:
-        _, spmv_ms = s.bench_run(args.steps, spmv_events=True)
+    legs = {}
+    if not args.no_legs:
+        if info["layout_name"] != "csr":
+            legs["csr"] = solver_leg(sysm, args.steps, args.warmup, "csr", b2b=True)
+        if wl["kind"] in ("lap3d", "lap2d") and info["layout_name"] != "dc":
+            legs["dc"] = solver_leg(sysm, args.steps, args.warmup, "dc")
+    csr = legs.get("csr")
+
+    # ---- roofline: SURVEY.md 8d's north-star figure, the plain-CSR SpMV on
+    # B_spmv = 12 nnz + 4 (n+1) + 16 n, in the CG iteration; the default
+    # layout's SpMV (its own bytes) beside it
+    if csr is not None:
+        ci = csr["info"]
+        c_gbs, c_frac = spmv_roofline(ci["spmv_bytes"], csr["spmv_us"] * 1e-3)
+        b_gbs, b_frac = spmv_roofline(ci["spmv_bytes"], csr["b2b_spmv_us"] * 1e-3)
+        roofline = dict(
+            bound="hbm", achieved=c_gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=c_frac,
+            traffic=load_traffic(f"{wl_name}_csr"), kernel=KERNELS["csr"] + ", in the CG iteration",
+            basis="SURVEY.md 8d B_spmv = 12 nnz + 4 (n+1) + 16 n (CSR int32 col + fp64 val, "
+                  "row_ptr, x read once, y written once)",
+            algorithmic_bytes_per_launch=int(ci["spmv_bytes"]), spmv_us=csr["spmv_us"],
+            csr=dict(frac=c_frac, achieved=c_gbs, spmv_us=csr["spmv_us"],
+                     b2b_spmv_us=csr["b2b_spmv_us"], b2b_achieved=b_gbs, b2b_frac=b_frac,
+                     cg_its=csr["value"], gathers_per_chunk=ci["gathers_per_chunk"],
+                     note="in_cg: average launch inside the CG iteration (HIP events); b2b: "
+                          "back-to-back y = A p launches (the standard SpMV benchmark, "
+                          "k_spmv_csr without the p.s epilogue)"))
+        roofline["default_layout"] = dict(
+            kernel=KERNELS.get(info["layout_name"], info["layout_name"]),
+            layout=layout_desc(info), spmv_us=round(spmv_ms * 1e3, 2), achieved=head_gbs,
+            frac=head_frac, algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
+            traffic=load_traffic(wl_name),
+            csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
+            note="the SpMV of the headline solve, priced on the bytes its layout moves")
     else:
-        _, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
-    # achieved: the bytes the SpMV must move in the layout it runs on (coded
-    # columns: 1 byte per nonzero instead of 4) over its measured time; the
-    # CSR-equivalent rate (SURVEY.md 8d's B_spmv over the same time) beside it
-    achieved = info["spmv_iter_bytes"] / (spmv_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.workload, alg)
-    label = spmv_layout_label(info, len(sysm["col"]) * (4 + sysm["val"].itemsize))
-    roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
-                    unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                    traffic=traffic, kernel=label,
-                    spmv_us=round(spmv_ms * 1e3, 2),
-                    algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
-                    csr_bytes_per_launch=int(info["spmv_bytes"]),
-                    csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1))
-
-    # on-box HBM ceilings (SURVEY.md 8d): STREAM triad (1/3 writes) and a
-    # read-only stream, 512 MiB arrays.  The SpMV is 92% reads (its only
-    # write is y), so the read ceiling is the one it is compared with.
-    triad = cgx.stream_bench(local_rank, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)
-    rd = cgx.stream_bench(local_rank, 64 * 2**20, 10, cgx.CGX_STREAM_READ)
+        roofline = dict(bound="hbm", achieved=head_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=head_frac, traffic=load_traffic(wl_name),
+                        kernel=KERNELS.get(info["layout_name"], info["layout_name"]),
+                        algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
+                        spmv_us=round(spmv_ms * 1e3, 2))
+    triad = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)
+    rd = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_READ)
     roofline["stream_triad_gbs"] = round(triad, 1)
     roofline["stream_read_gbs"] = round(rd, 1)
-    roofline["frac_of_stream_read"] = round(achieved / rd, 4)
 
-    # SURVEY.md 8f: matrix-free upper bound for the Laplacian runs -- the same
-    # operator as a stencil (bit-identical SpMV), only x and y move
-    # the same solve with plain 4-byte CSR columns (CGX_LAYOUT=csr): the
-    # layout SURVEY.md 8d's B_spmv prices, measured beside the coded one
-    def alt_layout(env, note):
-        """The same solve with other layout knobs (env), measured like the main line."""
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
-        try:
-            with cgx.Solver(local_rank, alg=cgx.CGX_ALG_CG1 if alg == "cg1" else cgx.CGX_ALG_HS) as cs:
-                cs.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
-                cs.set_rhs(sysm["b"])
-                cs.bench_prepare(args.warmup)
-                c_ms = cs.bench_run(args.steps, graph=True)[0]
-                _, c_spmv = cs.bench_run(args.steps, graph=False, spmv_events=True)
-                cinfo = cs.info()
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-        c_gbs = cinfo["spmv_iter_bytes"] / (c_spmv * 1e-3) / 1e9
-        return dict(value=round(args.steps / (c_ms * 1e-3), 2), unit="it/s",
-                    spmv_us=round(c_spmv * 1e3, 2), spmv_gbs=round(c_gbs, 1),
-                    frac=round(c_gbs / HBM_PEAK_GBS, 4),
-                    algorithmic_bytes_per_launch=int(cinfo["spmv_iter_bytes"]),
-                    kernel=spmv_layout_label(cinfo, len(sysm["col"]) * (4 + sysm["val"].itemsize)),
-                    note=note)
-
-    # the same solve with plain 4-byte CSR columns (CGX_LAYOUT=csr): the
-    # layout SURVEY.md 8d's B_spmv prices, measured beside the coded one; and
-    # with offset codes but the value stream kept (CGX_DC_VALS=0)
-    csr_plain = coded_offsets = None
-    if world == 1 and not use_dist and info.get("n_dict", 0) > 0:
-        csr_plain = alt_layout({"CGX_LAYOUT": "csr"},
-                               "same system, plain int32 CSR columns (CGX_LAYOUT=csr): "
-                               "B_spmv of SURVEY.md 8d")
-        if info.get("dict_vals", 0):
-            coded_offsets = alt_layout({"CGX_DC_VALS": "0"},
-                                       "same system, offset codes + the fp64 value stream "
-                                       "(CGX_DC_VALS=0)")
-
-    mf = None
-    if world == 1 and wl["kind"] in ("lap3d", "lap2d"):
-        with cgx.Solver(local_rank) as ms:
+    extra = {}
+    if not args.no_legs:
+        if "dc" in legs:
+            d = legs["dc"]
+            g, f = spmv_roofline(d["info"]["spmv_iter_bytes"], d["spmv_us"] * 1e-3)
+            extra["coded_offsets"] = dict(value=d["value"], unit="it/s", spmv_us=d["spmv_us"],
+                                          spmv_gbs=g, frac=f, kernel=KERNELS["dc"],
+                                          layout=layout_desc(d["info"]))
+        if csr is not None:
+            extra["csr_plain"] = dict(value=csr["value"], unit="it/s", spmv_us=csr["spmv_us"],
+                                      b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"],
+                                      note="the same solve on the reference's CSR (layout csr)")
+        if wl["kind"] in ("lap3d", "lap2d"):
             dims = wl["dims"]
-            ms.set_stencil(3 if wl["kind"] == "lap3d" else 2, dims[0], dims[1],
-                           dims[2] if len(dims) > 2 else 1)
-            ms.set_rhs(sysm["b"])
-            ms.bench_prepare(args.warmup)
-            mf_ms = ms.bench_run(args.steps, graph=True)[0]
-            _, mf_spmv = ms.bench_run(min(args.steps, 50), graph=False, spmv_events=True)
-        mf = dict(value=round(args.steps / (mf_ms * 1e-3), 2), unit="it/s",
-                  spmv_us=round(mf_spmv * 1e3, 2),
-                  note="matrix-free 7/5-point stencil SpMV (cgx_solver_set_stencil): "
-                       "not the CSR path, an upper bound for it")
+            with cgx.Solver(0) as ms:
+                ms.set_stencil(3 if wl["kind"] == "lap3d" else 2, dims[0], dims[1],
+                               dims[2] if len(dims) > 2 else 1)
+                ms.set_rhs(sysm["b"])
+                ms.bench_prepare(args.warmup)
+                mf_ms = ms.bench_run(args.steps, graph=True)[0]
+                _, mf_spmv = ms.bench_run(min(args.steps, 50), graph=False, spmv_events=True)
+            extra["matrix_free_upper_bound"] = dict(
+                value=round(args.steps / (mf_ms * 1e-3), 2), unit="it/s",
+                spmv_us=round(mf_spmv * 1e3, 2), kernel=KERNELS["stencil"],
+                note="the same operator without a stored matrix: an upper bound, not the CSR path")
+        if wl_name == "c3":
+            extra["c4_1gpu"] = c4_one_gpu(min(args.steps, 50), args.warmup)
+            extra["solve_e2e"] = solve_e2e(sysm)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if not args.no_cpu:
         cpu = cpu_baseline(sysm, args.cpu_seconds)
         cpu["cpu_model"] = cpu_model()
         cpu["nproc"] = os.cpu_count()
         cpu["all_cores"] = cpu_baseline_mt(sysm, args.cpu_seconds / 2)
         cpu["reference_c1"] = reference_c1()
 
-    # weak scaling (default): every rank owns one slab, value = slab-iterations/s
-    # summed over ranks; strong (c4): one system over all ranks, value = its it/s
-    strong = bool(wl.get("strong"))
-    value = (args.steps / wall) * (1 if strong else world)
     out = dict(
-        metric=METRIC, value=round(value, 2), unit="it/s", n_gpus=world,
+        metric=METRIC, value=round(args.steps / wall, 2), unit="it/s", n_gpus=1,
         steps=args.steps, warmup=args.warmup, ms_per_step=round(ms_per_step, 4),
-        higher_is_better=True, scaling="strong" if strong else "weak", vs_baseline=None,
-        dtype=wl["dtype"], data="synthetic",
-        config=dict(workload=wl["desc"], n=sysm["n_global"], nnz_local=int(len(sysm["col"])),
-                    alg=alg, alg_trial_ms_per_iter=trial if use_dist else None,
-                    graph=not use_dist or world == 1,
-                    parallelism=f"row-partition x{world}",
-                    layout=(f"CSR-VI: value-indexed coded columns ({info['n_dict']} "
-                            f"(col-row, value) pairs, 1 B/nnz, no value stream) + byte row lengths"
-                            if info.get("dict_vals", 0) else
-                            f"CSR with dictionary-coded columns ({info['n_dict']} col-row "
-                            f"offsets, 1 B/nnz) + byte row lengths"
-                            if info.get("n_dict", 0) else "CSR (int32 columns)"),
-                    halo_bytes_per_iter=(dinfo or {}).get("halo_bytes")),
+        higher_is_better=True, scaling="strong", vs_baseline=None, dtype=wl["dtype"],
+        data="synthetic",
+        config=dict(workload=wl["desc"], n=sysm["n_global"], nnz=int(len(sysm["col"])),
+                    alg="hs (the reference recurrence, cg.c:88-141)", graph=True,
+                    parallelism="single GPU", layout=layout_desc(info),
+                    layout_name=info["layout_name"]),
         device_ms_per_step=round(dev_ms / args.steps, 4),
-        # the C boundary takes host CSR buffers: one-time upload + plan, not in `value`
-        upload_ms=round(upload_ms, 1),
+        upload_ms=round(upload_ms, 1),  # host CSR -> HBM + layout encoding, not in `value`
         iter_bytes=int(info["iter_bytes"]),
-        iter_gbs=round(info["iter_bytes"] / (ms_per_step * 1e-3) / 1e9, 1),
-        # the iteration's bytes in the layout it runs on (SpMV as above + the
-        # vector kernels' 8d bytes) over the measured step
-        iter_layout_gbs=round((info["iter_bytes"] - info["spmv_bytes"] + info["spmv_iter_bytes"])
-                              / (ms_per_step * 1e-3) / 1e9, 1),
-        roofline=roofline, cpu_baseline=cpu, csr_plain=csr_plain, coded_offsets=coded_offsets,
-        matrix_free_upper_bound=mf,
-    )
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+        roofline=roofline, cpu_baseline=cpu, **extra)
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------ multi GPU
+
+def gather_x(x_local, n_global, world, rank):
+    """x of all ranks on every rank (all_gather over the default group)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import cgx
+    sizes = [cgx.partition_rows(n_global, world, q) for q in range(world)]
+    m = max(e - b for b, e in sizes)
+    t = torch.zeros(m, dtype=torch.float64, device="cuda")
+    t[:len(x_local)] = torch.from_numpy(x_local).cuda()
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return np.concatenate([parts[q][:e - b].cpu().numpy() for q, (b, e) in enumerate(sizes)])
+
+
+def parity_gate(world, rank, local_rank, uid, tol=1e-10):
+    """A small 3-D Laplacian (48 x 48 x 16 N rows) solved across the N ranks
+    to tol with both recurrences over RCCL; rank 0 checks the gathered x
+    against a single-GPU solve of the same system (cgx.Solver, HS), the
+    iteration count (within 1) and the true residual (scipy, on the host)."""
+    import numpy as np
+    import scipy.sparse as sp
+    import cgx
+    nx, ny, nz = 48, 48, 16 * world
+    n = nx * ny * nz
+    rb, re_ = cgx.partition_rows(n, world, rank)
+    rp, col, val = cgx.laplacian3d(nx, ny, nz, rb, re_)
+    b_full = np.random.default_rng(11).standard_normal(n)
+    res = {}
+    d = cgx.DistSolver(local_rank, world, rank, uid)
+    try:
+        d.set_matrix(n, rp, col, val)
+        d.set_rhs(b_full[rb:re_])
+        for name, alg in (("hs", cgx.CGX_ALG_HS), ("cg1", cgx.CGX_ALG_CG1)):
+            d.set_alg(alg)
+            its = d.run(5000, tol)
+            res[name] = (its, gather_x(d.x(), n, world, rank), d.info()["graph"])
+    finally:
+        d.close()
+    if rank != 0:
+        return None
+    grp, gcol, gval = cgx.laplacian3d(nx, ny, nz)
+    with cgx.Solver(local_rank) as s:
+        s.set_matrix(grp, gcol, gval)
+        s.set_rhs(b_full)
+        its1 = s.run(5000, tol)
+        x1 = s.x()
+    A = sp.csr_matrix((gval, gcol, grp), shape=(n, n))
+    out = dict(system=f"3-D Laplacian {nx}x{ny}x{nz} ({n} rows), b ~ N(0,1), tol {tol:g}",
+               reference="single-GPU cgx.Solver (HS) on rank 0 + true residual (scipy)",
+               single_gpu_iters=its1)
+    ok = True
+    for name, (its, x, graph) in res.items():
+        rel = float(np.linalg.norm(x - x1) / np.linalg.norm(x1))
+        tr = float(np.linalg.norm(b_full - A @ x) / np.linalg.norm(b_full))
+        good = rel <= 1e-9 and abs(its - its1) <= 1 and tr <= 10 * tol
+        ok = ok and good
+        out[name] = dict(iters=its, rel_diff=rel, true_rel_residual=tr, graph=graph, ok=good)
+    out["ok"] = ok
+    return out
+
+
+def run_dist(args, wl_name, world, rank, local_rank):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import cgx
+
+    wl = WORKLOADS[wl_name]
+    if wl["kind"] == "rand":
+        raise SystemExit("bench: C5 (random SPD) is a single-GPU configuration (BASELINE.json)")
+    torch.cuda.set_device(local_rank)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def allmax(v):
+        t = torch.tensor([float(v)], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allmin(v):
+        return -allmax(-v)
+
+    # one RCCL unique id per communicator (the parity system's, the bench's)
+    uids = [[cgx.dist_unique_id(), cgx.dist_unique_id()] if rank == 0 else None]
+    dist.broadcast_object_list(uids, src=0)
+    uid_parity, uid = uids[0]
+
+    # ---- parity gate (RCCL path, both recurrences) before anything is timed
+    parity = parity_gate(world, rank, local_rank, uid_parity)
+    ok = [parity["ok"] if rank == 0 else None]
+    dist.broadcast_object_list(ok, src=0)
+
+    sysm = make_system(wl, rank, world)
+    t_up = time.perf_counter()
+    s = cgx.DistSolver(local_rank, world, rank, uid)
+    s.set_matrix(sysm["n_global"], sysm["rp"], sysm["col"], sysm["val"])
+    s.set_rhs(sysm["b"])
+    dist.barrier()
+    upload_ms = 1e3 * (time.perf_counter() - t_up)
+
+    # ---- recurrence: HS pays two all-reduce latencies per iteration, CG1 one
+    # (and 8 B/row more traffic); a timed trial (max over ranks) picks
+    trial = {}
+    algs = {"hs": cgx.CGX_ALG_HS, "cg1": cgx.CGX_ALG_CG1}
+    for name in ([args.alg] if args.alg else ["hs", "cg1"]):
+        s.set_alg(algs[name])
+        s.bench_prepare(3)
+        dist.barrier()
+        trial[name] = round(allmax(s.bench_run(20)[0] / 20), 4)
+    alg = min(trial, key=trial.get)
+    s.set_alg(algs[alg])
+    info = s.info()
+
+    value = None
+    ms_per_step = dev_ms = spmv_ms = None
+    if ok[0]:
+        # ---- timed region: exactly K steps, barrier + sync on both sides
+        s.bench_prepare(args.warmup)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dev_ms = s.bench_run(args.steps)[0]
+        torch.cuda.synchronize()
+        dist.barrier()
+        wall = allmax(time.perf_counter() - t0)
+        ms_per_step = 1e3 * wall / args.steps
+        value = args.steps / wall  # CG iterations of the one 64M-row system per second
+        _, spmv_ms = s.bench_run(min(args.steps, 30), spmv_events=True)
+    info = s.info()
     s.close()
-    if world > 1:
-        dist.destroy_process_group()
+
+    roofline = None
+    if spmv_ms is not None:
+        # per-rank SpMV (interior + boundary launches) on its own layout bytes
+        gbs, frac = spmv_roofline(info["spmv_iter_bytes"], spmv_ms)
+        roofline = dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=frac,
+                        traffic=None, kernel=KERNELS.get(info["layout_name"], "?") + " (per rank)",
+                        algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
+                        spmv_us=round(spmv_ms * 1e3, 2),
+                        spmv_us_max_over_ranks=round(allmax(spmv_ms) * 1e3, 2),
+                        frac_min_over_ranks=round(allmin(frac), 4),
+                        csr_basis_bytes_per_rank=int(info["spmv_bytes"]))
+    halo = allmax(info["halo_bytes"])
+    dev = allmax(dev_ms / args.steps) if dev_ms is not None else None
+    if rank == 0:
+        out = dict(
+            metric=METRIC, value=None if value is None else round(value, 2), unit="it/s",
+            n_gpus=world, steps=args.steps, warmup=args.warmup,
+            ms_per_step=None if ms_per_step is None else round(ms_per_step, 4),
+            higher_is_better=True, scaling="strong", vs_baseline=None, dtype=wl["dtype"],
+            data="synthetic",
+            config=dict(workload=wl["desc"], n=sysm["n_global"], rows_per_rank=info["n_loc"],
+                        nnz_rank0=info["nnz"], alg=alg, alg_trial_ms_per_iter=trial,
+                        graph=info["graph"], parallelism=f"row-partition x{world} (RCCL)",
+                        layout=info["layout_name"], halo_bytes_per_iter_max_rank=halo),
+            device_ms_per_step=None if dev is None else round(dev, 4),
+            upload_ms=round(upload_ms, 1), iter_bytes_rank0=int(info["iter_bytes"]),
+            roofline=roofline, cpu_baseline=None, parity=parity)
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    if not ok[0]:
+        raise SystemExit(1)
+
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        # no GPU has been touched in this process: start the ranks as a child
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    wl_name = args.workload or ("c3" if world == 1 else "c4")
+    if world == 1:
+        run_single(args, wl_name)
+    else:
+        run_dist(args, wl_name, world, rank, local_rank)
 
 
 if __name__ == "__main__":

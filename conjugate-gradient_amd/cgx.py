@@ -90,6 +90,9 @@ _SIGS = {
     "solve": (ctypes.c_int, [_MVP, _MVP, _MVPP, ctypes.c_double, ctypes.c_int]),
     "cgx_free_mv_deep": (None, [_MVP]),
     "cgx_ops_counters": (ctypes.c_int, [ctypes.POINTER(ctypes.c_longlong)] * 2),
+    "cgx_ops_set_mode": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "cgx_ops_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "cgx_ops_last_timing": (ctypes.c_int, [_vp]),
     "cgx_last_error": (ctypes.c_char_p, []),
     "cgx_device_count": (ctypes.c_int, []),
     "cgx_stream_bench": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
@@ -479,6 +482,25 @@ def mv_mult(A: Mv, b: Mv):
     y = mv_values(out)
     lib().cgx_free_mv_deep(out)
     return y
+
+
+class CgxOpsTiming(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("setup_ms", ctypes.c_double),
+                ("hash_ms", ctypes.c_double), ("solve_ms", ctypes.c_double),
+                ("download_ms", ctypes.c_double), ("uploaded", ctypes.c_int),
+                ("iters", ctypes.c_int)]
+
+
+def ops_set_mode(mode=CGX_MODE_FAST, alg=CGX_ALG_HS):
+    """Numerics of conj_grad / solve / the mv_ops.h arithmetic (process-wide)."""
+    check(lib().cgx_ops_set_mode(mode, alg), "ops_set_mode")
+
+
+def ops_last_timing():
+    """Wall-clock split of the last conj_grad / solve call (cgx_ops_last_timing)."""
+    t = CgxOpsTiming()
+    check(lib().cgx_ops_last_timing(ctypes.byref(t)), "ops_last_timing")
+    return {k: getattr(t, k) for k, _ in CgxOpsTiming._fields_}
 
 
 def ops_counters():

@@ -5,7 +5,7 @@
 // Structs keep HOST pointers exactly as in the reference; the arithmetic of
 // mv_mult / dot_product / sv_mult / vec_add / vec_sub and the whole CG
 // iteration runs on the GPU through a process-wide default context (device
-// CGX_DEVICE, default 0), serialised by a mutex.  There is no CPU fallback:
+// 0 unless cgx_ops_set_device), serialised by a mutex.  There is no CPU fallback:
 // without a gfx950 device these calls fail (-2) and cgx_last_error() says why.
 //
 // Matrix residency: the reference's conj_grad calls mv_mult once per
@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -52,24 +53,21 @@ struct OpsCtx {
 };
 OpsCtx g_ops;
 
-int env_device() {
-  const char *v = getenv("CGX_DEVICE");
-  return (v && *v) ? atoi(v) : 0;
-}
+// Numerics and device of the entry points above: set through
+// cgx_ops_set_mode / cgx_ops_set_device (the library reads no environment;
+// the drop-in CLI maps CGX_MODE / CGX_ALG / CGX_DEVICE onto these calls).
+int g_device = 0, g_mode = CGX_MODE_FAST, g_alg = CGX_ALG_HS;
+cgx_ops_timing g_timing{};
 
-bool env_exact() {
-  const char *v = getenv("CGX_MODE");
-  return v && strcmp(v, "exact") == 0;
-}
-
-int env_alg() {
-  const char *v = getenv("CGX_ALG");
-  return (v && strcmp(v, "cg1") == 0) ? CGX_ALG_CG1 : CGX_ALG_HS;
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
 }
 
 int default_solver(cgx_solver **out) {
   if (!g_solver) {
-    int rc = cgx_solver_create(env_device(), &g_solver);
+    int rc = cgx_solver_create(g_device, &g_solver);
     if (rc) return rc;
   }
   *out = g_solver;
@@ -123,9 +121,11 @@ unsigned long long matrix_hash(const struct __mv_sparse *A) {
 
 // Makes A the default solver's matrix: a reuse when the struct's arrays,
 // sizes and contents are those already on the device, else one upload.
-int ensure_matrix(cgx_solver *s, const struct __mv_sparse *A) {
+int ensure_matrix(cgx_solver *s, const struct __mv_sparse *A, double *hash_ms = nullptr) {
   const int n = A->size, nnz = A->row_ptr[n];
+  const double th = now_ms();
   const unsigned long long h = matrix_hash(A);
+  if (hash_ms) *hash_ms = now_ms() - th;
   if (g_res.valid && g_res.rp == A->row_ptr && g_res.col == A->col_indices &&
       g_res.val == A->values && g_res.size == n && g_res.nnz == nnz && g_res.hash == h) {
     ++g_reuses;
@@ -147,7 +147,7 @@ int ensure_matrix(cgx_solver *s, const struct __mv_sparse *A) {
 
 int ops_ready(size_t n) {
   if (g_ops.device < 0) {
-    const int dev = env_device();
+    const int dev = g_device;
     int rc = check_device(dev, &g_ops.cus);
     if (rc) return rc;
     CGX_HIP(hipSetDevice(dev));
@@ -222,7 +222,7 @@ int device_dot(const double *a, const double *b, int n, double *out) {
   if (rc) return rc;
   CGX_HIP(hipMemcpyAsync(g_ops.a, a, (size_t)n * 8, hipMemcpyHostToDevice, g_ops.st));
   CGX_HIP(hipMemcpyAsync(g_ops.b, b, (size_t)n * 8, hipMemcpyHostToDevice, g_ops.st));
-  if (env_exact()) {
+  if (g_mode == CGX_MODE_EXACT) {
     CGX_HIP(launch_dot_seq<double>(n, g_ops.a, g_ops.b, g_ops.r, nullptr, g_ops.st));
   } else {
     const int g = vec_grid_for(n, g_ops.cus);
@@ -247,22 +247,33 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct _
     return CGX_EINVAL;
   }
   std::lock_guard<std::mutex> lk(g_mu);
+  const double t0 = now_ms();
+  cgx_ops_timing t{};
   cgx_solver *s = nullptr;
   int rc = default_solver(&s);
   if (rc) return rc;
-  if ((rc = cgx_solver_set_mode(s, env_exact() ? CGX_MODE_EXACT : CGX_MODE_FAST,
-                                env_exact() ? CGX_ALG_HS : env_alg())))
+  if ((rc = cgx_solver_set_mode(s, g_mode, g_mode == CGX_MODE_EXACT ? CGX_ALG_HS : g_alg)))
     return rc;
-  if ((rc = ensure_matrix(s, A))) return rc;
+  const long long up0 = g_uploads;
+  if ((rc = ensure_matrix(s, A, &t.hash_ms))) return rc;
+  const double t1 = now_ms();
+  t.uploaded = g_uploads > up0;
+  t.setup_ms = t1 - t0;
   if ((rc = cgx_solver_set_rhs(s, b->values))) return rc;
   int iters = maxit + 1;
   if (A->size > 0 && (rc = cgx_solver_run(s, maxit, tol, &iters))) return rc;
+  const double t2 = now_ms();
+  t.solve_ms = t2 - t1;
   struct __mv_sparse *xv = new_mv_struct_with_size(b->size);  // cg.c:104
   if (!xv) return CGX_ENOMEM;
   if (A->size > 0 && (rc = cgx_solver_get_x(s, xv->values))) {
     cgx_free_mv_deep(xv);
     return rc;
   }
+  t.download_ms = now_ms() - t2;
+  t.total_ms = now_ms() - t0;
+  t.iters = iters;
+  g_timing = t;
   *x = xv;  // cg.c:138 (any previous *x is not freed, as in the reference)
   return iters;
 }
@@ -413,6 +424,36 @@ int mv_mult(struct __mv_sparse *A, struct __mv_sparse *b, struct __mv_sparse **r
   if (rc == 0 && n > 0) memcpy((*r)->values, tmp, (size_t)n * 8);
   free(tmp);
   return rc;
+}
+
+int cgx_ops_set_mode(int mode, int alg) {
+  if ((mode != CGX_MODE_FAST && mode != CGX_MODE_EXACT) || (alg != CGX_ALG_HS && alg != CGX_ALG_CG1) ||
+      (mode == CGX_MODE_EXACT && alg != CGX_ALG_HS)) {
+    set_error("cgx_ops_set_mode: bad mode/alg (exact mode is HS only)");
+    return CGX_EINVAL;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_mode = mode;
+  g_alg = alg;
+  return 0;
+}
+
+int cgx_ops_set_device(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (device == g_device) return 0;
+  if (g_solver || g_ops.device >= 0) {
+    set_error("cgx_ops_set_device: call before the first mv_ops / conj_grad / solve call");
+    return CGX_EINVAL;
+  }
+  g_device = device;
+  return 0;
+}
+
+int cgx_ops_last_timing(cgx_ops_timing *t) {
+  if (!t) return CGX_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  *t = g_timing;
+  return 0;
 }
 
 int cgx_ops_counters(long long *uploads, long long *reuses) {

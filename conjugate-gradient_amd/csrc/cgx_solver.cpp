@@ -398,9 +398,10 @@ int bench_run_t(cgx_solver *s, int iters, int flags, double *total_ms, double *s
   CGX_HIP(hipEventRecord(e0, s->stream));
   if (spmv_only) {
     // back-to-back SpMVs y = A p (the standard SpMV benchmark), no iteration
+    // and no epilogue partials: the plain y = A x kernel
     for (int i = 0; i < iters && !rc; ++i) {
       if (per_spmv) CGX_HIP(hipEventRecord(s->events[2 + 2 * i], s->stream));
-      CGX_HIP(s->A.spmv<T>((T *)s->d_p, (T *)s->d_w, s->d_pb, nullptr, s->A.all_items(),
+      CGX_HIP(s->A.spmv<T>((T *)s->d_p, (T *)s->d_w, nullptr, nullptr, s->A.all_items(),
                            s->stream));
       if (per_spmv) CGX_HIP(hipEventRecord(s->events[3 + 2 * i], s->stream));
     }

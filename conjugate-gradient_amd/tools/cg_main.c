@@ -6,9 +6,14 @@
  * x, mv_ops.c:77-95); the solve runs on the MI355X through libcgx's
  * conj_grad.  Like the reference, the optional third argument is parsed
  * (cg.c:56-57) but does not change the output.  The input is read with
- * cgx_read_input_file (the reference's 4-line format, cg.c:146-218). */
+ * cgx_read_input_file (the reference's 4-line format, cg.c:146-218).
+ *
+ * Environment (read here, not by the library): CGX_MODE=exact -> the
+ * reference's sequential dot-product order (bit-identical x), CGX_ALG=cg1 ->
+ * Chronopoulos-Gear, CGX_DEVICE=<ordinal> -> the GPU. */
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <time.h>
 
 #include "cgx.h"
@@ -23,6 +28,15 @@ int main(int argc, char **argv)
   int max_iterations = (int)strtol(argv[2], NULL, 10);
   int no_output = (argc == 4 && argv[3][0] == 'y');
   (void)no_output;
+
+  const char *mode = getenv("CGX_MODE"), *alg = getenv("CGX_ALG"), *dev = getenv("CGX_DEVICE");
+  const int exact = mode && strcmp(mode, "exact") == 0;
+  if (cgx_ops_set_mode(exact ? CGX_MODE_EXACT : CGX_MODE_FAST,
+                       !exact && alg && strcmp(alg, "cg1") == 0 ? CGX_ALG_CG1 : CGX_ALG_HS) != 0 ||
+      (dev && *dev && cgx_ops_set_device(atoi(dev)) != 0)) {
+    fprintf(stderr, "cg: %s\n", cgx_last_error());
+    return 1;
+  }
 
   struct __mv_sparse *mat_A = new_mv_struct();
   struct __mv_sparse *vec_b = new_mv_struct();

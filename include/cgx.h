@@ -32,10 +32,7 @@ extern "C" {
  * *vec_x receives a freshly allocated host vector (any previous *vec_x is
  * ignored, as in the reference, cg.c:104,138).  Returns 0 (the reference
  * always returns 0) or < 0 on a device/argument failure.
- * Environment: CGX_MODE=exact selects the reference's sequential dot-product
- * order (bit-identical x on chained matrices); default is the parallel
- * reduction order (x within fp64 rounding of the reference).
- * CGX_DEVICE=<ordinal> picks the GPU (default 0). */
+ * Numerics and device: cgx_ops_set_mode / cgx_ops_set_device below. */
 int conj_grad(int max_iter, struct __mv_sparse *mat_A,
               struct __mv_sparse *vec_b, struct __mv_sparse **vec_x);
 
@@ -49,6 +46,28 @@ int solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
 /* Frees a struct and its arrays (the reference's free_mv_struct frees only
  * the shell, mv_ops.c:39-42, which libcgx keeps for drop-in safety). */
 void cgx_free_mv_deep(struct __mv_sparse *m);
+
+/* Numerics of the reference-compatible entry points (conj_grad, solve and
+ * the mv_ops.h arithmetic), process-wide; the library reads no environment.
+ *   mode CGX_MODE_FAST (default): two-stage parallel reductions, x within
+ *        fp64 rounding of the reference (tests: 1e-12 relative)
+ *   mode CGX_MODE_EXACT: the reference's sequential dot-product order, x
+ *        bit-identical to cg.c on chained matrices (HS only)
+ *   alg  CGX_ALG_HS (the reference recurrence, default) or CGX_ALG_CG1
+ * The drop-in CLI maps CGX_MODE=exact / CGX_ALG=cg1 onto this call. */
+int cgx_ops_set_mode(int mode, int alg);
+/* GPU of those entry points (default 0); before their first call only. */
+int cgx_ops_set_device(int device);
+
+/* Wall-clock split of the last conj_grad / solve call (what cg.c:71-75
+ * times around conj_grad): setup = content hash of A + upload and layout
+ * encoding when A is not resident (uploaded = 1), solve = device iterations
+ * incl. the rhs copy, download = x back to the host. */
+typedef struct {
+  double total_ms, setup_ms, hash_ms, solve_ms, download_ms;
+  int uploaded, iters;
+} cgx_ops_timing;
+int cgx_ops_last_timing(cgx_ops_timing *t);
 
 /* Matrix residency of the mv_ops.h / conj_grad / solve entry points: the
  * last matrix stays on the device, keyed by the struct's array pointers,

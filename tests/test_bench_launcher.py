@@ -1,0 +1,60 @@
+"""bench.py's N > 1 launcher (CPU only, no GPU touched): `--gpus N` without
+WORLD_SIZE starts this script under torch.distributed.run as a CHILD process
+(one rank per GPU, rendezvous on 127.0.0.1) and exits with its code; with
+WORLD_SIZE set it runs as a rank; a WORLD_SIZE that disagrees with --gpus is
+refused."""
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+import bench  # noqa: E402  (module import must not touch torch / the GPU)
+
+
+def test_module_import_is_gpu_free():
+    assert "torch" not in bench.__dict__ and "cgx" not in bench.__dict__
+
+
+def test_launch_cmd_for_two_gpus():
+    cmd = bench.launch_cmd(["--gpus", "2", "--steps", "5", "--warmup", "1"], 2, 29123)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=2" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29123" in cmd
+    i = cmd.index(str(REPO / "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", "2", "--steps", "5", "--warmup", "1"]
+
+
+def test_main_spawns_child_without_world_size(monkeypatch):
+    seen = {}
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return subprocess.CompletedProcess(cmd, 3)
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "7"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 3  # the child's exit code is forwarded
+    assert "--nproc-per-node=2" in seen["cmd"] and seen["cmd"][-4:] == ["--gpus", "2", "--steps", "7"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_world_size_mismatch_refused(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "WORLD_SIZE=4" in str(e.value.code)
+
+
+def test_default_workloads():
+    a = bench.parse_args(["--gpus", "8"])
+    assert a.workload is None and a.steps == 100 and a.warmup == 10
+    assert bench.WORKLOADS["c4"]["dims"] == (400, 400, 400)
+    assert bench.WORKLOADS["c3"]["dims"] == (216, 216, 216)

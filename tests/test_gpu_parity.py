@@ -15,7 +15,6 @@ Bars (stated here, checked below):
     ||b - A x|| / ||b|| <= tol after solve).
 """
 import ctypes
-import os
 
 import numpy as np
 import pytest
@@ -40,13 +39,11 @@ def solver():
 
 @pytest.fixture
 def exact_env():
-    old = os.environ.get("CGX_MODE")
-    os.environ["CGX_MODE"] = "exact"
+    """The op-level entry points in the reference's summation order
+    (cgx_ops_set_mode; the library reads no environment)."""
+    cgx.ops_set_mode(cgx.CGX_MODE_EXACT)
     yield
-    if old is None:
-        os.environ.pop("CGX_MODE", None)
-    else:
-        os.environ["CGX_MODE"] = old
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST)
 
 
 def rel(x, ref):
@@ -425,7 +422,7 @@ def test_vec_sub_in_place_alias():
 
 
 def test_dot_product_fast_mode_close():
-    os.environ.pop("CGX_MODE", None)
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST)
     a = cgx.Mv(np.random.default_rng(0).standard_normal(100003))
     b = cgx.Mv(np.random.default_rng(1).standard_normal(100003))
     d = cgx.lib().dot_product(a.ptr, b.ptr)
@@ -447,7 +444,7 @@ def test_conj_grad_exact_mode_bit_exact(name, exact_env):
 
 @pytest.mark.parametrize("name", CHAINED)
 def test_conj_grad_fast_mode_within_tolerance(name):
-    os.environ.pop("CGX_MODE", None)
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST)
     g = H.load_golden(name)
     A = cgx.Mv(g["val"], g["col"], g["row_ptr"])
     b = cgx.Mv(g["b"])
