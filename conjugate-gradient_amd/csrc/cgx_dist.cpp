@@ -105,7 +105,8 @@ struct cgx_dist {
   size_t ev_i = 0;
   // batches of graph_batch iterations replayed as a hipGraph (solo and
   // RCCL; the in-process group runs eager)
-  hipGraphExec_t gexec = nullptr;
+  hipGraphExec_t gexec = nullptr;   // graph_batch iterations
+  hipGraphExec_t gexec1 = nullptr;  // one iteration (remainders)
   int gexec_alg = -1;
   int graph_batch = 16;
   bool use_graph = true;
@@ -132,7 +133,8 @@ bool solo(const cgx_dist *d) { return !d->local && d->comm == nullptr; }
 
 void drop_graph(cgx_dist *d) {
   if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
-  d->gexec = nullptr;
+  if (d->gexec1) (void)hipGraphExecDestroy(d->gexec1);
+  d->gexec = d->gexec1 = nullptr;
   d->gexec_alg = -1;
 }
 
@@ -450,22 +452,26 @@ int phase_spmv(cgx_dist *d) {
     else fin = FinArgs{d->d_tick, d->d_pa, d->vec_grid, d->d_pb, np, d->d_sums};
   }
   const bool bnd_last = d->g_bnd > 0;
-  auto launch = [&](const Items &it, double *part, bool last) -> hipError_t {
-    if (it.count == 0) return hipSuccess;
+  // rec: kernel timing events (hipExtLaunchKernel) of the two launches; an
+  // empty launch records both of its events on the stream instead
+  auto launch = [&](const Items &it, double *part, bool last, int e) -> hipError_t {
+    LaunchEv ev;
+    if (rec) ev = LaunchEv{d->spmv_ev[d->ev_i + e], d->spmv_ev[d->ev_i + e + 1]};
+    if (it.count == 0) {
+      if (rec) {
+        hipError_t r = hipEventRecord(ev.start, d->st);
+        return r != hipSuccess ? r : hipEventRecord(ev.stop, d->st);
+      }
+      return hipSuccess;
+    }
     SpmvArgs<double> a = d->A.args<double>(spmv_x(d), spmv_y(d), part, &d->d_st->done, it);
     if (last) a.fin = fin;
-    return launch_spmv<double>(a, d->st);
+    return launch_spmv<double>(a, d->st, ev);
   };
-  if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i], d->st));
-  CGX_HIP(launch(d->it_int, d->d_pb, !bnd_last));
-  if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 1], d->st));
+  CGX_HIP(launch(d->it_int, d->d_pb, !bnd_last, 0));
   if (!solo(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
-  if (rec) CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 2], d->st));
-  CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, bnd_last));
-  if (rec) {
-    CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 3], d->st));
-    d->ev_i += 4;
-  }
+  CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, bnd_last, 2));
+  if (rec) d->ev_i += 4;
   if (solo(d)) return 0;
   if (np == 0)  // no rows here: the local sums are those of empty sets
     CGX_HIP(launch_finalize(d->alg == CGX_ALG_HS ? FIN_SUM : FIN_SUM2, d->d_pa,
@@ -605,44 +611,58 @@ int run_phases_eager(Group *g, bool init, long long iters) {
   return 0;
 }
 
-// Capture graph_batch iterations (kernels, halo send/recv on the comm
-// stream forked and joined by events, all-reduces) once; replay.
-int capture(cgx_dist *d, Group *g) {
+// Capture `nit` iterations (kernels, halo send/recv on the comm stream
+// forked and joined by events, all-reduces) into *out, without running them.
+int capture(cgx_dist *d, Group *g, int nit, hipGraphExec_t *out) {
   hipGraph_t gr = nullptr;
   CGX_HIP(hipSetDevice(d->device));
   CGX_HIP(hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal));
-  const int rc = run_phases_eager(g, false, d->graph_batch);
+  const int rc = run_phases_eager(g, false, nit);
   const hipError_t e = hipStreamEndCapture(d->st, &gr);
   hipError_t ei = hipSuccess;
-  if (rc == 0 && e == hipSuccess) ei = hipGraphInstantiate(&d->gexec, gr, nullptr, nullptr, 0);
+  if (rc == 0 && e == hipSuccess) ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
   if (gr) (void)hipGraphDestroy(gr);
   if (rc || e != hipSuccess || ei != hipSuccess) {
-    d->gexec = nullptr;
+    *out = nullptr;
     (void)hipGetLastError();
     return CGX_ENODEV;
   }
+  return 0;
+}
+
+bool graphs_on(const cgx_dist *d) {
+  return !d->local && d->use_graph && d->graph_state >= 0 && d->graph_batch > 0 && !d->rec_spmv;
+}
+
+// The replayed graphs of the current recurrence: graph_batch iterations and
+// one iteration (remainders), captured once -- by bench_prepare, so a timed
+// region only replays.  A capture the transport refuses leaves the solver
+// eager (graph_state -1); nothing was enqueued on the stream.
+int ensure_graphs(Group *g) {
+  cgx_dist *d = g->parts[0];
+  if (!graphs_on(d)) return 0;
+  if (d->gexec && d->gexec1 && d->gexec_alg == d->alg) return 0;
+  drop_graph(d);
+  if (capture(d, g, d->graph_batch, &d->gexec) || capture(d, g, 1, &d->gexec1)) {
+    drop_graph(d);
+    d->graph_state = -1;
+    return 0;
+  }
   d->gexec_alg = d->alg;
+  d->graph_state = 1;
   return 0;
 }
 
 int run_phases(Group *g, bool init, long long iters) {
   cgx_dist *d = g->parts[0];
-  const int B = d->graph_batch;
-  if (!init && !d->local && d->use_graph && d->graph_state >= 0 && B > 0 && iters >= B &&
-      !d->rec_spmv) {
-    if (!d->gexec || d->gexec_alg != d->alg) {
-      drop_graph(d);
-      if (capture(d, g)) {
-        // capture not supported here (e.g. a transport call refused it):
-        // stay eager; nothing was enqueued on the stream
-        d->graph_state = -1;
-        return run_phases_eager(g, init, iters);
-      }
-      d->graph_state = 1;
-    }
-    while (iters >= B) {
-      CGX_HIP(hipGraphLaunch(d->gexec, d->st));
-      iters -= B;
+  if (!init && graphs_on(d)) {
+    int rc = ensure_graphs(g);
+    if (rc) return rc;
+    if (d->gexec && d->gexec1) {
+      for (; iters >= d->graph_batch; iters -= d->graph_batch)
+        CGX_HIP(hipGraphLaunch(d->gexec, d->st));
+      for (; iters > 0; --iters) CGX_HIP(hipGraphLaunch(d->gexec1, d->st));
+      return 0;
     }
   }
   return run_phases_eager(g, init, iters);
@@ -698,13 +718,19 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
     if ((rc = read_states(g))) return rc;
   } else {
     long long done = 0, batch = 16;
+    double rr_prev = 0.0;
+    int k_prev = -1;
     for (;;) {
       const long long b = std::min(batch, total - done);
       if ((rc = run_phases(g, false, b))) return rc;
       done += b;
       if ((rc = read_states(g))) return rc;
-      if (g->parts[0]->h_st->done || done >= total) break;
-      batch = std::min<long long>(batch * 2, 256);
+      const CgState *h = g->parts[0]->h_st;
+      if (h->done || done >= total) break;
+      // every rank sees the same all-reduced r.r: the same batches everywhere
+      batch = next_batch(h->rr, h->tol2bb, h->k, rr_prev, k_prev, batch);
+      rr_prev = h->rr;
+      k_prev = h->k;
     }
   }
   const CgState *s0 = g->parts[0]->h_st;
@@ -725,6 +751,7 @@ int group_bench_prepare(Group *g, int warmup) {
   if ((rc = ensure_connected(g))) return rc;
   if ((rc = prepare_states(g, INT_MAX - 1, 0.0, 0))) return rc;
   if ((rc = run_phases(g, true, 1))) return rc;
+  if ((rc = ensure_graphs(g))) return rc;  // captured here, not in the timed region
   if ((rc = run_phases(g, false, warmup))) return rc;
   for (cgx_dist *d : g->parts) {
     CGX_HIP(hipStreamSynchronize(d->st));

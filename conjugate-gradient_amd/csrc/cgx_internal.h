@@ -208,11 +208,17 @@ struct SpmvArgs {
   double inv_nx, inv_pl;  // 1 / nx, 1 / (nx ny): exact floor divisions (fdiv)
 };
 
+// Optional kernel timing events of a launch (hipExtLaunchKernel: stamped at
+// the kernel's own start and end).
+struct LaunchEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+
 // Workgroups of one launch (= epilogue partials it writes).
 template <typename T>
 int spmv_grid(const SpmvArgs<T> &a);
 template <typename T>
-hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st);
+hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev = LaunchEv{});
 
 // ------------------------------------------------------------- vectors
 // All launchers are graph-capturable (no sync, no allocation).
@@ -284,6 +290,9 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                              hipStream_t st);
 
 int vec_grid_for(int n, int cus);
+// Iterations to run before the next stop-flag poll of a solve with a
+// tolerance, from r.r at this poll and the last (k = iteration index).
+long long next_batch(double rr, double tol2bb, int k, double rr_prev, int k_prev, long long batch);
 
 // Partition helpers (cgx_partition.cpp)
 long long part_begin(long long n, int G, int g);

@@ -16,6 +16,7 @@
 // Compiled with -ffp-contract=off: the reference never fuses multiply-add
 // (Makefile:2 builds -O0), and x + alpha*p must round twice to stay
 // bit-identical.  Every reduction has a fixed order: runs are bit-reproducible.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -346,18 +347,24 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
           __builtin_amdgcn_global_load_lds((const void *)(a.col + kb + i * kWave * 4 + lane * 4),
                                            (lds_void *)(lcol + i * kWave * 4), 16, 0, AUX);
     }
+    // row bounds: one row_ptr load per lane, the row end is the next lane's
+    // start (the block's last row ends at k1); x[row] for the epilogue is the
+    // diagonal entry's own gather when the row has one (-4% at C3 with both,
+    // tools/mb/spmv_lab.hip), else a load of its own
     int j0 = 0, j1 = 0;
     T xrow = T(0), acc = T(0);
+    bool have_x = false;
     if (lane < nr) {
       j0 = a.rp[r0 + lane];
-      j1 = a.rp[r0 + lane + 1];
-      if (EPI) xrow = a.x[r0 + lane];
       if (a.yacc) acc = a.yacc[r0 + lane];  // column panels: continue the row sum
     }
     if (fits) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      j1 = __shfl_down(j0, 1, kWave);
+      if (lane == nr - 1) j1 = k1;
       wave_lds_sync();
       if (lane < nr) {
+        const int row = r0 + lane;
         for (int j = j0 - kb; j < j1 - kb; j += U) {
           const int cnt = min(U, j1 - kb - j);
           int cc[U];
@@ -374,6 +381,10 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
           for (int u = 0; u < U; ++u) {
             const T pr = vv[u] * xx[u];
             acc = u < cnt ? acc + pr : acc;
+            if (EPI && u < cnt && cc[u] == row) {
+              xrow = xx[u];
+              have_x = true;
+            }
           }
         }
       }
@@ -389,7 +400,10 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
     }
     if (lane < nr) {
       st_y(a.y + r0 + lane, acc, NT);
-      if (EPI) dot = (double)xrow * (double)acc;
+      if (EPI) {
+        if (!have_x) xrow = a.x[r0 + lane];
+        dot = (double)xrow * (double)acc;
+      }
     }
   }
   if (EPI) epi_store<WPB>(dot, a.part, a.fin);
@@ -444,10 +458,8 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
     }
     int len = 0;
     T xrow = T(0), acc = T(0);
-    if (lane < nr) {
-      len = a.rlen[r0 + lane];
-      if (EPI) xrow = a.x[r0 + lane];
-    }
+    bool have_x = false;  // x[row]: the diagonal's gather (offset 0) when present
+    if (lane < nr) len = a.rlen[r0 + lane];
     int dv[ND / kWave];
 #pragma unroll
     for (int i = 0; i < ND / kWave; ++i) dv[i] = a.dict[i * kWave + lane];
@@ -471,12 +483,19 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
             code[u] = lcode[idx + co];
             vv[u] = lval[idx];
           }
+          int off[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) xx[u] = a.x[u < cnt ? row + ldict[code[u]] : row];
+          for (int u = 0; u < U; ++u) off[u] = u < cnt ? ldict[code[u]] : 0;
+#pragma unroll
+          for (int u = 0; u < U; ++u) xx[u] = a.x[row + off[u]];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const T pr = vv[u] * xx[u];
             acc = u < cnt ? acc + pr : acc;
+            if (EPI && u < cnt && off[u] == 0) {
+              xrow = xx[u];
+              have_x = true;
+            }
           }
         }
       }
@@ -495,7 +514,10 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
     }
     if (lane < nr) {
       st_y(a.y + row, acc, NT);
-      if (EPI) dot = (double)xrow * (double)acc;
+      if (EPI) {
+        if (!have_x) xrow = a.x[row];
+        dot = (double)xrow * (double)acc;
+      }
     }
   }
   if (EPI) epi_store<WPB>(dot, a.part, a.fin);
@@ -1397,74 +1419,91 @@ int spmv_grid(const SpmvArgs<T> &a) {
   }
 }
 
+// Every SpMV launch goes through launch_k: with timing events it is
+// hipExtLaunchKernel, whose start / stop events are stamped when the
+// kernel itself starts and ends (the kernel's duration, as rocprofv3 sees
+// it, without the queue's dispatch latency in front of it).
+template <typename T>
+static void launch_k(const void *k, int g, hipStream_t st, const LaunchEv &ev,
+                     const SpmvArgs<T> &a) {
+  void *args[] = {(void *)&a};
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256), args, 0, st, ev.start, ev.stop, 0);
+  else
+    (void)hipLaunchKernel(k, dim3(g), dim3(256), args, 0, st);
+}
+#define CGX_K(...) reinterpret_cast<const void *>(&__VA_ARGS__)
+
 // U: x gathers issued per row chunk -- 7 when the rows are short (a 7-point
 // row is then exactly one chunk: -4% at C3, tools/mb/spmv_lab.hip), else 8
 template <typename T, int CAPW, bool EPI, bool NT>
-static void launch_csr_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
+static void launch_csr_w(const SpmvArgs<T> &a, int g, hipStream_t st, const LaunchEv &ev) {
   const bool l = a.items.list != nullptr;
   if (a.gath == 7) {
-    if (l) hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 7, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 7, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+    if (l) launch_k(CGX_K(k_spmv_csr<T, CAPW, 7, EPI, NT, true>), g, st, ev, a);
+    else launch_k(CGX_K(k_spmv_csr<T, CAPW, 7, EPI, NT, false>), g, st, ev, a);
   } else {
-    if (l) hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 8, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_spmv_csr<T, CAPW, 8, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+    if (l) launch_k(CGX_K(k_spmv_csr<T, CAPW, 8, EPI, NT, true>), g, st, ev, a);
+    else launch_k(CGX_K(k_spmv_csr<T, CAPW, 8, EPI, NT, false>), g, st, ev, a);
   }
 }
 
 template <typename T, int CAPW, int ND, bool EPI, bool NT>
-static void launch_dc_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
+static void launch_dc_w(const SpmvArgs<T> &a, int g, hipStream_t st, const LaunchEv &ev) {
   const bool l = a.items.list != nullptr;
   if (a.gath == 7) {
-    if (l) hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 7, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 7, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+    if (l) launch_k(CGX_K(k_spmv_dc<T, CAPW, ND, 7, EPI, NT, true>), g, st, ev, a);
+    else launch_k(CGX_K(k_spmv_dc<T, CAPW, ND, 7, EPI, NT, false>), g, st, ev, a);
   } else {
-    if (l) hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 8, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_spmv_dc<T, CAPW, ND, 8, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+    if (l) launch_k(CGX_K(k_spmv_dc<T, CAPW, ND, 8, EPI, NT, true>), g, st, ev, a);
+    else launch_k(CGX_K(k_spmv_dc<T, CAPW, ND, 8, EPI, NT, false>), g, st, ev, a);
   }
 }
 
 template <typename T, int KW, bool EPI, bool NT>
-static void launch_dia_w(const SpmvArgs<T> &a, int g, hipStream_t st) {
-  if (a.items.list)
-    hipLaunchKernelGGL((k_spmv_dia<T, KW, EPI, NT, true>), dim3(g), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_spmv_dia<T, KW, EPI, NT, false>), dim3(g), dim3(256), 0, st, a);
+static void launch_dia_w(const SpmvArgs<T> &a, int g, hipStream_t st, const LaunchEv &ev) {
+  if (a.items.list) launch_k(CGX_K(k_spmv_dia<T, KW, EPI, NT, true>), g, st, ev, a);
+  else launch_k(CGX_K(k_spmv_dia<T, KW, EPI, NT, false>), g, st, ev, a);
 }
 
 template <typename T, bool EPI, bool NT>
-static hipError_t launch_spmv_en(const SpmvArgs<T> &a, int g, hipStream_t st) {
+static hipError_t launch_spmv_en(const SpmvArgs<T> &a, int g, hipStream_t st, const LaunchEv &ev) {
   switch (a.layout) {
     case L_CSR:
       if constexpr (sizeof(T) == 4) {
-        launch_csr_w<T, 1024, EPI, NT>(a, g, st);
+        launch_csr_w<T, 1024, EPI, NT>(a, g, st, ev);
       } else {
-        if (a.capw == 328) launch_csr_w<T, 328, EPI, NT>(a, g, st);
-        else if (a.capw == 512) launch_csr_w<T, 512, EPI, NT>(a, g, st);
+        if (a.capw == 328) launch_csr_w<T, 328, EPI, NT>(a, g, st, ev);
+        else if (a.capw == 456) launch_csr_w<T, 456, EPI, NT>(a, g, st, ev);
+        else if (a.capw == 512) launch_csr_w<T, 512, EPI, NT>(a, g, st, ev);
         else return hipErrorInvalidValue;
       }
       break;
     case L_DC: {
       const bool big = a.ndict_cap > 64;
       if constexpr (sizeof(T) == 4) {
-        if (big) launch_dc_w<T, 1024, 256, EPI, NT>(a, g, st);
-        else launch_dc_w<T, 1024, 64, EPI, NT>(a, g, st);
+        if (big) launch_dc_w<T, 1024, 256, EPI, NT>(a, g, st, ev);
+        else launch_dc_w<T, 1024, 64, EPI, NT>(a, g, st, ev);
       } else if (a.capw == 328) {
-        if (big) launch_dc_w<T, 328, 256, EPI, NT>(a, g, st);
-        else launch_dc_w<T, 328, 64, EPI, NT>(a, g, st);
+        if (big) launch_dc_w<T, 328, 256, EPI, NT>(a, g, st, ev);
+        else launch_dc_w<T, 328, 64, EPI, NT>(a, g, st, ev);
+      } else if (a.capw == 456) {
+        if (big) launch_dc_w<T, 456, 256, EPI, NT>(a, g, st, ev);
+        else launch_dc_w<T, 456, 64, EPI, NT>(a, g, st, ev);
       } else if (a.capw == 512) {
-        if (big) launch_dc_w<T, 512, 256, EPI, NT>(a, g, st);
-        else launch_dc_w<T, 512, 64, EPI, NT>(a, g, st);
+        if (big) launch_dc_w<T, 512, 256, EPI, NT>(a, g, st, ev);
+        else launch_dc_w<T, 512, 64, EPI, NT>(a, g, st, ev);
       } else {
         return hipErrorInvalidValue;
       }
       break;
     }
     case L_DIA:
-      if (a.ndiag <= 8) launch_dia_w<T, 1, EPI, NT>(a, g, st);
-      else launch_dia_w<T, 2, EPI, NT>(a, g, st);
+      if (a.ndiag <= 8) launch_dia_w<T, 1, EPI, NT>(a, g, st, ev);
+      else launch_dia_w<T, 2, EPI, NT>(a, g, st, ev);
       break;
     case L_STENCIL:
-      hipLaunchKernelGGL((k_stencil<T, EPI, NT>), dim3(g), dim3(256), 0, st, a);
+      launch_k(CGX_K(k_stencil<T, EPI, NT>), g, st, ev, a);
       break;
     default:
       return hipErrorInvalidValue;
@@ -1473,14 +1512,14 @@ static hipError_t launch_spmv_en(const SpmvArgs<T> &a, int g, hipStream_t st) {
 }
 
 template <typename T>
-hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st) {
+hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev) {
   const int g = spmv_grid(a);
   if (g <= 0) return hipSuccess;
   const bool epi = a.part != nullptr;
-  if (epi && a.nt) return launch_spmv_en<T, true, true>(a, g, st);
-  if (epi) return launch_spmv_en<T, true, false>(a, g, st);
-  if (a.nt) return launch_spmv_en<T, false, true>(a, g, st);
-  return launch_spmv_en<T, false, false>(a, g, st);
+  if (epi && a.nt) return launch_spmv_en<T, true, true>(a, g, st, ev);
+  if (epi) return launch_spmv_en<T, true, false>(a, g, st, ev);
+  if (a.nt) return launch_spmv_en<T, false, true>(a, g, st, ev);
+  return launch_spmv_en<T, false, false>(a, g, st, ev);
 }
 
 template <typename T>
@@ -1621,7 +1660,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
 
 #define CGX_INSTANTIATE(T)                                                                       \
   template int spmv_grid<T>(const SpmvArgs<T> &);                                                \
-  template hipError_t launch_spmv<T>(const SpmvArgs<T> &, hipStream_t);                          \
+  template hipError_t launch_spmv<T>(const SpmvArgs<T> &, hipStream_t, const LaunchEv &);      \
   template hipError_t launch_init_hs<T>(int, const T *, T *, T *, T *, double *, int,            \
                                         hipStream_t);                                            \
   template hipError_t launch_init_cg1<T>(int, const T *, T *, T *, T *, T *, double *, int,      \

@@ -547,6 +547,7 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
       int m = 0;
       for (int r = 0; r < n; r += 64) m = std::max(m, rp[std::min(r + 64, n)] - rp[r]);
       if (m + kPad <= 328) capw = 328;
+      else if (m + kPad <= 456) capw = 456;  // 7-point stencils (C3): 7 workgroups per CU, not 6
     }
     std::vector<int> blkrk;
     blk_row.clear();
@@ -726,17 +727,20 @@ int DevMatrix::partials(Items it) const {
 
 template <typename T>
 hipError_t DevMatrix::spmv(const T *x, T *y, double *part, const int *done, Items it,
-                           hipStream_t s, int *nparts) const {
+                           hipStream_t s, int *nparts, LaunchEv ev) const {
   if (nparts) *nparts = partials(it);
   if (layout == L_STENCIL) it = Items{nullptr, 0, (n + kDiaSliceRows - 1) / kDiaSliceRows};
-  if (npanel <= 1) return launch_spmv<T>(args<T>(x, y, part, done, it), s);
+  if (npanel <= 1) return launch_spmv<T>(args<T>(x, y, part, done, it), s, ev);
   for (int q = 0; q < npanel; ++q) {
     SpmvArgs<T> a = args<T>(x, y, q + 1 == npanel ? part : nullptr, done,
                             Items{nullptr, panel_first[q], panel_count[q]});
     a.rp = d_rp + (size_t)q * ((size_t)n + 1);
     a.yacc = q ? y : nullptr;
     a.capw = capw;
-    const hipError_t e = launch_spmv<T>(a, s);
+    LaunchEv e1;
+    e1.start = q == 0 ? ev.start : nullptr;
+    e1.stop = q + 1 == npanel ? ev.stop : nullptr;
+    const hipError_t e = launch_spmv<T>(a, s, e1);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -747,8 +751,8 @@ template SpmvArgs<double> DevMatrix::args<double>(const double *, double *, doub
 template SpmvArgs<float> DevMatrix::args<float>(const float *, float *, double *, const int *,
                                                 Items) const;
 template hipError_t DevMatrix::spmv<double>(const double *, double *, double *, const int *,
-                                            Items, hipStream_t, int *) const;
+                                            Items, hipStream_t, int *, LaunchEv) const;
 template hipError_t DevMatrix::spmv<float>(const float *, float *, double *, const int *, Items,
-                                           hipStream_t, int *) const;
+                                           hipStream_t, int *, LaunchEv) const;
 
 }  // namespace cgx

@@ -86,9 +86,11 @@ struct DevMatrix {
   Items all_items() const { return Items{d_order, 0, items()}; }
   // One SpMV (panels: one launch per panel, rows continuing their sums;
   // the epilogue partials on the last panel).  Returns the partial count.
+  // ev: timing events around the whole SpMV (start on its first launch,
+  // stop on its last).
   template <typename T>
   hipError_t spmv(const T *x, T *y, double *part, const int *done, Items it, hipStream_t s,
-                  int *nparts = nullptr) const;
+                  int *nparts = nullptr, LaunchEv ev = LaunchEv{}) const;
   // The number of partials spmv() writes for the given items.
   int partials(Items it) const;
 };

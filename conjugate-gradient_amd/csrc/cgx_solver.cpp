@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -130,7 +131,8 @@ struct cgx_solver {
   size_t vec_bytes = 0;
   bool have_matrix = false, have_rhs = false, bench_ready = false;
   int last_iters = 0;
-  hipGraphExec_t gexec = nullptr;
+  hipGraphExec_t gexec = nullptr;   // graph_batch iterations
+  hipGraphExec_t gexec1 = nullptr;  // one iteration (remainders)
   int gexec_key = -1;
   std::vector<hipEvent_t> events;
 };
@@ -143,7 +145,8 @@ size_t tsize(int dtype) { return dtype == CGX_F32 ? 4 : 8; }
 
 void drop_graph(cgx_solver *s) {
   if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-  s->gexec = nullptr;
+  if (s->gexec1) (void)hipGraphExecDestroy(s->gexec1);
+  s->gexec = s->gexec1 = nullptr;
   s->gexec_key = -1;
 }
 
@@ -241,7 +244,7 @@ int enqueue_init(cgx_solver *s) {
   return 0;
 }
 
-// One CG iteration.  ev0/ev1 (optional) bracket the SpMV launch.
+// One CG iteration.  ev0/ev1 (optional): the SpMV kernel's start / end.
 template <typename T>
 int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   hipStream_t st = s->stream;
@@ -250,10 +253,8 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   int np = 0;
   if (s->alg == CGX_ALG_HS) {
     const bool exact = s->mode == CGX_MODE_EXACT;
-    if (ev0) CGX_HIP(hipEventRecord(ev0, st));
     CGX_HIP(s->A.spmv<T>(p, sv, exact ? nullptr : s->d_pa, &s->d_st->done, s->A.all_items(), st,
-                         &np));  // cg.c:111
-    if (ev1) CGX_HIP(hipEventRecord(ev1, st));
+                         &np, LaunchEv{ev0, ev1}));  // cg.c:111
     if (exact) {
       CGX_HIP(launch_dot_seq<T>(n, p, sv, s->d_pa, &s->d_st->done, st));
       CGX_HIP(launch_finalize(FIN_HS_ALPHA, s->d_pa, 1, nullptr, 0, s->d_st, s->d_hist, nullptr,
@@ -270,9 +271,8 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     }
   } else {
     CGX_HIP(launch_cg1_update<T>(n, x, p, r, sv, w, s->d_st, s->d_pa, s->vec_grid, st));
-    if (ev0) CGX_HIP(hipEventRecord(ev0, st));
-    CGX_HIP(s->A.spmv<T>(r, w, s->d_pb, &s->d_st->done, s->A.all_items(), st, &np));
-    if (ev1) CGX_HIP(hipEventRecord(ev1, st));
+    CGX_HIP(s->A.spmv<T>(r, w, s->d_pb, &s->d_st->done, s->A.all_items(), st, &np,
+                         LaunchEv{ev0, ev1}));
     CGX_HIP(launch_finalize(FIN_CG1, s->d_pa, s->vec_grid, s->d_pb, np, s->d_st, s->d_hist,
                             nullptr, st));
   }
@@ -280,31 +280,49 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
 }
 
 template <typename T>
-int enqueue_iters(cgx_solver *s, long long count) {
-  const int B = s->graph_batch;
+int capture_iters(cgx_solver *s, int count, hipGraphExec_t *out) {
+  hipGraph_t g = nullptr;
+  CGX_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+  int rc = 0;
+  for (int i = 0; i < count && rc == 0; ++i) rc = enqueue_iter<T>(s, nullptr, nullptr);
+  hipError_t e = hipStreamEndCapture(s->stream, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  CGX_HIP(e);
+  e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  CGX_HIP(e);
+  return 0;
+}
+
+// The replayed graphs of the current mode / recurrence: graph_batch
+// iterations and one iteration (remainders), captured (not run) once.
+template <typename T>
+int ensure_graphs(cgx_solver *s) {
   const int key = s->alg * 2 + s->mode;
-  if (s->use_graph && count >= B) {
-    if (!s->gexec || s->gexec_key != key) {
-      drop_graph(s);
-      hipGraph_t g = nullptr;
-      CGX_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-      int rc = 0;
-      for (int i = 0; i < B && rc == 0; ++i) rc = enqueue_iter<T>(s, nullptr, nullptr);
-      hipError_t e = hipStreamEndCapture(s->stream, &g);
-      if (rc) {
-        if (g) (void)hipGraphDestroy(g);
-        return rc;
-      }
-      CGX_HIP(e);
-      e = hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
-      CGX_HIP(e);
-      s->gexec_key = key;
-    }
-    while (count >= B) {
+  if (s->gexec && s->gexec1 && s->gexec_key == key) return 0;
+  drop_graph(s);
+  int rc = capture_iters<T>(s, s->graph_batch, &s->gexec);
+  if (rc == 0) rc = capture_iters<T>(s, 1, &s->gexec1);
+  if (rc) {
+    drop_graph(s);
+    return rc;
+  }
+  s->gexec_key = key;
+  return 0;
+}
+
+template <typename T>
+int enqueue_iters(cgx_solver *s, long long count) {
+  if (s->use_graph && count > 0) {
+    int rc = ensure_graphs<T>(s);
+    if (rc) return rc;
+    for (; count >= s->graph_batch; count -= s->graph_batch)
       CGX_HIP(hipGraphLaunch(s->gexec, s->stream));
-      count -= B;
-    }
+    for (; count > 0; --count) CGX_HIP(hipGraphLaunch(s->gexec1, s->stream));
+    return 0;
   }
   for (long long i = 0; i < count; ++i) {
     int rc = enqueue_iter<T>(s, nullptr, nullptr);
@@ -312,6 +330,27 @@ int enqueue_iters(cgx_solver *s, long long count) {
   }
   return 0;
 }
+
+}  // namespace
+
+namespace cgx {
+
+long long next_batch(double rr, double tol2bb, int k, double rr_prev, int k_prev, long long batch) {
+  // iterations still needed if r.r keeps decaying at the rate seen since the
+  // last poll, +25% and 4 of slack; 16..256, at most doubling per poll
+  long long want = std::min<long long>(batch * 2, 256);
+  if (k_prev >= 0 && k > k_prev && rr_prev > 0.0 && rr > 0.0 && rr < rr_prev && tol2bb > 0.0) {
+    const double per_it = std::log(rr / rr_prev) / (double)(k - k_prev);  // < 0
+    const double need = std::log(tol2bb / rr) / per_it;                    // >= 0 when rr > tol2bb
+    if (std::isfinite(need) && need >= 0.0)
+      want = std::min(want, (long long)(need * 1.25) + 4);
+  }
+  return std::max<long long>(16, want);
+}
+
+}  // namespace cgx
+
+namespace {
 
 int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
   if (hist_cap > s->hist_alloc) {
@@ -348,17 +387,22 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
     if ((rc = enqueue_iters<T>(s, total))) return rc;
     if ((rc = read_state(s))) return rc;
   } else {
-    // poll the stop flag between batches of 16, 32, ... 256 iterations;
-    // iterations after the stop early-exit on the device flag, so the count
-    // is exactly the reference's
+    // poll the stop flag between batches; iterations after the stop
+    // early-exit on the device flag, so the count is exactly the
+    // reference's.  The batch follows the residual's observed decay rate
+    // (next_batch), so few launches run past the stop.
     long long done_iters = 0, batch = 16;
+    double rr_prev = 0.0;
+    int k_prev = -1;
     for (;;) {
       const long long b = std::min(batch, total - done_iters);
       if ((rc = enqueue_iters<T>(s, b))) return rc;
       done_iters += b;
       if ((rc = read_state(s))) return rc;
       if (s->h_st->done || done_iters >= total) break;
-      batch = std::min<long long>(batch * 2, 256);
+      batch = next_batch(s->h_st->rr, s->h_st->tol2bb, s->h_st->k, rr_prev, k_prev, batch);
+      rr_prev = s->h_st->rr;
+      k_prev = s->h_st->k;
     }
   }
   if (!s->h_st->done) {
@@ -375,6 +419,7 @@ int bench_prepare_t(cgx_solver *s, int warmup) {
   int rc;
   if ((rc = prepare_state(s, INT_MAX - 1, 0.0, 0))) return rc;
   if ((rc = enqueue_init<T>(s))) return rc;
+  if ((rc = ensure_graphs<T>(s))) return rc;  // captured here, not in a timed region
   if ((rc = enqueue_iters<T>(s, warmup))) return rc;
   CGX_HIP(hipStreamSynchronize(s->stream));
   s->bench_ready = true;
@@ -400,10 +445,10 @@ int bench_run_t(cgx_solver *s, int iters, int flags, double *total_ms, double *s
     // back-to-back SpMVs y = A p (the standard SpMV benchmark), no iteration
     // and no epilogue partials: the plain y = A x kernel
     for (int i = 0; i < iters && !rc; ++i) {
-      if (per_spmv) CGX_HIP(hipEventRecord(s->events[2 + 2 * i], s->stream));
+      LaunchEv ev;
+      if (per_spmv) ev = LaunchEv{s->events[2 + 2 * i], s->events[3 + 2 * i]};
       CGX_HIP(s->A.spmv<T>((T *)s->d_p, (T *)s->d_w, nullptr, nullptr, s->A.all_items(),
-                           s->stream));
-      if (per_spmv) CGX_HIP(hipEventRecord(s->events[3 + 2 * i], s->stream));
+                           s->stream, nullptr, ev));
     }
   } else if (per_spmv) {
     for (int i = 0; i < iters && !rc; ++i)

@@ -84,7 +84,8 @@ struct Csr {
 };
 
 // ------------------------------------------------------------------ CSR
-template <int CAPW, int U, bool NTY, int WPB = 4, bool PRIO = false, bool SHJ = false>
+template <int CAPW, int U, bool NTY, int WPB = 4, bool PRIO = false, bool SHJ = false,
+          bool DX = false>
 __global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
   __shared__ __attribute__((aligned(16))) double lval_all[WPB * CAPW];
   __shared__ __attribute__((aligned(16))) int lcol_all[WPB * CAPW];
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
     if (lane < nr) {
       j0 = a.rp[r0 + lane];
       if (!SHJ) j1 = a.rp[r0 + lane + 1];
-      xrow = a.x[r0 + lane];
+      if (!DX) xrow = a.x[r0 + lane];
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (SHJ) {  // row end = the next lane's row start; the block's last row ends at k1
@@ -122,6 +123,7 @@ __global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
     }
     wave_lds_sync();
     if (PRIO) __builtin_amdgcn_s_setprio(2);
+    bool dfound = false;
     if (lane < nr) {
       for (int j = j0 - kb; j < j1 - kb; j += U) {
         const int cnt = min(U, j1 - kb - j);
@@ -139,8 +141,13 @@ __global__ __launch_bounds__(WPB * 64) void k_csr(Csr a) {
         for (int u = 0; u < U; ++u) {
           const double pr = vv[u] * xx[u];
           acc = acc + (u < cnt ? pr : 0.0);
+          if (DX && u < cnt && cc[u] == r0 + lane) {  // the diagonal's gather is x[row]
+            xrow = xx[u];
+            dfound = true;
+          }
         }
       }
+      if (DX && !dfound) xrow = a.x[r0 + lane];
       if (NTY) __builtin_nontemporal_store(acc, a.y + r0 + lane);
       else a.y[r0 + lane] = acc;
       dot = xrow * acc;
@@ -748,6 +755,10 @@ int main(int argc, char **argv) {
       {"csr_u7sh", [&] { hipLaunchKernelGGL((k_csr<512, 7, true, 4, false, true>), dim3(g4), dim3(256), 0, 0, c); },
        (double)csr_bytes, true},
       {"csr_u7w456sh", [&] { hipLaunchKernelGGL((k_csr<456, 7, true, 4, false, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u7dx", [&] { hipLaunchKernelGGL((k_csr<512, 7, true, 4, false, false, true>), dim3(g4), dim3(256), 0, 0, c); },
+       (double)csr_bytes, true},
+      {"csr_u7shdx", [&] { hipLaunchKernelGGL((k_csr<512, 7, true, 4, false, true, true>), dim3(g4), dim3(256), 0, 0, c); },
        (double)csr_bytes, true},
       {"csr_u7", [&] { hipLaunchKernelGGL((k_csr<512, 7, true>), dim3(g4), dim3(256), 0, 0, c); },
        (double)csr_bytes, true},

@@ -12,6 +12,7 @@ export TMPDIR=/tmp
 TAG=$1; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+echo "$*" > $OUT/cmd.txt
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- "$@" > $OUT/trace.log 2>&1 || { echo "trace failed rc=$?"; tail -20 $OUT/trace.log; exit 3; }
 grep '"metric"' $OUT/trace.log | tail -1 | cut -c1-300
 for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum; do
