@@ -126,6 +126,24 @@ if spmv and alg_bytes:
 md_path = dst / f"{rnd}_{tag}.md"
 if not md_path.exists() or len(sys.argv) <= 6:
     md_path.write_text("\n".join(md) + "\n")
+agg = len(sys.argv) > 6 and sys.argv[6] == "sum"
+if spmv and agg:
+    # a multi-launch SpMV (column panels): the bytes of every matching
+    # launch, per SpMV (= per launch of the least-launched variant, the
+    # last pass with the epilogue)
+    ms = [x for x in stats if short(x["Name"]).startswith(want.split("<")[0] + "<")]
+    tot, per = 0.0, min(int(x["Calls"]) for x in ms)
+    for x in ms:
+        c = pmc.get(x["Name"], {})
+        g = lambda k: c.get(k, 0.0)  # noqa: E731
+        tot += int(x["Calls"]) * (128 * g("TCC_EA0_RDREQ_128B_sum") + 64 * g("TCC_EA0_RDREQ_64B_sum")
+                                  + 32 * g("TCC_EA0_RDREQ_32B_sum") + 64 * g("TCC_EA0_WRREQ_64B_sum")
+                                  + 32 * (g("TCC_EA0_WRREQ_sum") - g("TCC_EA0_WRREQ_64B_sum")))
+    spmv["spmv_hbm_bytes_per_launch"] = tot / per
+    spmv["aggregated"] = f"{len(ms)} kernel variants, {per} SpMVs"
+    md += ["", f"Multi-launch SpMV: EA bytes per SpMV over {len(ms)} kernel variants: "
+           f"{tot / per:.0f}" + (f" ({tot / per / alg_bytes:.3f}x algorithmic)" if alg_bytes else "")]
+    md_path.write_text("\n".join(md) + "\n")
 if spmv:
     spmv["algorithmic_bytes_per_launch"] = alg_bytes
     spmv["calibration_stream_read_bytes"] = calib
