@@ -139,11 +139,19 @@ def load_traffic(tag):
 
 KERNELS = {
     "dia": "k_spmv_dia (DIA-VI: value-indexed diagonal codes, two rows per thread, pair loads of x)",
+    "dia_fused": "k_spmv_dia_h (fused HS step on DIA-VI: x / p update of the previous iteration, "
+                 "p of the slice + halo in an LDS window, s = A p, p.s partials)",
     "dc": "k_spmv_dc (LDS-DMA code window + value window per 64-row block, dictionary-coded columns)",
     "csr": "k_spmv_csr (LDS-DMA val/col window per 64-row block, lane-per-row sums from LDS)",
     "panel": "k_spmv_csr over column panels",
     "stencil": "k_stencil (matrix-free, two rows per thread)",
 }
+
+
+def kernel_name(info):
+    if info["layout_name"] == "dia" and info.get("fused"):
+        return KERNELS["dia_fused"]
+    return KERNELS.get(info["layout_name"], info["layout_name"])
 
 
 def layout_desc(info):
@@ -388,16 +396,17 @@ def run_single(args, wl_name):
                           "back-to-back y = A p launches (the standard SpMV benchmark, "
                           "k_spmv_csr without the p.s epilogue)"))
         roofline["default_layout"] = dict(
-            kernel=KERNELS.get(info["layout_name"], info["layout_name"]),
+            kernel=kernel_name(info),
             layout=layout_desc(info), spmv_us=round(spmv_ms * 1e3, 2), achieved=head_gbs,
             frac=head_frac, algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
             traffic=load_traffic(wl_name),
             csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
-            note="the SpMV of the headline solve, priced on the bytes its layout moves")
+            note="the SpMV launch of the headline solve, priced on the bytes it moves (its "
+                 "layout; with the fused HS step also r, p_old, x, p_new)")
     else:
         roofline = dict(bound="hbm", achieved=head_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=head_frac, traffic=load_traffic(wl_name),
-                        kernel=KERNELS.get(info["layout_name"], info["layout_name"]),
+                        kernel=kernel_name(info),
                         algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
                         spmv_us=round(spmv_ms * 1e3, 2))
     triad = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)

@@ -54,7 +54,8 @@ class CgxInfo(ctypes.Structure):
                 ("n_dict", ctypes.c_int), ("tile_bands", ctypes.c_int), ("nt", ctypes.c_int),
                 ("code_bytes_per_row", ctypes.c_int), ("encode_fallback", ctypes.c_int),
                 ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double),
-                ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int)]
+                ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int),
+                ("fused", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):
@@ -101,6 +102,7 @@ _SIGS = {
     "cgx_solver_destroy": (None, [_vp]),
     "cgx_solver_set_mode": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "cgx_solver_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_solver_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_matrix": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                              _i32p, _i32p, _f64p]),
     "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
@@ -284,11 +286,13 @@ def is_chained(rp, col):
 class Solver:
     """Device-resident CG solver (cgx_solver_*)."""
 
-    def __init__(self, device=0, mode=CGX_MODE_FAST, alg=CGX_ALG_HS, layout=CGX_LAYOUT_AUTO):
+    def __init__(self, device=0, mode=CGX_MODE_FAST, alg=CGX_ALG_HS, layout=CGX_LAYOUT_AUTO,
+                 fused=True):
         self._h = _vp()
         check(lib().cgx_solver_create(device, ctypes.byref(self._h)), "cgx_solver_create")
         self.set_mode(mode, alg)
         self.set_layout(layout)
+        self.set_fused(fused)
         self.n = 0
         self.f32 = False
 
@@ -311,6 +315,10 @@ class Solver:
 
     def set_mode(self, mode, alg=CGX_ALG_HS):
         check(lib().cgx_solver_set_mode(self._h, mode, alg), "set_mode")
+
+    def set_fused(self, on):
+        """Fused HS step on DIA layouts (cgx_solver_set_fused)."""
+        check(lib().cgx_solver_set_fused(self._h, 1 if on else 0), "set_fused")
 
     def set_layout(self, layout):
         """CGX_LAYOUT_* (or its name) for the next set_matrix / gen_laplacian."""

@@ -72,8 +72,12 @@ struct CgState {
   int pad;
   double rr_u;
   double rr_x;
+  // fused HS step (k_spmv_dia_h): k_update_rf's last workgroup writes the
+  // canonical sum of its r.r partials here; k_u = -1 after the prologue
+  // marks "no previous iteration" (p = r, no x update)
+  double rr_new;
 };
-static_assert(sizeof(CgState) == 112, "CgState layout");
+static_assert(sizeof(CgState) == 120, "CgState layout");
 
 // Finalize ops (single-workgroup scalar steps of the recurrence).
 enum FinOp {
@@ -94,6 +98,7 @@ constexpr int kWindowPad = 1024;   // + one SpMV window (LDS-DMA reads 16-B piec
 constexpr int kDiaSliceRows = 512; // DIA-VI work item: one workgroup, 2 rows per thread
 constexpr int kDiaMax = 16;        // DIA-VI: diagonals (nibbles in a 64-bit row word)
 constexpr int kDiaVals = 15;       // DIA-VI: values per diagonal (nibble 15 = no entry)
+constexpr int kHaloMax = 1024;     // fused step: diagonals |d| <= this read p from the LDS window
 constexpr double kMallBytes = 256.0 * 1024 * 1024;  // Infinity Cache
 
 // ---------------------------------------------------- Laplacian operators
@@ -203,9 +208,28 @@ struct SpmvArgs {
   int doff[kDiaMax];      // diagonal offsets col - row, ascending
   int n;                  // rows (DIA, stencil)
   int ncols;              // entries of x (DIA pair loads stay inside)
+  // fused step (k_spmv_dia_h): the slice's LDS window covers rows
+  // [s0 - hl, s0 + 512 + hr); diagonal k is read from it when near bit k
+  int hl, hr;
+  unsigned near;
   // stencil
   LapSpec lap;
   double inv_nx, inv_pl;  // 1 / nx, 1 / (nx ny): exact floor divisions (fdiv)
+};
+
+// The fused HS step (single GPU, DIA layout): one launch does the previous
+// iteration's x += alpha p_old and p_new = r + beta p_old (beta and the stop
+// test from CgState; cg.c:115-116, 125-132), then s = A p_new with the
+// p_new.s partials.  p is double-buffered (the launch reads p_old while it
+// stores p_new).
+template <typename T>
+struct FuseArgs {
+  T *x;
+  const T *pold;
+  T *pnew;
+  const T *r;
+  CgState *st;
+  double *hist;
 };
 
 // Optional kernel timing events of a launch (hipExtLaunchKernel: stamped at
@@ -219,6 +243,11 @@ template <typename T>
 int spmv_grid(const SpmvArgs<T> &a);
 template <typename T>
 hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev = LaunchEv{});
+// The fused HS step on a DIA layout (a.x unused, a.y = s, a.part the
+// p_new.s partials).
+template <typename T>
+hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
+                             const LaunchEv &ev = LaunchEv{});
 
 // ------------------------------------------------------------- vectors
 // All launchers are graph-capturable (no sync, no allocation).

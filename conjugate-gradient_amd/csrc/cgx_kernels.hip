@@ -196,6 +196,7 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
       st->tol2bb = st->tol * st->tol * sa;
       st->k = 0;
       st->k_x = 0;
+      st->k_u = -1;  // fused step: no previous iteration yet
       st->done = 0;
       break;
     case FIN_HS_ALPHA:
@@ -624,6 +625,159 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
     if (r + 1 < a.n) dot = dot + (double)xr.y * (double)a1;
   }
   if (EPI) epi_store<4>(dot, a.part, a.fin);
+}
+
+// ------------------------------------------------- fused HS step (DIA-VI)
+// The scalar step at the top of a fused launch -- the folded k_xpay_xf's
+// logic (cg.c:125-129): r.r of the last r-update (k_update_rf's canonical
+// last-arriver sum, st->rr_new), the stop test, beta; every thread computes
+// it from the same state, workgroup 0 publishes.  A kernel never writes a
+// state field its own workgroups read; the stop flag follows the folded
+// path's protocol (1 here, 2 by the next k_update_rf).
+struct FuseStep {
+  bool first, stop;
+  double alpha, beta;
+};
+
+__device__ __forceinline__ FuseStep fuse_step(CgState *st, double *hist) {
+  FuseStep f;
+  const int k = st->k_u;
+  f.first = k < 0;
+  f.alpha = st->alpha;
+  f.beta = 0.0;
+  f.stop = false;
+  if (!f.first) {
+    const double rr_new = st->rr_new;
+    f.stop = k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb);
+    f.beta = rr_new / st->rr_u;  // cg.c:129
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (k < st->hist_cap) hist[k] = rr_new;
+      if (f.stop) {
+        st->k = k;
+        st->done = 1;
+      } else {
+        st->beta = f.beta;
+        st->rr = rr_new;
+        st->rr_x = rr_new;
+        st->k = k + 1;
+        st->k_x = k + 1;
+      }
+    }
+  }
+  return f;
+}
+
+// p_new = r + beta p_old (cg.c:131-132), two roundings as the reference
+template <typename T>
+__device__ __forceinline__ typename Pair<T>::type p_next(typename Pair<T>::type r,
+                                                         typename Pair<T>::type p, T beta) {
+  typename Pair<T>::type o;
+  const T b0 = beta * p.x, b1 = beta * p.y;
+  o.x = r.x + b0;
+  o.y = r.y + b1;
+  return o;
+}
+
+// k_spmv_dia's shape (two rows per thread, 512-row slice per workgroup)
+// with the previous iteration's vector update fused in.  p_new of the slice
+// and of its halo rows [s0 - hl, s0 + 512 + hr) is computed ONCE per
+// workgroup into an LDS window (NF pair passes per thread): every diagonal
+// with |d| <= kHaloMax reads p_new from there; the NFAR outermost diagonals
+// on each side (the +-nx*ny planes of a 3-D stencil) gather r and p_old and
+// compute p_new themselves.  Then x += alpha p_old and p_new for the own
+// rows, s = A p_new (the CSR row's order), the p_new.s partial.  Every value
+// is the unfused path's (same roundings): x and the r.r history are
+// bit-identical to SpMV + k_update_rf + k_xpay_xf.
+template <typename T, int NF, int NFAR, bool NT, bool LIST>
+__global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  T *win = reinterpret_cast<T *>(dyn_lds);
+  __shared__ T lv[8 * 16];
+  typedef typename Pair<T>::type P;
+  const int t = threadIdx.x;
+  const int wi = xcd_block();
+  const int s = LIST ? a.items.list[wi] : a.items.first + wi;
+  if (f.st->done > 1) return;  // uniform
+  const FuseStep fs = fuse_step(f.st, f.hist);
+  const T alpha = (T)fs.alpha, beta = (T)fs.beta;
+  const int s0 = s * kDiaSliceRows, r = s0 + 2 * t;
+  const int rs = r < a.n ? r : 0;
+  const P po = ld_pair(f.pold, rs), xo = ld_pair(f.x, rs);
+  if (fs.stop) {  // the stop iteration's x update only (cg.c:115-116, then the cg.c:125 break)
+    if (!fs.first && r < a.n) {
+      const T a0 = alpha * po.x, a1 = alpha * po.y;
+      st_pair(f.x, r, a.n, xo.x + a0, xo.y + a1, false);
+    }
+    return;
+  }
+  const uint2 cw = *reinterpret_cast<const uint2 *>(a.dcode + r);
+  const unsigned c0 = cw.x, c1 = cw.y;
+  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
+  // far diagonals: k = 0..NFAR-1 and ndiag-NFAR..ndiag-1 (ascending offsets)
+  P rf[2 * NFAR + 1], pf[2 * NFAR + 1];
+#pragma unroll
+  for (int q = 0; q < 2 * NFAR; ++q) {
+    const int k = q < NFAR ? q : a.ndiag - 2 * NFAR + q;
+    const unsigned n0 = (c0 >> (4 * k)) & 15u, n1 = (c1 >> (4 * k)) & 15u;
+    const int b = n0 != 15u || n1 != 15u ? r + a.doff[k] : rs;
+    rf[q] = ld_pair(f.r, b);
+    pf[q] = ld_pair(f.pold, b);
+  }
+  // the window: p_new of rows w0 + i, i < wn (pairs; rows outside [0, ncols)
+  // are loaded from a clamped address and never read)
+  const int w0 = s0 - a.hl, wn = kDiaSliceRows + a.hl + a.hr;
+  P wr[NF], wp[NF];
+#pragma unroll
+  for (int q = 0; q < NF; ++q) {
+    const int j = min(max(w0 + 2 * t + q * 2 * 256, -1), a.ncols - 1);
+    wr[q] = ld_pair(f.r, j);
+    wp[q] = ld_pair(f.pold, j);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every load above is in flight before the first use
+#pragma unroll
+  for (int q = 0; q < NF; ++q) {
+    const int i = 2 * t + q * 2 * 256;
+    const P pn = fs.first ? wr[q] : p_next<T>(wr[q], wp[q], beta);
+    if (i < wn) win[i] = pn.x;
+    if (i + 1 < wn) win[i + 1] = pn.y;
+  }
+  if (t < a.ndiag * 16) lv[t] = tv;
+  __syncthreads();
+  T a0 = T(0), a1 = T(0);
+  auto add = [&](int k, T v0, T v1) {
+    const unsigned n0 = (c0 >> (4 * k)) & 15u, n1 = (c1 >> (4 * k)) & 15u;
+    const T p0 = lv[k * 16 + n0] * v0, p1 = lv[k * 16 + n1] * v1;
+    a0 = n0 != 15u ? a0 + p0 : a0;
+    a1 = n1 != 15u ? a1 + p1 : a1;
+  };
+#pragma unroll
+  for (int q = 0; q < NFAR; ++q) {
+    const P pk = fs.first ? rf[q] : p_next<T>(rf[q], pf[q], beta);
+    add(q, pk.x, pk.y);
+  }
+  const int rw = r - w0;
+  for (int k = NFAR; k < a.ndiag - NFAR; ++k) {
+    const int i = rw + a.doff[k];
+    add(k, win[i], win[i + 1]);
+  }
+#pragma unroll
+  for (int q = NFAR; q < 2 * NFAR; ++q) {
+    const P pk = fs.first ? rf[q] : p_next<T>(rf[q], pf[q], beta);
+    add(a.ndiag - 2 * NFAR + q, pk.x, pk.y);
+  }
+  const T pn0 = win[rw], pn1 = win[rw + 1];
+  st_pair(a.y, r, a.n, a0, a1, NT);
+  double dot = 0.0;
+  if (r < a.n) {
+    st_pair(f.pnew, r, a.n, pn0, pn1, false);
+    if (!fs.first) {
+      const T x0 = alpha * po.x, x1 = alpha * po.y;
+      st_pair(f.x, r, a.n, xo.x + x0, xo.y + x1, false);
+    }
+    dot = (double)pn0 * (double)a0;
+    if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
+  }
+  epi_store<4>(dot, a.part, a.fin);
 }
 
 // -------------------------------------------------------------- k_stencil
@@ -1522,6 +1676,47 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev)
   return launch_spmv_en<T, false, false>(a, g, st, ev);
 }
 
+template <typename T, int NF, int NFAR>
+static const void *fused_kernel(bool nt, bool list) {
+  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false>))
+            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false>));
+}
+
+template <typename T>
+hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
+                             const LaunchEv &ev) {
+  const int g = spmv_grid(a);
+  if (g <= 0) return hipSuccess;
+  if (a.layout != L_DIA || a.ndiag > 8) return hipErrorInvalidValue;
+  const int wn = kDiaSliceRows + a.hl + a.hr;
+  const int nf = (wn + 511) / 512;
+  const int nfar = a.ndiag - __builtin_popcount(a.near & ((1u << a.ndiag) - 1));
+  if (nfar % 2 || nfar > 4 || nf > 5) return hipErrorInvalidValue;
+  const bool nt = a.nt != 0, l = a.items.list != nullptr;
+  const void *k = nullptr;
+  switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + nfar / 2) {
+    case 20: k = fused_kernel<T, 2, 0>(nt, l); break;
+    case 21: k = fused_kernel<T, 2, 1>(nt, l); break;
+    case 22: k = fused_kernel<T, 2, 2>(nt, l); break;
+    case 30: k = fused_kernel<T, 3, 0>(nt, l); break;
+    case 31: k = fused_kernel<T, 3, 1>(nt, l); break;
+    case 32: k = fused_kernel<T, 3, 2>(nt, l); break;
+    case 50: k = fused_kernel<T, 5, 0>(nt, l); break;
+    case 51: k = fused_kernel<T, 5, 1>(nt, l); break;
+    case 52: k = fused_kernel<T, 5, 2>(nt, l); break;
+    default: return hipErrorInvalidValue;
+  }
+  void *args[] = {(void *)&a, (void *)&f};
+  const size_t lds = (size_t)wn * sizeof(T) + 16;
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256), args, lds, st, ev.start, ev.stop, 0);
+  else
+    (void)hipLaunchKernel(k, dim3(g), dim3(256), args, lds, st);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_init_hs(int n, const T *b, T *x, T *r, T *p, double *part, int grid,
                           hipStream_t st) {
@@ -1661,6 +1856,8 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
 #define CGX_INSTANTIATE(T)                                                                       \
   template int spmv_grid<T>(const SpmvArgs<T> &);                                                \
   template hipError_t launch_spmv<T>(const SpmvArgs<T> &, hipStream_t, const LaunchEv &);      \
+  template hipError_t launch_spmv_fused<T>(const SpmvArgs<T> &, const FuseArgs<T> &, hipStream_t, \
+                                           const LaunchEv &);                                    \
   template hipError_t launch_init_hs<T>(int, const T *, T *, T *, T *, double *, int,            \
                                         hipStream_t);                                            \
   template hipError_t launch_init_cg1<T>(int, const T *, T *, T *, T *, T *, double *, int,      \

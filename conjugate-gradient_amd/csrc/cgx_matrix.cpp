@@ -653,6 +653,22 @@ int DevMatrix::items() const {
 
 int DevMatrix::padded_rows() const { return padded_rows_for(n); }
 
+bool DevMatrix::fusable() const {
+  if (layout != L_DIA || dia.ndiag > 8) return false;
+  int lfar = 0, rfar = 0;
+  for (int k = 0; k < dia.ndiag; ++k) {
+    if (k > 0 && dia.doff[k] <= dia.doff[k - 1]) return false;  // ascending
+    if (dia.doff[k] < -kHaloMax) {
+      if (k != lfar) return false;  // far ones outermost
+      ++lfar;
+    }
+  }
+  for (int k = dia.ndiag - 1; k >= 0 && dia.doff[k] > kHaloMax; --k) ++rfar;
+  for (int k = lfar; k < dia.ndiag - rfar; ++k)
+    if (std::abs(dia.doff[k]) > kHaloMax) return false;
+  return lfar == rfar && lfar <= 2 && dia.ndiag > 2 * lfar;
+}
+
 std::vector<int> DevMatrix::item_rows() const {
   if (layout == L_CSR || layout == L_DC) return blk_row;
   std::vector<int> r;
@@ -706,6 +722,15 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
   a.kdiag = kdiag;
   for (int k = 0; k < kDiaMax; ++k) a.doff[k] = dia.doff[k];
   a.ncols = ncols;
+  a.near = 0;
+  a.hl = a.hr = 0;
+  for (int k = 0; k < dia.ndiag; ++k)
+    if (std::abs(dia.doff[k]) <= kHaloMax) {
+      a.near |= 1u << k;
+      a.hl = std::max(a.hl, -dia.doff[k]);
+      a.hr = std::max(a.hr, dia.doff[k]);
+    }
+  a.hl = (a.hl + 1) & ~1;  // an even window start: aligned pair loads
   a.n = n;
   a.lap = lap;
   if (layout == L_STENCIL) {

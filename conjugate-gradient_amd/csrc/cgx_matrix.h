@@ -74,6 +74,10 @@ struct DevMatrix {
   int items() const;  // work items of the layout (blocks or slices)
   // host: first row of each item, items() + 1 entries
   std::vector<int> item_rows() const;
+  // The fused HS step applies (DIA, <= 8 diagonals in ascending offset
+  // order, the diagonals with |d| > kHaloMax the outermost ones and as many
+  // on each side, at most 2): k_spmv_dia_h's window and far diagonals.
+  bool fusable() const;
   // rows covered by the items (DIA pads to whole 512-row slices)
   int padded_rows() const;
   // algorithmic HBM bytes of one SpMV in the layout it runs on

@@ -123,6 +123,10 @@ struct cgx_solver {
   bool use_graph = true;
   void *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
        *d_w = nullptr;
+  void *d_p2 = nullptr;  // fused step: the second p buffer (p_old / p_new alternate)
+  int pbuf = 0;          // fused step: which buffer holds p_old (0: d_p)
+  bool fuse = true;      // cgx_solver_set_fused
+  unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
   int part_cap = 0;
   CgState *d_st = nullptr, *h_st = nullptr;
@@ -131,8 +135,8 @@ struct cgx_solver {
   size_t vec_bytes = 0;
   bool have_matrix = false, have_rhs = false, bench_ready = false;
   int last_iters = 0;
-  hipGraphExec_t gexec = nullptr;   // graph_batch iterations
-  hipGraphExec_t gexec1 = nullptr;  // one iteration (remainders)
+  hipGraphExec_t gexec[2] = {};   // graph_batch iterations, per p-buffer parity
+  hipGraphExec_t gexec1[2] = {};  // one iteration (remainders), per parity
   int gexec_key = -1;
   std::vector<hipEvent_t> events;
 };
@@ -144,10 +148,17 @@ using namespace cgx;
 size_t tsize(int dtype) { return dtype == CGX_F32 ? 4 : 8; }
 
 void drop_graph(cgx_solver *s) {
-  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-  if (s->gexec1) (void)hipGraphExecDestroy(s->gexec1);
-  s->gexec = s->gexec1 = nullptr;
+  for (int q = 0; q < 2; ++q) {
+    if (s->gexec[q]) (void)hipGraphExecDestroy(s->gexec[q]);
+    if (s->gexec1[q]) (void)hipGraphExecDestroy(s->gexec1[q]);
+    s->gexec[q] = s->gexec1[q] = nullptr;
+  }
   s->gexec_key = -1;
+}
+
+// The fused HS step applies: fast mode, HS, a fusable DIA layout.
+bool fused(const cgx_solver *s) {
+  return s->fuse && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST && s->A.fusable();
 }
 
 void free_system(cgx_solver *s) {
@@ -159,6 +170,7 @@ void free_system(cgx_solver *s) {
   dev_free(&s->d_p);
   dev_free(&s->d_s);
   dev_free(&s->d_w);
+  dev_free(&s->d_p2);
   dev_free(&s->d_pa);
   dev_free(&s->d_pb);
   dev_free(&s->d_hist);
@@ -178,6 +190,7 @@ int alloc_vectors(cgx_solver *s) {
   if ((rc = dev_alloc(&s->d_b, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_x, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_r, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_p, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_s, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_w, nv, &s->vec_bytes)) ||
+      (rc = dev_alloc(&s->d_p2, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pa, (size_t)s->part_cap * 8, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pb, (size_t)s->part_cap * 8, &s->vec_bytes))) {
     free_system(s);
@@ -186,6 +199,7 @@ int alloc_vectors(cgx_solver *s) {
   // padding entries stay 0 (16-B vector loads read them)
   CGX_HIP(hipMemsetAsync(s->d_x, 0, nv, s->stream));
   CGX_HIP(hipMemsetAsync(s->d_p, 0, nv, s->stream));
+  CGX_HIP(hipMemsetAsync(s->d_p2, 0, nv, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
   s->have_matrix = true;
   return 0;
@@ -224,6 +238,7 @@ int enqueue_init(cgx_solver *s) {
   hipStream_t st = s->stream;
   const int n = s->A.n;
   T *b = (T *)s->d_b, *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p;
+  s->pbuf = 0;  // the prologue writes p into d_p
   if (s->alg == CGX_ALG_HS) {
     if (s->mode == CGX_MODE_EXACT) {
       CGX_HIP(launch_init_hs<T>(n, b, x, r, p, nullptr, s->vec_grid, st));
@@ -251,6 +266,22 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = s->A.n;
   T *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p, *sv = (T *)s->d_s, *w = (T *)s->d_w;
   int np = 0;
+  if (fused(s)) {
+    // k_spmv_dia_h: the previous x / p update + s = A p_new (+ p_new.s
+    // partials); k_update_rf: alpha, r -= alpha s, r.r partials and their
+    // canonical sum (last workgroup) into st->rr_new for the next step
+    // (cg.c:111-132)
+    T *pold = (T *)(s->pbuf ? s->d_p2 : s->d_p), *pnew = (T *)(s->pbuf ? s->d_p : s->d_p2);
+    const SpmvArgs<T> a = s->A.args<T>(nullptr, sv, s->d_pa, &s->d_st->done, s->A.all_items());
+    const FuseArgs<T> f{x, pold, pnew, r, s->d_st, s->d_hist};
+    np = s->A.partials(s->A.all_items());
+    CGX_HIP(launch_spmv_fused<T>(a, f, st, LaunchEv{ev0, ev1}));
+    const int gf = s->vec_grid / 4;
+    const FinArgs fin{s->d_tick, s->d_pb, 4 * gf, nullptr, 0, &s->d_st->rr_new};
+    CGX_HIP(launch_update_rf<T>(n, r, sv, s->d_st, s->d_pa, np, s->d_pb, gf, st, &fin));
+    s->pbuf ^= 1;
+    return 0;
+  }
   if (s->alg == CGX_ALG_HS) {
     const bool exact = s->mode == CGX_MODE_EXACT;
     CGX_HIP(s->A.spmv<T>(p, sv, exact ? nullptr : s->d_pa, &s->d_st->done, s->A.all_items(), st,
@@ -280,12 +311,15 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
 }
 
 template <typename T>
-int capture_iters(cgx_solver *s, int count, hipGraphExec_t *out) {
+int capture_iters(cgx_solver *s, int count, int parity, hipGraphExec_t *out) {
   hipGraph_t g = nullptr;
+  const int saved = s->pbuf;
+  s->pbuf = parity;
   CGX_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
   int rc = 0;
   for (int i = 0; i < count && rc == 0; ++i) rc = enqueue_iter<T>(s, nullptr, nullptr);
   hipError_t e = hipStreamEndCapture(s->stream, &g);
+  s->pbuf = saved;
   if (rc) {
     if (g) (void)hipGraphDestroy(g);
     return rc;
@@ -298,14 +332,19 @@ int capture_iters(cgx_solver *s, int count, hipGraphExec_t *out) {
 }
 
 // The replayed graphs of the current mode / recurrence: graph_batch
-// iterations and one iteration (remainders), captured (not run) once.
+// iterations and one iteration (remainders), captured (not run) once -- for
+// both p-buffer parities when the fused step alternates them.
 template <typename T>
 int ensure_graphs(cgx_solver *s) {
-  const int key = s->alg * 2 + s->mode;
-  if (s->gexec && s->gexec1 && s->gexec_key == key) return 0;
+  const int key = s->alg * 4 + s->mode * 2 + (fused(s) ? 1 : 0);
+  const int nq = fused(s) ? 2 : 1;
+  if (s->gexec_key == key) return 0;
   drop_graph(s);
-  int rc = capture_iters<T>(s, s->graph_batch, &s->gexec);
-  if (rc == 0) rc = capture_iters<T>(s, 1, &s->gexec1);
+  int rc = 0;
+  for (int q = 0; q < nq && rc == 0; ++q) {
+    rc = capture_iters<T>(s, s->graph_batch, q, &s->gexec[q]);
+    if (rc == 0) rc = capture_iters<T>(s, 1, q, &s->gexec1[q]);
+  }
   if (rc) {
     drop_graph(s);
     return rc;
@@ -319,9 +358,15 @@ int enqueue_iters(cgx_solver *s, long long count) {
   if (s->use_graph && count > 0) {
     int rc = ensure_graphs<T>(s);
     if (rc) return rc;
-    for (; count >= s->graph_batch; count -= s->graph_batch)
-      CGX_HIP(hipGraphLaunch(s->gexec, s->stream));
-    for (; count > 0; --count) CGX_HIP(hipGraphLaunch(s->gexec1, s->stream));
+    const bool alt = fused(s);  // an even batch keeps the p parity, one iteration flips it
+    for (; count >= s->graph_batch; count -= s->graph_batch) {
+      CGX_HIP(hipGraphLaunch(s->gexec[alt ? s->pbuf : 0], s->stream));
+      if (alt && (s->graph_batch & 1)) s->pbuf ^= 1;
+    }
+    for (; count > 0; --count) {
+      CGX_HIP(hipGraphLaunch(s->gexec1[alt ? s->pbuf : 0], s->stream));
+      if (alt) s->pbuf ^= 1;
+    }
     return 0;
   }
   for (long long i = 0; i < count; ++i) {
@@ -367,6 +412,7 @@ int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
   s->h_st->max_iter = maxit;
   s->h_st->hist_cap = std::min(hist_cap, s->hist_alloc);
   CGX_HIP(hipMemcpyAsync(s->d_st, s->h_st, sizeof(CgState), hipMemcpyHostToDevice, s->stream));
+  CGX_HIP(hipMemsetAsync(s->d_tick, 0, 16, s->stream));
   return 0;
 }
 
@@ -382,7 +428,9 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
   s->bench_ready = false;
   if ((rc = prepare_state(s, maxit, tol, maxit + 1))) return rc;
   if ((rc = enqueue_init<T>(s))) return rc;
-  const long long total = (long long)maxit + 1;
+  // the fused step does an iteration's x update in the next launch: one
+  // more step carries the last one (and finds the stop)
+  const long long total = (long long)maxit + 1 + (fused(s) ? 1 : 0);
   if (tol <= 0.0) {
     if ((rc = enqueue_iters<T>(s, total))) return rc;
     if ((rc = read_state(s))) return rc;
@@ -574,6 +622,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->A.device = device;
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
+      hipMalloc((void **)&s->d_tick, 16) != hipSuccess || hipMemset(s->d_tick, 0, 16) != hipSuccess ||
       hipHostMalloc((void **)&s->h_st, sizeof(CgState), hipHostMallocDefault) != hipSuccess) {
     cgx::set_error("cgx_solver_create: stream/state allocation failed");
     cgx_solver_destroy(s);
@@ -591,6 +640,7 @@ void cgx_solver_destroy(cgx_solver *s) {
   free_system(s);
   for (hipEvent_t e : s->events) (void)hipEventDestroy(e);
   if (s->d_st) (void)hipFree(s->d_st);
+  if (s->d_tick) (void)hipFree(s->d_tick);
   if (s->h_st) (void)hipHostFree(s->h_st);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
@@ -608,6 +658,13 @@ int cgx_solver_set_mode(cgx_solver *s, int mode, int alg) {
   }
   s->mode = mode;
   s->alg = alg;
+  drop_graph(s);
+  return 0;
+}
+
+int cgx_solver_set_fused(cgx_solver *s, int on) {
+  if (!s) return CGX_EINVAL;
+  s->fuse = on != 0;
   drop_graph(s);
   return 0;
 }
@@ -747,6 +804,9 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->spmv_bytes = A.csr_bytes();
   info->iter_bytes = info->spmv_bytes + 9.0 * A.n * sv;
   info->spmv_iter_bytes = A.layout_bytes();
+  // the fused step also reads r, p_old, x and writes x, p_new (p read once
+  // through the window: the SpMV's own p read becomes the r / p_old reads)
+  if (s->have_matrix && fused(s)) info->spmv_iter_bytes += 4.0 * A.n * sv;
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;
@@ -758,6 +818,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->setup_host_ms = A.setup_host_ms;
   info->setup_device_ms = A.setup_dev_ms;
   info->encode_fallback = A.encode_fallback;
+  info->fused = s->have_matrix && fused(s) ? 1 : 0;
   return 0;
 }
 

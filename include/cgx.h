@@ -134,7 +134,8 @@ typedef struct {
   double spmv_iter_bytes; /* algorithmic bytes of one SpMV in the layout it
                              runs on (DIA: codes + x + y; DC: codes + values
                              + row lengths + x + y; PANEL: + P row_ptrs and
-                             y round trips)                                 */
+                             y round trips; fused HS step: + r, p_old, x
+                             read, x, p_new written, 4 n vectors net)                                 */
   size_t device_bytes;  /* device memory held by the solver                  */
   int n_panels;         /* column panels of the SpMV (1: none)               */
   int n_dict;           /* DC: distinct col - row offsets; DIA: diagonals;
@@ -149,11 +150,20 @@ typedef struct {
   double setup_device_ms; /* set_matrix: device time after the last submit  */
   int n_values;         /* DIA: values over all diagonal tables             */
   int gathers_per_chunk; /* CSR / DC: x gathers issued per row chunk (7|8)  */
+  int fused;            /* 1: the HS iteration runs fused (cgx_solver_set_fused) */
 } cgx_info;
 
 int  cgx_solver_create(int device, cgx_solver **out);
 void cgx_solver_destroy(cgx_solver *s);
 int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
+/* The HS iteration in fast mode on a DIA layout with <= 8 diagonals fuses
+ * the vector update into the SpMV (default on): one launch does the
+ * previous iteration's x += alpha p and p = r + beta p (cg.c:115-116,
+ * 131-132) -- p of its rows and their in-plane halo computed once into an
+ * LDS window -- then s = A p; the next launch updates r (cg.c:118-123).
+ * Two launches per iteration instead of three, 8 B per row less traffic;
+ * x and the r.r history are bit-identical to the unfused path (on = 0). */
+int  cgx_solver_set_fused(cgx_solver *s, int on);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);
 /* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.

@@ -553,6 +553,84 @@ def test_graph_and_eager_agree():
     assert np.all(np.isfinite(out[0]))
 
 
+def band_sym_rhs(n, offsets, seed):
+    """Symmetric banded matrix on the diagonals +-offsets (and 0), a few
+    distinct values per diagonal, strictly diagonally dominant."""
+    rng = np.random.default_rng(seed)
+    rows, cols, vals = [], [], []
+    dsum = np.zeros(n)
+    for d in offsets:
+        i = np.arange(n - d)
+        v = -rng.choice([0.25, 0.5, 0.75, 1.0], size=n - d)
+        for rr, cc in ((i, i + d), (i + d, i)):
+            rows.append(rr)
+            cols.append(cc)
+            vals.append(v)
+            np.add.at(dsum, rr, np.abs(v))
+    rows.append(np.arange(n))
+    cols.append(np.arange(n))
+    vals.append(np.ceil(dsum) + 1.0)
+    r, c, v = (np.concatenate(a) for a in (rows, cols, vals))
+    o = np.lexsort((c, r))
+    r, c, v = r[o], c[o], v[o]
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, r + 1, 1)
+    return (np.cumsum(rp).astype(np.int32), c.astype(np.int32), v.astype(np.float64),
+            rng.standard_normal(n))
+
+
+def fused_cases():
+    yield "lap3d_24x20x17", (*H.laplacian3d(24, 20, 17), None), True   # all near, NF 2
+    yield "lap3d_40x30x9", (*H.laplacian3d(40, 30, 9), None), True     # +-1200 far, NF 3
+    yield "band_1_37", band_sym_rhs(9001, [1, 37], 3), True              # odd halo (rounded)
+    yield "band_far2", band_sym_rhs(20000, [1, 1100, 2100], 4), True    # 2 far a side
+    yield "band_wide", band_sym_rhs(20000, [1, 1000, 1500], 7), True    # NF 5, 1 far a side
+    yield "band_one_far", band_sym_rhs(20000, [1, 1500], 5), True        # near + 1 far a side
+    yield "band_9", band_sym_rhs(8000, [1, 2, 3, 4, 5], 6), False        # 11 diagonals: unfused
+
+
+@pytest.mark.parametrize("case", list(fused_cases()), ids=lambda c: c[0])
+def test_fused_step_bit_identical_to_unfused(case):
+    """The fused HS step (k_spmv_dia_h: x / p update + s = A p in one
+    launch, p_new of the slice and its halo in LDS) computes every value
+    of the unfused SpMV + k_update_rf + k_xpay_xf sequence with the same
+    roundings: x, the iteration count and the r.r history are bit-identical
+    (maxit 0 / 1 / even / odd batch remainders, a tolerance stop, graph and
+    eager replays in bench_run)."""
+    _, (rp, col, val, b), fusable = case
+    n = len(rp) - 1
+    if b is None:
+        b = np.random.default_rng(9).standard_normal(n)
+    out = {}
+    for fused in (True, False):
+        res = []
+        with cgx.Solver(0, layout="dia", fused=fused) as s:
+            s.set_matrix(rp, col, val)
+            info = s.info()
+            assert info["layout_name"] == "dia"
+            assert info["fused"] == (1 if fused and fusable else 0)
+            for maxit, tol in [(0, 0.0), (1, 0.0), (16, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-9)]:
+                s.set_rhs(b)
+                its = s.run(maxit, tol)
+                res.append((its, s.x(), s.history(its)))
+            # bench_run: a fused step applies the previous iteration's x
+            # update, so 34 fused steps hold x of 33 iterations
+            for graph in (True, False):
+                s.set_rhs(b)
+                s.bench_prepare(0)
+                s.bench_run(34 if fused and fusable else 33, graph=graph)
+                res.append((33, s.x(), None))
+        out[fused] = res
+    for j, ((i0, x0, h0), (i1, x1, h1)) in enumerate(zip(out[True], out[False])):
+        assert i0 == i1, j
+        assert H.same_bits_or_both_nan(x0, x1), j
+        if h0 is not None:
+            assert H.same_bits_or_both_nan(h0, h1), j
+    its, x, _ = out[True][5]
+    assert its < 3000
+    assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 1.01e-9 * np.linalg.norm(b)
+
+
 @pytest.mark.parametrize("name", ["lap2d_32", "lap3d_12", "rand_spd_2000", "dense128"])
 def test_cg1_within_tolerance(name):
     g = H.load_golden(name)
