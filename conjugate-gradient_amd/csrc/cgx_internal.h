@@ -76,8 +76,11 @@ struct CgState {
   // canonical sum of its r.r partials here; k_u = -1 after the prologue
   // marks "no previous iteration" (p = r, no x update)
   double rr_new;
+  // fused step: alpha of an even iteration whose x update is deferred to the
+  // next (odd) one -- written by the launch that defers it
+  double alpha_def;
 };
-static_assert(sizeof(CgState) == 120, "CgState layout");
+static_assert(sizeof(CgState) == 128, "CgState layout");
 
 // Finalize ops (single-workgroup scalar steps of the recurrence).
 enum FinOp {
@@ -218,10 +221,11 @@ struct SpmvArgs {
 };
 
 // The fused HS step (single GPU, DIA layout): one launch does the previous
-// iteration's x += alpha p_old and p_new = r + beta p_old (beta and the stop
-// test from CgState; cg.c:115-116, 125-132), then s = A p_new with the
-// p_new.s partials.  p is double-buffered (the launch reads p_old while it
-// stores p_new).
+// iteration's p_new = r + beta p_old (beta and the stop test from CgState;
+// cg.c:125-132) and, every other launch, x += alpha p for two iterations
+// (cg.c:115-116), then s = A p_new with the p_new.s partials.  p is
+// double-buffered (the launch reads p_old while it stores p_new; the p_new
+// buffer holds p_{k-1} until then).
 template <typename T>
 struct FuseArgs {
   T *x;

@@ -684,8 +684,10 @@ __device__ __forceinline__ typename Pair<T>::type p_next(typename Pair<T>::type 
 // workgroup into an LDS window (NF pair passes per thread): every diagonal
 // with |d| <= kHaloMax reads p_new from there; the NFAR outermost diagonals
 // on each side (the +-nx*ny planes of a 3-D stencil) gather r and p_old and
-// compute p_new themselves.  Then x += alpha p_old and p_new for the own
-// rows, s = A p_new (the CSR row's order), the p_new.s partial.  Every value
+// compute p_new themselves.  Then p_new for the own rows (and every other
+// launch x, below), s = A p_new (the CSR row's order), the p_new.s partial.
+// Bytes per row: 4 code + 8 r + 8 p_old + 8 p_new + 8 s, + 24 (x read and
+// written, p_{k-1} read) every other launch: 48 on average.  Every value
 // is the unfused path's (same roundings): x and the r.r history are
 // bit-identical to SpMV + k_update_rf + k_xpay_xf.
 template <typename T, int NF, int NFAR, bool NT, bool LIST>
@@ -702,12 +704,33 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   const T alpha = (T)fs.alpha, beta = (T)fs.beta;
   const int s0 = s * kDiaSliceRows, r = s0 + 2 * t;
   const int rs = r < a.n ? r : 0;
-  const P po = ld_pair(f.pold, rs), xo = ld_pair(f.x, rs);
-  if (fs.stop) {  // the stop iteration's x update only (cg.c:115-116, then the cg.c:125 break)
-    if (!fs.first && r < a.n) {
-      const T a0 = alpha * po.x, a1 = alpha * po.y;
-      st_pair(f.x, r, a.n, xo.x + a0, xo.y + a1, false);
+  // x (cg.c:115-116) is updated every other iteration: an even iteration k
+  // defers x += alpha_k p_k, the odd k + 1 applies both terms in order (the
+  // same two roundings each), reading p_k from the p_new buffer before it is
+  // overwritten; a stop applies whatever is pending.
+  const int k = f.st->k_u;
+  const bool odd = (k & 1) != 0;
+  const bool xup = !fs.first && (odd || fs.stop);
+  const T alpha_d = (T)f.st->alpha_def;
+  if (!fs.first && !odd && !fs.stop && blockIdx.x == 0 && t == 0) f.st->alpha_def = fs.alpha;
+  P po = P(), xo = P(), pd = P();
+  if (xup) {
+    po = ld_pair(f.pold, rs);
+    xo = ld_pair(f.x, rs);
+    if (odd) pd = ld_pair((const T *)f.pnew, rs);
+  }
+  auto x_update = [&]() {
+    T x0 = xo.x, x1 = xo.y;
+    if (odd) {
+      const T d0 = alpha_d * pd.x, d1 = alpha_d * pd.y;
+      x0 = x0 + d0;
+      x1 = x1 + d1;
     }
+    const T a0 = alpha * po.x, a1 = alpha * po.y;
+    st_pair(f.x, r, a.n, x0 + a0, x1 + a1, false);
+  };
+  if (fs.stop) {  // the pending x updates only (then the cg.c:125 break)
+    if (xup && r < a.n) x_update();
     return;
   }
   const uint2 cw = *reinterpret_cast<const uint2 *>(a.dcode + r);
@@ -770,10 +793,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   double dot = 0.0;
   if (r < a.n) {
     st_pair(f.pnew, r, a.n, pn0, pn1, false);
-    if (!fs.first) {
-      const T x0 = alpha * po.x, x1 = alpha * po.y;
-      st_pair(f.x, r, a.n, xo.x + x0, xo.y + x1, false);
-    }
+    if (xup) x_update();
     dot = (double)pn0 * (double)a0;
     if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
   }

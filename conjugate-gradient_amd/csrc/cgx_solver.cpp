@@ -804,9 +804,10 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->spmv_bytes = A.csr_bytes();
   info->iter_bytes = info->spmv_bytes + 9.0 * A.n * sv;
   info->spmv_iter_bytes = A.layout_bytes();
-  // the fused step also reads r, p_old, x and writes x, p_new (p read once
-  // through the window: the SpMV's own p read becomes the r / p_old reads)
-  if (s->have_matrix && fused(s)) info->spmv_iter_bytes += 4.0 * A.n * sv;
+  // the fused step also reads r, p_old and writes p_new (the SpMV's own p
+  // read becomes the r / p_old reads: +2 vectors); every other launch reads
+  // x and p_{k-1}, writes x (+3 / 2): the average launch, +3.5 n vectors
+  if (s->have_matrix && fused(s)) info->spmv_iter_bytes += 3.5 * A.n * sv;
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;

@@ -134,8 +134,10 @@ typedef struct {
   double spmv_iter_bytes; /* algorithmic bytes of one SpMV in the layout it
                              runs on (DIA: codes + x + y; DC: codes + values
                              + row lengths + x + y; PANEL: + P row_ptrs and
-                             y round trips; fused HS step: + r, p_old, x
-                             read, x, p_new written, 4 n vectors net)                                 */
+                             y round trips; fused HS step, average of its
+                             two launch parities: + r, p_old read, p_new
+                             written, x / p_{k-1} read and x written
+                             every other launch: + 3.5 n vectors)                                 */
   size_t device_bytes;  /* device memory held by the solver                  */
   int n_panels;         /* column panels of the SpMV (1: none)               */
   int n_dict;           /* DC: distinct col - row offsets; DIA: diagonals;
@@ -158,11 +160,12 @@ void cgx_solver_destroy(cgx_solver *s);
 int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
 /* The HS iteration in fast mode on a DIA layout with <= 8 diagonals fuses
  * the vector update into the SpMV (default on): one launch does the
- * previous iteration's x += alpha p and p = r + beta p (cg.c:115-116,
- * 131-132) -- p of its rows and their in-plane halo computed once into an
- * LDS window -- then s = A p; the next launch updates r (cg.c:118-123).
- * Two launches per iteration instead of three, 8 B per row less traffic;
- * x and the r.r history are bit-identical to the unfused path (on = 0). */
+ * previous iteration's p = r + beta p (cg.c:131-132) -- p of its rows and
+ * their in-plane halo computed once into an LDS window -- then s = A p; the
+ * next launch updates r (cg.c:118-123).  x += alpha p (cg.c:115-116) runs
+ * every other launch for two iterations (same roundings, in order).  Two
+ * launches per iteration instead of three, 16 B per row less traffic; x and
+ * the r.r history are bit-identical to the unfused path (on = 0). */
 int  cgx_solver_set_fused(cgx_solver *s, int on);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);

@@ -613,13 +613,14 @@ def test_fused_step_bit_identical_to_unfused(case):
                 s.set_rhs(b)
                 its = s.run(maxit, tol)
                 res.append((its, s.x(), s.history(its)))
-            # bench_run: a fused step applies the previous iteration's x
-            # update, so 34 fused steps hold x of 33 iterations
+            # bench_run: fused launch j >= 2 finishes iteration j - 2 and
+            # applies x updates in pairs (odd iterations), so 35 fused
+            # launches hold x of 34 iterations
             for graph in (True, False):
                 s.set_rhs(b)
                 s.bench_prepare(0)
-                s.bench_run(34 if fused and fusable else 33, graph=graph)
-                res.append((33, s.x(), None))
+                s.bench_run(35 if fused and fusable else 34, graph=graph)
+                res.append((34, s.x(), None))
         out[fused] = res
     for j, ((i0, x0, h0), (i1, x1, h1)) in enumerate(zip(out[True], out[False])):
         assert i0 == i1, j
