@@ -179,7 +179,16 @@ struct DiaCand {
   int ndiag;
   int doff[kDiaMax];
   int nval[kDiaMax];
+  // packed row codes: diagonal k's field is bits [csh[k], csh[k] + cbits[k])
+  // of the row's word, value indices 0..nval-1, all ones = no entry; the
+  // word is cbytes (1, 2, 4 or 8) bytes (dia_pack)
+  int cbits[kDiaMax];
+  int csh[kDiaMax];
+  int cbytes;
 };
+// Field widths and word size from nval: 1 bit for one value (a Laplacian's
+// diagonals), 2 for <= 3, 3 for <= 7, 4 for <= 15.
+void dia_pack(DiaCand &c);
 
 template <typename T>
 struct SpmvArgs {
@@ -204,7 +213,10 @@ struct SpmvArgs {
   int ndict_cap;
   int gath;               // CSR / DC: x gathers per row chunk (7 or 8)
   // DIA
-  const unsigned *dcode;  // row r: dword r (<= 8 diagonals) or dwords 2r, 2r+1
+  const unsigned char *dcode;  // row r: bytes [cb r, cb (r + 1)) (DiaCand)
+  int cb;                 // code bytes per row: 1, 2, 4, 8
+  int csh[kDiaMax];       // diagonal k's field: (word >> csh[k]) & cmask[k]
+  unsigned cmask[kDiaMax];  // == cmask[k]: no entry on diagonal k
   const T *vtab;          // [16][16] values, vtab[16 k + v]
   int ndiag;              // diagonals
   int kdiag;              // index of the main diagonal (offset 0), -1: none
@@ -319,7 +331,7 @@ hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dic
 // columns do not strictly ascend.
 template <typename T>
 hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, const T *val,
-                             const DiaCand &c, const T *vtab, unsigned *code, int *err,
+                             const DiaCand &c, const T *vtab, unsigned char *code, int *err,
                              hipStream_t st);
 
 int vec_grid_for(int n, int cus);

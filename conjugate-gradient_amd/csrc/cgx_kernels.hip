@@ -528,10 +528,11 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
 // Value-indexed diagonal codes (DIA-VI).  A matrix whose nonzeros lie on at
 // most 16 diagonals d_0 < ... < d_{K-1} (col - row), with at most 15
 // distinct values (bit patterns) per diagonal -- stencils, banded matrices
-// with few coefficients -- stores per row one nibble per diagonal: the index
-// of the entry's value in that diagonal's value table, 15 = no entry
-// (4 bytes per row for K <= 8, 8 for K <= 16), and no column or value
-// stream.  A row's entries ascend in column, i.e. in diagonal (checked by the
+// with few coefficients -- stores per row one bit field per diagonal: the
+// index of the entry's value in that diagonal's value table, all ones = no
+// entry; fields 1-4 bits wide by the diagonal's value count (a Laplacian:
+// one bit per diagonal, one byte per row), the row's word 1, 2, 4 or 8
+// bytes; no column or value stream.  A row's entries ascend in column, i.e. in diagonal (checked by the
 // encoder), so summing k = 0..K-1 adds the CSR row's products in its order:
 // y is bit-identical to k_spmv_csr.  Two rows per thread, r even: the
 // neighbours x[r + d_k], x[r + 1 + d_k] of both rows are ONE 16-byte (fp64)
@@ -571,9 +572,40 @@ __device__ __forceinline__ void st_pair(T *y, int r, int n, T a0, T a1, bool nt)
   }
 }
 
+// The code words of rows r, r + 1 (r even): one load of 2 cb bytes (cb is
+// uniform: a scalar branch).  C = unsigned holds words of <= 4 bytes.
+template <typename C>
+__device__ __forceinline__ void ld_codes(const unsigned char *code, int cb, int r, C &c0, C &c1) {
+  const unsigned char *p = code + (long long)r * cb;
+  if (cb == 1) {
+    const unsigned w = *reinterpret_cast<const unsigned short *>(p);
+    c0 = w & 0xffu;
+    c1 = w >> 8;
+  } else if (cb == 2) {
+    const unsigned w = *reinterpret_cast<const unsigned *>(p);
+    c0 = w & 0xffffu;
+    c1 = w >> 16;
+  } else if (sizeof(C) == 4 || cb == 4) {
+    const uint2 w = *reinterpret_cast<const uint2 *>(p);
+    c0 = w.x;
+    c1 = w.y;
+  } else {
+    const uint4 w = *reinterpret_cast<const uint4 *>(p);
+    c0 = (C)((unsigned long long)w.x | ((unsigned long long)w.y << 32));
+    c1 = (C)((unsigned long long)w.z | ((unsigned long long)w.w << 32));
+  }
+}
+
+// diagonal k's field of a code word
+template <typename T, typename C>
+__device__ __forceinline__ unsigned fld(const SpmvArgs<T> &a, C c, int k) {
+  return (unsigned)(c >> a.csh[k]) & a.cmask[k];
+}
+
 template <typename T, int KW, bool EPI, bool NT, bool LIST>
 __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
-  constexpr int KM = 8 * KW;  // diagonals a code word holds
+  constexpr int KM = 8 * KW;  // diagonals unrolled (<= 8: 32-bit words)
+  typedef typename std::conditional<KW == 1, unsigned, unsigned long long>::type C;
   __shared__ T lv[KM * 16];
   typedef typename Pair<T>::type P;
   const int t = threadIdx.x;
@@ -582,25 +614,17 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
   const int s = LIST ? a.items.list[wi] : a.items.first + wi;
   if (stop) return;  // uniform: every thread of the grid reads the same flag
   const int r = s * kDiaSliceRows + 2 * t;
-  const int rs = r < a.n ? r : 0;  // a row pair past the end (codes all 15) reloads x[0]
-  unsigned long long c0, c1;  // nibble k of row r / r + 1
-  if (KW == 1) {
-    const uint2 w = *reinterpret_cast<const uint2 *>(a.dcode + r);
-    c0 = w.x;
-    c1 = w.y;
-  } else {
-    const uint4 w = *reinterpret_cast<const uint4 *>(a.dcode + 2 * r);
-    c0 = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
-    c1 = (unsigned long long)w.z | ((unsigned long long)w.w << 32);
-  }
+  const int rs = r < a.n ? r : 0;  // a row pair past the end (no entries) reloads x[0]
+  C c0, c1;  // the code words of row r / r + 1
+  ld_codes(a.dcode, a.cb, r, c0, c1);
   const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
   P xv[KM];
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     // unconditional (a lane whose rows hold no entry on diagonal k reloads
     // its own x[r]): a conditional load makes the compiler wait on it
-    const unsigned n0 = (unsigned)(c0 >> (4 * k)) & 15u, n1 = (unsigned)(c1 >> (4 * k)) & 15u;
-    xv[k] = ld_pair(a.x, k < a.ndiag && (n0 != 15u || n1 != 15u) ? r + a.doff[k] : rs);
+    const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
+    xv[k] = ld_pair(a.x, k < a.ndiag && (n0 != a.cmask[k] || n1 != a.cmask[k]) ? r + a.doff[k] : rs);
   }
   // x[r], x[r+1] for the epilogue: a pair load of its own (picking the main
   // diagonal's registers costs the compiler 4x the VGPRs)
@@ -612,10 +636,10 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     if (k < a.ndiag) {
-      const unsigned n0 = (unsigned)(c0 >> (4 * k)) & 15u, n1 = (unsigned)(c1 >> (4 * k)) & 15u;
+      const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
       const T p0 = lv[k * 16 + n0] * xv[k].x, p1 = lv[k * 16 + n1] * xv[k].y;
-      a0 = n0 != 15u ? a0 + p0 : a0;
-      a1 = n1 != 15u ? a1 + p1 : a1;
+      a0 = n0 != a.cmask[k] ? a0 + p0 : a0;
+      a1 = n1 != a.cmask[k] ? a1 + p1 : a1;
     }
   }
   st_pair(a.y, r, a.n, a0, a1, NT);
@@ -694,7 +718,7 @@ template <typename T, int NF, int NFAR, bool NT, bool LIST>
 __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *win = reinterpret_cast<T *>(dyn_lds);
-  __shared__ T lv[8 * 16];
+  __shared__ T lv[kDiaMax * 16];
   typedef typename Pair<T>::type P;
   const int t = threadIdx.x;
   const int wi = xcd_block();
@@ -733,16 +757,16 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     if (xup && r < a.n) x_update();
     return;
   }
-  const uint2 cw = *reinterpret_cast<const uint2 *>(a.dcode + r);
-  const unsigned c0 = cw.x, c1 = cw.y;
+  unsigned c0, c1;  // the code words of row r / r + 1 (<= 4 bytes: fusable())
+  ld_codes(a.dcode, a.cb, r, c0, c1);
   const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
   // far diagonals: k = 0..NFAR-1 and ndiag-NFAR..ndiag-1 (ascending offsets)
   P rf[2 * NFAR + 1], pf[2 * NFAR + 1];
 #pragma unroll
   for (int q = 0; q < 2 * NFAR; ++q) {
     const int k = q < NFAR ? q : a.ndiag - 2 * NFAR + q;
-    const unsigned n0 = (c0 >> (4 * k)) & 15u, n1 = (c1 >> (4 * k)) & 15u;
-    const int b = n0 != 15u || n1 != 15u ? r + a.doff[k] : rs;
+    const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
+    const int b = n0 != a.cmask[k] || n1 != a.cmask[k] ? r + a.doff[k] : rs;
     rf[q] = ld_pair(f.r, b);
     pf[q] = ld_pair(f.pold, b);
   }
@@ -768,10 +792,10 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   __syncthreads();
   T a0 = T(0), a1 = T(0);
   auto add = [&](int k, T v0, T v1) {
-    const unsigned n0 = (c0 >> (4 * k)) & 15u, n1 = (c1 >> (4 * k)) & 15u;
+    const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
     const T p0 = lv[k * 16 + n0] * v0, p1 = lv[k * 16 + n1] * v1;
-    a0 = n0 != 15u ? a0 + p0 : a0;
-    a1 = n1 != 15u ? a1 + p1 : a1;
+    a0 = n0 != a.cmask[k] ? a0 + p0 : a0;
+    a1 = n1 != a.cmask[k] ? a1 + p1 : a1;
   };
 #pragma unroll
   for (int q = 0; q < NFAR; ++q) {
@@ -1543,12 +1567,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_dia_encode(int n, int npad, const int *__restrict__ rp,
                                                     const int *__restrict__ col,
                                                     const T *__restrict__ val, DiaCand c,
-                                                    const T *__restrict__ vtab, int kw,
-                                                    unsigned *__restrict__ code,
+                                                    const T *__restrict__ vtab,
+                                                    unsigned char *__restrict__ code,
                                                     int *__restrict__ err) {
   typedef typename Bits<T>::U U;
+  unsigned long long empty = 0;  // every field all ones: no entry
+  for (int q = 0; q < c.ndiag; ++q) empty |= ((1ull << c.cbits[q]) - 1ull) << c.csh[q];
   for (int r = blockIdx.x * 256 + threadIdx.x; r < npad; r += gridDim.x * 256) {
-    unsigned long long w = ~0ull;
+    unsigned long long w = empty;
     if (r < n) {
       int prev = -1;
       for (int k = rp[r]; k < rp[r + 1]; ++k) {
@@ -1567,15 +1593,16 @@ __global__ __launch_bounds__(256) void k_dia_encode(int n, int npad, const int *
           atomicOr(err, 1);
           break;
         }
-        w &= ~(15ull << (4 * q));
-        w |= (unsigned long long)v << (4 * q);
+        w &= ~(((1ull << c.cbits[q]) - 1ull) << c.csh[q]);
+        w |= (unsigned long long)v << c.csh[q];
       }
     }
-    if (kw == 1) {
-      code[r] = (unsigned)w;
-    } else {
-      code[2 * (long long)r] = (unsigned)w;
-      code[2 * (long long)r + 1] = (unsigned)(w >> 32);
+    unsigned char *p = code + (long long)r * c.cbytes;
+    switch (c.cbytes) {
+      case 1: *p = (unsigned char)w; break;
+      case 2: *reinterpret_cast<unsigned short *>(p) = (unsigned short)w; break;
+      case 4: *reinterpret_cast<unsigned *>(p) = (unsigned)w; break;
+      default: *reinterpret_cast<unsigned long long *>(p) = w; break;
     }
   }
 }
@@ -1709,7 +1736,7 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
                              const LaunchEv &ev) {
   const int g = spmv_grid(a);
   if (g <= 0) return hipSuccess;
-  if (a.layout != L_DIA || a.ndiag > 8) return hipErrorInvalidValue;
+  if (a.layout != L_DIA || a.cb > 4) return hipErrorInvalidValue;
   const int wn = kDiaSliceRows + a.hl + a.hr;
   const int nf = (wn + 511) / 512;
   const int nfar = a.ndiag - __builtin_popcount(a.near & ((1u << a.ndiag) - 1));
@@ -1864,12 +1891,12 @@ hipError_t launch_dc_encode(int n, const int *rp, const int *col, const int *dic
 
 template <typename T>
 hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, const T *val,
-                             const DiaCand &c, const T *vtab, unsigned *code, int *err,
+                             const DiaCand &c, const T *vtab, unsigned char *code, int *err,
                              hipStream_t st) {
   if (npad <= 0) return hipSuccess;
   const int grid = std::max(1, std::min((npad + 255) / 256, 16384));
   hipLaunchKernelGGL((k_dia_encode<T>), dim3(grid), dim3(256), 0, st, n, npad, rp, col, val, c,
-                     vtab, c.ndiag <= 8 ? 1 : 2, code, err);
+                     vtab, code, err);
   return hipGetLastError();
 }
 
@@ -1898,7 +1925,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                                       hipStream_t);                                              \
   template hipError_t launch_gather<T>(int, const int *, const T *, T *, hipStream_t);           \
   template hipError_t launch_dia_encode<T>(int, int, const int *, const int *, const T *,       \
-                                           const DiaCand &, const T *, unsigned *, int *,       \
+                                           const DiaCand &, const T *, unsigned char *, int *,  \
                                            hipStream_t);
 
 CGX_INSTANTIATE(double)

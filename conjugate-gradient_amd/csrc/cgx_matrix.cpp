@@ -267,8 +267,24 @@ bool group_dia(int n, const int *rp, const int *col, bool sample, const std::vec
     if (c.nval[k] == kDiaVals) return false;
     vt[(size_t)k * 16 + c.nval[k]++] = pval[i];
   }
+  dia_pack(c);
   return true;
 }
+
+}  // namespace
+
+void dia_pack(DiaCand &c) {
+  int sh = 0;
+  for (int k = 0; k < kDiaMax; ++k) {
+    const int v = k < c.ndiag ? c.nval[k] : 0;
+    c.cbits[k] = k < c.ndiag ? (v <= 1 ? 1 : v <= 3 ? 2 : v <= 7 ? 3 : 4) : 0;
+    c.csh[k] = sh;
+    sh += c.cbits[k];
+  }
+  c.cbytes = sh <= 8 ? 1 : sh <= 16 ? 2 : sh <= 32 ? 4 : 8;
+}
+
+namespace {
 
 // L2 tiling of the item order for a wide stencil: the x lines a row needs sit
 // at its offsets; with P = the largest |offset| (a 3-D stencil's plane), an
@@ -495,10 +511,9 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   if (dia_ok) {
     const int npad = padded_rows_for(n);
     for (int attempt = 0; attempt < 2 && dia_ok; ++attempt) {
-      const int kw = dia.ndiag <= 8 ? 1 : 2;
       dev_free(&d_dcode);
       dev_free(&d_vtab);
-      if ((rc = dev_alloc(&d_dcode, ((size_t)npad * kw + 4) * 4, &dev_bytes)) ||
+      if ((rc = dev_alloc(&d_dcode, (size_t)npad * dia.cbytes + 16, &dev_bytes)) ||
           (rc = dev_alloc(&d_vtab, (size_t)kDiaMax * 16 * ts, &dev_bytes)))
         return fail(rc);
       CGX_HIP(hipMemcpyAsync(d_vtab, vt.data(), (size_t)kDiaMax * 16 * ts, hipMemcpyHostToDevice, st));
@@ -654,7 +669,7 @@ int DevMatrix::items() const {
 int DevMatrix::padded_rows() const { return padded_rows_for(n); }
 
 bool DevMatrix::fusable() const {
-  if (layout != L_DIA || dia.ndiag > 8) return false;
+  if (layout != L_DIA || dia.cbytes > 4) return false;
   int lfar = 0, rfar = 0;
   for (int k = 0; k < dia.ndiag; ++k) {
     if (k > 0 && dia.doff[k] <= dia.doff[k - 1]) return false;  // ascending
@@ -685,7 +700,7 @@ double DevMatrix::csr_bytes() const {
 double DevMatrix::layout_bytes() const {
   const double sv = dtype == CGX_F32 ? 4.0 : 8.0;
   switch (layout) {
-    case L_DIA: return (dia.ndiag <= 8 ? 4.0 : 8.0) * n + 2.0 * n * sv;
+    case L_DIA: return (double)dia.cbytes * n + 2.0 * n * sv;
     case L_DC: return (double)nnz * (sv + 1) + 1.0 * n + 2.0 * n * sv + 4.0 * ndict;
     case L_STENCIL: return 2.0 * n * sv;
     default:
@@ -717,6 +732,11 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
   a.ndict_cap = ndict <= 64 ? 64 : 256;
   a.gath = gath;
   a.dcode = d_dcode;
+  a.cb = dia.cbytes;
+  for (int k = 0; k < kDiaMax; ++k) {
+    a.csh[k] = dia.csh[k];
+    a.cmask[k] = (1u << dia.cbits[k]) - 1u;
+  }
   a.vtab = (const T *)d_vtab;
   a.ndiag = dia.ndiag;
   a.kdiag = kdiag;

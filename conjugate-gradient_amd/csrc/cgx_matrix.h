@@ -46,7 +46,7 @@ struct DevMatrix {
   int *d_dict = nullptr;
   int ndict = 0;
   // DIA
-  unsigned *d_dcode = nullptr;  // per row 1 (<= 8 diagonals) or 2 dwords of nibbles
+  unsigned char *d_dcode = nullptr;  // per row dia.cbytes bytes of packed value indices
   void *d_vtab = nullptr;       // [16][16] values
   DiaCand dia{};
   int kdiag = -1;               // main diagonal's index, -1: none
@@ -74,8 +74,8 @@ struct DevMatrix {
   int items() const;  // work items of the layout (blocks or slices)
   // host: first row of each item, items() + 1 entries
   std::vector<int> item_rows() const;
-  // The fused HS step applies (DIA, <= 8 diagonals in ascending offset
-  // order, the diagonals with |d| > kHaloMax the outermost ones and as many
+  // The fused HS step applies (DIA, <= 4 code bytes per row, ascending
+  // offset order, the diagonals with |d| > kHaloMax the outermost ones and as many
   // on each side, at most 2): k_spmv_dia_h's window and far diagonals.
   bool fusable() const;
   // rows covered by the items (DIA pads to whole 512-row slices)

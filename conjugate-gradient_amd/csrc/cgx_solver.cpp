@@ -813,7 +813,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;
   info->tile_bands = A.tile_bands;
   info->nt = A.nt ? 1 : 0;
-  info->code_bytes_per_row = A.layout == L_DIA ? (A.dia.ndiag <= 8 ? 4 : 8) : 0;
+  info->code_bytes_per_row = A.layout == L_DIA ? A.dia.cbytes : 0;
   for (int k = 0; k < A.dia.ndiag; ++k) info->n_values += A.dia.nval[k];
   info->gathers_per_chunk = A.layout == L_CSR || A.layout == L_DC ? A.gath : 0;
   info->setup_host_ms = A.setup_host_ms;

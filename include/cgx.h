@@ -145,7 +145,7 @@ typedef struct {
   int tile_bands;       /* L2-tiled item order: bands of the widest offset's
                            period swept one after another (0: natural)      */
   int nt;               /* 1: matrix stream and y store non-temporal        */
-  int code_bytes_per_row; /* DIA: 4 (<= 8 diagonals) or 8                   */
+  int code_bytes_per_row; /* DIA: 1, 2, 4 or 8 (packed value-index fields)  */
   int encode_fallback;  /* 1: the sampled candidates missed one; an exact
                            host scan was needed                             */
   double setup_host_ms;   /* set_matrix: host time (checks, plan, submit)    */

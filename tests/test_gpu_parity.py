@@ -292,6 +292,65 @@ def test_layout_selection_limits():
         check(s, rp, col, rng.standard_normal(len(col)), "csr")
 
 
+def diag_values_matrix(n, offsets, nvs, seed):
+    """Rows hold the diagonals `offsets` (ascending, 0 included) where they
+    fit; diagonal k draws its entries from nvs[k] distinct values, each
+    value used (entry-dependent choice); the main diagonal dominates."""
+    rng = np.random.default_rng(seed)
+    tabs = []
+    for d, nv in zip(offsets, nvs):
+        base = 60.0 if d == 0 else 0.0
+        tabs.append(base + rng.choice(np.linspace(-1, 1, 64), nv, replace=False))
+    r = np.repeat(np.arange(n), len(offsets))
+    k = np.tile(np.arange(len(offsets)), n)
+    c = r + np.asarray(offsets)[k]
+    keep = (c >= 0) & (c < n)
+    r, k, c = r[keep], k[keep], c[keep]
+    nv = np.asarray(nvs)[k]
+    vidx = (r * 7 + k * 3) % nv
+    val = np.array([tabs[kk][vv] for kk, vv in zip(k, vidx)])
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, r + 1, 1)
+    return np.cumsum(rp).astype(np.int32), c.astype(np.int32), val
+
+
+@pytest.mark.parametrize("offsets,nvs,cb", [
+    ([-7, -1, 0, 1, 7], [1] * 5, 1),                        # a 2-D stencil: 5 bits
+    ([-40, -9, -3, -1, 0, 1, 3, 9, 40], [1] * 9, 2),        # 9 one-value diagonals
+    ([-3, -1, 0, 1, 3], [3, 2, 3, 2, 3], 2),                # 2-bit fields
+    ([-1500, -2, -1, 0, 1, 2, 3, 1500], [2] + [15] * 6 + [3], 4),  # 28 bits, far pair
+    ([-4, -3, -2, -1, 0, 1, 2, 3], [15] * 8, 4),            # 32 bits
+    (list(range(-8, 8)), [1] * 16, 2),                      # 16 one-value diagonals
+    ([-4, -3, -2, -1, 0, 1, 2, 3, 4], [15] * 9, 8),         # 36 bits
+])
+def test_dia_code_widths(offsets, nvs, cb):
+    """DIA-VI packs a row's value indices into fields of 1-4 bits (by each
+    diagonal's value count), the word 1, 2, 4 or 8 bytes: every width is
+    bit-exact against the oracle SpMV (odd n: a half row pair at the end),
+    and the fused HS step (words <= 4 bytes) is bit-identical to the
+    unfused iteration."""
+    n = 6001
+    rp, col, val = diag_values_matrix(n, offsets, nvs, seed=len(offsets) * 10 + cb)
+    assert expect_layout(rp, col, val) == "dia"
+    x = np.random.default_rng(1).standard_normal(n)
+    b = np.random.default_rng(2).standard_normal(n)
+    out = []
+    for fused in (True, False):
+        with cgx.Solver(0, layout="dia", fused=fused) as s:
+            s.set_matrix(rp, col, val)
+            i = s.info()
+            assert i["layout_name"] == "dia" and i["code_bytes_per_row"] == cb
+            assert i["n_values"] == sum(nvs)
+            assert i["fused"] == (1 if fused and cb <= 4 else 0)
+            assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+            s.set_rhs(b)
+            its = s.run(21, 0.0)
+            out.append((its, s.x(), s.history(its)))
+    assert out[0][0] == out[1][0] == 22
+    assert H.same_bits_or_both_nan(out[0][1], out[1][1])
+    assert H.same_bits_or_both_nan(out[0][2], out[1][2])
+
+
 def test_bad_column_rejected():
     """A column outside [0, n) would be an out-of-bounds device gather: the
     upload refuses it on the host."""
@@ -306,7 +365,8 @@ def test_bad_column_rejected():
 def test_spmv_c3_full_size_bit_exact(layout):
     """BASELINE config C3 (3-D 7-pt 216^3, 10,077,696 rows): one SpMV,
     bit-exact against the oracle at full size in every layout; the automatic
-    choice is DIA (7 diagonals, one value each, 4 code bytes per row), found
+    choice is DIA (7 diagonals, one value each: one 1-bit field per diagonal,
+    1 code byte per row), found
     from the sampled rows without an exact host scan."""
     rp, col, val = cgx.laplacian3d(216, 216, 216)
     x = np.random.default_rng(2).standard_normal(len(rp) - 1)
@@ -316,7 +376,7 @@ def test_spmv_c3_full_size_bit_exact(layout):
         assert i["layout_name"] == {"auto": "dia"}.get(layout, layout)
         assert i["encode_fallback"] == 0 and i["nt"] == 1
         if i["layout_name"] == "dia":
-            assert i["n_dict"] == 7 and i["code_bytes_per_row"] == 4 and i["n_values"] == 7
+            assert i["n_dict"] == 7 and i["code_bytes_per_row"] == 1 and i["n_values"] == 7
             assert i["spmv_grid"] == -(-(len(rp) - 1) // 512)
         else:
             assert i["gathers_per_chunk"] == 7
