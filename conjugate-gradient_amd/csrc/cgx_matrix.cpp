@@ -75,12 +75,29 @@ struct PairSet {
 
 // Distinct (col - row, value bits) pairs of rows [lo, hi) -- with_vals false:
 // offsets only (vb = 0).  Returns false past cap distinct keys.
+// Entry j of a row usually repeats entry j of the previous scanned row
+// (stencils): those keys skip the hash set.
 template <typename T>
 bool scan_pairs(const int *rp, const int *col, const T *val, long long lo, long long hi,
                 long long step, bool with_vals, int cap, PairSet &S) {
-  for (long long r = lo; r < hi; r += step)
-    for (int k = rp[r]; k < rp[r + 1]; ++k)
-      if (!S.add(col[k] - (int)r, with_vals ? bits_of(val[k]) : 0ULL, cap)) return false;
+  constexpr int M = 32;
+  int po[M];
+  unsigned long long pb[M];
+  int plen = 0;
+  for (long long r = lo; r < hi; r += step) {
+    const int k0 = rp[r], len = rp[r + 1] - k0;
+    for (int j = 0; j < len; ++j) {
+      const int o = col[k0 + j] - (int)r;
+      const unsigned long long b = with_vals ? bits_of(val[k0 + j]) : 0ULL;
+      if (j < plen && po[j] == o && pb[j] == b) continue;
+      if (!S.add(o, b, cap)) return false;
+      if (j < M) {
+        po[j] = o;
+        pb[j] = b;
+      }
+    }
+    plen = std::min(len, M);
+  }
   return true;
 }
 
@@ -271,6 +288,78 @@ bool group_dia(int n, const int *rp, const int *col, bool sample, const std::vec
   return true;
 }
 
+// DIA-VI codes of every row on host threads, the device encoder's checks
+// (k_dia_encode) plus the column range: 0 = encoded, 1 = a row leaves the
+// candidates (diagonal, value or order), 2 = a column outside [0, ncols).
+// A row's entries follow the diagonal order, so the search for the next
+// entry's diagonal starts after the previous one's.
+template <typename T>
+int dia_encode_host(int n, int npad, int ncols, const int *rp, const int *col, const T *val,
+                    const DiaCand &c, const std::vector<T> &vt, std::vector<unsigned char> &code) {
+  const int cb = c.cbytes;
+  unsigned long long empty = 0;
+  for (int q = 0; q < c.ndiag; ++q) empty |= ((1ull << c.cbits[q]) - 1ull) << c.csh[q];
+  code.resize((size_t)npad * cb);
+  const int nt = host_threads(rp[n]);
+  std::vector<int> res((size_t)nt, 0);
+  parallel_rows(n, rp[n], [&](int t, long long lo, long long hi) {
+    // thread-local copies: the byte stores below may alias anything the
+    // compiler cannot prove private, and would force reloads per entry
+    int doff[kDiaMax], nval[kDiaMax], sh[kDiaMax];
+    unsigned long long fm[kDiaMax], vb[kDiaMax * 16];
+    const int K = c.ndiag;
+    for (int q = 0; q < K; ++q) {
+      doff[q] = c.doff[q];
+      nval[q] = c.nval[q];
+      sh[q] = c.csh[q];
+      fm[q] = ((1ull << c.cbits[q]) - 1ull) << c.csh[q];
+      for (int v = 0; v < nval[q]; ++v) vb[q * 16 + v] = bits_of(vt[(size_t)q * 16 + v]);
+    }
+    const unsigned nc = (unsigned)ncols;
+    const unsigned long long e0 = empty;
+    int err = 0;
+    for (long long r = lo; r < hi && !err; ++r) {
+      unsigned long long w = e0;
+      int q = 0;
+      const int k1 = rp[r + 1];
+      for (int k = rp[r]; k < k1; ++k) {
+        const int cl = col[k];
+        if ((unsigned)cl >= nc) {
+          err = 2;
+          break;
+        }
+        const int off = cl - (int)r;
+        while (q < K && doff[q] != off) ++q;
+        if (q == K) {
+          err = 1;
+          break;
+        }
+        const unsigned long long b = bits_of(val[k]);
+        int v = 0;
+        while (v < nval[q] && vb[q * 16 + v] != b) ++v;
+        if (v == nval[q]) {
+          err = 1;
+          break;
+        }
+        w = (w & ~fm[q]) | ((unsigned long long)v << sh[q]);
+        ++q;
+      }
+      unsigned char *p = code.data() + (size_t)r * cb;
+      switch (cb) {  // little-endian low bytes of the word
+        case 1: *p = (unsigned char)w; break;
+        case 2: memcpy(p, &w, 2); break;
+        case 4: memcpy(p, &w, 4); break;
+        default: memcpy(p, &w, 8); break;
+      }
+    }
+    res[(size_t)t] = err;
+  });
+  for (long long r = n; r < npad; ++r) memcpy(code.data() + (size_t)r * cb, &empty, (size_t)cb);
+  int e = 0;
+  for (int x : res) e = std::max(e, x);
+  return e;
+}
+
 }  // namespace
 
 void dia_pack(DiaCand &c) {
@@ -401,28 +490,37 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     set_error("set_matrix: row_ptr[0] must be 0 and row_ptr[n] == nnz");
     return CGX_EINVAL;
   }
-  // row_ptr non-decreasing and columns inside x: a bad index would be an
-  // out-of-bounds gather on the device, so it is rejected here
-  for (int r = 0; r < n_; ++r)
-    if (rp[r + 1] < rp[r]) {
-      set_error("set_matrix: row_ptr decreases at row %d", r);
-      return CGX_EINVAL;
-    }
-  if (!gen && nnz_ > 0) {
-    std::vector<int> bad((size_t)host_threads(nnz_), 0);
-    parallel_rows(nnz_, nnz_, [&](int t, long long lo, long long hi) {
-      for (long long k = lo; k < hi; ++k)
-        if ((unsigned)col[k] >= (unsigned)ncols_) {
-          bad[t] = 1;
+  // row_ptr non-decreasing (and the longest row) on host threads; columns
+  // inside x are checked by the DIA host encoder or, for the other layouts,
+  // before the upload: a bad index would be an out-of-bounds device gather
+  int maxlen = 0;
+  {
+    const int nt = host_threads(n_);
+    std::vector<int> bad((size_t)nt, -1), mx((size_t)nt, 0);
+    parallel_rows(n_, n_, [&](int t, long long lo, long long hi) {
+      int m = 0;
+      for (long long r = lo; r < hi; ++r) {
+        const int len = rp[r + 1] - rp[r];
+        if (len < 0) {
+          bad[(size_t)t] = (int)r;
           return;
         }
+        m = std::max(m, len);
+      }
+      mx[(size_t)t] = m;
     });
-    for (int b : bad)
-      if (b) {
-        set_error("set_matrix: a column index is outside [0, %d)", ncols_);
+    for (int t = 0; t < nt; ++t) {
+      if (bad[(size_t)t] >= 0) {
+        set_error("set_matrix: row_ptr decreases at row %d", bad[(size_t)t]);
         return CGX_EINVAL;
       }
+      maxlen = std::max(maxlen, mx[(size_t)t]);
+    }
   }
+  auto bad_column = [&]() {
+    set_error("set_matrix: a column index is outside [0, %d)", ncols_);
+    return CGX_EINVAL;
+  };
   release();
   dtype = sizeof(T) == 4 ? CGX_F32 : CGX_F64;
   n = n_;
@@ -437,8 +535,6 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   const bool want_dc = want_dia || want == CGX_LAYOUT_DC;
   std::vector<int> poff;  // (offset, value) keys, sorted
   std::vector<T> pval, vt;
-  int maxlen = 0;
-  for (int r = 0; r < n; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
   bool dia_ok = false, dc_ok = false;
   if (n > 0 && nnz > 0 && want_dia) {
     if (gen) {  // one value per offset: 2 dim on the diagonal, -1 off it
@@ -450,6 +546,57 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
                group_dia(n, rp, col, true, poff, pval, dia, vt);
     }
   }
+
+  // ---- DIA-VI from a host matrix: encoded on host threads (every row
+  // checked), only the codes and value tables go to the device -- no CSR
+  // upload (1 code byte per row instead of 12 bytes per nonzero over PCIe)
+  const int npad = padded_rows_for(n);
+  if (dia_ok && !gen) {
+    std::vector<unsigned char> hcode;
+    int e = dia_encode_host(n, npad, ncols, rp, col, val, dia, vt, hcode);
+    if (e == 1) {  // the sample missed a diagonal or a value: exact scan
+      encode_fallback = 1;
+      dia_ok = find_pairs(n, rp, col, val, true, kDiaMax * kDiaVals, false, poff, pval) &&
+               group_dia(n, rp, col, false, poff, pval, dia, vt);
+      if (dia_ok) e = dia_encode_host(n, npad, ncols, rp, col, val, dia, vt, hcode);
+    }
+    if (e == 2) {
+      release();
+      return bad_column();
+    }
+    dia_ok = dia_ok && e == 0;
+    if (dia_ok) {
+      if ((rc = dev_alloc(&d_dcode, hcode.size() + 16, &dev_bytes)) ||
+          (rc = dev_alloc(&d_vtab, (size_t)kDiaMax * 16 * ts, &dev_bytes))) {
+        release();
+        return rc;
+      }
+      CGX_HIP(hipMemcpyAsync(d_dcode, hcode.data(), hcode.size(), hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d_vtab, vt.data(), (size_t)kDiaMax * 16 * ts, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipStreamSynchronize(st));  // hcode goes out of scope
+      layout = L_DIA;
+      for (int k = 0; k < dia.ndiag; ++k)
+        if (dia.doff[k] == 0) kdiag = k;
+      return finish_upload(t0);
+    }
+    memset(&dia, 0, sizeof dia);
+  }
+  if (!gen && nnz > 0) {
+    std::vector<int> bad((size_t)host_threads(nnz), 0);
+    parallel_rows(nnz, nnz, [&](int t, long long lo, long long hi) {
+      for (long long k = lo; k < hi; ++k)
+        if ((unsigned)col[k] >= (unsigned)ncols) {
+          bad[(size_t)t] = 1;
+          return;
+        }
+    });
+    for (int b : bad)
+      if (b) {
+        release();
+        return bad_column();
+      }
+  }
+
   std::vector<int> doff;
   if (!dia_ok && n > 0 && nnz > 0 && want_dc && maxlen <= 255) {
     std::vector<T> dummy;
@@ -507,9 +654,9 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     return code;
   };
 
-  // ---- DIA-VI: device encode against the candidates, exact host scan on a miss
+  // ---- DIA-VI of a device-generated matrix: device encode against the
+  // stencil's candidates, then the generated CSR is dropped
   if (dia_ok) {
-    const int npad = padded_rows_for(n);
     for (int attempt = 0; attempt < 2 && dia_ok; ++attempt) {
       dev_free(&d_dcode);
       dev_free(&d_vtab);
@@ -523,19 +670,19 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
       int err = 0;
       if ((rc = read_err(&err))) return fail(rc);
       if (!err) break;
-      if (attempt == 0 && !gen) {  // the sample missed a diagonal or a value: exact scan
-        encode_fallback = 1;
-        dia_ok = find_pairs(n, rp, col, val, true, kDiaMax * kDiaVals, false, poff, pval) &&
-                 group_dia(n, rp, col, false, poff, pval, dia, vt);
-      } else {
-        dia_ok = false;  // e.g. a row whose columns do not ascend
-      }
+      dia_ok = false;
     }
     if (dia_ok) {
       layout = L_DIA;
       kdiag = -1;
       for (int k = 0; k < dia.ndiag; ++k)
         if (dia.doff[k] == 0) kdiag = k;
+      (void)hipFree(d_err);
+      CGX_HIP(hipStreamSynchronize(st));
+      dev_free(&d_rp);
+      dev_free(&d_col);
+      dev_free(&d_val);
+      return finish_upload(t0);
     } else {
       dev_free(&d_dcode);
       dev_free(&d_vtab);
@@ -623,6 +770,25 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     }
   }
   (void)hipFree(d_err);
+  return finish_upload(t0);
+}
+
+template int DevMatrix::upload<double>(int, int, int, const int *, const int *, const double *,
+                                       int, bool, const LapSpec *);
+template int DevMatrix::upload<float>(int, int, int, const int *, const int *, const float *,
+                                      int, bool, const LapSpec *);
+
+// The item order, the non-temporal choice and the setup times, once the
+// layout's arrays are on the device.
+int DevMatrix::finish_upload(double t0) {
+  const size_t ts = dtype == CGX_F32 ? 4 : 8;
+  int rc;
+  std::vector<int> doff;
+  if (layout == L_DC) {
+    std::vector<int> dd((size_t)ndict);
+    CGX_HIP(hipMemcpy(dd.data(), d_dict, (size_t)ndict * 4, hipMemcpyDeviceToHost));
+    doff = dd;
+  }
 
   // ---- L2-tiled item order for wide stencils (DC / DIA)
   if (layout == L_DC || layout == L_DIA) {
@@ -653,10 +819,39 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   return 0;
 }
 
-template int DevMatrix::upload<double>(int, int, int, const int *, const int *, const double *,
-                                       int, bool, const LapSpec *);
-template int DevMatrix::upload<float>(int, int, int, const int *, const int *, const float *,
-                                      int, bool, const LapSpec *);
+int DevMatrix::download_csr(int *row_ptr, int *col, double *val) const {
+  if (n == 0) return 0;
+  if (layout != L_DIA) {
+    CGX_HIP(hipMemcpy(row_ptr, d_rp, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost));
+    if (nnz > 0) {
+      CGX_HIP(hipMemcpy(col, d_col, (size_t)nnz * 4, hipMemcpyDeviceToHost));
+      CGX_HIP(hipMemcpy(val, d_val, (size_t)nnz * 8, hipMemcpyDeviceToHost));
+    }
+    return 0;
+  }
+  // DIA: every row's fields in diagonal order are its entries in column order
+  const int cb = dia.cbytes;
+  std::vector<unsigned char> code((size_t)n * cb);
+  std::vector<double> vt((size_t)kDiaMax * 16);
+  CGX_HIP(hipMemcpy(code.data(), d_dcode, code.size(), hipMemcpyDeviceToHost));
+  CGX_HIP(hipMemcpy(vt.data(), d_vtab, vt.size() * 8, hipMemcpyDeviceToHost));
+  long long k = 0;
+  row_ptr[0] = 0;
+  for (int r = 0; r < n; ++r) {
+    unsigned long long w = 0;
+    memcpy(&w, code.data() + (size_t)r * cb, (size_t)cb);
+    for (int q = 0; q < dia.ndiag; ++q) {
+      const unsigned m = (1u << dia.cbits[q]) - 1u;
+      const unsigned f = (unsigned)(w >> dia.csh[q]) & m;
+      if (f == m) continue;
+      if (k >= nnz) return CGX_EINVAL;
+      col[k] = r + dia.doff[q];
+      val[k++] = vt[(size_t)q * 16 + f];
+    }
+    row_ptr[r + 1] = (int)k;
+  }
+  return k == nnz ? 0 : CGX_EINVAL;
+}
 
 int DevMatrix::items() const {
   switch (layout) {

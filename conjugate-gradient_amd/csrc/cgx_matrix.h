@@ -3,18 +3,18 @@
 // layout choice, encoding, upload, and the SpMV launch.
 //
 // The C ABI takes the reference's CSR (mv_ops.h:17-23: int32 row_ptr and
-// col_indices, fp64 values; fp32 for SURVEY.md C5).  The CSR arrays always
-// stay resident; on top of them the matrix picks, once per upload, the
-// layout the SpMV streams (cgx_internal.h, Layout):
+// col_indices, fp64 values; fp32 for SURVEY.md C5).  The matrix picks, once
+// per upload, the layout the SpMV streams (cgx_internal.h, Layout); only
+// that layout's arrays are resident (DIA: codes and value tables, no CSR):
 //   auto: DIA-VI when the nonzeros lie on <= 16 diagonals (col - row) with
 //         <= 15 distinct values each and every row's columns ascend; else
 //         CSR-DC when they use <= 256 distinct offsets (rows <= 255
 //         entries); else plain CSR, with column panels when the gathers
 //         have no locality (C5).
-// Candidates (pairs / offsets) come from a sample of rows on the host; the
-// device encoder then checks every nonzero against them, and a miss falls
-// back to an exact host scan -- so the setup of a 10 M-row stencil is one
-// pass over row_ptr on the host plus one device pass over col/val.
+// Candidates (pairs / offsets) come from a sample of rows on the host; an
+// encoder then checks every nonzero against them (DIA: host threads, so only
+// the 1-8 code bytes per row cross PCIe; DC: the device, over the uploaded
+// CSR), and a miss falls back to an exact host scan.
 #pragma once
 
 #include <vector>
@@ -32,7 +32,7 @@ struct DevMatrix {
   int layout = L_CSR;
   bool nt = false;           // matrix stream + y store non-temporal
   size_t dev_bytes = 0;
-  // CSR (always resident; panels: P row_ptrs back to back, panel-major col/val)
+  // CSR (CSR / DC / panels; panels: P row_ptrs back to back, panel-major col/val)
   int *d_rp = nullptr, *d_col = nullptr;
   void *d_val = nullptr;
   // CSR / DC row blocks
@@ -68,7 +68,10 @@ struct DevMatrix {
   template <typename T>
   int upload(int n, int ncols, int nnz, const int *rp, const int *col, const T *val, int want,
              bool allow_panels, const LapSpec *gen = nullptr);
+  int finish_upload(double t0);
   int set_stencil(const LapSpec &g);
+  // The matrix as CSR on the host (fp64; DIA decodes its codes).
+  int download_csr(int *row_ptr, int *col, double *val) const;
   void release();
 
   int items() const;  // work items of the layout (blocks or slices)

@@ -720,14 +720,7 @@ int cgx_solver_get_matrix(cgx_solver *s, int *row_ptr, int *col, double *val) {
     return CGX_EINVAL;
   }
   CGX_HIP(hipSetDevice(s->device));
-  if (s->A.n > 0) {
-    CGX_HIP(hipMemcpy(row_ptr, s->A.d_rp, ((size_t)s->A.n + 1) * 4, hipMemcpyDeviceToHost));
-    if (s->A.nnz > 0) {
-      CGX_HIP(hipMemcpy(col, s->A.d_col, (size_t)s->A.nnz * 4, hipMemcpyDeviceToHost));
-      CGX_HIP(hipMemcpy(val, s->A.d_val, (size_t)s->A.nnz * 8, hipMemcpyDeviceToHost));
-    }
-  }
-  return 0;
+  return s->A.download_csr(row_ptr, col, val);
 }
 
 int cgx_solver_set_rhs(cgx_solver *s, const double *b) { return s ? upload_rhs<double>(s, b) : CGX_EINVAL; }
