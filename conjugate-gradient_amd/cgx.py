@@ -66,7 +66,7 @@ class CgxDistStats(ctypes.Structure):
                 ("iter_bytes", ctypes.c_double), ("halo_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("spmv_iter_bytes", ctypes.c_double),
                 ("layout", ctypes.c_int), ("n_dict", ctypes.c_int), ("graph", ctypes.c_int),
-                ("alg", ctypes.c_int)]
+                ("alg", ctypes.c_int), ("fused", ctypes.c_int)]
 
 
 _MVP = ctypes.POINTER(MvSparse)
@@ -169,6 +169,7 @@ _SIGS = {
     "cgx_dist_set_alg": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_graph": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
                                     ctypes.POINTER(ctypes.c_int)]),
     "cgx_dist_get_x": (ctypes.c_int, [_vp, _f64p]),
@@ -647,6 +648,10 @@ class DistSolver:
 
     def set_graph(self, on):
         check(lib().cgx_dist_set_graph(self._h, 1 if on else 0), "dist_set_graph")
+
+    def set_fused(self, on):
+        """The fused HS step where every rank's DIA layout takes it."""
+        check(lib().cgx_dist_set_fused(self._h, 1 if on else 0), "dist_set_fused")
 
     def run(self, maxit, tol=0.0):
         it = ctypes.c_int(0)

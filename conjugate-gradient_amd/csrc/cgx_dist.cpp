@@ -20,6 +20,14 @@
 //                the r.r partials) -> ncclAllReduce(r.r)
 //                k_xpay_xf (beta, stop test, x += alpha p, p = r + beta p)
 //                pack p[send rows] for the next halo
+//       fused (DIA layouts k_spmv_dia_h takes on every rank; cgx_dist_set_fused):
+//                pack p_new = r + beta p_old at the send rows (k_pack_pnext)
+//       st_comm: halo of p_new into the p_new buffer's ghost tail
+//       st:      k_spmv_dia_h over INTERIOR items: beta, p_new, x (every
+//                other iteration), s = A p_new || halo; wait; BOUNDARY items
+//                (ghost diagonals read the received p_new) -> local p.s
+//                ncclAllReduce(p.s); k_update_rf -> ncclAllReduce(r.r)
+//                -- two launches and one pack per iteration instead of four
 //   CG1 (Chronopoulos-Gear): ONE all-reduce of (gamma, delta) per iteration,
 //       rounding-level different from HS, 8 B per row more vector traffic.
 // Every rank derives alpha, beta and the stop test from the same all-reduced
@@ -84,6 +92,10 @@ struct cgx_dist {
   int g_int = 0, g_bnd = 0;  // SpMV partials of each launch
   double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
          *d_w = nullptr;
+  double *d_p2 = nullptr;  // fused step: the second p buffer (with ghost tail)
+  int pbuf = 0;            // fused step: which buffer holds p_old (0: d_p)
+  bool fuse = true;        // cgx_dist_set_fused
+  bool fz_all = false;     // every partition's layout takes the fused step (ensure_connected)
   int *d_send_idx = nullptr;
   double *d_sendbuf = nullptr;
   std::vector<int> send_count, send_off, recv_count, recv_off;
@@ -105,8 +117,8 @@ struct cgx_dist {
   size_t ev_i = 0;
   // batches of graph_batch iterations replayed as a hipGraph (solo and
   // RCCL; the in-process group runs eager)
-  hipGraphExec_t gexec = nullptr;   // graph_batch iterations
-  hipGraphExec_t gexec1 = nullptr;  // one iteration (remainders)
+  hipGraphExec_t gexec[2] = {};   // graph_batch iterations, per p-buffer parity
+  hipGraphExec_t gexec1[2] = {};  // one iteration (remainders), per parity
   int gexec_alg = -1;
   int graph_batch = 16;
   bool use_graph = true;
@@ -132,11 +144,17 @@ bool solo(const cgx_dist *d) { return !d->local && d->comm == nullptr; }
   } while (0)
 
 void drop_graph(cgx_dist *d) {
-  if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
-  if (d->gexec1) (void)hipGraphExecDestroy(d->gexec1);
-  d->gexec = d->gexec1 = nullptr;
+  for (int q = 0; q < 2; ++q) {
+    if (d->gexec[q]) (void)hipGraphExecDestroy(d->gexec[q]);
+    if (d->gexec1[q]) (void)hipGraphExecDestroy(d->gexec1[q]);
+    d->gexec[q] = d->gexec1[q] = nullptr;
+  }
   d->gexec_alg = -1;
 }
+
+// The fused HS step (k_spmv_dia_h) runs when every partition's layout
+// takes it (decided once per connection: the ranks' phase sequences match).
+bool fz(const cgx_dist *d) { return d->fuse && d->fz_all && d->alg == CGX_ALG_HS; }
 
 void free_system(cgx_dist *d) {
   drop_graph(d);
@@ -149,6 +167,7 @@ void free_system(cgx_dist *d) {
   dev_free(&d->d_p);
   dev_free(&d->d_s);
   dev_free(&d->d_w);
+  dev_free(&d->d_p2);
   dev_free(&d->d_send_idx);
   dev_free(&d->d_sendbuf);
   dev_free(&d->d_pa);
@@ -264,6 +283,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
   if ((rc = dev_alloc(&d->d_b, nv * 8, cb)) || (rc = dev_alloc(&d->d_x, nv * 8, cb)) ||
       (rc = dev_alloc(&d->d_r, ng * 8, cb)) || (rc = dev_alloc(&d->d_p, ng * 8, cb)) ||
       (rc = dev_alloc(&d->d_s, nv * 8, cb)) || (rc = dev_alloc(&d->d_w, nv * 8, cb)) ||
+      (rc = dev_alloc(&d->d_p2, ng * 8, cb)) ||
       (rc = dev_alloc(&d->d_pa, ((size_t)d->vec_grid + 8) * 8, cb)) ||
       (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb))) {
     free_system(d);
@@ -271,6 +291,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
   }
   CGX_HIP(hipMemsetAsync(d->d_r, 0, ng * 8, d->st));
   CGX_HIP(hipMemsetAsync(d->d_p, 0, ng * 8, d->st));
+  CGX_HIP(hipMemsetAsync(d->d_p2, 0, ng * 8, d->st));
   CGX_HIP(hipMemsetAsync(d->d_x, 0, nv * 8, d->st));
   CGX_HIP(hipStreamSynchronize(d->st));
   d->have_matrix = true;
@@ -381,6 +402,22 @@ int connect_local(Group *g) {
   return 0;
 }
 
+// Every rank's layout takes the fused step: MIN over the ranks (RCCL).
+int agree_fusable(cgx_dist *d, int mine, int *all) {
+  *all = mine;
+  if (d->comm == nullptr || d->nranks < 2) return 0;
+  int *d_f = nullptr;
+  CGX_HIP(hipMalloc((void **)&d_f, 2 * sizeof(int)));
+  CGX_HIP(hipMemcpy(d_f, &mine, sizeof(int), hipMemcpyHostToDevice));
+  ncclResult_t r = ncclAllReduce(d_f, d_f + 1, 1, ncclInt32, ncclMin, d->comm, d->st);
+  hipError_t e = r == ncclSuccess ? hipStreamSynchronize(d->st) : hipSuccess;
+  if (r == ncclSuccess && e == hipSuccess) e = hipMemcpy(all, d_f + 1, sizeof(int), hipMemcpyDeviceToHost);
+  (void)hipFree(d_f);
+  CGX_NCCL(r);
+  CGX_HIP(e);
+  return 0;
+}
+
 int ensure_connected(Group *g) {
   if (g->connected) return 0;
   for (cgx_dist *d : g->parts)
@@ -388,22 +425,45 @@ int ensure_connected(Group *g) {
       set_error("dist: every partition needs set_matrix before solving");
       return CGX_EINVAL;
     }
-  if (g->parts[0]->local) return connect_local(g);
-  int rc = connect_rccl(g->parts[0]);
-  if (rc == 0) g->connected = true;
-  return rc;
+  int rc;
+  if (g->parts[0]->local) {
+    if ((rc = connect_local(g))) return rc;
+    bool all = true;
+    for (cgx_dist *d : g->parts) all = all && d->A.fusable();
+    for (cgx_dist *d : g->parts) d->fz_all = all;
+    return 0;
+  }
+  cgx_dist *d = g->parts[0];
+  if ((rc = connect_rccl(d))) return rc;
+  int all = 0;
+  if ((rc = agree_fusable(d, d->A.fusable() ? 1 : 0, &all))) return rc;
+  d->fz_all = all != 0;
+  g->connected = true;
+  return 0;
 }
 
 // ---------------------------------------------------------- phase helpers
 
-// the vector the SpMV gathers (its ghost tail is the halo) and its output
-double *spmv_x(cgx_dist *d) { return d->alg == CGX_ALG_HS ? d->d_p : d->d_r; }
+// the vector the SpMV gathers (its ghost tail is the halo) and its output;
+// fused: the p_new buffer
+double *p_old(cgx_dist *d) { return d->pbuf ? d->d_p2 : d->d_p; }
+double *p_new(cgx_dist *d) { return d->pbuf ? d->d_p : d->d_p2; }
+double *spmv_x(cgx_dist *d) {
+  return d->alg != CGX_ALG_HS ? d->d_r : fz(d) ? p_new(d) : d->d_p;
+}
+// r.r of the last r update, as the fused step reads it
+const double *rr_new_src(cgx_dist *d) { return solo(d) ? &d->d_st->rr_new : d->d_gsums + 1; }
 double *spmv_y(cgx_dist *d) { return d->alg == CGX_ALG_HS ? d->d_s : d->d_w; }
 
-// pack the send rows of the gathered vector (after its update)
+// pack the send rows of the gathered vector (after its update; fused:
+// p_new = r + beta p_old computed at the send rows)
 int phase_pack(cgx_dist *d) {
   if (solo(d)) return 0;
-  CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, spmv_x(d), d->d_sendbuf, d->st));
+  if (fz(d))
+    CGX_HIP(launch_pack_pnext<double>(d->n_send, d->d_send_idx, d->d_r, p_old(d), d->d_sendbuf,
+                                      d->d_st, rr_new_src(d), d->st));
+  else
+    CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, spmv_x(d), d->d_sendbuf, d->st));
   CGX_HIP(hipEventRecord(d->ev_packed, d->st));
   return 0;
 }
@@ -466,6 +526,14 @@ int phase_spmv(cgx_dist *d) {
     }
     SpmvArgs<double> a = d->A.args<double>(spmv_x(d), spmv_y(d), part, &d->d_st->done, it);
     if (last) a.fin = fin;
+    if (fz(d)) {
+      // the first non-empty launch publishes the scalar step
+      // boundary items (e == 2) read ghost columns' p_new from the halo
+      const int pub = (e == 0 || d->it_int.count == 0) ? 1 : 0;
+      const FuseArgs<double> f{d->d_x, p_old(d), p_new(d), d->d_r, d->d_st, d->d_hist,
+                               rr_new_src(d), pub, e == 2 ? 1 : 0};
+      return launch_spmv_fused<double>(a, f, d->st, ev);
+    }
     return launch_spmv<double>(a, d->st, ev);
   };
   CGX_HIP(launch(d->it_int, d->d_pb, !bnd_last, 0));
@@ -526,8 +594,10 @@ int hs_alpha(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const int gf = d->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
   if (solo(d)) {
+    const FinArgs fin{d->d_tick + 1, d->d_pa, 4 * gf, nullptr, 0, &d->d_st->rr_new};
     CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_pb,
-                                     d->g_int + d->g_bnd, d->d_pa, gf, d->st));
+                                     d->g_int + d->g_bnd, d->d_pa, gf, d->st,
+                                     fz(d) ? &fin : nullptr));
     return 0;
   }
   int rc = allreduce(d, 0, 1);
@@ -582,13 +652,35 @@ int cg1_reduce(cgx_dist *d, bool init) {
   return 0;
 }
 
+// fused: the all-reduce of the local r.r (the next iteration's beta), and
+// the p buffers swap roles
+int fz_close(cgx_dist *d) {
+  if (!solo(d)) {
+    int rc = allreduce(d, 1, 1);
+    if (rc) return rc;
+  }
+  d->pbuf ^= 1;
+  return 0;
+}
+
 int run_phases_eager(Group *g, bool init, long long iters) {
   auto &P = g->parts;
   int rc;
   if (P[0]->alg == CGX_ALG_HS) {
     if (init) {
+      for (cgx_dist *d : P) d->pbuf = 0;  // the prologue writes p into d_p
       for (cgx_dist *d : P) if ((rc = hs_init(d))) return rc;
       for (cgx_dist *d : P) if ((rc = hs_init_reduce(d))) return rc;
+      return 0;
+    }
+    if (fz(P[0])) {
+      for (long long it = 0; it < iters; ++it) {
+        for (cgx_dist *d : P) if ((rc = phase_pack(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = phase_spmv(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = hs_alpha(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = fz_close(d))) return rc;
+      }
       return 0;
     }
     // each iteration packs its own halo first, so a captured batch has no
@@ -613,12 +705,15 @@ int run_phases_eager(Group *g, bool init, long long iters) {
 
 // Capture `nit` iterations (kernels, halo send/recv on the comm stream
 // forked and joined by events, all-reduces) into *out, without running them.
-int capture(cgx_dist *d, Group *g, int nit, hipGraphExec_t *out) {
+int capture(cgx_dist *d, Group *g, int nit, int parity, hipGraphExec_t *out) {
   hipGraph_t gr = nullptr;
   CGX_HIP(hipSetDevice(d->device));
+  const int saved = d->pbuf;
+  d->pbuf = parity;
   CGX_HIP(hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal));
   const int rc = run_phases_eager(g, false, nit);
   const hipError_t e = hipStreamEndCapture(d->st, &gr);
+  d->pbuf = saved;
   hipError_t ei = hipSuccess;
   if (rc == 0 && e == hipSuccess) ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
   if (gr) (void)hipGraphDestroy(gr);
@@ -641,14 +736,17 @@ bool graphs_on(const cgx_dist *d) {
 int ensure_graphs(Group *g) {
   cgx_dist *d = g->parts[0];
   if (!graphs_on(d)) return 0;
-  if (d->gexec && d->gexec1 && d->gexec_alg == d->alg) return 0;
+  const int key = d->alg * 2 + (fz(d) ? 1 : 0);
+  if (d->gexec[0] && d->gexec1[0] && d->gexec_alg == key) return 0;
   drop_graph(d);
-  if (capture(d, g, d->graph_batch, &d->gexec) || capture(d, g, 1, &d->gexec1)) {
-    drop_graph(d);
-    d->graph_state = -1;
-    return 0;
-  }
-  d->gexec_alg = d->alg;
+  const int nq = fz(d) ? 2 : 1;
+  for (int q = 0; q < nq; ++q)
+    if (capture(d, g, d->graph_batch, q, &d->gexec[q]) || capture(d, g, 1, q, &d->gexec1[q])) {
+      drop_graph(d);
+      d->graph_state = -1;
+      return 0;
+    }
+  d->gexec_alg = key;
   d->graph_state = 1;
   return 0;
 }
@@ -658,10 +756,16 @@ int run_phases(Group *g, bool init, long long iters) {
   if (!init && graphs_on(d)) {
     int rc = ensure_graphs(g);
     if (rc) return rc;
-    if (d->gexec && d->gexec1) {
-      for (; iters >= d->graph_batch; iters -= d->graph_batch)
-        CGX_HIP(hipGraphLaunch(d->gexec, d->st));
-      for (; iters > 0; --iters) CGX_HIP(hipGraphLaunch(d->gexec1, d->st));
+    if (d->gexec[0] && d->gexec1[0]) {
+      const bool alt = fz(d);  // an even batch keeps the p parity, one iteration flips it
+      for (; iters >= d->graph_batch; iters -= d->graph_batch) {
+        CGX_HIP(hipGraphLaunch(d->gexec[alt ? d->pbuf : 0], d->st));
+        if (alt && (d->graph_batch & 1)) d->pbuf ^= 1;
+      }
+      for (; iters > 0; --iters) {
+        CGX_HIP(hipGraphLaunch(d->gexec1[alt ? d->pbuf : 0], d->st));
+        if (alt) d->pbuf ^= 1;
+      }
       return 0;
     }
   }
@@ -671,8 +775,9 @@ int run_phases(Group *g, bool init, long long iters) {
 int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
   for (cgx_dist *d : g->parts) {
     CGX_HIP(hipSetDevice(d->device));
+    CGX_HIP(hipMemsetAsync(d->d_tick, 0, 4 * sizeof(unsigned), d->st));
     if (hist_cap > d->hist_alloc) {
-      if (d->gexec) {  // the captured graph holds the old history pointer
+      if (d->gexec[0]) {  // the captured graph holds the old history pointer
         CGX_HIP(hipStreamSynchronize(d->st));
         drop_graph(d);
       }
@@ -712,7 +817,9 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
   for (cgx_dist *d : g->parts) d->bench_ready = false;
   if ((rc = prepare_states(g, maxit, tol, maxit + 1))) return rc;
   if ((rc = run_phases(g, true, 1))) return rc;
-  const long long total = (long long)maxit + 1;
+  // the fused step does an iteration's x update in the next launch: one
+  // more step carries the last one (and finds the stop)
+  const long long total = (long long)maxit + 1 + (fz(g->parts[0]) ? 1 : 0);
   if (tol <= 0.0) {
     if ((rc = run_phases(g, false, total))) return rc;
     if ((rc = read_states(g))) return rc;
@@ -928,6 +1035,19 @@ int cgx_dist_set_layout(cgx_dist *d, int layout) {
   return 0;
 }
 
+int cgx_dist_set_fused(cgx_dist *d, int on) {
+  if (!d || (d->local && !d->owns_group)) return CGX_EINVAL;
+  for (cgx_dist *o : d->group->parts) {
+    if (o->gexec[0]) {
+      (void)hipStreamSynchronize(o->st);
+      drop_graph(o);
+    }
+    o->fuse = on != 0;
+    o->bench_ready = false;
+  }
+  return 0;
+}
+
 int cgx_dist_set_graph(cgx_dist *d, int on) {
   if (!d) return CGX_EINVAL;
   d->use_graph = on != 0;
@@ -988,7 +1108,7 @@ int cgx_dist_set_alg(cgx_dist *d, int alg) {
   if (!d || (alg != CGX_ALG_HS && alg != CGX_ALG_CG1) || (d->local && !d->owns_group))
     return CGX_EINVAL;
   for (cgx_dist *o : d->group->parts) {
-    if (o->alg != alg && o->gexec) {  // a captured graph holds the other recurrence
+    if (o->alg != alg && o->gexec[0]) {  // a captured graph holds the other recurrence
       (void)hipStreamSynchronize(o->st);
       drop_graph(o);
     }
@@ -1014,6 +1134,10 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   s->halo_bytes = 8.0 * (d->n_ghost + d->n_send);
   s->device_bytes = d->A.dev_bytes + d->vec_bytes;
   s->spmv_iter_bytes = d->have_matrix ? d->A.layout_bytes() : 0.0;
+  // fused: + r, p_old read and p_new written, x / p_{k-1} read and x
+  // written every other launch (cgx_info)
+  if (d->have_matrix && fz(d)) s->spmv_iter_bytes += 3.5 * d->n_loc * 8.0;
+  s->fused = fz(d) ? 1 : 0;
   s->layout = d->have_matrix ? cgx::public_layout(d->A) : CGX_LAYOUT_AUTO;
   s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_DIA ? d->A.dia.ndiag : 0;
   s->graph = d->graph_state;

@@ -227,6 +227,7 @@ struct SpmvArgs {
   // [s0 - hl, s0 + 512 + hr); diagonal k is read from it when near bit k
   int hl, hr;
   unsigned near;
+  int fark[4];      // the far (not near) diagonals, -1: unused slot
   // stencil
   LapSpec lap;
   double inv_nx, inv_pl;  // 1 / nx, 1 / (nx ny): exact floor divisions (fdiv)
@@ -246,6 +247,9 @@ struct FuseArgs {
   const T *r;
   CgState *st;
   double *hist;
+  const double *rr_new;  // r.r of the last r update (&st->rr_new, or all-reduced)
+  int publish;           // this launch's workgroup 0 writes the scalar state back
+  int ghost;             // columns >= n are ghosts: p_new from pnew's ghost tail
 };
 
 // Optional kernel timing events of a launch (hipExtLaunchKernel: stamped at
@@ -264,6 +268,11 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev 
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev = LaunchEv{});
+// out[i] = p_new[idx[i]] = r + beta p_old (the fused partitioned step's halo
+// send rows; beta from *rr_new and st, r on the first iteration)
+template <typename T>
+hipError_t launch_pack_pnext(int n_send, const int *idx, const T *r, const T *pold, T *out,
+                             const CgState *stt, const double *rr_new, hipStream_t st);
 
 // ------------------------------------------------------------- vectors
 // All launchers are graph-capturable (no sync, no allocation).

@@ -653,17 +653,19 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
 
 // ------------------------------------------------- fused HS step (DIA-VI)
 // The scalar step at the top of a fused launch -- the folded k_xpay_xf's
-// logic (cg.c:125-129): r.r of the last r-update (k_update_rf's canonical
-// last-arriver sum, st->rr_new), the stop test, beta; every thread computes
-// it from the same state, workgroup 0 publishes.  A kernel never writes a
-// state field its own workgroups read; the stop flag follows the folded
-// path's protocol (1 here, 2 by the next k_update_rf).
+// logic (cg.c:125-129): r.r of the last r-update (*rr_new: k_update_rf's
+// canonical last-arriver sum, or its all-reduce over the ranks), the stop
+// test, beta; every thread computes it from the same state, workgroup 0 of
+// the publishing launch writes it back.  A kernel never writes a state field
+// its own workgroups read; the stop flag follows the folded path's protocol
+// (1 here, 2 by the next k_update_rf).
 struct FuseStep {
   bool first, stop;
   double alpha, beta;
 };
 
-__device__ __forceinline__ FuseStep fuse_step(CgState *st, double *hist) {
+__device__ __forceinline__ FuseStep fuse_step(CgState *st, double *hist, const double *rr_new_p,
+                                              bool publish) {
   FuseStep f;
   const int k = st->k_u;
   f.first = k < 0;
@@ -671,10 +673,10 @@ __device__ __forceinline__ FuseStep fuse_step(CgState *st, double *hist) {
   f.beta = 0.0;
   f.stop = false;
   if (!f.first) {
-    const double rr_new = st->rr_new;
+    const double rr_new = *rr_new_p;
     f.stop = k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb);
     f.beta = rr_new / st->rr_u;  // cg.c:129
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (publish && blockIdx.x == 0 && threadIdx.x == 0) {
       if (k < st->hist_cap) hist[k] = rr_new;
       if (f.stop) {
         st->k = k;
@@ -705,16 +707,19 @@ __device__ __forceinline__ typename Pair<T>::type p_next(typename Pair<T>::type 
 // k_spmv_dia's shape (two rows per thread, 512-row slice per workgroup)
 // with the previous iteration's vector update fused in.  p_new of the slice
 // and of its halo rows [s0 - hl, s0 + 512 + hr) is computed ONCE per
-// workgroup into an LDS window (NF pair passes per thread): every diagonal
-// with |d| <= kHaloMax reads p_new from there; the NFAR outermost diagonals
-// on each side (the +-nx*ny planes of a 3-D stencil) gather r and p_old and
-// compute p_new themselves.  Then p_new for the own rows (and every other
-// launch x, below), s = A p_new (the CSR row's order), the p_new.s partial.
-// Bytes per row: 4 code + 8 r + 8 p_old + 8 p_new + 8 s, + 24 (x read and
-// written, p_{k-1} read) every other launch: 48 on average.  Every value
-// is the unfused path's (same roundings): x and the r.r history are
-// bit-identical to SpMV + k_update_rf + k_xpay_xf.
-template <typename T, int NF, int NFAR, bool NT, bool LIST>
+// workgroup into an LDS window (NF pair passes per thread): every "near"
+// diagonal (|d| <= kHaloMax) reads p_new from there; the far ones (the
+// +-nx*ny planes of a 3-D stencil; NFAR >= their count, slots a.fark) gather
+// r and p_old and compute p_new themselves.  GH (a partition's boundary
+// items): a column >= n is a ghost, whose p_new the halo exchange put in the
+// p_new buffer's ghost tail -- read there, element by element, in the window
+// and the far slots.  Then p_new for the own rows (and every other
+// launch x, below), s = A p_new summed in diagonal order (the CSR row's
+// order), the p_new.s partial.  Bytes per row: 1-4 code + 8 r + 8 p_old +
+// 8 p_new + 8 s, + 24 (x read and written, p_{k-1} read) every other
+// launch.  Every value is the unfused path's (same roundings): x and the
+// r.r history are bit-identical to SpMV + k_update_rf + k_xpay_xf.
+template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH>
 __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *win = reinterpret_cast<T *>(dyn_lds);
@@ -724,7 +729,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   const int wi = xcd_block();
   const int s = LIST ? a.items.list[wi] : a.items.first + wi;
   if (f.st->done > 1) return;  // uniform
-  const FuseStep fs = fuse_step(f.st, f.hist);
+  const FuseStep fs = fuse_step(f.st, f.hist, f.rr_new, f.publish != 0);
   const T alpha = (T)fs.alpha, beta = (T)fs.beta;
   const int s0 = s * kDiaSliceRows, r = s0 + 2 * t;
   const int rs = r < a.n ? r : 0;
@@ -736,7 +741,8 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   const bool odd = (k & 1) != 0;
   const bool xup = !fs.first && (odd || fs.stop);
   const T alpha_d = (T)f.st->alpha_def;
-  if (!fs.first && !odd && !fs.stop && blockIdx.x == 0 && t == 0) f.st->alpha_def = fs.alpha;
+  if (f.publish && !fs.first && !odd && !fs.stop && blockIdx.x == 0 && t == 0)
+    f.st->alpha_def = fs.alpha;
   P po = P(), xo = P(), pd = P();
   if (xup) {
     po = ld_pair(f.pold, rs);
@@ -760,57 +766,83 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   unsigned c0, c1;  // the code words of row r / r + 1 (<= 4 bytes: fusable())
   ld_codes(a.dcode, a.cb, r, c0, c1);
   const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
-  // far diagonals: k = 0..NFAR-1 and ndiag-NFAR..ndiag-1 (ascending offsets)
-  P rf[2 * NFAR + 1], pf[2 * NFAR + 1];
+  // far diagonals: slot q holds diagonal a.fark[q] (-1: an unused slot)
+  constexpr int NS = NFAR > 0 ? NFAR : 1;
+  P rf[NS], pf[NS], gf[NS];
+  int fb[NS];
 #pragma unroll
-  for (int q = 0; q < 2 * NFAR; ++q) {
-    const int k = q < NFAR ? q : a.ndiag - 2 * NFAR + q;
-    const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
-    const int b = n0 != a.cmask[k] || n1 != a.cmask[k] ? r + a.doff[k] : rs;
+  for (int q = 0; q < NFAR; ++q) {
+    const int kq = a.fark[q];
+    int b = rs;
+    if (kq >= 0) {
+      const unsigned n0 = fld(a, c0, kq), n1 = fld(a, c1, kq);
+      if (n0 != a.cmask[kq] || n1 != a.cmask[kq]) b = r + a.doff[kq];
+    }
+    fb[q] = b;
     rf[q] = ld_pair(f.r, b);
     pf[q] = ld_pair(f.pold, b);
+    if (GH) gf[q] = ld_pair((const T *)f.pnew, b);
   }
   // the window: p_new of rows w0 + i, i < wn (pairs; rows outside [0, ncols)
   // are loaded from a clamped address and never read)
   const int w0 = s0 - a.hl, wn = kDiaSliceRows + a.hl + a.hr;
-  P wr[NF], wp[NF];
+  P wr[NF], wp[NF], wg[NF];
+  int wj[NF];
 #pragma unroll
   for (int q = 0; q < NF; ++q) {
     const int j = min(max(w0 + 2 * t + q * 2 * 256, -1), a.ncols - 1);
+    wj[q] = j;
     wr[q] = ld_pair(f.r, j);
     wp[q] = ld_pair(f.pold, j);
+    if (GH) wg[q] = ld_pair((const T *)f.pnew, j);
   }
   __builtin_amdgcn_sched_barrier(0);  // every load above is in flight before the first use
+  // p_new of a pair at column j: r + beta p_old, or the received ghost value
+  auto pnext_at = [&](P rv, P pv, P gv, int j) {
+    P o = fs.first ? rv : p_next<T>(rv, pv, beta);
+    if (GH) {
+      if (j >= a.n) o.x = gv.x;
+      if (j + 1 >= a.n) o.y = gv.y;
+    }
+    return o;
+  };
 #pragma unroll
   for (int q = 0; q < NF; ++q) {
     const int i = 2 * t + q * 2 * 256;
-    const P pn = fs.first ? wr[q] : p_next<T>(wr[q], wp[q], beta);
+    const P pn = pnext_at(wr[q], wp[q], wg[q], wj[q]);
     if (i < wn) win[i] = pn.x;
     if (i + 1 < wn) win[i + 1] = pn.y;
   }
+  P pk[NS];
+#pragma unroll
+  for (int q = 0; q < NFAR; ++q) pk[q] = pnext_at(rf[q], pf[q], gf[q], fb[q]);
   if (t < a.ndiag * 16) lv[t] = tv;
   __syncthreads();
-  T a0 = T(0), a1 = T(0);
-  auto add = [&](int k, T v0, T v1) {
-    const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
-    const T p0 = lv[k * 16 + n0] * v0, p1 = lv[k * 16 + n1] * v1;
-    a0 = n0 != a.cmask[k] ? a0 + p0 : a0;
-    a1 = n1 != a.cmask[k] ? a1 + p1 : a1;
-  };
-#pragma unroll
-  for (int q = 0; q < NFAR; ++q) {
-    const P pk = fs.first ? rf[q] : p_next<T>(rf[q], pf[q], beta);
-    add(q, pk.x, pk.y);
-  }
+  // s = A p_new in diagonal order: near diagonals from the window, far ones
+  // from their slot (the number of far diagonals before k)
   const int rw = r - w0;
-  for (int k = NFAR; k < a.ndiag - NFAR; ++k) {
-    const int i = rw + a.doff[k];
-    add(k, win[i], win[i + 1]);
-  }
+  T a0 = T(0), a1 = T(0);
 #pragma unroll
-  for (int q = NFAR; q < 2 * NFAR; ++q) {
-    const P pk = fs.first ? rf[q] : p_next<T>(rf[q], pf[q], beta);
-    add(a.ndiag - 2 * NFAR + q, pk.x, pk.y);
+  for (int kk = 0; kk < kDiaMax; ++kk) {
+    if (kk < a.ndiag) {
+      T v0, v1;
+      if ((a.near >> kk) & 1u) {
+        const int i = rw + a.doff[kk];
+        v0 = win[i];
+        v1 = win[i + 1];
+      } else {
+        const int slot = __builtin_popcount(~a.near & ((1u << kk) - 1u));
+        P v = pk[0];
+#pragma unroll
+        for (int q = 1; q < NFAR; ++q) v = slot == q ? pk[q] : v;
+        v0 = v.x;
+        v1 = v.y;
+      }
+      const unsigned n0 = fld(a, c0, kk), n1 = fld(a, c1, kk);
+      const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
+      a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
+      a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
+    }
   }
   const T pn0 = win[rw], pn1 = win[rw + 1];
   st_pair(a.y, r, a.n, a0, a1, NT);
@@ -822,6 +854,30 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
   }
   epi_store<4>(dot, a.part, a.fin);
+}
+
+// The send rows of p_new for the fused partitioned step: p_new = r + beta
+// p_old at the rows the neighbours gather (the unfused path packs p after
+// k_xpay_xf; the fused step computes p inside the SpMV launch, after the
+// halo is needed).  Same roundings as p_next.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_pnext(int n_send, const int *__restrict__ idx,
+                                                    const T *__restrict__ r,
+                                                    const T *__restrict__ pold,
+                                                    T *__restrict__ out, const CgState *st,
+                                                    const double *rr_new) {
+  const int k = st->k_u;
+  const bool first = k < 0;
+  const T beta = first ? T(0) : (T)(*rr_new / st->rr_u);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n_send; i += gridDim.x * 256) {
+    const int j = idx[i];
+    if (first) {
+      out[i] = r[j];
+    } else {
+      const T b = beta * pold[j];
+      out[i] = r[j] + b;
+    }
+  }
 }
 
 // -------------------------------------------------------------- k_stencil
@@ -1723,12 +1779,18 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev)
   return launch_spmv_en<T, false, false>(a, g, st, ev);
 }
 
+template <typename T, int NF, int NFAR, bool GH>
+static const void *fused_kernel_g(bool nt, bool list) {
+  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, GH>))
+            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, GH>));
+}
+
 template <typename T, int NF, int NFAR>
-static const void *fused_kernel(bool nt, bool list) {
-  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false>))
-            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false>));
+static const void *fused_kernel(bool nt, bool list, bool gh) {
+  return gh ? fused_kernel_g<T, NF, NFAR, true>(nt, list)
+            : fused_kernel_g<T, NF, NFAR, false>(nt, list);
 }
 
 template <typename T>
@@ -1739,20 +1801,21 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
   if (a.layout != L_DIA || a.cb > 4) return hipErrorInvalidValue;
   const int wn = kDiaSliceRows + a.hl + a.hr;
   const int nf = (wn + 511) / 512;
-  const int nfar = a.ndiag - __builtin_popcount(a.near & ((1u << a.ndiag) - 1));
-  if (nfar % 2 || nfar > 4 || nf > 5) return hipErrorInvalidValue;
-  const bool nt = a.nt != 0, l = a.items.list != nullptr;
+  int nfar = 0;
+  for (int q = 0; q < 4; ++q) nfar += a.fark[q] >= 0;
+  if (nf > 5) return hipErrorInvalidValue;
+  const bool nt = a.nt != 0, l = a.items.list != nullptr, gh = f.ghost != 0;
   const void *k = nullptr;
-  switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + nfar / 2) {
-    case 20: k = fused_kernel<T, 2, 0>(nt, l); break;
-    case 21: k = fused_kernel<T, 2, 1>(nt, l); break;
-    case 22: k = fused_kernel<T, 2, 2>(nt, l); break;
-    case 30: k = fused_kernel<T, 3, 0>(nt, l); break;
-    case 31: k = fused_kernel<T, 3, 1>(nt, l); break;
-    case 32: k = fused_kernel<T, 3, 2>(nt, l); break;
-    case 50: k = fused_kernel<T, 5, 0>(nt, l); break;
-    case 51: k = fused_kernel<T, 5, 1>(nt, l); break;
-    case 52: k = fused_kernel<T, 5, 2>(nt, l); break;
+  switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + (nfar == 0 ? 0 : nfar <= 2 ? 2 : 4)) {
+    case 20: k = fused_kernel<T, 2, 0>(nt, l, gh); break;
+    case 22: k = fused_kernel<T, 2, 2>(nt, l, gh); break;
+    case 24: k = fused_kernel<T, 2, 4>(nt, l, gh); break;
+    case 30: k = fused_kernel<T, 3, 0>(nt, l, gh); break;
+    case 32: k = fused_kernel<T, 3, 2>(nt, l, gh); break;
+    case 34: k = fused_kernel<T, 3, 4>(nt, l, gh); break;
+    case 50: k = fused_kernel<T, 5, 0>(nt, l, gh); break;
+    case 52: k = fused_kernel<T, 5, 2>(nt, l, gh); break;
+    case 54: k = fused_kernel<T, 5, 4>(nt, l, gh); break;
     default: return hipErrorInvalidValue;
   }
   void *args[] = {(void *)&a, (void *)&f};
@@ -1791,6 +1854,16 @@ hipError_t launch_update_xr(int n, T *x, const T *p, T *r, const T *s, const CgS
 template <typename T>
 hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid, hipStream_t st) {
   hipLaunchKernelGGL((k_xpay<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n, p, r, stt);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_pack_pnext(int n_send, const int *idx, const T *r, const T *pold, T *out,
+                             const CgState *stt, const double *rr_new, hipStream_t st) {
+  if (n_send <= 0) return hipSuccess;
+  const int grid = std::min((n_send + 255) / 256, 1024);
+  hipLaunchKernelGGL((k_pack_pnext<T>), dim3(grid), dim3(256), 0, st, n_send, idx, r, pold, out,
+                     stt, rr_new);
   return hipGetLastError();
 }
 
@@ -1912,6 +1985,8 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template hipError_t launch_update_xr<T>(int, T *, const T *, T *, const T *, const CgState *,  \
                                           double *, int, hipStream_t);                           \
   template hipError_t launch_xpay<T>(int, T *, const T *, const CgState *, int, hipStream_t);    \
+  template hipError_t launch_pack_pnext<T>(int, const int *, const T *, const T *, T *,          \
+                                           const CgState *, const double *, hipStream_t);        \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
                                           double *, int, hipStream_t, const FinArgs *);          \
   template hipError_t launch_xpay_xf<T>(int, T *, T *, const T *, CgState *, const double *,     \

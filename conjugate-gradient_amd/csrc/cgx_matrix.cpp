@@ -863,20 +863,13 @@ int DevMatrix::items() const {
 
 int DevMatrix::padded_rows() const { return padded_rows_for(n); }
 
+bool DevMatrix::near_diag(int k) const { return std::abs(dia.doff[k]) <= kHaloMax; }
+
 bool DevMatrix::fusable() const {
   if (layout != L_DIA || dia.cbytes > 4) return false;
-  int lfar = 0, rfar = 0;
-  for (int k = 0; k < dia.ndiag; ++k) {
-    if (k > 0 && dia.doff[k] <= dia.doff[k - 1]) return false;  // ascending
-    if (dia.doff[k] < -kHaloMax) {
-      if (k != lfar) return false;  // far ones outermost
-      ++lfar;
-    }
-  }
-  for (int k = dia.ndiag - 1; k >= 0 && dia.doff[k] > kHaloMax; --k) ++rfar;
-  for (int k = lfar; k < dia.ndiag - rfar; ++k)
-    if (std::abs(dia.doff[k]) > kHaloMax) return false;
-  return lfar == rfar && lfar <= 2 && dia.ndiag > 2 * lfar;
+  int nfar = 0;
+  for (int k = 0; k < dia.ndiag; ++k) nfar += !near_diag(k);
+  return nfar <= 4;
 }
 
 std::vector<int> DevMatrix::item_rows() const {
@@ -939,11 +932,15 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
   a.ncols = ncols;
   a.near = 0;
   a.hl = a.hr = 0;
+  int nf = 0;
+  for (int q = 0; q < 4; ++q) a.fark[q] = -1;
   for (int k = 0; k < dia.ndiag; ++k)
-    if (std::abs(dia.doff[k]) <= kHaloMax) {
+    if (near_diag(k)) {
       a.near |= 1u << k;
       a.hl = std::max(a.hl, -dia.doff[k]);
       a.hr = std::max(a.hr, dia.doff[k]);
+    } else if (nf < 4) {
+      a.fark[nf++] = k;
     }
   a.hl = (a.hl + 1) & ~1;  // an even window start: aligned pair loads
   a.n = n;

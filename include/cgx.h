@@ -306,6 +306,8 @@ typedef struct {
                                             hipGraph, 0 not (yet), -1 the
                                             capture failed: eager        */
   int alg;                               /* CGX_ALG_* in use              */
+  int fused;                             /* 1: the fused HS step runs (set
+                                            once the ranks are connected) */
 } cgx_dist_stats;
 
 /* Rank 0 creates the id and distributes it (e.g. torch.distributed). */
@@ -331,6 +333,13 @@ int  cgx_dist_set_rhs(cgx_dist *d, const double *b_local);
  * rank (every part of a local group) must use the same one; on a local
  * group, setting it on part 0 sets the group. */
 int  cgx_dist_set_alg(cgx_dist *d, int alg);
+/* The fused HS step (cgx_solver_set_fused) on every rank whose DIA layout
+ * takes it -- all ranks or none, agreed at connection: the halo carries
+ * p_new = r + beta p_old computed at the send rows, the interior and
+ * boundary k_spmv_dia_h launches replace k_xpay_xf + the SpMV.  On by
+ * default; x and the history are bit-identical to the unfused path.  On a
+ * local group, setting it on part 0 sets the group. */
+int  cgx_dist_set_fused(cgx_dist *d, int on);
 /* hipGraph replay of the iteration batches (RCCL calls included); on by
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
 int  cgx_dist_set_graph(cgx_dist *d, int on);

@@ -289,3 +289,88 @@ def test_local_group_sums_match_solver_bit_exact():
             assert s.run(40) == its == 41
             assert H.same_bits_or_both_nan(x, s.x()), layout
             assert H.same_bits_or_both_nan(hist, s.history(41)), layout
+
+
+def solve_local_fz(rp, col, val, b, P, runs, fused):
+    """A local HS group with the fused step on or off; (its, x, hist) per
+    (maxit, tol) of `runs`, and the partitions' stats."""
+    n = len(rp) - 1
+    parts = cgx.DistSolver.local_group(0, P)
+    out = []
+    try:
+        parts[0].set_alg(cgx.CGX_ALG_HS)
+        parts[0].set_fused(fused)
+        for g, d in enumerate(parts):
+            rb, re_ = cgx.partition_rows(n, P, g)
+            d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+            d.set_rhs(b[rb:re_])
+        for maxit, tol in runs:
+            its = parts[0].run(maxit, tol)
+            out.append((its, np.concatenate([d.x() for d in parts]), parts[0].history(its)))
+        stats = [d.info() for d in parts]
+    finally:
+        parts[0].close()
+    return out, stats
+
+
+@pytest.mark.parametrize("shape,P", [((24, 20, 30), 1), ((24, 20, 30), 2), ((24, 20, 30), 3),
+                                     ((24, 20, 30), 8), ((40, 30, 16), 2), ((40, 30, 16), 4),
+                                     ((40, 30, 24), 8)])
+def test_fused_partitions_bit_identical_to_unfused(shape, P):
+    """The fused partitioned HS step (halo of p_new = r + beta p_old packed
+    at the send rows, k_spmv_dia_h over interior then boundary items, ghost
+    diagonals reading the received p_new, x every other iteration) computes
+    every value of the unfused phases with the same roundings: x, the
+    iteration count and the history are bit-identical at every partition
+    count (24x20x30: +-nx*ny near, read through the LDS window, partitions
+    cutting planes at P = 8; 40x30x16 / x24: +-1200 far, plane-aligned slabs
+    of >= 3 planes with four far diagonals including the ghost faces, as
+    C4's 400^3 slabs)."""
+    rp, col, val = cgx.laplacian3d(*shape)
+    b = np.random.default_rng(3).standard_normal(len(rp) - 1)
+    runs = [(0, 0.0), (1, 0.0), (16, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]
+    fz, st_f = solve_local_fz(rp, col, val, b, P, runs, True)
+    uf, st_u = solve_local_fz(rp, col, val, b, P, runs, False)
+    assert all(s["fused"] == 1 for s in st_f) and all(s["layout_name"] == "dia" for s in st_f)
+    assert all(s["fused"] == 0 for s in st_u)
+    for j, ((i0, x0, h0), (i1, x1, h1)) in enumerate(zip(fz, uf)):
+        assert i0 == i1, j
+        assert H.same_bits_or_both_nan(x0, x1), j
+        assert H.same_bits_or_both_nan(h0, h1), j
+    its, x, _ = fz[-1]
+    assert its < 3000
+    assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 1.01e-10 * np.linalg.norm(b)
+
+
+def test_fused_rccl_one_rank_graph_parity():
+    """The fused step through a 1-rank RCCL communicator: replayed graphs of
+    both p-buffer parities (odd batch remainders) and eager launches give
+    bit-identical x; equal to the unfused communicator's."""
+    rp, col, val = cgx.laplacian3d(24, 20, 30)
+    b = np.random.default_rng(6).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    res = {}
+    for fused, graph in ((True, True), (True, False), (False, True)):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+        try:
+            d.set_alg(cgx.CGX_ALG_HS)
+            d.set_fused(fused)
+            d.set_graph(graph)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            out = []
+            for maxit in (17, 33, 40):
+                its = d.run(maxit, 0.0)
+                out.append((its, d.x(), d.history(its)))
+            its = d.run(3000, 1e-10)
+            out.append((its, d.x(), d.history(its)))
+            assert d.info()["fused"] == (1 if fused else 0)
+            assert d.info()["graph"] == (1 if graph else 0)
+        finally:
+            d.close()
+        res[(fused, graph)] = out
+    for key in ((True, False), (False, True)):
+        for (i0, x0, h0), (i1, x1, h1) in zip(res[(True, True)], res[key]):
+            assert i0 == i1
+            assert H.same_bits_or_both_nan(x0, x1), key
+            assert H.same_bits_or_both_nan(h0, h1), key
