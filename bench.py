@@ -605,7 +605,7 @@ def run_dist(args, wl_name, world, rank, local_rank):
         # per-rank SpMV (interior + boundary launches) on its own layout bytes
         gbs, frac = spmv_roofline(info["spmv_iter_bytes"], spmv_ms)
         roofline = dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=frac,
-                        traffic=None, kernel=KERNELS.get(info["layout_name"], "?") + " (per rank)",
+                        traffic=None, kernel=kernel_name(info) + " (per rank)",
                         algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
                         spmv_us=round(spmv_ms * 1e3, 2),
                         spmv_us_max_over_ranks=round(allmax(spmv_ms) * 1e3, 2),
@@ -622,7 +622,8 @@ def run_dist(args, wl_name, world, rank, local_rank):
             data="synthetic",
             config=dict(workload=wl["desc"], n=sysm["n_global"], rows_per_rank=info["n_loc"],
                         nnz_rank0=info["nnz"], alg=alg, alg_trial_ms_per_iter=trial,
-                        graph=info["graph"], parallelism=f"row-partition x{world} (RCCL)",
+                        graph=info["graph"], fused=info["fused"],
+                        parallelism=f"row-partition x{world} (RCCL)",
                         layout=info["layout_name"], halo_bytes_per_iter_max_rank=halo),
             device_ms_per_step=None if dev is None else round(dev, 4),
             upload_ms=round(upload_ms, 1), iter_bytes_rank0=int(info["iter_bytes"]),

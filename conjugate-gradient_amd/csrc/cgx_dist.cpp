@@ -13,8 +13,8 @@
 //                ghost tail), created at the device's highest priority so its
 //                kernel is dispatched ahead of the interior SpMV's workgroups
 //       st:      SpMV s = A p over INTERIOR work items (no ghost columns)
-//                || halo; wait; SpMV over BOUNDARY items -- its last
-//                workgroup also sums every p.s partial (local p.s)
+//                || halo; wait; SpMV over BOUNDARY items; one finalize
+//                workgroup sums the p.s partials (local p.s)
 //                ncclAllReduce(p.s)
 //                k_update_rf (alpha, r -= alpha s; its last workgroup sums
 //                the r.r partials) -> ncclAllReduce(r.r)
@@ -204,8 +204,9 @@ int init_common(cgx_dist *d, int device) {
   CGX_HIP(hipMalloc((void **)&d->d_st, sizeof(CgState)));
   CGX_HIP(hipMalloc((void **)&d->d_sums, 4 * sizeof(double)));
   CGX_HIP(hipMemset(d->d_sums, 0, 4 * sizeof(double)));
-  CGX_HIP(hipMalloc((void **)&d->d_tick, 4 * sizeof(unsigned)));
-  CGX_HIP(hipMemset(d->d_tick, 0, 4 * sizeof(unsigned)));
+  // two ticket regions: the SpMV's local sums, k_update_rf's
+  CGX_HIP(hipMalloc((void **)&d->d_tick, 2 * kTickRegion * sizeof(unsigned)));
+  CGX_HIP(hipMemset(d->d_tick, 0, 2 * kTickRegion * sizeof(unsigned)));
   CGX_HIP(hipHostMalloc((void **)&d->h_st, sizeof(CgState), hipHostMallocDefault));
   d->d_gsums = d->d_sums + 2;
   return 0;
@@ -500,21 +501,18 @@ int phase_halo(cgx_dist *d) {
 }
 
 // SpMV over interior items (overlapping the halo), then boundary items; with
-// a transport, the last launch's last workgroup writes the local sums (HS:
-// p.s -> sums[0]; CG1: gamma, delta -> sums[0..1]).
+// a transport, one k_finalize workgroup sums the partials in the canonical
+// order into the local sums (HS: p.s -> sums[0]; CG1: gamma, delta ->
+// sums[0..1]).  (An in-kernel last-arriver sum costs every one of the
+// SpMV's ~15 K workgroups a drained store and a device-scope atomic before
+// it may retire: 70 us on an 8 M-row slab, against ~5 us for the launch.)
 int phase_spmv(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
   const int np = d->g_int + d->g_bnd;
-  FinArgs fin{};
-  if (!solo(d) && np > 0) {
-    if (d->alg == CGX_ALG_HS) fin = FinArgs{d->d_tick, d->d_pb, np, nullptr, 0, d->d_sums};
-    else fin = FinArgs{d->d_tick, d->d_pa, d->vec_grid, d->d_pb, np, d->d_sums};
-  }
-  const bool bnd_last = d->g_bnd > 0;
   // rec: kernel timing events (hipExtLaunchKernel) of the two launches; an
   // empty launch records both of its events on the stream instead
-  auto launch = [&](const Items &it, double *part, bool last, int e) -> hipError_t {
+  auto launch = [&](const Items &it, double *part, int e) -> hipError_t {
     LaunchEv ev;
     if (rec) ev = LaunchEv{d->spmv_ev[d->ev_i + e], d->spmv_ev[d->ev_i + e + 1]};
     if (it.count == 0) {
@@ -525,10 +523,9 @@ int phase_spmv(cgx_dist *d) {
       return hipSuccess;
     }
     SpmvArgs<double> a = d->A.args<double>(spmv_x(d), spmv_y(d), part, &d->d_st->done, it);
-    if (last) a.fin = fin;
     if (fz(d)) {
-      // the first non-empty launch publishes the scalar step
-      // boundary items (e == 2) read ghost columns' p_new from the halo
+      // the first non-empty launch publishes the scalar step; boundary
+      // items (e == 2) read ghost columns' p_new from the halo
       const int pub = (e == 0 || d->it_int.count == 0) ? 1 : 0;
       const FuseArgs<double> f{d->d_x, p_old(d), p_new(d), d->d_r, d->d_st, d->d_hist,
                                rr_new_src(d), pub, e == 2 ? 1 : 0};
@@ -536,15 +533,17 @@ int phase_spmv(cgx_dist *d) {
     }
     return launch_spmv<double>(a, d->st, ev);
   };
-  CGX_HIP(launch(d->it_int, d->d_pb, !bnd_last, 0));
+  CGX_HIP(launch(d->it_int, d->d_pb, 0));
   if (!solo(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
-  CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, bnd_last, 2));
+  CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, 2));
   if (rec) d->ev_i += 4;
   if (solo(d)) return 0;
-  if (np == 0)  // no rows here: the local sums are those of empty sets
-    CGX_HIP(launch_finalize(d->alg == CGX_ALG_HS ? FIN_SUM : FIN_SUM2, d->d_pa,
-                            d->alg == CGX_ALG_HS ? 0 : d->vec_grid, d->alg == CGX_ALG_HS ? nullptr : d->d_pb, 0,
-                            d->d_st, d->d_hist, d->d_sums, d->st));
+  if (d->alg == CGX_ALG_HS)
+    CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
+                            d->st));
+  else
+    CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, d->vec_grid, d->d_pb, np, d->d_st, d->d_hist,
+                            d->d_sums, d->st));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
@@ -594,7 +593,7 @@ int hs_alpha(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const int gf = d->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
   if (solo(d)) {
-    const FinArgs fin{d->d_tick + 1, d->d_pa, 4 * gf, nullptr, 0, &d->d_st->rr_new};
+    const FinArgs fin{d->d_tick + kTickRegion, d->d_pa, 4 * gf, nullptr, 0, &d->d_st->rr_new};
     CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_pb,
                                      d->g_int + d->g_bnd, d->d_pa, gf, d->st,
                                      fz(d) ? &fin : nullptr));
@@ -602,7 +601,7 @@ int hs_alpha(cgx_dist *d) {
   }
   int rc = allreduce(d, 0, 1);
   if (rc) return rc;
-  const FinArgs fin{d->d_tick + 1, d->d_pa, 4 * gf, nullptr, 0, d->d_sums + 1};
+  const FinArgs fin{d->d_tick + kTickRegion, d->d_pa, 4 * gf, nullptr, 0, d->d_sums + 1};
   CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_gsums, 1, d->d_pa, gf,
                                    d->st, &fin));  // cg.c:113, 118-123
   CGX_HIP(hipEventRecord(d->ev_sums2, d->st));
@@ -775,7 +774,7 @@ int run_phases(Group *g, bool init, long long iters) {
 int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
   for (cgx_dist *d : g->parts) {
     CGX_HIP(hipSetDevice(d->device));
-    CGX_HIP(hipMemsetAsync(d->d_tick, 0, 4 * sizeof(unsigned), d->st));
+    CGX_HIP(hipMemsetAsync(d->d_tick, 0, 2 * kTickRegion * sizeof(unsigned), d->st));
     if (hist_cap > d->hist_alloc) {
       if (d->gexec[0]) {  // the captured graph holds the old history pointer
         CGX_HIP(hipStreamSynchronize(d->st));

@@ -164,6 +164,11 @@ struct Items {
 // k_finalize and the folded vector kernels use -- writes out[0] (out[1]) and
 // re-arms the counter.  Replaces a separate k_finalize(FIN_SUM) launch in
 // front of the multi-GPU all-reduces.  cnt == nullptr: off.
+// Tickets: two levels (cgx_kernels.hip take_ticket), cnt[0] for the launch
+// and cnt[1 + g] per group of kTicketGroup workgroups; a ticket region holds
+// kTickRegion counters (grids up to (kTickRegion - 1) * kTicketGroup).
+constexpr int kTicketGroup = 128;
+constexpr int kTickRegion = 4096;
 struct FinArgs {
   unsigned *cnt;
   const double *pa;

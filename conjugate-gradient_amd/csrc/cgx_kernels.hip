@@ -79,13 +79,24 @@ __device__ __forceinline__ void publish(double *slot, double v) {
 __device__ __forceinline__ double ld_pub(const double *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool take_ticket(unsigned *cnt, unsigned n) {
+__device__ __forceinline__ bool take_ticket1(unsigned *cnt, unsigned n) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t != n - 1) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
+}
+
+// Two levels, so no counter sees more than kTicketGroup (or the group
+// count) device-scope atomics per launch: one counter per group of
+// kTicketGroup consecutive workgroups (cnt[1 + g]), whose last arriver
+// takes the launch's ticket (cnt[0]).  A single counter serialised every
+// workgroup's atomic: ~10 ns each, 150 us for a 15,625-slice SpMV.
+__device__ __forceinline__ bool take_ticket(unsigned *cnt, unsigned n) {
+  const unsigned g = blockIdx.x / kTicketGroup, ng = (n + kTicketGroup - 1) / kTicketGroup;
+  const unsigned gs = min((unsigned)kTicketGroup, n - g * kTicketGroup);
+  return take_ticket1(cnt + 1 + g, gs) && take_ticket1(cnt, ng);
 }
 
 // sum_parts<1024>'s result (below) computed by a BS-thread workgroup

@@ -412,7 +412,7 @@ int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
   s->h_st->max_iter = maxit;
   s->h_st->hist_cap = std::min(hist_cap, s->hist_alloc);
   CGX_HIP(hipMemcpyAsync(s->d_st, s->h_st, sizeof(CgState), hipMemcpyHostToDevice, s->stream));
-  CGX_HIP(hipMemsetAsync(s->d_tick, 0, 16, s->stream));
+  CGX_HIP(hipMemsetAsync(s->d_tick, 0, kTickRegion * sizeof(unsigned), s->stream));
   return 0;
 }
 
@@ -622,7 +622,8 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->A.device = device;
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
-      hipMalloc((void **)&s->d_tick, 16) != hipSuccess || hipMemset(s->d_tick, 0, 16) != hipSuccess ||
+      hipMalloc((void **)&s->d_tick, kTickRegion * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(s->d_tick, 0, kTickRegion * sizeof(unsigned)) != hipSuccess ||
       hipHostMalloc((void **)&s->h_st, sizeof(CgState), hipHostMallocDefault) != hipSuccess) {
     cgx::set_error("cgx_solver_create: stream/state allocation failed");
     cgx_solver_destroy(s);

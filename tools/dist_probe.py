@@ -1,0 +1,28 @@
+"""Per-rank iteration time of the partitioned solver on ONE GPU: a 1-rank
+RCCL communicator (the multi-GPU phase code: pack, halo loop with no peers,
+ncclAllReduce) on a slab of C4 (400 x 400 x nz planes, 8M rows at nz = 50 =
+C4's slab at N = 8), HS fused / unfused and CG1, graph-replayed."""
+import sys, time
+sys.path.insert(0, "conjugate-gradient_amd")
+import numpy as np, cgx
+
+nz = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+rp, col, val = cgx.laplacian3d(400, 400, nz)
+n = len(rp) - 1
+b = np.ones(n)
+for name, alg, fused in (("hs_fused", cgx.CGX_ALG_HS, True), ("hs", cgx.CGX_ALG_HS, False),
+                         ("cg1", cgx.CGX_ALG_CG1, False)):
+    d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+    try:
+        d.set_alg(alg)
+        d.set_fused(fused)
+        d.set_matrix(n, rp, col, val)
+        d.set_rhs(b)
+        d.bench_prepare(5)
+        ms, _ = d.bench_run(100)
+        _, sp = d.bench_run(30, graph=False, spmv_events=True)
+        i = d.info()
+        print("%-9s n %d  %.1f us/iter  spmv(launches) %.1f us  fused %d layout %s" %
+              (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["layout"]), flush=True)
+    finally:
+        d.close()
