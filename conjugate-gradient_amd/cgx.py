@@ -182,6 +182,18 @@ _SIGS = {
 _lib = None
 
 
+CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON = 0, 1, 2
+
+
+def fuse_mode(mode):
+    """cgx_*_set_fused mode from "auto" / True / False (or the constant)."""
+    if isinstance(mode, str):
+        return {"auto": CGX_FUSE_AUTO, "on": CGX_FUSE_ON, "off": CGX_FUSE_OFF}[mode]
+    if isinstance(mode, bool):
+        return CGX_FUSE_ON if mode else CGX_FUSE_OFF
+    return int(mode)
+
+
 def lib():
     """Load libcgx.so (fails loudly if it has not been built)."""
     global _lib
@@ -288,7 +300,7 @@ class Solver:
     """Device-resident CG solver (cgx_solver_*)."""
 
     def __init__(self, device=0, mode=CGX_MODE_FAST, alg=CGX_ALG_HS, layout=CGX_LAYOUT_AUTO,
-                 fused=True):
+                 fused="auto"):
         self._h = _vp()
         check(lib().cgx_solver_create(device, ctypes.byref(self._h)), "cgx_solver_create")
         self.set_mode(mode, alg)
@@ -317,9 +329,10 @@ class Solver:
     def set_mode(self, mode, alg=CGX_ALG_HS):
         check(lib().cgx_solver_set_mode(self._h, mode, alg), "set_mode")
 
-    def set_fused(self, on):
-        """Fused HS step on DIA layouts (cgx_solver_set_fused)."""
-        check(lib().cgx_solver_set_fused(self._h, 1 if on else 0), "set_fused")
+    def set_fused(self, mode):
+        """Fused HS step on DIA layouts (cgx_solver_set_fused): "auto",
+        True (wherever the layout takes it) or False."""
+        check(lib().cgx_solver_set_fused(self._h, fuse_mode(mode)), "set_fused")
 
     def set_layout(self, layout):
         """CGX_LAYOUT_* (or its name) for the next set_matrix / gen_laplacian."""
@@ -649,9 +662,9 @@ class DistSolver:
     def set_graph(self, on):
         check(lib().cgx_dist_set_graph(self._h, 1 if on else 0), "dist_set_graph")
 
-    def set_fused(self, on):
-        """The fused HS step where every rank's DIA layout takes it."""
-        check(lib().cgx_dist_set_fused(self._h, 1 if on else 0), "dist_set_fused")
+    def set_fused(self, mode):
+        """The fused HS step on all ranks or none: "auto", True, False."""
+        check(lib().cgx_dist_set_fused(self._h, fuse_mode(mode)), "dist_set_fused")
 
     def run(self, maxit, tol=0.0):
         it = ctypes.c_int(0)

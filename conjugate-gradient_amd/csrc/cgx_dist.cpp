@@ -68,6 +68,7 @@ struct Group {
   std::vector<cgx_dist *> parts;    // RCCL mode: just this rank
   const double **d_srcs = nullptr;  // local mode: every part's d_sums
   bool connected = false;
+  bool fz_known = false;  // fz_all decided for the current matrices and fuse modes
 };
 
 }  // namespace
@@ -94,7 +95,7 @@ struct cgx_dist {
          *d_w = nullptr;
   double *d_p2 = nullptr;  // fused step: the second p buffer (with ghost tail)
   int pbuf = 0;            // fused step: which buffer holds p_old (0: d_p)
-  bool fuse = true;        // cgx_dist_set_fused
+  int fuse = CGX_FUSE_AUTO;  // cgx_dist_set_fused
   bool fz_all = false;     // every partition's layout takes the fused step (ensure_connected)
   int *d_send_idx = nullptr;
   double *d_sendbuf = nullptr;
@@ -154,7 +155,13 @@ void drop_graph(cgx_dist *d) {
 
 // The fused HS step (k_spmv_dia_h) runs when every partition's layout
 // takes it (decided once per connection: the ranks' phase sequences match).
-bool fz(const cgx_dist *d) { return d->fuse && d->fz_all && d->alg == CGX_ALG_HS; }
+bool fz(const cgx_dist *d) { return d->fz_all && d->alg == CGX_ALG_HS; }
+
+// this partition takes the fused step (cgx_solver.cpp fused(): auto needs a
+// working set beyond the Infinity Cache)
+bool part_fusable(const cgx_dist *d) {
+  return d->fuse != CGX_FUSE_OFF && d->A.fusable() && (d->fuse == CGX_FUSE_ON || d->A.nt);
+}
 
 void free_system(cgx_dist *d) {
   drop_graph(d);
@@ -419,28 +426,38 @@ int agree_fusable(cgx_dist *d, int mine, int *all) {
   return 0;
 }
 
-int ensure_connected(Group *g) {
-  if (g->connected) return 0;
-  for (cgx_dist *d : g->parts)
-    if (!d->have_matrix) {
-      set_error("dist: every partition needs set_matrix before solving");
-      return CGX_EINVAL;
-    }
-  int rc;
+// The fused step's group decision (all partitions or none), once per
+// connection and after every cgx_dist_set_fused; collective over RCCL.
+int ensure_fused_known(Group *g) {
+  if (g->fz_known) return 0;
   if (g->parts[0]->local) {
-    if ((rc = connect_local(g))) return rc;
     bool all = true;
-    for (cgx_dist *d : g->parts) all = all && d->A.fusable();
+    for (cgx_dist *d : g->parts) all = all && part_fusable(d);
     for (cgx_dist *d : g->parts) d->fz_all = all;
-    return 0;
+  } else {
+    cgx_dist *d = g->parts[0];
+    int all = 0;
+    int rc = agree_fusable(d, part_fusable(d) ? 1 : 0, &all);
+    if (rc) return rc;
+    d->fz_all = all != 0;
   }
-  cgx_dist *d = g->parts[0];
-  if ((rc = connect_rccl(d))) return rc;
-  int all = 0;
-  if ((rc = agree_fusable(d, d->A.fusable() ? 1 : 0, &all))) return rc;
-  d->fz_all = all != 0;
-  g->connected = true;
+  g->fz_known = true;
   return 0;
+}
+
+int ensure_connected(Group *g) {
+  if (!g->connected) {
+    for (cgx_dist *d : g->parts)
+      if (!d->have_matrix) {
+        set_error("dist: every partition needs set_matrix before solving");
+        return CGX_EINVAL;
+      }
+    int rc = g->parts[0]->local ? connect_local(g) : connect_rccl(g->parts[0]);
+    if (rc) return rc;
+    g->connected = true;
+    g->fz_known = false;
+  }
+  return ensure_fused_known(g);
 }
 
 // ---------------------------------------------------------- phase helpers
@@ -1034,16 +1051,18 @@ int cgx_dist_set_layout(cgx_dist *d, int layout) {
   return 0;
 }
 
-int cgx_dist_set_fused(cgx_dist *d, int on) {
-  if (!d || (d->local && !d->owns_group)) return CGX_EINVAL;
+int cgx_dist_set_fused(cgx_dist *d, int mode) {
+  if (!d || (d->local && !d->owns_group) || mode < CGX_FUSE_OFF || mode > CGX_FUSE_ON)
+    return CGX_EINVAL;
   for (cgx_dist *o : d->group->parts) {
     if (o->gexec[0]) {
       (void)hipStreamSynchronize(o->st);
       drop_graph(o);
     }
-    o->fuse = on != 0;
+    o->fuse = mode;
     o->bench_ready = false;
   }
+  d->group->fz_known = false;
   return 0;
 }
 

@@ -158,15 +158,22 @@ typedef struct {
 int  cgx_solver_create(int device, cgx_solver **out);
 void cgx_solver_destroy(cgx_solver *s);
 int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
-/* The HS iteration in fast mode on a DIA layout with <= 8 diagonals fuses
- * the vector update into the SpMV (default on): one launch does the
- * previous iteration's p = r + beta p (cg.c:131-132) -- p of its rows and
- * their in-plane halo computed once into an LDS window -- then s = A p; the
- * next launch updates r (cg.c:118-123).  x += alpha p (cg.c:115-116) runs
- * every other launch for two iterations (same roundings, in order).  Two
- * launches per iteration instead of three, 16 B per row less traffic; x and
- * the r.r history are bit-identical to the unfused path (on = 0). */
-int  cgx_solver_set_fused(cgx_solver *s, int on);
+/* The HS iteration in fast mode on a DIA layout (<= 4-byte row words, <= 4
+ * diagonals with |d| > 1024) can fuse the vector update into the SpMV: one
+ * launch does the previous iteration's p = r + beta p (cg.c:131-132) -- p of
+ * its rows and their in-plane halo computed once into an LDS window -- then
+ * s = A p; the next launch updates r (cg.c:118-123).  x += alpha p
+ * (cg.c:115-116) runs every other launch for two iterations (same roundings,
+ * in order).  Two launches per iteration instead of three, 12 B per row less
+ * traffic; x and the r.r history are bit-identical to the unfused path.
+ * mode: CGX_FUSE_OFF, CGX_FUSE_AUTO (default: where the layout takes it and
+ * the working set exceeds the 256 MiB Infinity Cache -- cache-resident
+ * systems are latency-bound and run faster unfused), CGX_FUSE_ON (wherever
+ * the layout takes it). */
+#define CGX_FUSE_OFF  0
+#define CGX_FUSE_AUTO 1
+#define CGX_FUSE_ON   2
+int  cgx_solver_set_fused(cgx_solver *s, int mode);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);
 /* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.
@@ -333,13 +340,13 @@ int  cgx_dist_set_rhs(cgx_dist *d, const double *b_local);
  * rank (every part of a local group) must use the same one; on a local
  * group, setting it on part 0 sets the group. */
 int  cgx_dist_set_alg(cgx_dist *d, int alg);
-/* The fused HS step (cgx_solver_set_fused) on every rank whose DIA layout
- * takes it -- all ranks or none, agreed at connection: the halo carries
+/* The fused HS step (cgx_solver_set_fused modes) on all ranks or none --
+ * agreed collectively at the next run / bench_prepare: the halo carries
  * p_new = r + beta p_old computed at the send rows, the interior and
- * boundary k_spmv_dia_h launches replace k_xpay_xf + the SpMV.  On by
- * default; x and the history are bit-identical to the unfused path.  On a
- * local group, setting it on part 0 sets the group. */
-int  cgx_dist_set_fused(cgx_dist *d, int on);
+ * boundary k_spmv_dia_h launches replace k_xpay_xf + the SpMV; x and the
+ * history are bit-identical to the unfused path.  Call on every rank (on a
+ * local group, part 0 sets the group). */
+int  cgx_dist_set_fused(cgx_dist *d, int mode);
 /* hipGraph replay of the iteration batches (RCCL calls included); on by
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
 int  cgx_dist_set_graph(cgx_dist *d, int on);
