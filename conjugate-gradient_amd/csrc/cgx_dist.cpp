@@ -637,8 +637,8 @@ int hs_beta(cgx_dist *d) {
     rr = d->d_gsums + 1;
     nrr = 1;
   }
-  CGX_HIP(launch_xpay_xf<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_st, rr, nrr, d->d_hist,
-                                 gf, d->st));  // cg.c:115-116, 125-132
+  CGX_HIP(launch_xpay_xf<double>(d->n_loc, d->d_x, d->d_p, d->d_p, d->d_r, d->d_st, rr, nrr,
+                                 d->d_hist, gf, d->st));  // cg.c:115-116, 125-132
   return 0;
 }
 

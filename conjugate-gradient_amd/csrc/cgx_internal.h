@@ -301,8 +301,10 @@ template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
                             const FinArgs *fin = nullptr);
+// p -> pn (pn == p: in place, x every iteration; pn != p: x every other
+// iteration, k_xpay_xf)
 template <typename T>
-hipError_t launch_xpay_xf(int n, T *x, T *p, const T *r, CgState *stt,
+hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *stt,
                           const double *rr_part, int nrr, double *hist, int grid,
                           hipStream_t st);
 template <typename T>

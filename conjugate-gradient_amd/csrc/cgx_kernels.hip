@@ -1289,8 +1289,15 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
   }
 }
 
+// pn != p (double-buffered p, the single-GPU solver): x is updated every
+// other iteration, as in the fused step -- an even k defers x += alpha_k p_k
+// (alpha to st->alpha_def), the odd k + 1 adds alpha_{k-1} p_{k-1} (read
+// from pn before p_new overwrites it) and then alpha_k p_k, the same two
+// roundings in order; a stop applies what is pending.  8 B per row less on
+// average, and the SpMV after an even iteration finds half the dirty lines.
+// pn == p: x every iteration, p in place.
 template <typename T>
-__global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, T *__restrict__ p,
+__global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, const T *p, T *pn,
                                                      const T *__restrict__ r,
                                                      CgState *__restrict__ st,
                                                      const double *__restrict__ rr_part, int nrr,
@@ -1303,15 +1310,19 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, T
   constexpr int W = Vec16<T>::W;
   const int nv = n / W;
   const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
-  V pv0 = V(), xv0 = V(), rv0 = V();
+  const int kk = st->k_u;
+  const bool defer = pn != p, odd = (kk & 1) != 0;
+  const bool xpre = !defer || odd;  // x (and p_{k-1}) needed unless a stop says so
+  V pv0 = V(), rv0 = V(), xv0 = V(), pd0 = V();
   if (gid < nv) {
     pv0 = reinterpret_cast<const V *>(p)[gid];
-    xv0 = reinterpret_cast<const V *>(x)[gid];
     rv0 = reinterpret_cast<const V *>(r)[gid];
+    if (xpre) xv0 = reinterpret_cast<const V *>(x)[gid];
+    if (xpre && defer) pd0 = reinterpret_cast<const V *>(pn)[gid];
   }
   const double rr_new = sum_parts<kFoldBS>(rr_part, nrr, red);
   if (threadIdx.x == 0) {
-    const int k = st->k_u;
+    const int k = kk;
     const bool stop = k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb);
     const double beta = rr_new / st->rr_u;  // cg.c:129
     bcast = beta;
@@ -1327,46 +1338,64 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, T
         st->rr_x = rr_new;
         st->k = k + 1;
         st->k_x = k + 1;
+        if (defer && !odd) st->alpha_def = st->alpha;
       }
     }
   }
   __syncthreads();
   const bool stop = bstop != 0;
-  const T alpha = (T)st->alpha, beta = (T)bcast;
-  auto step = [&](int i, V pv, V xv, const V rv) {
+  const bool xup = !defer || odd || stop, two = defer && odd;
+  const T alpha = (T)st->alpha, beta = (T)bcast, alpha_d = (T)st->alpha_def;
+  auto step = [&](int i, V pv, const V rv, bool pre) {
+    if (xup) {
+      V xv = pre && xpre ? xv0 : reinterpret_cast<const V *>(x)[i];
+      if (two) {
+        const V pd = pre ? pd0 : reinterpret_cast<const V *>(pn)[i];
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const T ap = alpha * pv[j];
-      xv[j] = xv[j] + ap;
+        for (int j = 0; j < W; ++j) {
+          const T ap = alpha_d * pd[j];
+          xv[j] = xv[j] + ap;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T ap = alpha * pv[j];
+        xv[j] = xv[j] + ap;
+      }
+      reinterpret_cast<V *>(x)[i] = xv;
     }
-    reinterpret_cast<V *>(x)[i] = xv;
     if (!stop) {
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         const T bp = beta * pv[j];
         pv[j] = rv[j] + bp;
       }
-      reinterpret_cast<V *>(p)[i] = pv;
+      reinterpret_cast<V *>(pn)[i] = pv;
     }
   };
   int i = gid;
   if (i < nv) {
-    step(i, pv0, xv0, rv0);
+    step(i, pv0, rv0, true);
     i += stride;
   }
-  for (; i < nv; i += stride) {
-    const V pv = reinterpret_cast<const V *>(p)[i];
-    const V xv = reinterpret_cast<const V *>(x)[i];
-    step(i, pv, xv, stop ? V() : reinterpret_cast<const V *>(r)[i]);
-  }
+  for (; i < nv; i += stride)
+    step(i, reinterpret_cast<const V *>(p)[i], stop ? V() : reinterpret_cast<const V *>(r)[i],
+         false);
   if (gid == 0)
     for (int k = nv * W; k < n; ++k) {
       const T pk = p[k];
-      const T ap = alpha * pk;
-      x[k] = x[k] + ap;
+      if (xup) {
+        T xk = x[k];
+        if (two) {
+          const T ad = alpha_d * pn[k];
+          xk = xk + ad;
+        }
+        const T ap = alpha * pk;
+        x[k] = xk + ap;
+      }
       if (!stop) {
         const T bp = beta * pk;
-        p[k] = r[k] + bp;
+        pn[k] = r[k] + bp;
       }
     }
 }
@@ -1889,10 +1918,10 @@ hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double 
 }
 
 template <typename T>
-hipError_t launch_xpay_xf(int n, T *x, T *p, const T *r, CgState *stt, const double *rr_part,
-                          int nrr, double *hist, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((k_xpay_xf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, r, stt, rr_part,
-                     nrr, hist);
+hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *stt,
+                          const double *rr_part, int nrr, double *hist, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((k_xpay_xf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, pn, r, stt,
+                     rr_part, nrr, hist);
   return hipGetLastError();
 }
 
@@ -2000,8 +2029,8 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                                            const CgState *, const double *, hipStream_t);        \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
                                           double *, int, hipStream_t, const FinArgs *);          \
-  template hipError_t launch_xpay_xf<T>(int, T *, T *, const T *, CgState *, const double *,     \
-                                        int, double *, int, hipStream_t);                        \
+  template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \
+                                        const double *, int, double *, int, hipStream_t);        \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *, const T *, const CgState *,  \
                                            double *, int, hipStream_t);                          \
   template hipError_t launch_dot_seq<T>(int, const T *, const T *, double *, const int *,        \

@@ -165,6 +165,12 @@ bool fused(const cgx_solver *s) {
          s->A.fusable() && (s->fuse == CGX_FUSE_ON || s->A.nt);
 }
 
+// p double-buffered, its buffers alternating per iteration: the fused step,
+// and the unfused folded HS step (k_xpay_xf's every-other-iteration x).
+bool alternating(const cgx_solver *s) {
+  return s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST;
+}
+
 void free_system(cgx_solver *s) {
   drop_graph(s);
   s->A.release();
@@ -288,6 +294,11 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   }
   if (s->alg == CGX_ALG_HS) {
     const bool exact = s->mode == CGX_MODE_EXACT;
+    T *pn = p;  // exact mode: p in place
+    if (alternating(s)) {
+      p = (T *)(s->pbuf ? s->d_p2 : s->d_p);
+      pn = (T *)(s->pbuf ? s->d_p : s->d_p2);
+    }
     CGX_HIP(s->A.spmv<T>(p, sv, exact ? nullptr : s->d_pa, &s->d_st->done, s->A.all_items(), st,
                          &np, LaunchEv{ev0, ev1}));  // cg.c:111
     if (exact) {
@@ -302,7 +313,8 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     } else {
       const int gf = s->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
       CGX_HIP(launch_update_rf<T>(n, r, sv, s->d_st, s->d_pa, np, s->d_pb, gf, st));
-      CGX_HIP(launch_xpay_xf<T>(n, x, p, r, s->d_st, s->d_pb, 4 * gf, s->d_hist, gf, st));
+      CGX_HIP(launch_xpay_xf<T>(n, x, p, pn, r, s->d_st, s->d_pb, 4 * gf, s->d_hist, gf, st));
+      s->pbuf ^= 1;
     }
   } else {
     CGX_HIP(launch_cg1_update<T>(n, x, p, r, sv, w, s->d_st, s->d_pa, s->vec_grid, st));
@@ -337,11 +349,11 @@ int capture_iters(cgx_solver *s, int count, int parity, hipGraphExec_t *out) {
 
 // The replayed graphs of the current mode / recurrence: graph_batch
 // iterations and one iteration (remainders), captured (not run) once -- for
-// both p-buffer parities when the fused step alternates them.
+// both p-buffer parities when the HS step alternates them (alternating()).
 template <typename T>
 int ensure_graphs(cgx_solver *s) {
   const int key = s->alg * 4 + s->mode * 2 + (fused(s) ? 1 : 0);
-  const int nq = fused(s) ? 2 : 1;
+  const int nq = alternating(s) ? 2 : 1;
   if (s->gexec_key == key) return 0;
   drop_graph(s);
   int rc = 0;
@@ -362,7 +374,7 @@ int enqueue_iters(cgx_solver *s, long long count) {
   if (s->use_graph && count > 0) {
     int rc = ensure_graphs<T>(s);
     if (rc) return rc;
-    const bool alt = fused(s);  // an even batch keeps the p parity, one iteration flips it
+    const bool alt = alternating(s);  // an even batch keeps the p parity, one iteration flips it
     for (; count >= s->graph_batch; count -= s->graph_batch) {
       CGX_HIP(hipGraphLaunch(s->gexec[alt ? s->pbuf : 0], s->stream));
       if (alt && (s->graph_batch & 1)) s->pbuf ^= 1;
