@@ -94,6 +94,9 @@ def parse_args(argv=None):
                     help="N > 1: recurrence (default: a timed trial of both)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="at one rank (under torch.distributed.run --nproc-per-node 1): run the "
+                         "N > 1 path -- parity gate, RCCL communicator, C4 -- on one GPU")
     ap.add_argument("--no-legs", action="store_true",
                     help="N = 1: only the headline solve (no CSR/DC/stencil/C4/e2e legs)")
     return ap.parse_args(argv)
@@ -486,7 +489,7 @@ def gather_x(x_local, n_global, world, rank):
 
 def parity_gate(world, rank, local_rank, uid, tol=1e-10):
     """A small 3-D Laplacian (48 x 48 x 16 N rows) solved across the N ranks
-    to tol with both recurrences over RCCL; rank 0 checks the gathered x
+    to tol with both recurrences (HS unfused and fused) over RCCL; rank 0 checks the gathered x
     against a single-GPU solve of the same system (cgx.Solver, HS), the
     iteration count (within 1) and the true residual (scipy, on the host)."""
     import numpy as np
@@ -502,10 +505,16 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
     try:
         d.set_matrix(n, rp, col, val)
         d.set_rhs(b_full[rb:re_])
-        for name, alg in (("hs", cgx.CGX_ALG_HS), ("cg1", cgx.CGX_ALG_CG1)):
+        # the fused HS step forced on: the timed C4 run takes it (auto), this
+        # small system would not
+        for name, alg, fused in (("hs", cgx.CGX_ALG_HS, False), ("hs_fused", cgx.CGX_ALG_HS, True),
+                                 ("cg1", cgx.CGX_ALG_CG1, False)):
             d.set_alg(alg)
+            d.set_fused(fused)
             its = d.run(5000, tol)
-            res[name] = (its, gather_x(d.x(), n, world, rank), d.info()["graph"])
+            i = d.info()
+            res[name] = (its, gather_x(d.x(), n, world, rank), i["graph"], i["fused"] == int(fused))
+        d.set_fused("auto")
     finally:
         d.close()
     if rank != 0:
@@ -521,10 +530,10 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
                reference="single-GPU cgx.Solver (HS) on rank 0 + true residual (scipy)",
                single_gpu_iters=its1)
     ok = True
-    for name, (its, x, graph) in res.items():
+    for name, (its, x, graph, fused_ok) in res.items():
         rel = float(np.linalg.norm(x - x1) / np.linalg.norm(x1))
         tr = float(np.linalg.norm(b_full - A @ x) / np.linalg.norm(b_full))
-        good = rel <= 1e-9 and abs(its - its1) <= 1 and tr <= 10 * tol
+        good = rel <= 1e-9 and abs(its - its1) <= 1 and tr <= 10 * tol and fused_ok
         ok = ok and good
         out[name] = dict(iters=its, rel_diff=rel, true_rel_residual=tr, graph=graph, ok=good)
     out["ok"] = ok
@@ -645,8 +654,9 @@ def main():
         sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    wl_name = args.workload or ("c3" if world == 1 else "c4")
-    if world == 1:
+    dist_path = world > 1 or args.dist_rehearsal
+    wl_name = args.workload or ("c4" if dist_path else "c3")
+    if not dist_path:
         run_single(args, wl_name)
     else:
         run_dist(args, wl_name, world, rank, local_rank)
