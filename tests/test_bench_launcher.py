@@ -58,3 +58,18 @@ def test_default_workloads():
     assert a.workload is None and a.steps == 100 and a.warmup == 10
     assert bench.WORKLOADS["c4"]["dims"] == (400, 400, 400)
     assert bench.WORKLOADS["c3"]["dims"] == (216, 216, 216)
+
+
+@pytest.mark.parametrize("argv,expect", [(["--gpus", "1"], ("single", "c3")),
+                                         (["--gpus", "1", "--dist-rehearsal"], ("dist", "c4")),
+                                         (["--gpus", "1", "--workload", "c2"], ("single", "c2"))])
+def test_rank_path_selection(monkeypatch, argv, expect):
+    """One rank runs the single-GPU line (C3) unless --dist-rehearsal asks for
+    the N > 1 path (C4 over a 1-rank RCCL communicator)."""
+    seen = {}
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    monkeypatch.setattr(bench, "run_single", lambda a, w: seen.update(path="single", wl=w))
+    monkeypatch.setattr(bench, "run_dist", lambda a, w, *r: seen.update(path="dist", wl=w))
+    bench.main()
+    assert (seen["path"], seen["wl"]) == expect
