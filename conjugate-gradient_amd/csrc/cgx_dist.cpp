@@ -211,9 +211,9 @@ int init_common(cgx_dist *d, int device) {
   CGX_HIP(hipMalloc((void **)&d->d_st, sizeof(CgState)));
   CGX_HIP(hipMalloc((void **)&d->d_sums, 4 * sizeof(double)));
   CGX_HIP(hipMemset(d->d_sums, 0, 4 * sizeof(double)));
-  // two ticket regions: the SpMV's local sums, k_update_rf's
-  CGX_HIP(hipMalloc((void **)&d->d_tick, 2 * kTickRegion * sizeof(unsigned)));
-  CGX_HIP(hipMemset(d->d_tick, 0, 2 * kTickRegion * sizeof(unsigned)));
+  // the ticket region of k_update_rf's local r.r sums
+  CGX_HIP(hipMalloc((void **)&d->d_tick, kTickRegion * sizeof(unsigned)));
+  CGX_HIP(hipMemset(d->d_tick, 0, kTickRegion * sizeof(unsigned)));
   CGX_HIP(hipHostMalloc((void **)&d->h_st, sizeof(CgState), hipHostMallocDefault));
   d->d_gsums = d->d_sums + 2;
   return 0;
@@ -610,7 +610,7 @@ int hs_alpha(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const int gf = d->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
   if (solo(d)) {
-    const FinArgs fin{d->d_tick + kTickRegion, d->d_pa, 4 * gf, nullptr, 0, &d->d_st->rr_new};
+    const FinArgs fin{d->d_tick, d->d_pa, 4 * gf, &d->d_st->rr_new};
     CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_pb,
                                      d->g_int + d->g_bnd, d->d_pa, gf, d->st,
                                      fz(d) ? &fin : nullptr));
@@ -618,7 +618,7 @@ int hs_alpha(cgx_dist *d) {
   }
   int rc = allreduce(d, 0, 1);
   if (rc) return rc;
-  const FinArgs fin{d->d_tick + kTickRegion, d->d_pa, 4 * gf, nullptr, 0, d->d_sums + 1};
+  const FinArgs fin{d->d_tick, d->d_pa, 4 * gf, d->d_sums + 1};
   CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_gsums, 1, d->d_pa, gf,
                                    d->st, &fin));  // cg.c:113, 118-123
   CGX_HIP(hipEventRecord(d->ev_sums2, d->st));
@@ -791,7 +791,7 @@ int run_phases(Group *g, bool init, long long iters) {
 int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
   for (cgx_dist *d : g->parts) {
     CGX_HIP(hipSetDevice(d->device));
-    CGX_HIP(hipMemsetAsync(d->d_tick, 0, 2 * kTickRegion * sizeof(unsigned), d->st));
+    CGX_HIP(hipMemsetAsync(d->d_tick, 0, kTickRegion * sizeof(unsigned), d->st));
     if (hist_cap > d->hist_alloc) {
       if (d->gexec[0]) {  // the captured graph holds the old history pointer
         CGX_HIP(hipStreamSynchronize(d->st));

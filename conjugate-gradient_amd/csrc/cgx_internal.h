@@ -158,12 +158,15 @@ struct Items {
   int count;
 };
 
-// In-kernel local sums ("last arriver"): every workgroup publishes its
-// partial and takes a ticket on *cnt; the last one sums pa[0, na) (and
-// pb[0, nb)) in the canonical order -- sum_parts<1024>'s, the order
-// k_finalize and the folded vector kernels use -- writes out[0] (out[1]) and
-// re-arms the counter.  Replaces a separate k_finalize(FIN_SUM) launch in
-// front of the multi-GPU all-reduces.  cnt == nullptr: off.
+// In-kernel local sums of k_update_rf ("last arriver"): every workgroup
+// publishes its partials and takes a ticket on *cnt; the last one sums
+// pa[0, na) in the canonical order -- sum_parts<1024>'s, the order k_finalize
+// and the folded vector kernels use -- writes out[0] and re-arms the counter
+// (the fused step's r.r, the partitioned solver's local r.r).  Only for
+// grids of a few hundred workgroups: every workgroup drains its stores and
+// takes a device-scope atomic before it retires (an SpMV of 15 K workgroups
+// paid 70 us for it; its local sums are a k_finalize launch).  cnt ==
+// nullptr: off.
 // Tickets: two levels (cgx_kernels.hip take_ticket), cnt[0] for the launch
 // and cnt[1 + g] per group of kTicketGroup workgroups; a ticket region holds
 // kTickRegion counters (grids up to (kTickRegion - 1) * kTicketGroup).
@@ -173,8 +176,6 @@ struct FinArgs {
   unsigned *cnt;
   const double *pa;
   int na;
-  const double *pb;
-  int nb;
   double *out;
 };
 
@@ -198,7 +199,6 @@ void dia_pack(DiaCand &c);
 template <typename T>
 struct SpmvArgs {
   int layout;
-  FinArgs fin;      // epilogue local sum (needs part; see FinArgs)
   const T *x;
   T *y;
   double *part;     // one x[row]*y[row] partial per workgroup (nullptr: none)

@@ -148,31 +148,10 @@ __device__ double canon_sum(const double *pa, int na, double *red16) {
   return s;
 }
 
-// A workgroup's last step when FinArgs is on: publish `mine` (valid in thread
-// 0) at slot, take a ticket; the last workgroup writes the canonical sums.
-template <int BS>
-__device__ void fin_finish(double mine, double *slot, const FinArgs &f) {
-  __shared__ double red16[1024 / kWave];
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    publish(slot, mine);
-    last = take_ticket(f.cnt, gridDim.x);
-  }
-  __syncthreads();
-  if (!last) return;
-  const double sa = canon_sum<BS, true>(f.pa, f.na, red16);
-  double sb = 0.0;
-  if (f.pb) sb = canon_sum<BS, true>(f.pb, f.nb, red16);
-  if (threadIdx.x == 0) {
-    f.out[0] = sa;
-    if (f.pb) f.out[1] = sb;
-  }
-}
-
 // The SpMV epilogue: the workgroup's x[row]*y[row] terms, wave sums added in
-// wave order, one partial per workgroup (and the local sum, FinArgs).
+// wave order, one partial per workgroup.
 template <int WPB>
-__device__ __forceinline__ void epi_store(double dot, double *part, const FinArgs &fin) {
+__device__ __forceinline__ void epi_store(double dot, double *part) {
   __shared__ double red[WPB];
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   dot = wave_sum(dot);
@@ -183,9 +162,8 @@ __device__ __forceinline__ void epi_store(double dot, double *part, const FinArg
     s = red[0];
 #pragma unroll
     for (int w = 1; w < WPB; ++w) s = s + red[w];
-    if (!fin.cnt) part[blockIdx.x] = s;
+    part[blockIdx.x] = s;
   }
-  if (fin.cnt) fin_finish<WPB * kWave>(s, part + blockIdx.x, fin);
 }
 
 // The scalar lines of the recurrence (cg.c:113, 125-129; CG1 analogues) on
@@ -418,7 +396,7 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
       }
     }
   }
-  if (EPI) epi_store<WPB>(dot, a.part, a.fin);
+  if (EPI) epi_store<WPB>(dot, a.part);
 }
 
 // ------------------------------------------------------------- k_spmv_dc
@@ -532,7 +510,7 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
       }
     }
   }
-  if (EPI) epi_store<WPB>(dot, a.part, a.fin);
+  if (EPI) epi_store<WPB>(dot, a.part);
 }
 
 // ------------------------------------------------------------ k_spmv_dia
@@ -659,7 +637,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
     if (r < a.n) dot = (double)xr.x * (double)a0;
     if (r + 1 < a.n) dot = dot + (double)xr.y * (double)a1;
   }
-  if (EPI) epi_store<4>(dot, a.part, a.fin);
+  if (EPI) epi_store<4>(dot, a.part);
 }
 
 // ------------------------------------------------- fused HS step (DIA-VI)
@@ -864,7 +842,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     dot = (double)pn0 * (double)a0;
     if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
   }
-  epi_store<4>(dot, a.part, a.fin);
+  epi_store<4>(dot, a.part);
 }
 
 // The send rows of p_new for the fused partitioned step: p_new = r + beta
@@ -973,7 +951,7 @@ __global__ __launch_bounds__(256) void k_stencil(SpmvArgs<T> a) {
       if (v1) dot = dot + (double)c.y * (double)a1;
     }
   }
-  if (EPI) epi_store<4>(dot, a.part, a.fin);
+  if (EPI) epi_store<4>(dot, a.part);
 }
 
 // ------------------------------------------------------- vector kernels

@@ -287,7 +287,7 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     np = s->A.partials(s->A.all_items());
     CGX_HIP(launch_spmv_fused<T>(a, f, st, LaunchEv{ev0, ev1}));
     const int gf = s->vec_grid / 4;
-    const FinArgs fin{s->d_tick, s->d_pb, 4 * gf, nullptr, 0, &s->d_st->rr_new};
+    const FinArgs fin{s->d_tick, s->d_pb, 4 * gf, &s->d_st->rr_new};
     CGX_HIP(launch_update_rf<T>(n, r, sv, s->d_st, s->d_pa, np, s->d_pb, gf, st, &fin));
     s->pbuf ^= 1;
     return 0;
