@@ -153,10 +153,12 @@ bool find_pairs(int n, const int *rp, const int *col, const T *val, bool with_va
 // from the Infinity Cache.  Splitting the columns into panels whose x slice
 // fits an L2 and running one SpMV pass per panel keeps the gathers
 // L2-resident, for P row_ptr reads and P-1 y round trips more.  Auto: x >
-// 8 MiB and >= 30 % of (sampled) entries more than a panel width (2 MiB of
-// x) from the diagonal.
+// 8 MiB and >= 30 % of (sampled) entries more than a panel width (3.5 MiB of
+// x, of the L2's 4: C5's sweep -- 1 / 3 / 5 / 6 / 7 / 8 / 10 / 14 / 20
+// panels: 221 / 392 / 560 / 626 / 622 / 604 / 593 / 550 / 489 it/s) from the
+// diagonal.
 int choose_panels(int n, const int *rp, const int *col, size_t tsize, bool force) {
-  const long long pcols = std::max<long long>(1024, 2048LL * 1024 / (long long)tsize);
+  const long long pcols = std::max<long long>(1024, 3584LL * 1024 / (long long)tsize);
   if (n <= pcols) return 1;
   if (!force) {
     if ((double)n * (double)tsize <= 8.0 * 1024 * 1024) return 1;

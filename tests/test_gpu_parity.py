@@ -64,8 +64,8 @@ def expect_layout(rp, col, val, want="auto"):
     falls back DIA -> DC -> CSR."""
     rp, col = np.asarray(rp), np.asarray(col)
     n = len(rp) - 1
-    if want == "panel":  # column panels need x wider than one 2 MiB panel
-        pcols = max(1024, 2 * 2**20 // np.asarray(val).itemsize)
+    if want == "panel":  # column panels need x wider than one 3.5 MiB panel
+        pcols = max(1024, 3584 * 1024 // np.asarray(val).itemsize)
         return "panel" if len(col) and n > pcols else "csr"
     if want == "csr" or len(col) == 0:
         return "csr"
@@ -812,8 +812,8 @@ def test_column_panels_bit_exact():
     """Column-panel layout: rows continue their sequential sums panel after
     panel, so SpMV stays bit-exact in fp64 and fp32, rows longer than a window
     (dense rows crossing every panel) included; CG matches the oracle."""
-    rp, col, val = cgx.random_spd(300000, 9, 31)
-    b = np.random.default_rng(31).standard_normal(300000)
+    rp, col, val = cgx.random_spd(600000, 9, 31)  # x: 4.8 MB, two 3.5 MiB panels
+    b = np.random.default_rng(31).standard_normal(600000)
     with cgx.Solver(0, layout="panel") as s:
         s.set_matrix(rp, col, val)
         assert s.info()["layout_name"] == "panel" and s.info()["n_panels"] > 1
@@ -826,8 +826,8 @@ def test_column_panels_bit_exact():
         s.set_matrix(rp2, col2, val2)
         assert s.info()["n_panels"] > 1
         assert H.same_bits_or_both_nan(s.spmv(x2), H.o_spmv(rp2, col2, val2, x2))
-        rp32, col32, v32 = cgx.random_spd(600000, 40, 9, f32=True)
-        x32 = np.random.default_rng(2).standard_normal(600000).astype(np.float32)
+        rp32, col32, v32 = cgx.random_spd(1200000, 20, 9, f32=True)
+        x32 = np.random.default_rng(2).standard_normal(1200000).astype(np.float32)
         s.set_matrix(rp32, col32, v32)
         assert s.info()["n_panels"] > 1
         assert same32(s.spmv(x32), H.o_spmv_f32(rp32, col32, v32, x32))
@@ -840,7 +840,7 @@ def test_column_panels_auto_c5():
     x = np.random.default_rng(3).standard_normal(len(rp) - 1).astype(np.float32)
     with cgx.Solver(0) as s:
         s.set_matrix(rp, col, val)
-        assert s.info()["layout_name"] == "panel" and s.info()["n_panels"] == 10
+        assert s.info()["layout_name"] == "panel" and s.info()["n_panels"] == 6
         assert same32(s.spmv(x), H.o_spmv_f32(rp, col, val, x))
     del rp, col, val
     rp, col, val = cgx.laplacian3d(128, 128, 128)
