@@ -99,8 +99,8 @@ constexpr int kFoldBS = 1024;
 constexpr int kPad = 8;            // val/col/vectors padded by this many entries
 constexpr int kWindowPad = 1024;   // + one SpMV window (LDS-DMA reads 16-B pieces)
 constexpr int kDiaSliceRows = 512; // DIA-VI work item: one workgroup, 2 rows per thread
-constexpr int kDiaMax = 16;        // DIA-VI: diagonals (nibbles in a 64-bit row word)
-constexpr int kDiaVals = 15;       // DIA-VI: values per diagonal (nibble 15 = no entry)
+constexpr int kDiaMax = 16;        // DIA-VI: diagonals (fields of a <= 64-bit row word)
+constexpr int kDiaVals = 15;       // DIA-VI: values per diagonal (all-ones field = no entry)
 constexpr int kHaloMax = 1024;     // fused step: diagonals |d| <= this read p from the LDS window
 constexpr double kMallBytes = 256.0 * 1024 * 1024;  // Infinity Cache
 
@@ -141,9 +141,10 @@ std::vector<int> lap_offsets(const LapSpec &g);
 //              byte per nonzero + byte row lengths, value stream kept
 //                                                            (k_spmv_dc)
 //   L_DIA      value-indexed diagonal codes (DIA-VI): <= 16 diagonals
-//              (col - row), <= 15 values each; per row one nibble per
-//              diagonal (value index, 15 = no entry), no column or value
-//              stream; two rows per thread, pair loads of x   (k_spmv_dia)
+//              (col - row), <= 15 values each; per row a 1-4 bit field
+//              per diagonal (value index, all ones = no entry) in a 1-8
+//              byte word, no column or value stream; two rows per thread,
+//              pair loads of x (k_spmv_dia; fused step k_spmv_dia_h)
 //   L_STENCIL  matrix-free 5/7-point Laplacian                (k_stencil)
 // Every kernel sums each row sequentially in column order from 0.0 with
 // separately rounded products: y is bit-identical across layouts and to the

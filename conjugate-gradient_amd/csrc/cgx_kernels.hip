@@ -1616,11 +1616,11 @@ __global__ __launch_bounds__(256) void k_dc_encode(int n, const int *__restrict_
   }
 }
 
-// DIA-VI codes of a device-resident CSR (host: the candidate diagonals and
-// their value tables; device: one pass over col/val).  Row r gets nibble k =
-// the index of its entry's value in diagonal k's table (bit patterns, so
-// -0.0, +0.0 and every NaN payload stay distinct), 15 where it has no entry;
-// rows [n, npad) are all 15.  err |= 1 when an entry's diagonal or value is
+// DIA-VI codes of a device-resident CSR (a device-generated Laplacian; host
+// matrices are encoded on the host, cgx_matrix.cpp dia_encode_host).  Row r's
+// field k = the index of its entry's value in diagonal k's table (bit
+// patterns, so -0.0, +0.0 and every NaN payload stay distinct), all ones
+// where it has no entry; rows [n, npad) are all ones.  err |= 1 when an entry's diagonal or value is
 // not among the candidates, or a row's columns do not strictly ascend (the
 // diagonal order would then not be the row's order); the host then keeps
 // another layout.

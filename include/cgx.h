@@ -110,8 +110,9 @@ enum { CGX_F64 = 0, CGX_F32 = 1 };
  *            one code byte per nonzero + the value stream, rows <= 255
  *   DIA      value-indexed diagonal codes: nonzeros on <= 16 diagonals
  *            (col - row) with <= 15 distinct values each, every row's
- *            columns ascending; one nibble per (row, diagonal) names the
- *            entry's value or "no entry" -- no column or value stream
+ *            columns ascending; a 1-4 bit field per (row, diagonal) names
+ *            the entry's value or "no entry" (a Laplacian: one byte per
+ *            row) -- no column or value stream
  *            (stencils, banded matrices with few coefficients)
  *   PANEL    CSR split into column panels (one SpMV pass per panel)
  *   STENCIL  matrix-free Laplacian (cgx_solver_set_stencil; info only)

@@ -26,3 +26,25 @@ for name, alg, fused in (("hs_fused", cgx.CGX_ALG_HS, True), ("hs", cgx.CGX_ALG_
               (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["layout"]), flush=True)
     finally:
         d.close()
+
+# partitions with ghost faces: an in-process group of 3 slabs of nz planes
+# each (part 0's SpMV launches timed: its far slots are -nx*ny, +nx*ny and
+# the ghost face above, NFAR = 4 instances)
+if len(sys.argv) > 2 and sys.argv[2] == "local3":
+    rp, col, val = cgx.laplacian3d(400, 400, 3 * nz)
+    n = len(rp) - 1
+    for fused in (True, False):
+        parts = cgx.DistSolver.local_group(0, 3)
+        try:
+            parts[0].set_alg(cgx.CGX_ALG_HS)
+            parts[0].set_fused(fused)
+            for g, d in enumerate(parts):
+                rb, re_ = cgx.partition_rows(n, 3, g)
+                d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+                d.set_rhs(np.ones(re_ - rb))
+            parts[0].bench_prepare(3)
+            ms, sp = parts[0].bench_run(20, spmv_events=True)
+            print("local3 fused %d: part-0 SpMV launches %.1f us, group iteration %.1f us" %
+                  (parts[0].info()["fused"], 1e3 * sp, 1e3 * ms / 20), flush=True)
+        finally:
+            parts[0].close()
