@@ -953,3 +953,30 @@ def test_c4_full_size_spmv_device_generated():
         s.set_stencil(3, 400, 400, 400)
         y2 = s.spmv(x)
     assert H.same_bits_or_both_nan(y, y2)
+
+
+def test_fused_step_fp32_bit_identical_to_unfused():
+    """The fused step's fp32 instances (C5's precision on a DIA matrix): x
+    and the history bit-identical to the unfused fp32 iteration, and the
+    solve converges."""
+    rp, col, val = cgx.laplacian3d(40, 36, 30)
+    v32 = val.astype(np.float32)
+    b = np.random.default_rng(12).standard_normal(len(rp) - 1).astype(np.float32)
+    out = []
+    for fused in (True, False):
+        with cgx.Solver(0, layout="dia", fused=fused) as s:
+            s.set_matrix(rp, col, v32)
+            assert s.info()["fused"] == (1 if fused else 0) and s.info()["dtype"] == cgx.CGX_F32
+            res = []
+            for maxit, tol in [(17, 0.0), (40, 0.0), (500, 1e-5)]:
+                s.set_rhs(b)
+                its = s.run(maxit, tol)
+                res.append((its, s.x(), s.history(its)))
+            out.append(res)
+    for (i0, x0, h0), (i1, x1, h1) in zip(*out):
+        assert i0 == i1
+        assert np.array_equal(x0.view(np.uint32), x1.view(np.uint32))
+        assert H.same_bits_or_both_nan(h0, h1)
+    its, x, _ = out[0][-1]
+    r = b.astype(np.float64) - H.o_spmv(rp, col, val, x.astype(np.float64))
+    assert its < 500 and np.linalg.norm(r) <= 2e-5 * np.linalg.norm(b)
