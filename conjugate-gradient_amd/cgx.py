@@ -142,6 +142,8 @@ _SIGS = {
                                                _f32p]),
     "cgx_csr_is_chained": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p]),
     "cgx_read_input_file": (ctypes.c_int, [ctypes.c_char_p, _MVP, _MVP]),
+    "cgx_read_input_cached": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, _MVP, _MVP,
+                                             ctypes.POINTER(ctypes.c_int)]),
     # partition layer
     "cgx_partition_rows": (None, [ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),

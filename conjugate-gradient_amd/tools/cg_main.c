@@ -10,7 +10,9 @@
  *
  * Environment (read here, not by the library): CGX_MODE=exact -> the
  * reference's sequential dot-product order (bit-identical x), CGX_ALG=cg1 ->
- * Chronopoulos-Gear, CGX_DEVICE=<ordinal> -> the GPU. */
+ * Chronopoulos-Gear, CGX_DEVICE=<ordinal> -> the GPU, CGX_INPUT_CACHE=<path>
+ * -> read the input through the binary cache at <path>
+ * (cgx_read_input_cached: the text is parsed once per input version). */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -41,7 +43,9 @@ int main(int argc, char **argv)
   struct __mv_sparse *mat_A = new_mv_struct();
   struct __mv_sparse *vec_b = new_mv_struct();
   struct __mv_sparse *vec_x = NULL;
-  if (cgx_read_input_file(input_file, mat_A, vec_b) != 0)
+  const char *cache = getenv("CGX_INPUT_CACHE");
+  if ((cache && *cache ? cgx_read_input_cached(input_file, cache, mat_A, vec_b, NULL)
+                       : cgx_read_input_file(input_file, mat_A, vec_b)) != 0)
     return -1;
 
   time_t start = time(NULL);

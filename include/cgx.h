@@ -257,6 +257,14 @@ long long cgx_gen_random_spd(int n, int partners, unsigned long long seed,
  * Re-entrant, bounds-safe, accepts a missing final newline.  0 or -1. */
 int cgx_read_input_file(const char *path, struct __mv_sparse *A,
                         struct __mv_sparse *b);
+/* The same with a binary cache at cache_path: valid while path keeps the
+ * size and modification time recorded in it, the text is then not parsed;
+ * otherwise the text is parsed and the cache (re)written (best effort: an
+ * unwritable cache_path only costs the next parse).  *from_cache (may be
+ * NULL) = 1 when the cache was used.  0 or -1. */
+int cgx_read_input_cached(const char *path, const char *cache_path,
+                          struct __mv_sparse *A, struct __mv_sparse *b,
+                          int *from_cache);
 
 /* 1 if the CSR is "chained" (ascending cols, no empty row,
  * first_col(r+1) <= last_col(r)): the class on which the reference's

@@ -13,9 +13,14 @@ import helpers as H
 CLI = H.REPO / "conjugate-gradient_amd" / "bin" / "cg"
 
 
-def read(path):
+def read(path, cache=None):
     A, b = cgx.lib().new_mv_struct(), cgx.lib().new_mv_struct()
-    rc = cgx.lib().cgx_read_input_file(str(path).encode(), A, b)
+    hit = ctypes.c_int(-1)
+    if cache is None:
+        rc = cgx.lib().cgx_read_input_file(str(path).encode(), A, b)
+    else:
+        rc = cgx.lib().cgx_read_input_cached(str(path).encode(), str(cache).encode(), A, b,
+                                             ctypes.byref(hit))
     if rc != 0:
         return None
     a, bb = A.contents, b.contents
@@ -23,7 +28,8 @@ def read(path):
     col = np.ctypeslib.as_array(a.col_indices, shape=(max(rp[-1], 1),))[:rp[-1]].copy()
     val = np.ctypeslib.as_array(a.values, shape=(max(a.nnz, 1),))[:a.nnz].copy()
     bv = np.ctypeslib.as_array(bb.values, shape=(max(bb.size, 1),))[:bb.size].copy()
-    out = dict(n=a.size, nnz=a.nnz, rp=rp, col=col, val=val, b=bv, bsize=bb.size, bnnz=bb.nnz)
+    out = dict(n=a.size, nnz=a.nnz, rp=rp, col=col, val=val, b=bv, bsize=bb.size, bnnz=bb.nnz,
+               from_cache=hit.value)
     cgx.lib().cgx_free_mv_deep(A)
     cgx.lib().cgx_free_mv_deep(b)
     return out
@@ -52,6 +58,60 @@ def test_reader_edge_cases(tmp_path):
     r = read(p)
     assert list(r["col"]) == [0, 0, 1]
     assert read(tmp_path / "missing.txt") is None
+
+
+def test_reader_token_rules(tmp_path):
+    """The reference's token rules (cg.c:317-350): a line ended by a newline
+    has one token more than commas (empty -> 0, also after a trailing
+    comma); the unterminated last line drops a trailing empty token; text
+    after the fourth line is ignored."""
+    p = tmp_path / "t.txt"
+    p.write_text("0,1,\n0,2,3\n1,,3\n4,5,\n7,8\n")
+    r = read(p)
+    assert list(r["col"]) == [0, 1, 0] and list(r["val"]) == [1.0, 0.0, 3.0]
+    assert list(r["b"]) == [4.0, 5.0, 0.0]
+    p.write_text("0,1\n0,1,2\n1,2\n4,5,")
+    assert list(read(p)["b"]) == [4.0, 5.0]
+    p.write_text("0\n0,1\n\n")  # an empty third line: one 0 token; no b line
+    r = read(p)
+    assert list(r["val"]) == [0.0] and r["bsize"] == 0
+
+
+def _big_text(n, seed):
+    """A random CSR as the reference's text, lines of several MB (the
+    reader's threaded chunking) with every number format %.17g writes."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, 12, n)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1]))
+    val = rng.standard_normal(len(col)) * 10.0 ** rng.integers(-30, 30, len(col))
+    val[::97] = 0.0
+    b = rng.standard_normal(n)
+    lines = [",".join(map(str, col)), ",".join(map(str, rp)),
+             ",".join("%.17g" % v for v in val), ",".join("%.17g" % v for v in b)]
+    return "\n".join(lines) + "\n", rp, col, val, b
+
+
+def test_reader_large_lines_and_cache(tmp_path):
+    """Multi-MB lines parse identically through the threaded chunks; the
+    binary cache returns the same arrays without parsing, and a changed
+    input invalidates it."""
+    txt, rp, col, val, b = _big_text(300000, 5)
+    p, c = tmp_path / "big.txt", tmp_path / "big.cgxbin"
+    p.write_text(txt)
+    for want_hit in (0, 1, 1):
+        r = read(p, cache=c)
+        assert r["from_cache"] == want_hit
+        assert np.array_equal(r["rp"], rp) and np.array_equal(r["col"], col)
+        assert np.array_equal(r["val"].view(np.uint64), val.view(np.uint64))
+        assert np.array_equal(r["b"].view(np.uint64), b.view(np.uint64))
+    r0 = read(p)
+    assert np.array_equal(r0["val"].view(np.uint64), val.view(np.uint64))
+    txt2, rp2, _, _, _ = _big_text(1000, 6)
+    p.write_text(txt2)
+    r = read(p, cache=c)
+    assert r["from_cache"] == 0 and np.array_equal(r["rp"], rp2)
+    assert read(tmp_path / "missing.txt", cache=c) is None
 
 
 @pytest.mark.gpu
