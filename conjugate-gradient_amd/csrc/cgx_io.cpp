@@ -35,7 +35,7 @@ T parse_tok(const char *p, const char *q) {
     big.resize(len + 1);
     s = big.data();
   }
-  memcpy(s, p, len);
+  if (len) memcpy(s, p, len);
   s[len] = '\0';
   if (std::is_integral<T>::value) return (T)strtol(s, nullptr, 10);
   return (T)strtod(s, nullptr);
@@ -55,7 +55,7 @@ std::vector<T> parse_line(const char *p, const char *e, bool terminated) {
   std::vector<const char *> cut{p};
   for (int t = 1; t < want; ++t) {
     const char *c = std::max(p + len * t / want, cut.back());
-    c = (const char *)memchr(c, ',', (size_t)(e - c));
+    c = c < e ? (const char *)memchr(c, ',', (size_t)(e - c)) : nullptr;
     if (c && c + 1 < e && c + 1 > cut.back()) cut.push_back(c + 1);
   }
   const int m = (int)cut.size();
@@ -78,7 +78,7 @@ std::vector<T> parse_line(const char *p, const char *e, bool terminated) {
   run([&](int t) {
     const char *x = cut[(size_t)t];
     for (long long k = off[(size_t)t]; k < off[(size_t)t + 1]; ++k) {
-      const char *q = (const char *)memchr(x, ',', (size_t)(e - x));
+      const char *q = x < e ? (const char *)memchr(x, ',', (size_t)(e - x)) : nullptr;
       if (!q) q = e;
       out[(size_t)k] = parse_tok<T>(x, q);
       x = q + 1;
@@ -138,7 +138,7 @@ int read_text(const char *path, std::vector<int> &col, std::vector<int> &rp,
       *e = a = end;
       return end;
     }
-    const char *q = (const char *)memchr(x, '\n', (size_t)(end - x));
+    const char *q = x < end ? (const char *)memchr(x, '\n', (size_t)(end - x)) : nullptr;
     *term = q != nullptr;
     *e = q ? q : end;
     x = q ? q + 1 : end + 1;
