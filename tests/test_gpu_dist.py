@@ -374,3 +374,27 @@ def test_fused_rccl_one_rank_graph_parity():
             assert i0 == i1
             assert H.same_bits_or_both_nan(x0, x1), key
             assert H.same_bits_or_both_nan(h0, h1), key
+
+
+def test_bench_dist_path_rehearsal(tmp_path):
+    """bench.py's N > 1 path at one rank (torch.distributed.run, a 1-rank
+    RCCL communicator): the parity gate (HS, fused HS, CG1 against the
+    single-GPU solve) passes and the timed line is well formed."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(H.REPO / "bench.py"),
+           "--gpus", "1", "--dist-rehearsal", "--workload", "c3", "--steps", "10", "--warmup", "2"]
+    env = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["parity"]["ok"] and set(line["parity"]) >= {"hs", "hs_fused", "cg1"}
+    assert line["n_gpus"] == 1 and line["value"] > 0 and line["config"]["fused"] in (0, 1)
