@@ -777,11 +777,13 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   if (f.publish && !fs.first && !odd && !fs.stop && blockIdx.x == 0 && t == 0)
     f.st->alpha_def = fs.alpha;
   P po = P(), xo = P(), pd = P();
-  if (xup) {
-    po = ld_pair(f.pold, rs);
-    xo = ld_pair(f.x, rs);
-    if (odd) pd = ld_pair((const T *)f.pnew, rs);
-  }
+  auto load_x = [&]() {
+    if (xup) {
+      po = ld_pair(f.pold, rs);
+      xo = ld_pair(f.x, rs);
+      if (odd) pd = ld_pair((const T *)f.pnew, rs);
+    }
+  };
   auto x_update = [&]() {
     T x0 = xo.x, x1 = xo.y;
     if (odd) {
@@ -793,6 +795,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     st_pair(f.x, r, a.n, x0 + a0, x1 + a1, false);
   };
   if (fs.stop) {  // the pending x updates only (then the cg.c:125 break)
+    load_x();
     if (xup && r < a.n) x_update();
     return;
   }
@@ -856,6 +859,9 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   for (int q = 0; q < NFAR; ++q) pk[q] = pnext_at(rf[q], pf[q], gf[q], fb[q]);
   if (t < a.ndiag * 16) lv[t] = tv;
   __syncthreads();
+  // the x update's operands are loaded here, where the window's and the far
+  // slots' load registers are dead (70 -> fewer VGPRs over the launch)
+  load_x();
   // s = A p_new in diagonal order: near diagonals from the window, far ones
   // from their slot (the number of far diagonals before k)
   const int rw = r - w0;
