@@ -148,8 +148,6 @@ KERNELS = {
     "csr": "k_spmv_csr (LDS-DMA val/col window per 64-row block, lane-per-row sums from LDS)",
     "panel": "k_spmv_csr over column panels",
     "stencil": "k_stencil (matrix-free, two rows per thread)",
-    "stencil_fused": "k_spmv_dia_h (fused HS step, matrix-free: each row's diagonal fields "
-                     "from its grid position, no matrix bytes)",
 }
 
 
@@ -440,11 +438,9 @@ def run_single(args, wl_name):
                 ms.bench_prepare(args.warmup)
                 mf_ms = ms.bench_run(args.steps, graph=True)[0]
                 _, mf_spmv = ms.bench_run(min(args.steps, 50), graph=False, spmv_events=True)
-                mf_fused = ms.info()["fused"]
             extra["matrix_free_upper_bound"] = dict(
                 value=round(args.steps / (mf_ms * 1e-3), 2), unit="it/s",
-                spmv_us=round(mf_spmv * 1e3, 2),
-                kernel=KERNELS["stencil_fused"] if mf_fused else KERNELS["stencil"],
+                spmv_us=round(mf_spmv * 1e3, 2), kernel=KERNELS["stencil"],
                 note="the same operator without a stored matrix: an upper bound, not the CSR path")
         if wl_name == "c3":
             extra["c4_1gpu"] = c4_one_gpu(min(args.steps, 50), args.warmup)

@@ -640,30 +640,6 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
   if (EPI) epi_store<4>(dot, a.part);
 }
 
-// Grid coordinates of a Laplacian row from exact reciprocal divisions
-// (k_stencil, and the fused step's matrix-free rows).
-__device__ __forceinline__ int fdiv(int a, int d, double inv) {
-  int q = (int)((double)a * inv);  // exact floor(a / d) for 0 <= a < 2^31
-  q -= q * d > a;
-  q += (q + 1) * d <= a;
-  return q;
-}
-
-struct LapFlags {
-  bool ml, mj, mi, pi, pj, pL;  // neighbour present: -pl, -nx, -1, +1, +nx, +pl
-};
-
-__device__ __forceinline__ LapFlags lap_flags(int r, const LapSpec &g, double inv_pl,
-                                              double inv_nx) {
-  const int pl = g.nx * g.ny;
-  const int l = g.dim == 3 ? fdiv(r, pl, inv_pl) : 0;
-  const int rem = r - l * pl;
-  const int j = fdiv(rem, g.nx, inv_nx);
-  const int i = rem - j * g.nx;
-  return LapFlags{g.dim == 3 && l > 0, j > 0,           i > 0,
-                  i < g.nx - 1,        j < g.ny - 1,    g.dim == 3 && l < g.nz - 1};
-}
-
 // ------------------------------------------------- fused HS step (DIA-VI)
 // The scalar step at the top of a fused launch -- the folded k_xpay_xf's
 // logic (cg.c:125-129): r.r of the last r-update (*rr_new: k_update_rf's
@@ -732,27 +708,7 @@ __device__ __forceinline__ typename Pair<T>::type p_next(typename Pair<T>::type 
 // 8 p_new + 8 s, + 24 (x read and written, p_{k-1} read) every other
 // launch.  Every value is the unfused path's (same roundings): x and the
 // r.r history are bit-identical to SpMV + k_update_rf + k_xpay_xf.
-// The fields of row r for the matrix-free stencil (STEN): diagonal k
-// (1-bit fields, bit k) is present when the grid neighbour at offset doff[k]
-// exists -- the stored DIA-VI word of the same Laplacian.
-__device__ __forceinline__ unsigned sten_word(int r, int n, const int *doff, int nd,
-                                              const LapSpec &g, double inv_pl, double inv_nx) {
-  if (r >= n) return (1u << nd) - 1u;
-  const LapFlags f = lap_flags(r, g, inv_pl, inv_nx);
-  const int nx = g.nx, pl = g.nx * g.ny;
-  unsigned w = 0;
-#pragma unroll
-  for (int k = 0; k < kDiaMax; ++k) {
-    if (k >= nd) break;
-    const int d = doff[k];
-    const bool have = d == 0 || (d == -1 && f.mi) || (d == 1 && f.pi) || (d == -nx && f.mj) ||
-                      (d == nx && f.pj) || (g.dim == 3 && ((d == -pl && f.ml) || (d == pl && f.pL)));
-    w |= have ? 0u : 1u << k;
-  }
-  return w;
-}
-
-template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH, bool STEN>
+template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH>
 __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *win = reinterpret_cast<T *>(dyn_lds);
@@ -800,12 +756,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     return;
   }
   unsigned c0, c1;  // the code words of row r / r + 1 (<= 4 bytes: fusable())
-  if (STEN) {
-    c0 = sten_word(r, a.n, a.doff, a.ndiag, a.lap, a.inv_pl, a.inv_nx);
-    c1 = sten_word(r + 1, a.n, a.doff, a.ndiag, a.lap, a.inv_pl, a.inv_nx);
-  } else {
-    ld_codes(a.dcode, a.cb, r, c0, c1);
-  }
+  ld_codes(a.dcode, a.cb, r, c0, c1);
   const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
   // far diagonals: slot q holds diagonal a.fark[q] (-1: an unused slot)
   constexpr int NS = NFAR > 0 ? NFAR : 1;
@@ -932,6 +883,28 @@ __global__ __launch_bounds__(256) void k_pack_pnext(int n_send, const int *__res
 // k_spmv_dia: x[r +- nx], x[r +- nx*ny] and x[r], x[r+1] are pair loads,
 // x[r-1] / x[r+2] the neighbouring lanes' centre pair (one extra load at the
 // wave edges); grid coordinates from exact reciprocal divisions.
+__device__ __forceinline__ int fdiv(int a, int d, double inv) {
+  int q = (int)((double)a * inv);  // exact floor(a / d) for 0 <= a < 2^31
+  q -= q * d > a;
+  q += (q + 1) * d <= a;
+  return q;
+}
+
+struct LapFlags {
+  bool ml, mj, mi, pi, pj, pL;  // neighbour present: -pl, -nx, -1, +1, +nx, +pl
+};
+
+__device__ __forceinline__ LapFlags lap_flags(int r, const LapSpec &g, double inv_pl,
+                                              double inv_nx) {
+  const int pl = g.nx * g.ny;
+  const int l = g.dim == 3 ? fdiv(r, pl, inv_pl) : 0;
+  const int rem = r - l * pl;
+  const int j = fdiv(rem, g.nx, inv_nx);
+  const int i = rem - j * g.nx;
+  return LapFlags{g.dim == 3 && l > 0, j > 0,           i > 0,
+                  i < g.nx - 1,        j < g.ny - 1,    g.dim == 3 && l < g.nz - 1};
+}
+
 template <typename T, bool EPI, bool NT>
 __global__ __launch_bounds__(256) void k_stencil(SpmvArgs<T> a) {
   typedef typename Pair<T>::type P;
@@ -1832,18 +1805,14 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev)
 
 template <typename T, int NF, int NFAR, bool GH>
 static const void *fused_kernel_g(bool nt, bool list) {
-  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true, GH, false>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, GH, false>))
-            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true, GH, false>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, GH, false>));
+  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, GH>))
+            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, GH>));
 }
 
-// the matrix-free stencil: natural item order, no ghosts
 template <typename T, int NF, int NFAR>
-static const void *fused_kernel(bool nt, bool list, bool gh, bool sten) {
-  if (sten)
-    return nt ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, false, true>)
-              : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, false, true>);
+static const void *fused_kernel(bool nt, bool list, bool gh) {
   return gh ? fused_kernel_g<T, NF, NFAR, true>(nt, list)
             : fused_kernel_g<T, NF, NFAR, false>(nt, list);
 }
@@ -1853,9 +1822,7 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
                              const LaunchEv &ev) {
   const int g = spmv_grid(a);
   if (g <= 0) return hipSuccess;
-  const bool sten = a.layout == L_STENCIL;
-  if ((a.layout != L_DIA && !sten) || a.cb > 4 || (sten && (a.items.list || f.ghost)))
-    return hipErrorInvalidValue;
+  if (a.layout != L_DIA || a.cb > 4) return hipErrorInvalidValue;
   const int wn = kDiaSliceRows + a.hl + a.hr;
   const int nf = (wn + 511) / 512;
   int nfar = 0;
@@ -1864,15 +1831,15 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
   const bool nt = a.nt != 0, l = a.items.list != nullptr, gh = f.ghost != 0;
   const void *k = nullptr;
   switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + (nfar == 0 ? 0 : nfar <= 2 ? 2 : 4)) {
-    case 20: k = fused_kernel<T, 2, 0>(nt, l, gh, sten); break;
-    case 22: k = fused_kernel<T, 2, 2>(nt, l, gh, sten); break;
-    case 24: k = fused_kernel<T, 2, 4>(nt, l, gh, sten); break;
-    case 30: k = fused_kernel<T, 3, 0>(nt, l, gh, sten); break;
-    case 32: k = fused_kernel<T, 3, 2>(nt, l, gh, sten); break;
-    case 34: k = fused_kernel<T, 3, 4>(nt, l, gh, sten); break;
-    case 50: k = fused_kernel<T, 5, 0>(nt, l, gh, sten); break;
-    case 52: k = fused_kernel<T, 5, 2>(nt, l, gh, sten); break;
-    case 54: k = fused_kernel<T, 5, 4>(nt, l, gh, sten); break;
+    case 20: k = fused_kernel<T, 2, 0>(nt, l, gh); break;
+    case 22: k = fused_kernel<T, 2, 2>(nt, l, gh); break;
+    case 24: k = fused_kernel<T, 2, 4>(nt, l, gh); break;
+    case 30: k = fused_kernel<T, 3, 0>(nt, l, gh); break;
+    case 32: k = fused_kernel<T, 3, 2>(nt, l, gh); break;
+    case 34: k = fused_kernel<T, 3, 4>(nt, l, gh); break;
+    case 50: k = fused_kernel<T, 5, 0>(nt, l, gh); break;
+    case 52: k = fused_kernel<T, 5, 2>(nt, l, gh); break;
+    case 54: k = fused_kernel<T, 5, 4>(nt, l, gh); break;
     default: return hipErrorInvalidValue;
   }
   void *args[] = {(void *)&a, (void *)&f};

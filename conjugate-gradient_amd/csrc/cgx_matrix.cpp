@@ -476,25 +476,6 @@ int DevMatrix::set_stencil(const LapSpec &g) {
   layout = L_STENCIL;
   lap = g;
   nt = 16.0 * n + 40.0 * n > kMallBytes;
-  // the stencil as DIA-VI diagonals with one value each, for the fused HS
-  // step (k_spmv_dia_h computes each row's fields from its grid position):
-  // the value tables are the only matrix bytes on the device
-  const std::vector<int> offs = lap_offsets(g);
-  memset(&dia, 0, sizeof dia);
-  dia.ndiag = (int)offs.size();
-  std::vector<double> vt((size_t)kDiaMax * 16, 0.0);
-  for (int k = 0; k < dia.ndiag; ++k) {
-    dia.doff[k] = offs[(size_t)k];
-    dia.nval[k] = 1;
-    vt[(size_t)k * 16] = offs[(size_t)k] == 0 ? 2.0 * g.dim : -1.0;  // the CSR values (cgx_gen)
-  }
-  dia_pack(dia);
-  int rc = dev_alloc(&d_vtab, vt.size() * 8, &dev_bytes);
-  if (rc) {
-    release();
-    return rc;
-  }
-  CGX_HIP(hipMemcpy(d_vtab, vt.data(), vt.size() * 8, hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -887,7 +868,7 @@ int DevMatrix::padded_rows() const { return padded_rows_for(n); }
 bool DevMatrix::near_diag(int k) const { return std::abs(dia.doff[k]) <= kHaloMax; }
 
 bool DevMatrix::fusable() const {
-  if ((layout != L_DIA && layout != L_STENCIL) || dia.cbytes > 4) return false;
+  if (layout != L_DIA || dia.cbytes > 4) return false;
   int nfar = 0;
   for (int k = 0; k < dia.ndiag; ++k) nfar += !near_diag(k);
   return nfar <= 4;

@@ -77,9 +77,8 @@ struct DevMatrix {
   int items() const;  // work items of the layout (blocks or slices)
   // host: first row of each item, items() + 1 entries
   std::vector<int> item_rows() const;
-  // The fused HS step applies (DIA with <= 4 code bytes per row, or the
-  // matrix-free stencil; at most 4 far diagonals, |d| > kHaloMax):
-  // k_spmv_dia_h's window and far slots.
+  // The fused HS step applies (DIA, <= 4 code bytes per row, at most 4
+  // far diagonals, |d| > kHaloMax): k_spmv_dia_h's window and far slots.
   bool fusable() const;
   bool near_diag(int k) const;  // read from k_spmv_dia_h's LDS window
   // rows covered by the items (DIA pads to whole 512-row slices)

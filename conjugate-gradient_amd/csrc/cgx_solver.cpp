@@ -156,16 +156,13 @@ void drop_graph(cgx_solver *s) {
   s->gexec_key = -1;
 }
 
-// The fused HS step applies: fast mode, HS, a fusable layout and, in auto
-// mode, a stored DIA matrix whose working set exceeds the Infinity Cache
-// (cache-resident systems are launch- and latency-bound: the heavier fused
-// workgroup loses, C2 29.1 vs 26.8 us per iteration; the matrix-free
-// stencil's grid-coordinate fields cost more ALU in the fused workgroup than
-// they save, C3 157.0 vs 152.6 us).
+// The fused HS step applies: fast mode, HS, a fusable DIA layout and, in
+// auto mode, a working set beyond the Infinity Cache (cache-resident
+// systems are launch- and latency-bound: the heavier fused workgroup loses,
+// C2 29.1 vs 26.8 us per iteration).
 bool fused(const cgx_solver *s) {
   return s->fuse != CGX_FUSE_OFF && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST &&
-         s->A.fusable() &&
-         (s->fuse == CGX_FUSE_ON || (s->A.nt && s->A.layout == L_DIA));
+         s->A.fusable() && (s->fuse == CGX_FUSE_ON || s->A.nt);
 }
 
 // p double-buffered, its buffers alternating per iteration: the fused step,

@@ -167,11 +167,10 @@ int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
  * (cg.c:115-116) runs every other launch for two iterations (same roundings,
  * in order).  Two launches per iteration instead of three, 12 B per row less
  * traffic; x and the r.r history are bit-identical to the unfused path.
- * mode: CGX_FUSE_OFF, CGX_FUSE_AUTO (default: a stored DIA matrix whose
- * working set exceeds the 256 MiB Infinity Cache -- cache-resident systems
- * are latency-bound and run faster unfused, and so does the matrix-free
- * stencil), CGX_FUSE_ON (wherever the layout takes it, the matrix-free
- * stencil included). */
+ * mode: CGX_FUSE_OFF, CGX_FUSE_AUTO (default: where the layout takes it and
+ * the working set exceeds the 256 MiB Infinity Cache -- cache-resident
+ * systems are latency-bound and run faster unfused), CGX_FUSE_ON (wherever
+ * the layout takes it). */
 #define CGX_FUSE_OFF  0
 #define CGX_FUSE_AUTO 1
 #define CGX_FUSE_ON   2

@@ -980,34 +980,3 @@ def test_fused_step_fp32_bit_identical_to_unfused():
     its, x, _ = out[0][-1]
     r = b.astype(np.float64) - H.o_spmv(rp, col, val, x.astype(np.float64))
     assert its < 500 and np.linalg.norm(r) <= 2e-5 * np.linalg.norm(b)
-
-
-@pytest.mark.parametrize("shape", [(24, 20, 17), (40, 30, 9), (70, 1, 9)])
-def test_fused_stencil_bit_identical(shape):
-    """The matrix-free stencil takes the fused step too (k_spmv_dia_h with
-    each row's diagonal fields computed from its grid position): x and the
-    history are bit-identical to the stored DIA matrix's fused and unfused
-    iterations and to the unfused stencil (ny = 1: the +-nx and +-nx*ny
-    offsets coincide)."""
-    nx, ny, nz = shape
-    rp, col, val = cgx.laplacian3d(nx, ny, nz)
-    b = np.random.default_rng(8).standard_normal(len(rp) - 1)
-    out = []
-    for kind, fused in (("sten", True), ("sten", False), ("dia", True), ("dia", False)):
-        with cgx.Solver(0, layout="dia", fused=fused) as s:
-            if kind == "sten":
-                s.set_stencil(3, nx, ny, nz)
-            else:
-                s.set_matrix(rp, col, val)
-            assert s.info()["fused"] == (1 if fused else 0)
-            res = []
-            for maxit, tol in [(17, 0.0), (40, 0.0), (3000, 1e-10)]:
-                s.set_rhs(b)
-                its = s.run(maxit, tol)
-                res.append((its, s.x(), s.history(its)))
-            out.append(res)
-    for other in out[1:]:
-        for (i0, x0, h0), (i1, x1, h1) in zip(out[0], other):
-            assert i0 == i1
-            assert H.same_bits_or_both_nan(x0, x1)
-            assert H.same_bits_or_both_nan(h0, h1)
