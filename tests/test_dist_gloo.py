@@ -3,7 +3,9 @@ builds its partition with libcgx's partition layer, exchanges ghost requests,
 then runs the distributed recurrence with the same communication pattern as
 the GPU solver -- Chronopoulos-Gear: halo of r point-to-point, ONE all-reduce
 of (gamma, delta) per iteration; HS: halo of p, one all-reduce of p.s and one
-of r.r -- and the gathered x is checked against the serial oracle."""
+of r.r; fused HS: the halo carries p_new = r + beta p_old computed at the send
+rows, x updated in pairs -- and the gathered x is checked against the serial
+oracle (fused HS: bit-identical to the HS protocol's)."""
 import os
 import socket
 
@@ -86,7 +88,68 @@ def _worker(rank, world, port, kind, out_path, alg="cg1"):
         dist.all_reduce(t)
         return float(t[0]), float(t[1])
 
+    def halo_vals(vals_for, own):
+        # the fused step's halo: each rank sends values it computes at its
+        # send rows (p_new = r + beta p_old), received into the ghost tail
+        reqs, bufs = [], {}
+        for q in range(world):
+            if q == rank:
+                continue
+            if scount[q]:
+                t = torch.from_numpy(vals_for(slocal[soff[q]:soff[q] + scount[q]]).copy())
+                reqs.append(dist.isend(t, q))
+            if recv[q]:
+                bufs[q] = torch.empty(int(recv[q]), dtype=torch.float64)
+                reqs.append(dist.irecv(bufs[q], q))
+        for rq in reqs:
+            rq.wait()
+        ext = np.zeros(len(ghosts))
+        for q, t in bufs.items():
+            ext[roff[q]:roff[q] + recv[q]] = t.numpy()
+        return np.concatenate([own, ext])
+
     maxit, tol = 500, 1e-10
+    if alg == "hs_fused":  # cgx_dist.cpp's fused step: pack p_new, x in pairs
+        def allreduce1(a):
+            t = torch.tensor([a], dtype=torch.float64)
+            dist.all_reduce(t)
+            return float(t[0])
+        x = np.zeros(n_loc)
+        r = b.copy()
+        p_old = b.copy()
+        rr = allreduce1(float(np.dot(r, r)))
+        bb, k, beta, first = rr, 0, 0.0, True
+        pend = []  # deferred (alpha, p) x updates, applied in pairs
+        while True:
+            if first:
+                p_new = r.copy()
+                ext = halo_vals(lambda idx: r[idx], p_new)
+            else:
+                p_new = r + beta * p_old
+                ext = halo_vals(lambda idx: r[idx] + beta * p_old[idx], p_new)
+            s = H.o_spmv(rp, lcol, val, ext)
+            alpha = rr / allreduce1(float(np.dot(p_new, s)))
+            pend.append((alpha, p_new))
+            r = r - alpha * s
+            rr_new = allreduce1(float(np.dot(r, r)))
+            stop = k == maxit or rr_new <= tol * tol * bb
+            if len(pend) == 2 or stop:
+                for a_, p_ in pend:
+                    x = x + a_ * p_
+                pend = []
+            if stop:
+                break
+            beta, first = rr_new / rr, False
+            p_old = p_new
+            rr = rr_new
+            k += 1
+        xs = [None] * world
+        dist.all_gather_object(xs, x.tolist())
+        if rank == 0:
+            np.save(out_path, np.array(sum(xs, [])))
+            np.save(out_path + ".its.npy", np.array([k + 1]))
+        dist.destroy_process_group()
+        return
     if alg == "hs":  # cg.c:88-141 with the two dots all-reduced
         def allreduce1(a):
             t = torch.tensor([a], dtype=torch.float64)
@@ -144,7 +207,7 @@ def _worker(rank, world, port, kind, out_path, alg="cg1"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("alg", ["cg1", "hs"])
+@pytest.mark.parametrize("alg", ["cg1", "hs", "hs_fused"])
 @pytest.mark.parametrize("kind", ["lap3d", "rand"])
 def test_distributed_world2_gloo(kind, alg, tmp_path):
     import helpers as H
@@ -161,6 +224,12 @@ def test_distributed_world2_gloo(kind, alg, tmp_path):
         rp, col, val = cgx.random_spd(1200, 6, 3)
         b = np.random.default_rng(9).standard_normal(1200)
     x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=alg == "cg1")
+    if alg == "hs_fused":  # the same values as the HS protocol's, bit for bit
+        out2 = str(tmp_path / "x_hs.npy")
+        mp.start_processes(_worker, args=(2, _free_port(), kind, out2, "hs"), nprocs=2,
+                           join=True, start_method="spawn")
+        assert its == int(np.load(out2 + ".its.npy")[0])
+        assert np.array_equal(x.view(np.uint64), np.load(out2).view(np.uint64))
     assert abs(its - its_ref) <= 1
     assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
     res = b - H.o_spmv(rp, col, val, x)
