@@ -633,6 +633,9 @@ def run_dist(args, wl_name, world, rank, local_rank):
                         nnz_rank0=info["nnz"], alg=alg, alg_trial_ms_per_iter=trial,
                         graph=info["graph"], fused=info["fused"],
                         parallelism=f"row-partition x{world} (RCCL)",
+                        scaling_base="the N = 1 point of this C4 curve is the N = 1 line's "
+                                     "c4_1gpu leg (same solver, one GPU); the N = 1 line's "
+                                     "value is C3",
                         layout=info["layout_name"], halo_bytes_per_iter_max_rank=halo),
             device_ms_per_step=None if dev is None else round(dev, 4),
             upload_ms=round(upload_ms, 1), iter_bytes_rank0=int(info["iter_bytes"]),
