@@ -1,0 +1,318 @@
+// xtile_lab.hip -- C5-shaped SpMV (random columns, fp32, ~64 nnz/row) with x
+// in LDS instead of L2 gathers.  Measurement lab, not
+// product code.
+//
+// Layout: row blocks of K * 1024 rows (one 1024-thread workgroup each, thread
+// t owns rows t + 1024 k); column panels of W entries of x.  Tile (block,
+// panel) holds, for each thread, its rows' entries with a column in the
+// panel, ordered (row slot k, column): u32 (k << 14 | local column) + f32
+// value.  Per tile: a u8 entry count per thread, an entry offset per wave.
+// The workgroup walks the panels in order: x panel -> LDS, every thread adds
+// its entries' products to its rows' sums (LDS, one slot per owned row) --
+// each row's products in column order from 0.0, the reference's sequential
+// sum, so y is bit-identical to a row-by-row float sum.  Prefetch: the next
+// panel's x and the next tile's entries are in flight while a tile is summed.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o xtile_lab xtile_lab.hip
+// Run:   ./xtile_lab [n] [partners per row] [reps]       (default 5000000 32 20)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+constexpr int BS = 1024, K = 20, W = 16384, RB = BS * K, E = 12;  // E: entries held in VGPRs
+
+static unsigned long long sm64(unsigned long long &s) {
+  unsigned long long z = (s += 0x9e3779b97f4a7c15ULL);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+  int inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(inc, off, 64);
+    inc += lane >= off ? t : 0;
+  }
+  return inc - v;
+}
+
+struct Tiles {
+  const unsigned *ent;
+  const float *val;
+  const unsigned char *cnt;  // [block][panel][BS]
+  const int *wb;             // [block][panel][16]
+  int n, ncols, P;
+};
+
+__global__ __launch_bounds__(BS) void k_xtile(Tiles T, const float *__restrict__ x,
+                                              float *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float *xs = lds;       // W
+  float *acc = lds + W;  // K * BS
+  const int t = threadIdx.x, wid = t >> 6;
+  const int b = blockIdx.x;
+  const int P = T.P;
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k * BS + t] = 0.f;
+  // x panel p into registers: 16 floats per thread (4 x float4)
+  float4 xr[W / BS / 4];
+  auto load_x = [&](int p) {
+    const int c0 = p * W;
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) {
+      const int j = (i * BS + t) * 4;
+      if (c0 + j + 3 < T.ncols) {
+        xr[i] = *reinterpret_cast<const float4 *>(x + c0 + j);
+      } else {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c0 + j + 0 < T.ncols) v.x = x[c0 + j + 0];
+        if (c0 + j + 1 < T.ncols) v.y = x[c0 + j + 1];
+        if (c0 + j + 2 < T.ncols) v.z = x[c0 + j + 2];
+        v.w = 0.f;
+        xr[i] = v;
+      }
+    }
+  };
+  unsigned en[E];
+  float ev[E];
+  int c_cur = 0, o_cur = 0;
+  auto meta = [&](int p, int &c, int &o) {
+    const long long tile = (long long)b * P + p;
+    c = T.cnt[tile * BS + t];
+    o = T.wb[tile * 16 + wid] + wave_excl_scan(c);
+  };
+  auto load_ent = [&](int c, int o) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int q = j < c ? o + j : o;  // a clamped, valid address
+      en[j] = T.ent[q];
+      ev[j] = T.val[q];
+    }
+  };
+  load_x(0);
+  meta(0, c_cur, o_cur);
+  load_ent(c_cur, o_cur);
+  int c_nx = 0, o_nx = 0;
+  if (P > 1) meta(1, c_nx, o_nx);
+  for (int p = 0; p < P; ++p) {
+    __syncthreads();  // every thread is done with the previous panel
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) reinterpret_cast<float4 *>(xs)[i * BS + t] = xr[i];
+    __syncthreads();
+    if (p + 1 < P) load_x(p + 1);
+    // this tile's entries (held since the previous iteration)
+    unsigned cen[E];
+    float cev[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      cen[j] = en[j];
+      cev[j] = ev[j];
+    }
+    const int c = c_cur, o = o_cur;
+    // next tile's entries and the meta of the one after
+    if (p + 1 < P) {
+      load_ent(c_nx, o_nx);
+      c_cur = c_nx;
+      o_cur = o_nx;
+      if (p + 2 < P) meta(p + 2, c_nx, o_nx);
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (j < c) {
+        const unsigned e = cen[j];
+        const float pr = cev[j] * xs[e & (W - 1)];
+        float &s = acc[(e >> 14) * BS + t];
+        s = s + pr;
+      }
+    for (int j = E; j < c; ++j) {  // rare: more entries than registers
+      const unsigned e = T.ent[o + j];
+      const float pr = T.val[o + j] * xs[e & (W - 1)];
+      float &s = acc[(e >> 14) * BS + t];
+      s = s + pr;
+    }
+  }
+  const int r0 = b * RB;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = r0 + k * BS + t;
+    if (r < T.n) y[r] = acc[k * BS + t];
+  }
+}
+
+// plain CSR, one row per thread, sequential float sum (the reference order)
+__global__ __launch_bounds__(256) void k_csr_row(int n, const int *rp, const int *col,
+                                                 const float *val, const float *x, float *y) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  float s = 0.f;
+  for (int k = rp[r]; k < rp[r + 1]; ++k) {
+    const float pr = val[k] * x[col[k]];
+    s = s + pr;
+  }
+  y[r] = s;
+}
+
+int main(int argc, char **argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 5000000;
+  const int partners = argc > 2 ? atoi(argv[2]) : 32;
+  const int reps = argc > 3 ? atoi(argv[3]) : 20;
+  // random rows: the diagonal + 2 * partners random columns (C5's nnz per
+  // row; symmetry does not matter for the SpMV's access pattern)
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<int> rp(n + 1);
+  std::vector<int> col;
+  std::vector<float> val;
+  col.reserve((size_t)n * (2 * partners + 1));
+  val.reserve(col.capacity());
+  unsigned long long s = 42;
+  std::vector<int> row;
+  for (int r = 0; r < n; ++r) {
+    rp[r] = (int)col.size();
+    row.clear();
+    row.push_back(r);
+    for (int j = 0; j < 2 * partners; ++j) row.push_back((int)(sm64(s) % (unsigned long long)n));
+    std::sort(row.begin(), row.end());
+    row.erase(std::unique(row.begin(), row.end()), row.end());
+    for (int c : row) {
+      col.push_back(c);
+      val.push_back(c == r ? 70.f : -(float)((sm64(s) >> 40) + 1) / 16777216.f);
+    }
+  }
+  rp[n] = (int)col.size();
+  const long long nnz = rp[n];
+  std::vector<float> xh(n);
+  for (int i = 0; i < n; ++i) xh[i] = (float)((sm64(s) >> 40) + 1) / 16777216.f;
+  // tiles
+  const int nb = (n + RB - 1) / RB, P = (n + W - 1) / W;
+  std::vector<unsigned char> cnt((size_t)nb * P * BS, 0);
+  std::vector<int> wb((size_t)nb * P * 16, 0);
+  std::vector<unsigned> ent((size_t)nnz + 64);
+  std::vector<float> tv((size_t)nnz + 64);
+  long long off = 0;
+  std::vector<int> tc((size_t)P * BS);
+  for (int b = 0; b < nb; ++b) {
+    std::fill(tc.begin(), tc.end(), 0);
+    for (int k = 0; k < K; ++k)
+      for (int t = 0; t < BS; ++t) {
+        const int r = b * RB + k * BS + t;
+        if (r >= n) continue;
+        for (int q = rp[r]; q < rp[r + 1]; ++q) tc[(size_t)(col[q] / W) * BS + t]++;
+      }
+    // offsets: tile-major, wave, lane, then (k, column)
+    std::vector<long long> pos((size_t)P * BS);
+    for (int p = 0; p < P; ++p)
+      for (int t = 0; t < BS; ++t) {
+        const int c = tc[(size_t)p * BS + t];
+        if (c > 255) {
+          fprintf(stderr, "count overflow\n");
+          return 1;
+        }
+        cnt[((size_t)b * P + p) * BS + t] = (unsigned char)c;
+        if ((t & 63) == 0) wb[((size_t)b * P + p) * 16 + t / 64] = (int)off;
+        pos[(size_t)p * BS + t] = off;
+        off += c;
+      }
+    for (int k = 0; k < K; ++k)
+      for (int t = 0; t < BS; ++t) {
+        const int r = b * RB + k * BS + t;
+        if (r >= n) continue;
+        for (int q = rp[r]; q < rp[r + 1]; ++q) {
+          const int p = col[q] / W;
+          const long long o = pos[(size_t)p * BS + t]++;
+          ent[(size_t)o] = ((unsigned)k << 14) | (unsigned)(col[q] - p * W);
+          tv[(size_t)o] = val[q];
+        }
+      }
+  }
+  // entries of a (tile, thread) must be ordered (k, column): k outer in the
+  // fill loop above, columns ascending within a row -- true by construction
+  const double host_s =
+      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  printf("n %d nnz %lld blocks %d panels %d host %.1f s\n", n, nnz, nb, P, host_s);
+
+  int *d_rp, *d_col, *d_wb;
+  float *d_val, *d_x, *d_y, *d_y2, *d_tv;
+  unsigned *d_ent;
+  unsigned char *d_cnt;
+  CK(hipMalloc(&d_rp, (n + 1) * 4));
+  CK(hipMalloc(&d_col, nnz * 4));
+  CK(hipMalloc(&d_val, nnz * 4));
+  CK(hipMalloc(&d_x, ((size_t)P * W + 64) * 4));
+  CK(hipMalloc(&d_y, (size_t)n * 4));
+  CK(hipMalloc(&d_y2, (size_t)n * 4));
+  CK(hipMalloc(&d_ent, ent.size() * 4));
+  CK(hipMalloc(&d_tv, tv.size() * 4));
+  CK(hipMalloc(&d_cnt, cnt.size()));
+  CK(hipMalloc(&d_wb, wb.size() * 4));
+  CK(hipMemset(d_x, 0, ((size_t)P * W + 64) * 4));
+  CK(hipMemcpy(d_rp, rp.data(), (n + 1) * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_col, col.data(), nnz * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_val, val.data(), nnz * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_x, xh.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_ent, ent.data(), ent.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_tv, tv.data(), tv.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_cnt, cnt.data(), cnt.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_wb, wb.data(), wb.size() * 4, hipMemcpyHostToDevice));
+  const Tiles T{d_ent, d_tv, d_cnt, d_wb, n, n, P};
+  const size_t lds = (size_t)(W + K * BS) * 4;
+  CK(hipFuncSetAttribute((const void *)k_xtile, hipFuncAttributeMaxDynamicSharedMemorySize,
+                         (int)lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto run = [&](int which) {
+    if (which == 0)
+      hipLaunchKernelGGL(k_xtile, dim3(nb), dim3(BS), lds, 0, T, d_x, d_y);
+    else
+      hipLaunchKernelGGL(k_csr_row, dim3((n + 255) / 256), dim3(256), 0, 0, n, d_rp, d_col,
+                         d_val, d_x, d_y2);
+  };
+  for (int which = 0; which < 2; ++which) {
+    run(which);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) run(which);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / reps;
+    const double bytes = (double)nnz * 8 + 4.0 * (n + 1) + 8.0 * n;
+    printf("%-10s %8.1f us  %6.0f GB/s on the CSR basis (%.0f MB)\n",
+           which == 0 ? "xtile" : "csr-row", us, bytes / us * 1e-3, bytes * 1e-6);
+  }
+  // bit-for-bit against the host row sums (every 97th row) and the CSR kernel (all)
+  std::vector<float> y(n), y2(n);
+  CK(hipMemcpy(y.data(), d_y, (size_t)n * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(y2.data(), d_y2, (size_t)n * 4, hipMemcpyDeviceToHost));
+  long long bad = 0, badh = 0;
+  for (int r = 0; r < n; ++r)
+    if (memcmp(&y[r], &y2[r], 4)) ++bad;
+  for (int r = 0; r < n; r += 97) {
+    float sum = 0.f;
+    for (int q = rp[r]; q < rp[r + 1]; ++q) {
+      const float pr = val[q] * xh[col[q]];
+      sum = sum + pr;
+    }
+    if (memcmp(&sum, &y[r], 4)) ++badh;
+  }
+  printf("mismatches: vs csr-row kernel %lld of %d rows, vs host %lld sampled\n", bad, n, badh);
+  return bad || badh ? 2 : 0;
+}
