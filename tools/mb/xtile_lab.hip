@@ -62,7 +62,7 @@ struct Tiles {
 };
 
 __global__ __launch_bounds__(BS) void k_xtile(Tiles T, const float *__restrict__ x,
-                                              float *__restrict__ y) {
+                                              float *__restrict__ y, int mode) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float *xs = lds;       // W
   float *acc = lds + W;  // K * BS
@@ -113,10 +113,12 @@ __global__ __launch_bounds__(BS) void k_xtile(Tiles T, const float *__restrict__
   if (P > 1) meta(1, c_nx, o_nx);
   for (int p = 0; p < P; ++p) {
     __syncthreads();  // every thread is done with the previous panel
+    if (!(mode & 2)) {
 #pragma unroll
-    for (int i = 0; i < W / BS / 4; ++i) reinterpret_cast<float4 *>(xs)[i * BS + t] = xr[i];
+      for (int i = 0; i < W / BS / 4; ++i) reinterpret_cast<float4 *>(xs)[i * BS + t] = xr[i];
+    }
     __syncthreads();
-    if (p + 1 < P) load_x(p + 1);
+    if (p + 1 < P && !(mode & 2)) load_x(p + 1);
     // this tile's entries (held since the previous iteration)
     unsigned cen[E];
     float cev[E];
@@ -127,12 +129,13 @@ __global__ __launch_bounds__(BS) void k_xtile(Tiles T, const float *__restrict__
     }
     const int c = c_cur, o = o_cur;
     // next tile's entries and the meta of the one after
-    if (p + 1 < P) {
+    if (p + 1 < P && !(mode & 1)) {
       load_ent(c_nx, o_nx);
       c_cur = c_nx;
       o_cur = o_nx;
       if (p + 2 < P) meta(p + 2, c_nx, o_nx);
     }
+    if (mode & 1) continue;
 #pragma unroll
     for (int j = 0; j < E; ++j)
       if (j < c) {
@@ -278,13 +281,14 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto run = [&](int which) {
-    if (which == 0)
-      hipLaunchKernelGGL(k_xtile, dim3(nb), dim3(BS), lds, 0, T, d_x, d_y);
+    if (which == 0 || which >= 2)
+      hipLaunchKernelGGL(k_xtile, dim3(nb), dim3(BS), lds, 0, T, d_x, which >= 2 ? d_y2 : d_y,
+                         which >= 2 ? which - 1 : 0);
     else
       hipLaunchKernelGGL(k_csr_row, dim3((n + 255) / 256), dim3(256), 0, 0, n, d_rp, d_col,
                          d_val, d_x, d_y2);
   };
-  for (int which = 0; which < 2; ++which) {
+  for (int which : {2, 3, 4, 0, 1}) {  // 2: x sweep only, 3: entries only, 4: syncs only
     run(which);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
@@ -295,8 +299,9 @@ int main(int argc, char **argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = 1e3 * ms / reps;
     const double bytes = (double)nnz * 8 + 4.0 * (n + 1) + 8.0 * n;
-    printf("%-10s %8.1f us  %6.0f GB/s on the CSR basis (%.0f MB)\n",
-           which == 0 ? "xtile" : "csr-row", us, bytes / us * 1e-3, bytes * 1e-6);
+    static const char *nm[] = {"xtile", "csr-row", "x-sweep", "entries", "syncs"};
+    printf("%-10s %8.1f us  %6.0f GB/s on the CSR basis (%.0f MB)\n", nm[which], us,
+           bytes / us * 1e-3, bytes * 1e-6);
   }
   // bit-for-bit against the host row sums (every 97th row) and the CSR kernel (all)
   std::vector<float> y(n), y2(n);
