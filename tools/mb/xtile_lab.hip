@@ -33,7 +33,8 @@
     }                                                                                \
   } while (0)
 
-constexpr int BS = 1024, K = 20, W = 16384, RB = BS * K, E = 12;  // E: entries held in VGPRs
+constexpr int BS = 1024, K = 20, W = 12288, RB = BS * K, E = 12;  // E: entries held in VGPRs
+constexpr int CH = 256;  // k_xtile2: entries of a wave's tile staged in LDS
 
 static unsigned long long sm64(unsigned long long &s) {
   unsigned long long z = (s += 0x9e3779b97f4a7c15ULL);
@@ -140,13 +141,113 @@ __global__ __launch_bounds__(BS) void k_xtile(Tiles T, const float *__restrict__
     for (int j = 0; j < E; ++j)
       if (j < c) {
         const unsigned e = cen[j];
-        const float pr = cev[j] * xs[e & (W - 1)];
+        const float pr = cev[j] * xs[e & 0x3fff];
         float &s = acc[(e >> 14) * BS + t];
         s = s + pr;
       }
     for (int j = E; j < c; ++j) {  // rare: more entries than registers
       const unsigned e = T.ent[o + j];
-      const float pr = T.val[o + j] * xs[e & (W - 1)];
+      const float pr = T.val[o + j] * xs[e & 0x3fff];
+      float &s = acc[(e >> 14) * BS + t];
+      s = s + pr;
+    }
+  }
+  const int r0 = b * RB;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = r0 + k * BS + t;
+    if (r < T.n) y[r] = acc[k * BS + t];
+  }
+}
+
+
+// v2: each wave's tile entries (contiguous, lane order) are loaded
+// cooperatively -- CH consecutive entries per wave, 4 + 4 coalesced loads
+// per lane, one tile ahead -- and staged in LDS; every lane then reads its
+// own entries there at its prefix offset (beyond CH: from memory, rare).
+__global__ __launch_bounds__(BS) void k_xtile2(Tiles T, const float *__restrict__ x,
+                                               float *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float *xs = lds;                                                   // W
+  float *acc = lds + W;                                              // K * BS
+  unsigned *se = reinterpret_cast<unsigned *>(lds + W + K * BS);     // 16 * CH
+  float *sv = lds + W + K * BS + 16 * CH;                            // 16 * CH
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int b = blockIdx.x;
+  const int P = T.P;
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k * BS + t] = 0.f;
+  float4 xr[W / BS / 4];
+  auto load_x = [&](int p) {
+    const int c0 = p * W;
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) {
+      const int j = (i * BS + t) * 4;
+      if (c0 + j + 3 < T.ncols) {
+        xr[i] = *reinterpret_cast<const float4 *>(x + c0 + j);
+      } else {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c0 + j + 0 < T.ncols) v.x = x[c0 + j + 0];
+        if (c0 + j + 1 < T.ncols) v.y = x[c0 + j + 1];
+        if (c0 + j + 2 < T.ncols) v.z = x[c0 + j + 2];
+        xr[i] = v;
+      }
+    }
+  };
+  unsigned cr[CH / 64];
+  float vr[CH / 64];
+  auto load_chunk = [&](int p) {
+    const long long tile = (long long)b * P + p;
+    const int w0 = T.wb[tile * 16 + wid];
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      cr[i] = T.ent[w0 + i * 64 + lane];  // padded arrays: always in bounds
+      vr[i] = T.val[w0 + i * 64 + lane];
+    }
+  };
+  // meta of tile p: this lane's count and its offset inside the wave's chunk
+  int c_a = 0, o_a = 0, c_b = 0, o_b = 0;
+  auto meta = [&](int p, int &c, int &o) {
+    const long long tile = (long long)b * P + p;
+    c = T.cnt[tile * BS + t];
+    o = wave_excl_scan(c);
+  };
+  load_x(0);
+  load_chunk(0);
+  meta(0, c_a, o_a);
+  if (P > 1) meta(1, c_b, o_b);
+  for (int p = 0; p < P; ++p) {
+    __syncthreads();  // the previous tile's reads of xs and the stage are done
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) reinterpret_cast<float4 *>(xs)[i * BS + t] = xr[i];
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      se[wid * CH + i * 64 + lane] = cr[i];
+      sv[wid * CH + i * 64 + lane] = vr[i];
+    }
+    __syncthreads();
+    const int c = c_a, o = o_a;
+    const long long tile = (long long)b * P + p;
+    if (p + 1 < P) {
+      load_x(p + 1);
+      load_chunk(p + 1);
+      c_a = c_b;
+      o_a = o_b;
+      if (p + 2 < P) meta(p + 2, c_b, o_b);
+    }
+    for (int j = 0; j < c; ++j) {
+      const int q = o + j;
+      unsigned e;
+      float v;
+      if (q < CH) {
+        e = se[wid * CH + q];
+        v = sv[wid * CH + q];
+      } else {
+        const int w0 = T.wb[tile * 16 + wid];
+        e = T.ent[w0 + q];
+        v = T.val[w0 + q];
+      }
+      const float pr = v * xs[e & 0x3fff];
       float &s = acc[(e >> 14) * BS + t];
       s = s + pr;
     }
@@ -205,9 +306,9 @@ int main(int argc, char **argv) {
   // tiles
   const int nb = (n + RB - 1) / RB, P = (n + W - 1) / W;
   std::vector<unsigned char> cnt((size_t)nb * P * BS, 0);
-  std::vector<int> wb((size_t)nb * P * 16, 0);
-  std::vector<unsigned> ent((size_t)nnz + 64);
-  std::vector<float> tv((size_t)nnz + 64);
+  std::vector<int> wb((size_t)nb * P * 16 + 1, 0);
+  std::vector<unsigned> ent((size_t)nnz + 2 * CH);
+  std::vector<float> tv((size_t)nnz + 2 * CH);
   long long off = 0;
   std::vector<int> tc((size_t)P * BS);
   for (int b = 0; b < nb; ++b) {
@@ -244,6 +345,7 @@ int main(int argc, char **argv) {
         }
       }
   }
+  wb[(size_t)nb * P * 16] = (int)off;
   // entries of a (tile, thread) must be ordered (k, column): k outer in the
   // fill loop above, columns ascending within a row -- true by construction
   const double host_s =
@@ -277,10 +379,17 @@ int main(int argc, char **argv) {
   const size_t lds = (size_t)(W + K * BS) * 4;
   CK(hipFuncSetAttribute((const void *)k_xtile, hipFuncAttributeMaxDynamicSharedMemorySize,
                          (int)lds));
+  const size_t lds2 = (size_t)(W + K * BS + 2 * 16 * CH) * 4;
+  CK(hipFuncSetAttribute((const void *)k_xtile2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                         (int)lds2));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto run = [&](int which) {
+    if (which == 5) {
+      hipLaunchKernelGGL(k_xtile2, dim3(nb), dim3(BS), lds2, 0, T, d_x, d_y);
+      return;
+    }
     if (which == 0 || which >= 2)
       hipLaunchKernelGGL(k_xtile, dim3(nb), dim3(BS), lds, 0, T, d_x, which >= 2 ? d_y2 : d_y,
                          which >= 2 ? which - 1 : 0);
@@ -288,7 +397,8 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k_csr_row, dim3((n + 255) / 256), dim3(256), 0, 0, n, d_rp, d_col,
                          d_val, d_x, d_y2);
   };
-  for (int which : {2, 3, 4, 0, 1}) {  // 2: x sweep only, 3: entries only, 4: syncs only
+  // 2: x sweep only, 3: entries only, 4: syncs only; 5 (v2) runs last and its y is checked
+  for (int which : {2, 3, 4, 0, 1, 5}) {
     run(which);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
@@ -299,7 +409,7 @@ int main(int argc, char **argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = 1e3 * ms / reps;
     const double bytes = (double)nnz * 8 + 4.0 * (n + 1) + 8.0 * n;
-    static const char *nm[] = {"xtile", "csr-row", "x-sweep", "entries", "syncs"};
+    static const char *nm[] = {"xtile", "csr-row", "x-sweep", "entries", "syncs", "xtile2"};
     printf("%-10s %8.1f us  %6.0f GB/s on the CSR basis (%.0f MB)\n", nm[which], us,
            bytes / us * 1e-3, bytes * 1e-6);
   }
