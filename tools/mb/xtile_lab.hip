@@ -260,6 +260,115 @@ __global__ __launch_bounds__(BS) void k_xtile2(Tiles T, const float *__restrict_
   }
 }
 
+// v3: v2 with the products formed balanced -- lane l multiplies chunk entries
+// l, l + 64, ... (from its load registers) and stages the products; the owner
+// lanes then only add them in order (2 LDS reads + the row-sum update each).
+// v2 (kept for the A/B): each wave's tile entries (contiguous, lane order) are loaded
+// cooperatively -- CH consecutive entries per wave, 4 + 4 coalesced loads
+// per lane, one tile ahead -- and staged in LDS; every lane then reads its
+// own entries there at its prefix offset (beyond CH: from memory, rare).
+__global__ __launch_bounds__(BS) void k_xtile3(Tiles T, const float *__restrict__ x,
+                                               float *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float *xs = lds;                                                   // W
+  float *acc = lds + W;                                              // K * BS
+  unsigned *se = reinterpret_cast<unsigned *>(lds + W + K * BS);     // 16 * CH
+  float *sv = lds + W + K * BS + 16 * CH;                            // 16 * CH
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int b = blockIdx.x;
+  const int P = T.P;
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k * BS + t] = 0.f;
+  float4 xr[W / BS / 4];
+  auto load_x = [&](int p) {
+    const int c0 = p * W;
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) {
+      const int j = (i * BS + t) * 4;
+      if (c0 + j + 3 < T.ncols) {
+        xr[i] = *reinterpret_cast<const float4 *>(x + c0 + j);
+      } else {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c0 + j + 0 < T.ncols) v.x = x[c0 + j + 0];
+        if (c0 + j + 1 < T.ncols) v.y = x[c0 + j + 1];
+        if (c0 + j + 2 < T.ncols) v.z = x[c0 + j + 2];
+        xr[i] = v;
+      }
+    }
+  };
+  unsigned cr[CH / 64];
+  float vr[CH / 64];
+  auto load_chunk = [&](int p) {
+    const long long tile = (long long)b * P + p;
+    const int w0 = T.wb[tile * 16 + wid];
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      cr[i] = T.ent[w0 + i * 64 + lane];  // padded arrays: always in bounds
+      vr[i] = T.val[w0 + i * 64 + lane];
+    }
+  };
+  // meta of tile p: this lane's count and its offset inside the wave's chunk
+  int c_a = 0, o_a = 0, c_b = 0, o_b = 0;
+  auto meta = [&](int p, int &c, int &o) {
+    const long long tile = (long long)b * P + p;
+    c = T.cnt[tile * BS + t];
+    o = wave_excl_scan(c);
+  };
+  load_x(0);
+  load_chunk(0);
+  meta(0, c_a, o_a);
+  if (P > 1) meta(1, c_b, o_b);
+  for (int p = 0; p < P; ++p) {
+    __syncthreads();  // the previous tile's reads of xs and the stage are done
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) reinterpret_cast<float4 *>(xs)[i * BS + t] = xr[i];
+    __syncthreads();
+    // products of the staged chunk, balanced over the wave's lanes (entries
+    // past the wave's tile are padding: their product is never read)
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      const float pr = vr[i] * xs[cr[i] & 0x3fff];
+      se[wid * CH + i * 64 + lane] = cr[i];
+      sv[wid * CH + i * 64 + lane] = pr;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int c = c_a, o = o_a;
+    const long long tile = (long long)b * P + p;
+    if (p + 1 < P) {
+      load_x(p + 1);
+      load_chunk(p + 1);
+      c_a = c_b;
+      o_a = o_b;
+      if (p + 2 < P) meta(p + 2, c_b, o_b);
+    }
+    for (int j = 0; j < c; ++j) {
+      const int q = o + j;
+      unsigned e;
+      float v;
+      float pr;
+      if (q < CH) {
+        e = se[wid * CH + q];
+        pr = sv[wid * CH + q];
+      } else {
+        const int w0 = T.wb[tile * 16 + wid];
+        e = T.ent[w0 + q];
+        v = T.val[w0 + q];
+        pr = v * xs[e & 0x3fff];
+      }
+      float &s = acc[(e >> 14) * BS + t];
+      s = s + pr;
+    }
+  }
+  const int r0 = b * RB;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = r0 + k * BS + t;
+    if (r < T.n) y[r] = acc[k * BS + t];
+  }
+}
+
 // plain CSR, one row per thread, sequential float sum (the reference order)
 __global__ __launch_bounds__(256) void k_csr_row(int n, const int *rp, const int *col,
                                                  const float *val, const float *x, float *y) {
@@ -382,12 +491,18 @@ int main(int argc, char **argv) {
   const size_t lds2 = (size_t)(W + K * BS + 2 * 16 * CH) * 4;
   CK(hipFuncSetAttribute((const void *)k_xtile2, hipFuncAttributeMaxDynamicSharedMemorySize,
                          (int)lds2));
+  CK(hipFuncSetAttribute((const void *)k_xtile3, hipFuncAttributeMaxDynamicSharedMemorySize,
+                         (int)lds2));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto run = [&](int which) {
     if (which == 5) {
       hipLaunchKernelGGL(k_xtile2, dim3(nb), dim3(BS), lds2, 0, T, d_x, d_y);
+      return;
+    }
+    if (which == 6) {
+      hipLaunchKernelGGL(k_xtile3, dim3(nb), dim3(BS), lds2, 0, T, d_x, d_y);
       return;
     }
     if (which == 0 || which >= 2)
@@ -397,8 +512,8 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k_csr_row, dim3((n + 255) / 256), dim3(256), 0, 0, n, d_rp, d_col,
                          d_val, d_x, d_y2);
   };
-  // 2: x sweep only, 3: entries only, 4: syncs only; 5 (v2) runs last and its y is checked
-  for (int which : {2, 3, 4, 0, 1, 5}) {
+  // 2: x sweep only, 3: entries only, 4: syncs only (v1), 5: v2, 6: v3
+  for (int which : {2, 4, 1, 5, 6, 5, 6}) {  // v3 last: its y is checked
     run(which);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
@@ -409,7 +524,8 @@ int main(int argc, char **argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = 1e3 * ms / reps;
     const double bytes = (double)nnz * 8 + 4.0 * (n + 1) + 8.0 * n;
-    static const char *nm[] = {"xtile", "csr-row", "x-sweep", "entries", "syncs", "xtile2"};
+    static const char *nm[] = {"xtile", "csr-row", "x-sweep", "entries", "syncs", "xtile2",
+                               "xtile3"};
     printf("%-10s %8.1f us  %6.0f GB/s on the CSR basis (%.0f MB)\n", nm[which], us,
            bytes / us * 1e-3, bytes * 1e-6);
   }
