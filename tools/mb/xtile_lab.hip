@@ -5,7 +5,7 @@
 // Layout: row blocks of K * 1024 rows (one 1024-thread workgroup each, thread
 // t owns rows t + 1024 k); column panels of W entries of x.  Tile (block,
 // panel) holds, for each thread, its rows' entries with a column in the
-// panel, ordered (row slot k, column): u32 (k << 14 | local column) + f32
+// panel, ordered (row slot k, column): u32 (k << 15 | local column) + f32
 // value.  Per tile: a u8 entry count per thread, an entry offset per wave.
 // The workgroup walks the panels in order: x panel -> LDS, every thread adds
 // its entries' products to its rows' sums (LDS, one slot per owned row) --
@@ -13,7 +13,8 @@
 // sum, so y is bit-identical to a row-by-row float sum.  Prefetch: the next
 // panel's x and the next tile's entries are in flight while a tile is summed.
 //
-// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o xtile_lab xtile_lab.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off [-DXW=24576 -DXCH=512] -o xtile_lab xtile_lab.hip
+//        (XW: x entries per panel, XCH: staged entries per wave; v1-v3 run when they fit LDS)
 // Run:   ./xtile_lab [n] [partners per row] [reps]       (default 5000000 32 20)
 #include <hip/hip_runtime.h>
 
@@ -33,8 +34,14 @@
     }                                                                                \
   } while (0)
 
-constexpr int BS = 1024, K = 20, W = 12288, RB = BS * K, E = 12;  // E: entries held in VGPRs
-constexpr int CH = 256;  // k_xtile2: entries of a wave's tile staged in LDS
+#ifndef XW
+#define XW 12288
+#endif
+#ifndef XCH
+#define XCH 256
+#endif
+constexpr int BS = 1024, K = 20, W = XW, RB = BS * K, E = 12;  // E: entries held in VGPRs
+constexpr int CH = XCH;  // k_xtile2/3/4: entries of a wave's tile staged in LDS
 
 static unsigned long long sm64(unsigned long long &s) {
   unsigned long long z = (s += 0x9e3779b97f4a7c15ULL);
@@ -141,14 +148,14 @@ __global__ __launch_bounds__(BS) void k_xtile(Tiles T, const float *__restrict__
     for (int j = 0; j < E; ++j)
       if (j < c) {
         const unsigned e = cen[j];
-        const float pr = cev[j] * xs[e & 0x3fff];
-        float &s = acc[(e >> 14) * BS + t];
+        const float pr = cev[j] * xs[e & 0x7fff];
+        float &s = acc[(e >> 15) * BS + t];
         s = s + pr;
       }
     for (int j = E; j < c; ++j) {  // rare: more entries than registers
       const unsigned e = T.ent[o + j];
-      const float pr = T.val[o + j] * xs[e & 0x3fff];
-      float &s = acc[(e >> 14) * BS + t];
+      const float pr = T.val[o + j] * xs[e & 0x7fff];
+      float &s = acc[(e >> 15) * BS + t];
       s = s + pr;
     }
   }
@@ -247,8 +254,8 @@ __global__ __launch_bounds__(BS) void k_xtile2(Tiles T, const float *__restrict_
         e = T.ent[w0 + q];
         v = T.val[w0 + q];
       }
-      const float pr = v * xs[e & 0x3fff];
-      float &s = acc[(e >> 14) * BS + t];
+      const float pr = v * xs[e & 0x7fff];
+      float &s = acc[(e >> 15) * BS + t];
       s = s + pr;
     }
   }
@@ -327,7 +334,7 @@ __global__ __launch_bounds__(BS) void k_xtile3(Tiles T, const float *__restrict_
     // past the wave's tile are padding: their product is never read)
 #pragma unroll
     for (int i = 0; i < CH / 64; ++i) {
-      const float pr = vr[i] * xs[cr[i] & 0x3fff];
+      const float pr = vr[i] * xs[cr[i] & 0x7fff];
       se[wid * CH + i * 64 + lane] = cr[i];
       sv[wid * CH + i * 64 + lane] = pr;
     }
@@ -355,9 +362,9 @@ __global__ __launch_bounds__(BS) void k_xtile3(Tiles T, const float *__restrict_
         const int w0 = T.wb[tile * 16 + wid];
         e = T.ent[w0 + q];
         v = T.val[w0 + q];
-        pr = v * xs[e & 0x3fff];
+        pr = v * xs[e & 0x7fff];
       }
-      float &s = acc[(e >> 14) * BS + t];
+      float &s = acc[(e >> 15) * BS + t];
       s = s + pr;
     }
   }
@@ -366,6 +373,118 @@ __global__ __launch_bounds__(BS) void k_xtile3(Tiles T, const float *__restrict_
   for (int k = 0; k < K; ++k) {
     const int r = r0 + k * BS + t;
     if (r < T.n) y[r] = acc[k * BS + t];
+  }
+}
+
+// v4: v3 with the row sums in VGPRs (acc[k] selected per entry, no LDS row
+// sums), so x panels can take most of the LDS: fewer, wider panel steps.
+// v2 (kept for the A/B): each wave's tile entries (contiguous, lane order) are loaded
+// cooperatively -- CH consecutive entries per wave, 4 + 4 coalesced loads
+// per lane, one tile ahead -- and staged in LDS; every lane then reads its
+// own entries there at its prefix offset (beyond CH: from memory, rare).
+__global__ __launch_bounds__(BS) void k_xtile4(Tiles T, const float *__restrict__ x,
+                                               float *__restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float *xs = lds;                                           // W
+  unsigned *se = reinterpret_cast<unsigned *>(lds + W);      // 16 * CH
+  float *sv = lds + W + 16 * CH;                             // 16 * CH
+  const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+  const int b = blockIdx.x;
+  const int P = T.P;
+  float acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.f;
+  float4 xr[W / BS / 4];
+  auto load_x = [&](int p) {
+    const int c0 = p * W;
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) {
+      const int j = (i * BS + t) * 4;
+      if (c0 + j + 3 < T.ncols) {
+        xr[i] = *reinterpret_cast<const float4 *>(x + c0 + j);
+      } else {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c0 + j + 0 < T.ncols) v.x = x[c0 + j + 0];
+        if (c0 + j + 1 < T.ncols) v.y = x[c0 + j + 1];
+        if (c0 + j + 2 < T.ncols) v.z = x[c0 + j + 2];
+        xr[i] = v;
+      }
+    }
+  };
+  unsigned cr[CH / 64];
+  float vr[CH / 64];
+  auto load_chunk = [&](int p) {
+    const long long tile = (long long)b * P + p;
+    const int w0 = T.wb[tile * 16 + wid];
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      cr[i] = T.ent[w0 + i * 64 + lane];  // padded arrays: always in bounds
+      vr[i] = T.val[w0 + i * 64 + lane];
+    }
+  };
+  // meta of tile p: this lane's count and its offset inside the wave's chunk
+  int c_a = 0, o_a = 0, c_b = 0, o_b = 0;
+  auto meta = [&](int p, int &c, int &o) {
+    const long long tile = (long long)b * P + p;
+    c = T.cnt[tile * BS + t];
+    o = wave_excl_scan(c);
+  };
+  load_x(0);
+  load_chunk(0);
+  meta(0, c_a, o_a);
+  if (P > 1) meta(1, c_b, o_b);
+  for (int p = 0; p < P; ++p) {
+    __syncthreads();  // the previous tile's reads of xs and the stage are done
+#pragma unroll
+    for (int i = 0; i < W / BS / 4; ++i) reinterpret_cast<float4 *>(xs)[i * BS + t] = xr[i];
+    __syncthreads();
+    // products of the staged chunk, balanced over the wave's lanes (entries
+    // past the wave's tile are padding: their product is never read)
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      const float pr = vr[i] * xs[cr[i] & 0x7fff];
+      se[wid * CH + i * 64 + lane] = cr[i];
+      sv[wid * CH + i * 64 + lane] = pr;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int c = c_a, o = o_a;
+    const long long tile = (long long)b * P + p;
+    if (p + 1 < P) {
+      load_x(p + 1);
+      load_chunk(p + 1);
+      c_a = c_b;
+      o_a = o_b;
+      if (p + 2 < P) meta(p + 2, c_b, o_b);
+    }
+    for (int j = 0; j < c; ++j) {
+      const int q = o + j;
+      unsigned e;
+      float v;
+      float pr;
+      if (q < CH) {
+        e = se[wid * CH + q];
+        pr = sv[wid * CH + q];
+      } else {
+        const int w0 = T.wb[tile * 16 + wid];
+        e = T.ent[w0 + q];
+        v = T.val[w0 + q];
+        pr = v * xs[e & 0x7fff];
+      }
+      const unsigned slot = e >> 15;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float a2 = acc[k] + pr;
+        acc[k] = slot == (unsigned)k ? a2 : acc[k];
+      }
+    }
+  }
+  const int r0 = b * RB;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int r = r0 + k * BS + t;
+    if (r < T.n) y[r] = acc[k];
   }
 }
 
@@ -449,7 +568,7 @@ int main(int argc, char **argv) {
         for (int q = rp[r]; q < rp[r + 1]; ++q) {
           const int p = col[q] / W;
           const long long o = pos[(size_t)p * BS + t]++;
-          ent[(size_t)o] = ((unsigned)k << 14) | (unsigned)(col[q] - p * W);
+          ent[(size_t)o] = ((unsigned)k << 15) | (unsigned)(col[q] - p * W);
           tv[(size_t)o] = val[q];
         }
       }
@@ -486,13 +605,19 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(d_wb, wb.data(), wb.size() * 4, hipMemcpyHostToDevice));
   const Tiles T{d_ent, d_tv, d_cnt, d_wb, n, n, P};
   const size_t lds = (size_t)(W + K * BS) * 4;
-  CK(hipFuncSetAttribute((const void *)k_xtile, hipFuncAttributeMaxDynamicSharedMemorySize,
-                         (int)lds));
   const size_t lds2 = (size_t)(W + K * BS + 2 * 16 * CH) * 4;
-  CK(hipFuncSetAttribute((const void *)k_xtile2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                         (int)lds2));
-  CK(hipFuncSetAttribute((const void *)k_xtile3, hipFuncAttributeMaxDynamicSharedMemorySize,
-                         (int)lds2));
+  const size_t lds4 = (size_t)(W + 2 * 16 * CH) * 4;
+  const bool small = lds2 <= 163840;  // v1-v3 fit next to the LDS row sums
+  if (small) {
+    CK(hipFuncSetAttribute((const void *)k_xtile, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)lds));
+    CK(hipFuncSetAttribute((const void *)k_xtile2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)lds2));
+    CK(hipFuncSetAttribute((const void *)k_xtile3, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)lds2));
+  }
+  CK(hipFuncSetAttribute((const void *)k_xtile4, hipFuncAttributeMaxDynamicSharedMemorySize,
+                         (int)lds4));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -505,6 +630,10 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL(k_xtile3, dim3(nb), dim3(BS), lds2, 0, T, d_x, d_y);
       return;
     }
+    if (which == 7) {
+      hipLaunchKernelGGL(k_xtile4, dim3(nb), dim3(BS), lds4, 0, T, d_x, d_y);
+      return;
+    }
     if (which == 0 || which >= 2)
       hipLaunchKernelGGL(k_xtile, dim3(nb), dim3(BS), lds, 0, T, d_x, which >= 2 ? d_y2 : d_y,
                          which >= 2 ? which - 1 : 0);
@@ -513,7 +642,8 @@ int main(int argc, char **argv) {
                          d_val, d_x, d_y2);
   };
   // 2: x sweep only, 3: entries only, 4: syncs only (v1), 5: v2, 6: v3
-  for (int which : {2, 4, 1, 5, 6, 5, 6}) {  // v3 last: its y is checked
+  std::vector<int> order = small ? std::vector<int>{1, 6, 7, 6, 7} : std::vector<int>{1, 7, 7};
+  for (int which : order) {  // the last one's y is checked
     run(which);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
@@ -525,7 +655,7 @@ int main(int argc, char **argv) {
     const double us = 1e3 * ms / reps;
     const double bytes = (double)nnz * 8 + 4.0 * (n + 1) + 8.0 * n;
     static const char *nm[] = {"xtile", "csr-row", "x-sweep", "entries", "syncs", "xtile2",
-                               "xtile3"};
+                               "xtile3", "xtile4"};
     printf("%-10s %8.1f us  %6.0f GB/s on the CSR basis (%.0f MB)\n", nm[which], us,
            bytes / us * 1e-3, bytes * 1e-6);
   }
