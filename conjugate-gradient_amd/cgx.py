@@ -140,6 +140,9 @@ _SIGS = {
                                                ctypes.c_ulonglong, ctypes.c_int,
                                                ctypes.c_int, _i32p, _i32p, _f64p,
                                                _f32p]),
+    "cgx_gen_varcoef3d": (ctypes.c_longlong, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_ulonglong, ctypes.c_int, ctypes.c_int,
+                                              _i32p, _i32p, _f64p]),
     "cgx_csr_is_chained": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p]),
     "cgx_read_input_file": (ctypes.c_int, [ctypes.c_char_p, _MVP, _MVP]),
     "cgx_read_input_cached": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, _MVP, _MVP,
@@ -280,6 +283,14 @@ def laplacian_row_ptr(dim, nx, ny, nz=1, row_begin=0, row_end=None):
 def laplacian3d(nx, ny, nz, row_begin=0, row_end=None):
     row_end = nx * ny * nz if row_end is None else row_end
     return _gen("cgx_gen_laplacian3d", (nx, ny, nz, row_begin, row_end),
+                row_end - row_begin)
+
+
+def varcoef3d(nx, ny, nz, seed=7, row_begin=0, row_end=None):
+    """7-point pattern, one random SPD coefficient per grid edge
+    (cgx_gen_varcoef3d): no layout can index its values."""
+    row_end = nx * ny * nz if row_end is None else row_end
+    return _gen("cgx_gen_varcoef3d", (nx, ny, nz, seed, row_begin, row_end),
                 row_end - row_begin)
 
 

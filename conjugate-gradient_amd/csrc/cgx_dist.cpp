@@ -4,7 +4,7 @@
 // 8e; north star in BASELINE.json).  Each rank's rows live in a DevMatrix
 // (cgx_matrix.h) with local column numbering: owned rows -> [0, n_loc),
 // ghosts -> n_loc + position, so the halo exchange writes the gathered
-// vector's ghost tail directly and every layout (CSR, CSR-DC, CSR-VI) works
+// vector's ghost tail directly and every layout (CSR, CSR-DC, DIA-VI) works
 // unchanged -- a slab's ghost columns are one more constant offset per face.
 //
 // Recurrences (cgx_dist_set_alg):
@@ -82,6 +82,7 @@ struct cgx_dist {
   int cus = 256;
   hipStream_t st = nullptr, st_comm = nullptr;
   hipEvent_t ev_packed = nullptr, ev_halo = nullptr, ev_sums = nullptr, ev_sums2 = nullptr;
+  hipEvent_t ev_red = nullptr;  // local transport: this part's last group sum has read d_sums
   cgx_part *part = nullptr;
   long long n_global = 0;
   int row_begin = 0, n_loc = 0, n_ghost = 0, nnz = 0;
@@ -94,7 +95,10 @@ struct cgx_dist {
   double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
          *d_w = nullptr;
   double *d_p2 = nullptr;  // fused step: the second p buffer (with ghost tail)
-  int pbuf = 0;            // fused step: which buffer holds p_old (0: d_p)
+  // fused CG1 step: the second r, s, w buffers (with ghost tails)
+  double *d_r2 = nullptr, *d_s2 = nullptr, *d_w2 = nullptr;
+  int pbuf = 0;            // fused step: which buffer holds p_old (0: d_p) / r, s, w_old
+  bool in_init = false;    // the CG1 prologue's phases (unfused SpMV w = A r)
   int fuse = CGX_FUSE_AUTO;  // cgx_dist_set_fused
   bool fz_all = false;     // every partition's layout takes the fused step (ensure_connected)
   int *d_send_idx = nullptr;
@@ -156,6 +160,8 @@ void drop_graph(cgx_dist *d) {
 // The fused HS step (k_spmv_dia_h) runs when every partition's layout
 // takes it (decided once per connection: the ranks' phase sequences match).
 bool fz(const cgx_dist *d) { return d->fz_all && d->alg == CGX_ALG_HS; }
+// The fused CG1 step (k_cg1_dia_h), same rule; not in the prologue.
+bool fz1(const cgx_dist *d) { return d->fz_all && d->alg == CGX_ALG_CG1 && !d->in_init; }
 
 // this partition takes the fused step (cgx_solver.cpp fused(): auto needs a
 // working set beyond the Infinity Cache)
@@ -175,6 +181,9 @@ void free_system(cgx_dist *d) {
   dev_free(&d->d_s);
   dev_free(&d->d_w);
   dev_free(&d->d_p2);
+  dev_free(&d->d_r2);
+  dev_free(&d->d_s2);
+  dev_free(&d->d_w2);
   dev_free(&d->d_send_idx);
   dev_free(&d->d_sendbuf);
   dev_free(&d->d_pa);
@@ -208,6 +217,7 @@ int init_common(cgx_dist *d, int device) {
   CGX_HIP(hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums2, hipEventDisableTiming));
+  CGX_HIP(hipEventCreateWithFlags(&d->ev_red, hipEventDisableTiming));
   CGX_HIP(hipMalloc((void **)&d->d_st, sizeof(CgState)));
   CGX_HIP(hipMalloc((void **)&d->d_sums, 4 * sizeof(double)));
   CGX_HIP(hipMemset(d->d_sums, 0, 4 * sizeof(double)));
@@ -287,19 +297,23 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
   d->vec_grid = vec_grid_for(n_loc, d->cus);
   d->vec_grid = (std::max(d->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
   const size_t nv = (size_t)n_loc + kPad, ng = nv + (size_t)d->n_ghost;
+  // d_pa: the vector kernels' partials, or the fused CG1 step's gamma partials
+  const size_t npa = (size_t)std::max(d->vec_grid, d->g_int + d->g_bnd) + 8;
   size_t *cb = &d->vec_bytes;
+  // r, p, s, w and their second buffers carry the ghost tail (s, w: the fused
+  // CG1 step's window / far-slot loads reach it; only zeros are read there)
   if ((rc = dev_alloc(&d->d_b, nv * 8, cb)) || (rc = dev_alloc(&d->d_x, nv * 8, cb)) ||
       (rc = dev_alloc(&d->d_r, ng * 8, cb)) || (rc = dev_alloc(&d->d_p, ng * 8, cb)) ||
-      (rc = dev_alloc(&d->d_s, nv * 8, cb)) || (rc = dev_alloc(&d->d_w, nv * 8, cb)) ||
-      (rc = dev_alloc(&d->d_p2, ng * 8, cb)) ||
-      (rc = dev_alloc(&d->d_pa, ((size_t)d->vec_grid + 8) * 8, cb)) ||
+      (rc = dev_alloc(&d->d_s, ng * 8, cb)) || (rc = dev_alloc(&d->d_w, ng * 8, cb)) ||
+      (rc = dev_alloc(&d->d_p2, ng * 8, cb)) || (rc = dev_alloc(&d->d_r2, ng * 8, cb)) ||
+      (rc = dev_alloc(&d->d_s2, ng * 8, cb)) || (rc = dev_alloc(&d->d_w2, ng * 8, cb)) ||
+      (rc = dev_alloc(&d->d_pa, npa * 8, cb)) ||
       (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb))) {
     free_system(d);
     return rc;
   }
-  CGX_HIP(hipMemsetAsync(d->d_r, 0, ng * 8, d->st));
-  CGX_HIP(hipMemsetAsync(d->d_p, 0, ng * 8, d->st));
-  CGX_HIP(hipMemsetAsync(d->d_p2, 0, ng * 8, d->st));
+  for (double *v : {d->d_r, d->d_p, d->d_p2, d->d_s, d->d_w, d->d_r2, d->d_s2, d->d_w2})
+    CGX_HIP(hipMemsetAsync(v, 0, ng * 8, d->st));
   CGX_HIP(hipMemsetAsync(d->d_x, 0, nv * 8, d->st));
   CGX_HIP(hipStreamSynchronize(d->st));
   d->have_matrix = true;
@@ -466,12 +480,22 @@ int ensure_connected(Group *g) {
 // fused: the p_new buffer
 double *p_old(cgx_dist *d) { return d->pbuf ? d->d_p2 : d->d_p; }
 double *p_new(cgx_dist *d) { return d->pbuf ? d->d_p : d->d_p2; }
+// fused CG1: r, s, w of the last iteration (read) and of this one (written)
+double *r_old(cgx_dist *d) { return d->pbuf ? d->d_r2 : d->d_r; }
+double *r_new(cgx_dist *d) { return d->pbuf ? d->d_r : d->d_r2; }
+double *s_old(cgx_dist *d) { return d->pbuf ? d->d_s2 : d->d_s; }
+double *s_new(cgx_dist *d) { return d->pbuf ? d->d_s : d->d_s2; }
+double *w_old(cgx_dist *d) { return d->pbuf ? d->d_w2 : d->d_w; }
+double *w_new(cgx_dist *d) { return d->pbuf ? d->d_w : d->d_w2; }
 double *spmv_x(cgx_dist *d) {
-  return d->alg != CGX_ALG_HS ? d->d_r : fz(d) ? p_new(d) : d->d_p;
+  if (d->alg != CGX_ALG_HS) return fz1(d) ? r_new(d) : d->d_r;
+  return fz(d) ? p_new(d) : d->d_p;
 }
 // r.r of the last r update, as the fused step reads it
 const double *rr_new_src(cgx_dist *d) { return solo(d) ? &d->d_st->rr_new : d->d_gsums + 1; }
-double *spmv_y(cgx_dist *d) { return d->alg == CGX_ALG_HS ? d->d_s : d->d_w; }
+double *spmv_y(cgx_dist *d) {
+  return d->alg == CGX_ALG_HS ? d->d_s : fz1(d) ? w_new(d) : d->d_w;
+}
 
 // pack the send rows of the gathered vector (after its update; fused:
 // p_new = r + beta p_old computed at the send rows)
@@ -480,6 +504,9 @@ int phase_pack(cgx_dist *d) {
   if (fz(d))
     CGX_HIP(launch_pack_pnext<double>(d->n_send, d->d_send_idx, d->d_r, p_old(d), d->d_sendbuf,
                                       d->d_st, rr_new_src(d), d->st));
+  else if (fz1(d))
+    CGX_HIP(launch_pack_rnext<double>(d->n_send, d->d_send_idx, r_old(d), w_old(d), s_old(d),
+                                      d->d_sendbuf, d->d_st, d->st));
   else
     CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, spmv_x(d), d->d_sendbuf, d->st));
   CGX_HIP(hipEventRecord(d->ev_packed, d->st));
@@ -540,6 +567,13 @@ int phase_spmv(cgx_dist *d) {
       return hipSuccess;
     }
     SpmvArgs<double> a = d->A.args<double>(spmv_x(d), spmv_y(d), part, &d->d_st->done, it);
+    if (fz1(d)) {
+      // gamma partials beside the delta ones (d_pa / d_pb, same offsets)
+      const Cg1Args<double> f{d->d_x,   d->d_p,     r_old(d), s_old(d), w_old(d),
+                              r_new(d), s_new(d),   d->d_st,  d->d_pa + (part - d->d_pb),
+                              e == 2 ? 1 : 0};
+      return launch_cg1_fused<double>(a, f, d->st, ev);
+    }
     if (fz(d)) {
       // the first non-empty launch publishes the scalar step; boundary
       // items (e == 2) read ghost columns' p_new from the halo
@@ -555,12 +589,21 @@ int phase_spmv(cgx_dist *d) {
   CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, 2));
   if (rec) d->ev_i += 4;
   if (solo(d)) return 0;
+  // local transport: every part's group sum of the last reduction must have
+  // read this part's local sums before they are overwritten.  The halo orders
+  // this part only after its NEIGHBOURS' packs, so without the wait a part
+  // could overwrite its prologue b.b (or last r.r) while a distant part was
+  // still summing it: a race at P >= 3, seen on C4's 8 slabs (x wrong in the
+  // first group of a process).  RCCL ranks reduce on their own stream.
+  if (d->local)
+    for (cgx_dist *o : d->group->parts)
+      if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
   if (d->alg == CGX_ALG_HS)
     CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
                             d->st));
   else
-    CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, d->vec_grid, d->d_pb, np, d->d_st, d->d_hist,
-                            d->d_sums, d->st));
+    CGX_HIP(launch_finalize(FIN_SUM2, d->d_pa, fz1(d) ? np : d->vec_grid, d->d_pb, np, d->d_st,
+                            d->d_hist, d->d_sums, d->st));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
@@ -572,6 +615,7 @@ int allreduce(cgx_dist *d, int i, int count) {
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, i == 0 ? o->ev_sums : o->ev_sums2, 0));
     CGX_HIP(launch_group_sum(d->group->d_srcs, (int)d->group->parts.size(), count, d->d_gsums,
                              d->st, i));
+    CGX_HIP(hipEventRecord(d->ev_red, d->st));
   } else {
     CGX_NCCL(ncclAllReduce(d->d_sums + i, d->d_gsums + i, count, ncclFloat64, ncclSum, d->comm,
                            d->st));
@@ -643,12 +687,14 @@ int hs_beta(cgx_dist *d) {
 }
 
 // ---- CG1
+// (fused CG1: the vector recurrences run inside the SpMV launch; only the
+// halo rows of r_new are packed here)
 int cg1_update(cgx_dist *d, bool init) {
   CGX_HIP(hipSetDevice(d->device));
   if (init)
     CGX_HIP(launch_init_cg1<double>(d->n_loc, d->d_b, d->d_x, d->d_r, d->d_p, d->d_s, d->d_pa,
                                     d->vec_grid, d->st));
-  else
+  else if (!fz1(d))
     CGX_HIP(launch_cg1_update<double>(d->n_loc, d->d_x, d->d_p, d->d_r, d->d_s, d->d_w, d->d_st,
                                       d->d_pa, d->vec_grid, d->st));
   return phase_pack(d);
@@ -657,14 +703,17 @@ int cg1_update(cgx_dist *d, bool init) {
 int cg1_reduce(cgx_dist *d, bool init) {
   CGX_HIP(hipSetDevice(d->device));
   const int op = init ? FIN_INIT_CG1 : FIN_CG1;
+  const int np = d->g_int + d->g_bnd;
   if (solo(d)) {
-    CGX_HIP(launch_finalize(op, d->d_pa, d->vec_grid, d->d_pb, d->g_int + d->g_bnd, d->d_st,
+    CGX_HIP(launch_finalize(op, d->d_pa, fz1(d) ? np : d->vec_grid, d->d_pb, np, d->d_st,
                             d->d_hist, nullptr, d->st));
+    if (fz1(d)) d->pbuf ^= 1;
     return 0;
   }
   int rc = allreduce(d, 0, 2);
   if (rc) return rc;
   CGX_HIP(launch_finalize(op, d->d_gsums, 1, d->d_gsums + 1, 1, d->d_st, d->d_hist, nullptr, d->st));
+  if (fz1(d)) d->pbuf ^= 1;
   return 0;
 }
 
@@ -710,13 +759,20 @@ int run_phases_eager(Group *g, bool init, long long iters) {
     }
     return 0;
   }
-  for (long long it = 0; it < (init ? 1 : iters); ++it) {
-    for (cgx_dist *d : P) if ((rc = cg1_update(d, init))) return rc;
-    for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
-    for (cgx_dist *d : P) if ((rc = phase_spmv(d))) return rc;
-    for (cgx_dist *d : P) if ((rc = cg1_reduce(d, init))) return rc;
+  // the prologue (x = 0, r = b, w = A r) runs the unfused phases
+  for (cgx_dist *d : P) {
+    d->in_init = init;
+    if (init) d->pbuf = 0;  // the prologue writes r, s, w into the first buffers
   }
-  return 0;
+  rc = 0;
+  for (long long it = 0; it < (init ? 1 : iters) && rc == 0; ++it) {
+    for (cgx_dist *d : P) if (rc == 0) rc = cg1_update(d, init);
+    for (cgx_dist *d : P) if (rc == 0) rc = phase_halo(d);
+    for (cgx_dist *d : P) if (rc == 0) rc = phase_spmv(d);
+    for (cgx_dist *d : P) if (rc == 0) rc = cg1_reduce(d, init);
+  }
+  for (cgx_dist *d : P) d->in_init = false;
+  return rc;
 }
 
 // Capture `nit` iterations (kernels, halo send/recv on the comm stream
@@ -752,10 +808,10 @@ bool graphs_on(const cgx_dist *d) {
 int ensure_graphs(Group *g) {
   cgx_dist *d = g->parts[0];
   if (!graphs_on(d)) return 0;
-  const int key = d->alg * 2 + (fz(d) ? 1 : 0);
+  const int key = d->alg * 2 + (fz(d) || fz1(d) ? 1 : 0);
   if (d->gexec[0] && d->gexec1[0] && d->gexec_alg == key) return 0;
   drop_graph(d);
-  const int nq = fz(d) ? 2 : 1;
+  const int nq = fz(d) || fz1(d) ? 2 : 1;
   for (int q = 0; q < nq; ++q)
     if (capture(d, g, d->graph_batch, q, &d->gexec[q]) || capture(d, g, 1, q, &d->gexec1[q])) {
       drop_graph(d);
@@ -773,7 +829,7 @@ int run_phases(Group *g, bool init, long long iters) {
     int rc = ensure_graphs(g);
     if (rc) return rc;
     if (d->gexec[0] && d->gexec1[0]) {
-      const bool alt = fz(d);  // an even batch keeps the p parity, one iteration flips it
+      const bool alt = fz(d) || fz1(d);  // an even batch keeps the parity, one iteration flips it
       for (; iters >= d->graph_batch; iters -= d->graph_batch) {
         CGX_HIP(hipGraphLaunch(d->gexec[alt ? d->pbuf : 0], d->st));
         if (alt && (d->graph_batch & 1)) d->pbuf ^= 1;
@@ -950,6 +1006,7 @@ void destroy_one(cgx_dist *d) {
   if (d->ev_halo) (void)hipEventDestroy(d->ev_halo);
   if (d->ev_sums) (void)hipEventDestroy(d->ev_sums);
   if (d->ev_sums2) (void)hipEventDestroy(d->ev_sums2);
+  if (d->ev_red) (void)hipEventDestroy(d->ev_red);
   for (hipEvent_t e : d->spmv_ev) (void)hipEventDestroy(e);
   if (d->d_st) (void)hipFree(d->d_st);
   if (d->d_sums) (void)hipFree(d->d_sums);
@@ -1155,7 +1212,9 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   // fused: + r, p_old read and p_new written, x / p_{k-1} read and x
   // written every other launch (cgx_info)
   if (d->have_matrix && fz(d)) s->spmv_iter_bytes += 3.5 * d->n_loc * 8.0;
-  s->fused = fz(d) ? 1 : 0;
+  // fused CG1: + r, w, s, p, x read and p, s, r, w, x written (cgx_info)
+  if (d->have_matrix && fz1(d)) s->spmv_iter_bytes += 8.0 * d->n_loc * 8.0;
+  s->fused = fz(d) || fz1(d) ? 1 : 0;
   s->layout = d->have_matrix ? cgx::public_layout(d->A) : CGX_LAYOUT_AUTO;
   s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_DIA ? d->A.dia.ndiag : 0;
   s->graph = d->graph_state;

@@ -91,6 +91,50 @@ long long cgx_gen_laplacian3d(int nx, int ny, int nz, int row_begin,
   return k;
 }
 
+// The 7-point pattern of cgx_gen_laplacian3d with a random coefficient per
+// grid edge: a_ij = a_ji = -(0.5 + U(0,1]) from the unordered pair {i, j}
+// (symmetric by construction), diagonal = sum |a_ij| over the row + 0.01
+// (strictly diagonally dominant, so SPD).  Every off-diagonal value is its
+// own, so no layout can index the values (DIA-VI needs <= 15 per
+// diagonal): the general-coefficient CSR case at a BASELINE shape.
+long long cgx_gen_varcoef3d(int nx, int ny, int nz, unsigned long long seed, int row_begin,
+                            int row_end, int *row_ptr, int *col, double *val) {
+  const long long n = (long long)nx * ny * nz;
+  if (nx < 1 || ny < 1 || nz < 1 || bad_range(n, row_begin, row_end)) return CGX_EINVAL;
+  const int pl = nx * ny;
+  long long k = 0;
+  if (row_ptr) row_ptr[0] = 0;
+  for (int r = row_begin; r < row_end; ++r) {
+    const int i = r % nx, j = (r / nx) % ny, l = r / pl;
+    int c[7];
+    int m = 0;
+    if (l > 0) c[m++] = r - pl;
+    if (j > 0) c[m++] = r - nx;
+    if (i > 0) c[m++] = r - 1;
+    c[m++] = r;
+    if (i < nx - 1) c[m++] = r + 1;
+    if (j < ny - 1) c[m++] = r + nx;
+    if (l < nz - 1) c[m++] = r + pl;
+    if (row_ptr) {
+      double diag = 0.01;
+      double v[7];
+      for (int q = 0; q < m; ++q) {
+        if (c[q] == r) continue;
+        v[q] = pair_value(seed, r, c[q]) - 0.5;  // -U(0,1] - 0.5
+        diag += -v[q];
+      }
+      for (int q = 0; q < m; ++q) {
+        col[k + q] = c[q];
+        val[k + q] = c[q] == r ? diag : v[q];
+      }
+      row_ptr[r - row_begin + 1] = (int)(k + m);
+    }
+    k += m;
+  }
+  if (k > INT32_MAX) return CGX_EINVAL;
+  return k;
+}
+
 long long cgx_gen_random_spd(int n, int partners, unsigned long long seed,
                              int row_begin, int row_end, int *row_ptr,
                              int *col, double *val, float *val32) {

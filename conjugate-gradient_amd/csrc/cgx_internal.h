@@ -258,6 +258,21 @@ struct FuseArgs {
   int ghost;             // columns >= n are ghosts: p_new from pnew's ghost tail
 };
 
+// The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
+// launch does k_cg1_update's p / s / x / r recurrences (alpha, beta and the
+// stop flag from CgState) and w = A r_new, writing the gamma = r.r (pg) and
+// delta = w.r (SpmvArgs::part) partials of the iteration's single
+// reduction.  r, s, w are double-buffered (read _o, write _n; w_n = a.y).
+template <typename T>
+struct Cg1Args {
+  T *x, *p;
+  const T *r_o, *s_o, *w_o;
+  T *r_n, *s_n;
+  const CgState *st;
+  double *pg;
+  int ghost;  // columns >= n are ghosts: r_new from r_n's ghost tail
+};
+
 // Optional kernel timing events of a launch (hipExtLaunchKernel: stamped at
 // the kernel's own start and end).
 struct LaunchEv {
@@ -274,6 +289,14 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev 
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev = LaunchEv{});
+template <typename T>
+hipError_t launch_cg1_fused(const SpmvArgs<T> &a, const Cg1Args<T> &f, hipStream_t st,
+                            const LaunchEv &ev = LaunchEv{});
+// out[i] = r_new[idx[i]] = r - alpha (w + beta s) (the fused partitioned CG1
+// step's halo send rows)
+template <typename T>
+hipError_t launch_pack_rnext(int n_send, const int *idx, const T *r, const T *w, const T *s,
+                             T *out, const CgState *stt, hipStream_t st);
 // out[i] = p_new[idx[i]] = r + beta p_old (the fused partitioned step's halo
 // send rows; beta from *rr_new and st, r on the first iteration)
 template <typename T>

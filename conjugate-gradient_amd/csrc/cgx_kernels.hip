@@ -851,6 +851,193 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   epi_store<4>(dot, a.part);
 }
 
+// ---------------------------------------- fused CG1 step (DIA-VI)
+// The Chronopoulos-Gear iteration in ONE launch: k_cg1_update's vector
+// recurrences (p = r + beta p; s = w + beta s; x += alpha p; r -= alpha s)
+// and the SpMV w = A r of the new r, with both dot products of the single
+// all-reduce (gamma = r.r, delta = w.r) as per-workgroup partials.  alpha,
+// beta and the stop flag come from CgState (k_finalize FIN_CG1 of the last
+// launch's sums, all-reduced across ranks when partitioned).  r, s and w are
+// double-buffered (this launch reads r_o, s_o, w_o -- also at its halo
+// rows -- and writes r_n, s_n, w_n); p and x are read and written at the own
+// rows only.  r_new of the slice and its halo rows is computed ONCE per
+// workgroup into an LDS window (NF pair passes per thread): the near
+// diagonals read it there, the far ones compute r_new of their column from
+// r, w, s gathers (NFAR slots).  GH (a partition's boundary items): a
+// column >= n is a ghost whose r_new the halo exchange put in r_n's ghost
+// tail.  Every element is computed with k_cg1_update's roundings and summed
+// in the row's diagonal (= column) order, so x matches the unfused CG1 to
+// the grouping of the two dot products.  Bytes per row: 1-4 code + 24 (r,
+// s, w) + 16 (p, x) read, 40 written (p, s, r, w, x).
+template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH>
+__global__ __launch_bounds__(256) void k_cg1_dia_h(SpmvArgs<T> a, Cg1Args<T> f) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  T *win = reinterpret_cast<T *>(dyn_lds);
+  __shared__ T lv[kDiaMax * 16];
+  __shared__ double red[8];
+  typedef typename Pair<T>::type P;
+  const int t = threadIdx.x;
+  const int wi = xcd_block();
+  const int sl = LIST ? a.items.list[wi] : a.items.first + wi;
+  if (f.st->done) return;  // uniform (FIN_CG1 set it after the last x update)
+  const T alpha = (T)f.st->alpha, beta = (T)f.st->beta;
+  const int s0 = sl * kDiaSliceRows, r = s0 + 2 * t;
+  const int rs = r < a.n ? r : 0;
+  unsigned c0, c1;
+  ld_codes(a.dcode, a.cb, r, c0, c1);
+  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
+  constexpr int NS = NFAR > 0 ? NFAR : 1;
+  P fr[NS], fw[NS], fs[NS], fg[NS];
+  int fb[NS];
+#pragma unroll
+  for (int q = 0; q < NFAR; ++q) {
+    const int kq = a.fark[q];
+    int b = rs;
+    if (kq >= 0) {
+      const unsigned n0 = fld(a, c0, kq), n1 = fld(a, c1, kq);
+      if (n0 != a.cmask[kq] || n1 != a.cmask[kq]) b = r + a.doff[kq];
+    }
+    fb[q] = b;
+    fr[q] = ld_pair(f.r_o, b);
+    fw[q] = ld_pair(f.w_o, b);
+    fs[q] = ld_pair(f.s_o, b);
+    if (GH) fg[q] = ld_pair((const T *)f.r_n, b);
+  }
+  const int w0 = s0 - a.hl, wn = kDiaSliceRows + a.hl + a.hr;
+  P wr[NF], ww[NF], ws[NF], wg[NF];
+  int wj[NF];
+#pragma unroll
+  for (int q = 0; q < NF; ++q) {
+    const int j = min(max(w0 + 2 * t + q * 2 * 256, -1), a.ncols - 1);
+    wj[q] = j;
+    wr[q] = ld_pair(f.r_o, j);
+    ww[q] = ld_pair(f.w_o, j);
+    ws[q] = ld_pair(f.s_o, j);
+    if (GH) wg[q] = ld_pair((const T *)f.r_n, j);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every load above is in flight before the first use
+  // r_new of a pair: r - alpha (w + beta s), k_cg1_update's roundings; or the
+  // received ghost value
+  auto rnext = [&](P rv, P wv, P sv, P gv, int j) {
+    P o;
+    const T b0 = beta * sv.x, b1 = beta * sv.y;
+    const T s0v = wv.x + b0, s1v = wv.y + b1;
+    const T a0 = alpha * s0v, a1 = alpha * s1v;
+    o.x = rv.x - a0;
+    o.y = rv.y - a1;
+    if (GH) {
+      if (j >= a.n) o.x = gv.x;
+      if (j + 1 >= a.n) o.y = gv.y;
+    }
+    return o;
+  };
+#pragma unroll
+  for (int q = 0; q < NF; ++q) {
+    const int i = 2 * t + q * 2 * 256;
+    const P rn = rnext(wr[q], ww[q], ws[q], wg[q], wj[q]);
+    if (i < wn) win[i] = rn.x;
+    if (i + 1 < wn) win[i + 1] = rn.y;
+  }
+  P rk[NS];
+#pragma unroll
+  for (int q = 0; q < NFAR; ++q) rk[q] = rnext(fr[q], fw[q], fs[q], fg[q], fb[q]);
+  if (t < a.ndiag * 16) lv[t] = tv;
+  __syncthreads();
+  // own rows' operands (after the window's load registers are dead)
+  P ro = P(), so = P(), wo = P(), po = P(), xo = P();
+  if (r < a.n) {
+    ro = ld_pair(f.r_o, r);
+    so = ld_pair(f.s_o, r);
+    wo = ld_pair(f.w_o, r);
+    po = ld_pair((const T *)f.p, r);
+    xo = ld_pair((const T *)f.x, r);
+  }
+  const int rw = r - w0;
+  T a0 = T(0), a1 = T(0);
+#pragma unroll
+  for (int kk = 0; kk < kDiaMax; ++kk) {
+    if (kk < a.ndiag) {
+      T v0, v1;
+      if ((a.near >> kk) & 1u) {
+        const int i = rw + a.doff[kk];
+        v0 = win[i];
+        v1 = win[i + 1];
+      } else {
+        const int slot = __builtin_popcount(~a.near & ((1u << kk) - 1u));
+        P v = rk[0];
+#pragma unroll
+        for (int q = 1; q < NFAR; ++q) v = slot == q ? rk[q] : v;
+        v0 = v.x;
+        v1 = v.y;
+      }
+      const unsigned n0 = fld(a, c0, kk), n1 = fld(a, c1, kk);
+      const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
+      a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
+      a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
+    }
+  }
+  double gam = 0.0, del = 0.0;
+  if (r < a.n) {
+    const T rn0 = win[rw], rn1 = win[rw + 1];
+    // k_cg1_update's order: p, s, x, r (r_new == the window's value)
+    const T bp0 = beta * po.x, bp1 = beta * po.y;
+    const T pn0 = ro.x + bp0, pn1 = ro.y + bp1;
+    const T bs0 = beta * so.x, bs1 = beta * so.y;
+    const T sn0 = wo.x + bs0, sn1 = wo.y + bs1;
+    const T ap0 = alpha * pn0, ap1 = alpha * pn1;
+    st_pair(f.p, r, a.n, pn0, pn1, false);
+    st_pair(f.s_n, r, a.n, sn0, sn1, false);
+    st_pair(f.x, r, a.n, xo.x + ap0, xo.y + ap1, false);
+    st_pair(f.r_n, r, a.n, rn0, rn1, false);
+    st_pair(a.y, r, a.n, a0, a1, NT);
+    gam = (double)rn0 * (double)rn0;
+    del = (double)rn0 * (double)a0;
+    if (r + 1 < a.n) {
+      gam = gam + (double)rn1 * (double)rn1;
+      del = del + (double)rn1 * (double)a1;
+    }
+  }
+  // the two partials, each reduced like epi_store<4>
+  gam = wave_sum(gam);
+  del = wave_sum(del);
+  const int lane = t & (kWave - 1), wid = t / kWave;
+  if (lane == 0) {
+    red[wid] = gam;
+    red[4 + wid] = del;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double g = red[0], d = red[4];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      g = g + red[q];
+      d = d + red[4 + q];
+    }
+    f.pg[blockIdx.x] = g;
+    a.part[blockIdx.x] = d;
+  }
+}
+
+// The send rows of r_new for the fused partitioned CG1 step: r_new = r -
+// alpha (w + beta s) at the rows the neighbours gather (the same roundings
+// as k_cg1_dia_h's window).
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_rnext(int n_send, const int *__restrict__ idx,
+                                                    const T *__restrict__ r,
+                                                    const T *__restrict__ w,
+                                                    const T *__restrict__ s,
+                                                    T *__restrict__ out, const CgState *st) {
+  if (st->done) return;
+  const T alpha = (T)st->alpha, beta = (T)st->beta;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n_send; i += gridDim.x * 256) {
+    const int j = idx[i];
+    const T bs = beta * s[j];
+    const T sn = w[j] + bs;
+    const T as = alpha * sn;
+    out[i] = r[j] - as;
+  }
+}
+
 // The send rows of p_new for the fused partitioned step: p_new = r + beta
 // p_old at the rows the neighbours gather (the unfused path packs p after
 // k_xpay_xf; the fused step computes p inside the SpMV launch, after the
@@ -1851,6 +2038,63 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
   return hipGetLastError();
 }
 
+template <typename T, int NF, int NFAR, bool GH>
+static const void *cg1_kernel_g(bool nt, bool list) {
+  return nt ? (list ? CGX_K(k_cg1_dia_h<T, NF, NFAR, true, true, GH>)
+                    : CGX_K(k_cg1_dia_h<T, NF, NFAR, true, false, GH>))
+            : (list ? CGX_K(k_cg1_dia_h<T, NF, NFAR, false, true, GH>)
+                    : CGX_K(k_cg1_dia_h<T, NF, NFAR, false, false, GH>));
+}
+
+template <typename T, int NF, int NFAR>
+static const void *cg1_kernel(bool nt, bool list, bool gh) {
+  return gh ? cg1_kernel_g<T, NF, NFAR, true>(nt, list) : cg1_kernel_g<T, NF, NFAR, false>(nt, list);
+}
+
+template <typename T>
+hipError_t launch_cg1_fused(const SpmvArgs<T> &a, const Cg1Args<T> &f, hipStream_t st,
+                            const LaunchEv &ev) {
+  const int g = spmv_grid(a);
+  if (g <= 0) return hipSuccess;
+  if (a.layout != L_DIA || a.cb > 4 || !a.part || !f.pg) return hipErrorInvalidValue;
+  const int wn = kDiaSliceRows + a.hl + a.hr;
+  const int nf = (wn + 511) / 512;
+  int nfar = 0;
+  for (int q = 0; q < 4; ++q) nfar += a.fark[q] >= 0;
+  if (nf > 5) return hipErrorInvalidValue;
+  const bool nt = a.nt != 0, l = a.items.list != nullptr, gh = f.ghost != 0;
+  const void *k = nullptr;
+  switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + (nfar == 0 ? 0 : nfar <= 2 ? 2 : 4)) {
+    case 20: k = cg1_kernel<T, 2, 0>(nt, l, gh); break;
+    case 22: k = cg1_kernel<T, 2, 2>(nt, l, gh); break;
+    case 24: k = cg1_kernel<T, 2, 4>(nt, l, gh); break;
+    case 30: k = cg1_kernel<T, 3, 0>(nt, l, gh); break;
+    case 32: k = cg1_kernel<T, 3, 2>(nt, l, gh); break;
+    case 34: k = cg1_kernel<T, 3, 4>(nt, l, gh); break;
+    case 50: k = cg1_kernel<T, 5, 0>(nt, l, gh); break;
+    case 52: k = cg1_kernel<T, 5, 2>(nt, l, gh); break;
+    case 54: k = cg1_kernel<T, 5, 4>(nt, l, gh); break;
+    default: return hipErrorInvalidValue;
+  }
+  void *args[] = {(void *)&a, (void *)&f};
+  const size_t lds = (size_t)wn * sizeof(T) + 16;
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256), args, lds, st, ev.start, ev.stop, 0);
+  else
+    (void)hipLaunchKernel(k, dim3(g), dim3(256), args, lds, st);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_pack_rnext(int n_send, const int *idx, const T *r, const T *w, const T *s,
+                             T *out, const CgState *stt, hipStream_t st) {
+  if (n_send <= 0) return hipSuccess;
+  const int grid = std::min((n_send + 255) / 256, 1024);
+  hipLaunchKernelGGL((k_pack_rnext<T>), dim3(grid), dim3(256), 0, st, n_send, idx, r, w, s, out,
+                     stt);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_init_hs(int n, const T *b, T *x, T *r, T *p, double *part, int grid,
                           hipStream_t st) {
@@ -2011,6 +2255,10 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template hipError_t launch_xpay<T>(int, T *, const T *, const CgState *, int, hipStream_t);    \
   template hipError_t launch_pack_pnext<T>(int, const int *, const T *, const T *, T *,          \
                                            const CgState *, const double *, hipStream_t);        \
+  template hipError_t launch_cg1_fused<T>(const SpmvArgs<T> &, const Cg1Args<T> &, hipStream_t,  \
+                                          const LaunchEv &);                                     \
+  template hipError_t launch_pack_rnext<T>(int, const int *, const T *, const T *, const T *,    \
+                                           T *, const CgState *, hipStream_t);                   \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
                                           double *, int, hipStream_t, const FinArgs *);          \
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \

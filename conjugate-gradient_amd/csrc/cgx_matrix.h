@@ -51,7 +51,7 @@ struct DevMatrix {
   DiaCand dia{};
   int kdiag = -1;               // main diagonal's index, -1: none
   int gath = 8;                 // CSR / DC: gathers per row chunk
-  // L2-tiled order of the work items (DC / VI, wide stencils; nullptr: natural)
+  // L2-tiled order of the work items (DC / DIA, wide stencils; nullptr: natural)
   int *d_order = nullptr;
   std::vector<int> order;    // host copy of the tiled order (empty: natural)
   int tile_bands = 0;
@@ -62,7 +62,7 @@ struct DevMatrix {
   int encode_fallback = 0;   // 1: a sampled candidate set missed, exact host scan used
 
   // Host CSR -> device.  want: CGX_LAYOUT_* request (a layout that does not
-  // apply falls back along VI -> DC -> CSR).  ncols: columns of x (>= n for
+  // apply falls back along DIA -> DC -> CSR).  ncols: columns of x (>= n for
   // the partitioned solver's ghost tail).  gen: col/val generated on the
   // device (rp is the host closed form).  allow_panels: single-GPU only.
   template <typename T>

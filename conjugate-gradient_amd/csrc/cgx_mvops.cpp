@@ -11,10 +11,11 @@
 // Matrix residency: the reference's conj_grad calls mv_mult once per
 // iteration on the same A (cg.c:111 -> mv_ops.c:160-201).  The default
 // context keeps the last matrix on the device, keyed by the struct's
-// pointers and sizes plus a 64-bit hash of row_ptr, col_indices and values
-// (one threaded pass over host memory, a fraction of a PCIe upload), so a
-// caller linked at the op level uploads A once, not once per iteration --
-// and a caller that edits A in place between calls still gets its new A.
+// pointers and sizes and checked against a 64-bit content hash of row_ptr,
+// col_indices and values computed on host threads WHILE the device works
+// (with_matrix), so a caller linked at the op level uploads A once, not once
+// per iteration, pays ~nothing for the check -- and a caller that edits A in
+// place between calls still gets its new A (the call is redone).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -74,8 +75,31 @@ int default_solver(cgx_solver **out) {
   return 0;
 }
 
-// 64-bit hash of a byte range: 4 independent multiply-xor lanes per thread
-// over 8-byte words, chunks on host threads, chunk hashes combined in order.
+// 64-bit content hash of a byte range (xxHash64's construction, written
+// here): each 8-byte word goes through a multiply-rotate-multiply round of
+// one of 4 lanes, so a bit flip in any word diffuses over the lane and two
+// flips cannot cancel the way they did in the round-2 multiply-xor lanes
+// (negating a symmetric pair a_ij / a_ji left the hash
+// unchanged).  Chunks on host threads (the count depends on the size only),
+// chunk hashes folded in order, final avalanche.
+constexpr unsigned long long kP1 = 0x9E3779B185EBCA87ULL, kP2 = 0xC2B2AE3D27D4EB4FULL,
+                             kP3 = 0x165667B19E3779F9ULL, kP4 = 0x85EBCA77C2B2AE63ULL,
+                             kP5 = 0x27D4EB2F165667C5ULL;
+inline unsigned long long rotl64(unsigned long long x, int r) { return (x << r) | (x >> (64 - r)); }
+inline unsigned long long hround(unsigned long long acc, unsigned long long w) {
+  return rotl64(acc + w * kP2, 31) * kP1;
+}
+inline unsigned long long hmerge(unsigned long long h, unsigned long long v) {
+  return (h ^ hround(0, v)) * kP1 + kP4;
+}
+inline unsigned long long avalanche(unsigned long long h) {
+  h ^= h >> 33;
+  h *= kP2;
+  h ^= h >> 29;
+  h *= kP3;
+  return h ^ (h >> 32);
+}
+
 unsigned long long hash_bytes(const void *p, size_t bytes) {
   const unsigned char *b = (const unsigned char *)p;
   const size_t words = bytes / 8;
@@ -83,54 +107,46 @@ unsigned long long hash_bytes(const void *p, size_t bytes) {
   std::vector<unsigned long long> part((size_t)nt);
   auto work = [&](int t) {
     const size_t lo = words * t / nt, hi = words * (t + 1) / nt;
-    unsigned long long h[4] = {0x9e3779b97f4a7c15ULL, 0xbf58476d1ce4e5b9ULL,
-                               0x94d049bb133111ebULL, 0x2545f4914f6cdd1dULL};
+    unsigned long long v[4] = {kP1 + kP2, kP2, 0, 0ULL - kP1};
     size_t i = lo;
     for (; i + 4 <= hi; i += 4)
       for (int l = 0; l < 4; ++l) {
         unsigned long long w;
         memcpy(&w, b + 8 * (i + l), 8);
-        h[l] = (h[l] ^ w) * 0x100000001b3ULL;
+        v[l] = hround(v[l], w);
       }
+    unsigned long long h = rotl64(v[0], 1) + rotl64(v[1], 7) + rotl64(v[2], 12) + rotl64(v[3], 18);
+    for (int l = 0; l < 4; ++l) h = hmerge(h, v[l]);
+    h += (unsigned long long)(hi - lo) * 8;
     for (; i < hi; ++i) {
       unsigned long long w;
       memcpy(&w, b + 8 * i, 8);
-      h[0] = (h[0] ^ w) * 0x100000001b3ULL;
+      h = rotl64(h ^ hround(0, w), 27) * kP1 + kP4;
     }
-    part[(size_t)t] = h[0] ^ (h[1] * 3) ^ (h[2] * 5) ^ (h[3] * 7);
+    part[(size_t)t] = avalanche(h);
   };
   std::vector<std::thread> th;
   for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
   work(0);
   for (auto &x : th) x.join();
-  unsigned long long h = 0xcbf29ce484222325ULL ^ bytes;
-  for (unsigned long long x : part) h = (h ^ x) * 0x100000001b3ULL;
-  for (size_t i = words * 8; i < bytes; ++i) h = (h ^ b[i]) * 0x100000001b3ULL;
-  return h;
+  unsigned long long h = kP5 + bytes;
+  for (unsigned long long x : part) h = hmerge(h, x);
+  for (size_t i = words * 8; i < bytes; ++i) h = rotl64(h ^ (b[i] * kP5), 11) * kP1;
+  return avalanche(h);
 }
 
 unsigned long long matrix_hash(const struct __mv_sparse *A) {
   const int n = A->size, nnz = A->row_ptr[n];
   unsigned long long h = hash_bytes(A->row_ptr, ((size_t)n + 1) * 4);
   if (nnz > 0) {
-    h = h * 31 + hash_bytes(A->col_indices, (size_t)nnz * 4);
-    h = h * 31 + hash_bytes(A->values, (size_t)nnz * 8);
+    h = hmerge(h, hash_bytes(A->col_indices, (size_t)nnz * 4));
+    h = hmerge(h, hash_bytes(A->values, (size_t)nnz * 8));
   }
-  return h;
+  return avalanche(h);
 }
 
-// Makes A the default solver's matrix: a reuse when the struct's arrays,
-// sizes and contents are those already on the device, else one upload.
-int ensure_matrix(cgx_solver *s, const struct __mv_sparse *A, double *hash_ms = nullptr) {
+int upload_matrix(cgx_solver *s, const struct __mv_sparse *A, unsigned long long h) {
   const int n = A->size, nnz = A->row_ptr[n];
-  const double th = now_ms();
-  const unsigned long long h = matrix_hash(A);
-  if (hash_ms) *hash_ms = now_ms() - th;
-  if (g_res.valid && g_res.rp == A->row_ptr && g_res.col == A->col_indices &&
-      g_res.val == A->values && g_res.size == n && g_res.nnz == nnz && g_res.hash == h) {
-    ++g_reuses;
-    return 0;
-  }
   g_res.valid = false;
   int rc = cgx_solver_set_matrix(s, n, nnz, A->row_ptr, A->col_indices, A->values);
   if (rc) return rc;
@@ -143,6 +159,65 @@ int ensure_matrix(cgx_solver *s, const struct __mv_sparse *A, double *hash_ms = 
   g_res.hash = h;
   g_res.valid = true;
   return 0;
+}
+
+// Runs op() (device work on the default solver's matrix) with A as that
+// matrix.  When the struct's arrays and sizes are those of the resident
+// matrix, op() starts at once on it while the content hash of A runs on
+// host threads beside it (the check costs the caller only what it does not
+// overlap: ~0 for a C3 solve, whose hash takes ~5-8 ms); a hash that differs
+// (A edited in place since the upload) re-uploads A and runs op() again, so
+// the result is always that of the A passed in.  Otherwise A is hashed and
+// uploaded first.
+struct MatTiming {
+  double hash_ms = 0, upload_ms = 0, op_ms = 0;  // hash: time spent waiting for it
+  bool uploaded = false;
+};
+
+template <typename F>
+int with_matrix(cgx_solver *s, const struct __mv_sparse *A, F &&op, MatTiming *tm = nullptr) {
+  MatTiming t;
+  const int n = A->size, nnz = A->row_ptr[n];
+  const bool same_key = g_res.valid && g_res.rp == A->row_ptr && g_res.col == A->col_indices &&
+                        g_res.val == A->values && g_res.size == n && g_res.nnz == nnz;
+  auto upload = [&](unsigned long long h) {
+    const double t0 = now_ms();
+    const int rc = upload_matrix(s, A, h);
+    t.upload_ms += now_ms() - t0;
+    t.uploaded = true;
+    return rc;
+  };
+  auto run = [&] {
+    const double t0 = now_ms();
+    const int rc = op();
+    t.op_ms = now_ms() - t0;
+    return rc;
+  };
+  int rc = 0;
+  if (!same_key) {
+    const double th = now_ms();
+    const unsigned long long h = matrix_hash(A);
+    t.hash_ms = now_ms() - th;
+    rc = upload(h);
+    if (rc == 0) rc = run();
+  } else {
+    unsigned long long h = 0;
+    std::thread th([&] { h = matrix_hash(A); });
+    rc = run();
+    const double tw = now_ms();
+    th.join();
+    t.hash_ms = now_ms() - tw;
+    if (rc == 0) {
+      if (h == g_res.hash) {
+        ++g_reuses;
+      } else {  // A changed in place: the result came from the stale device copy
+        rc = upload(h);
+        if (rc == 0) rc = run();
+      }
+    }
+  }
+  if (tm) *tm = t;
+  return rc;
 }
 
 int ops_ready(size_t n) {
@@ -254,16 +329,19 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct _
   if (rc) return rc;
   if ((rc = cgx_solver_set_mode(s, g_mode, g_mode == CGX_MODE_EXACT ? CGX_ALG_HS : g_alg)))
     return rc;
-  const long long up0 = g_uploads;
-  if ((rc = ensure_matrix(s, A, &t.hash_ms))) return rc;
-  const double t1 = now_ms();
-  t.uploaded = g_uploads > up0;
-  t.setup_ms = t1 - t0;
-  if ((rc = cgx_solver_set_rhs(s, b->values))) return rc;
   int iters = maxit + 1;
-  if (A->size > 0 && (rc = cgx_solver_run(s, maxit, tol, &iters))) return rc;
+  MatTiming mt;
+  rc = with_matrix(s, A, [&] {
+    int r = cgx_solver_set_rhs(s, b->values);
+    if (r == 0 && A->size > 0) r = cgx_solver_run(s, maxit, tol, &iters);
+    return r;
+  }, &mt);
+  if (rc) return rc;
+  t.uploaded = mt.uploaded;
+  t.hash_ms = mt.hash_ms;
+  t.setup_ms = mt.hash_ms + mt.upload_ms;
+  t.solve_ms = mt.op_ms;
   const double t2 = now_ms();
-  t.solve_ms = t2 - t1;
   struct __mv_sparse *xv = new_mv_struct_with_size(b->size);  // cg.c:104
   if (!xv) return CGX_ENOMEM;
   if (A->size > 0 && (rc = cgx_solver_get_x(s, xv->values))) {
@@ -417,8 +495,8 @@ int mv_mult(struct __mv_sparse *A, struct __mv_sparse *b, struct __mv_sparse **r
   if (n > 0) {
     cgx_solver *s = nullptr;
     rc = default_solver(&s);
-    if (rc == 0) rc = ensure_matrix(s, A);  // resident across calls (see top)
-    if (rc == 0) rc = cgx_solver_spmv(s, b->values, tmp);
+    if (rc == 0)  // A resident across calls (with_matrix)
+      rc = with_matrix(s, A, [&] { return cgx_solver_spmv(s, b->values, tmp); });
   }
   if (rc == 0) rc = prepare_out(r, n, b->nnz, true);
   if (rc == 0 && n > 0) memcpy((*r)->values, tmp, (size_t)n * 8);

@@ -124,7 +124,9 @@ struct cgx_solver {
   void *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
        *d_w = nullptr;
   void *d_p2 = nullptr;  // fused step: the second p buffer (p_old / p_new alternate)
-  int pbuf = 0;          // fused step: which buffer holds p_old (0: d_p)
+  // fused CG1 step: the second r, s, w buffers (read one set, write the other)
+  void *d_r2 = nullptr, *d_s2 = nullptr, *d_w2 = nullptr;
+  int pbuf = 0;          // fused step: which buffer holds p_old (0: d_p) / r, s, w_old
   int fuse = CGX_FUSE_AUTO;  // cgx_solver_set_fused
   unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
@@ -156,19 +158,21 @@ void drop_graph(cgx_solver *s) {
   s->gexec_key = -1;
 }
 
-// The fused HS step applies: fast mode, HS, a fusable DIA layout and, in
-// auto mode, a working set beyond the Infinity Cache (cache-resident
-// systems are launch- and latency-bound: the heavier fused workgroup loses,
-// C2 29.1 vs 26.8 us per iteration).
+// The fused step (HS: k_spmv_dia_h + k_update_rf; CG1: k_cg1_dia_h +
+// k_finalize) applies: fast mode, a fusable DIA layout and, in auto mode, a
+// working set beyond the Infinity Cache (cache-resident systems are launch-
+// and latency-bound: the heavier fused workgroup loses, C2 29.1 vs 26.8 us
+// per HS iteration).
 bool fused(const cgx_solver *s) {
-  return s->fuse != CGX_FUSE_OFF && s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST &&
-         s->A.fusable() && (s->fuse == CGX_FUSE_ON || s->A.nt);
+  return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
+         (s->fuse == CGX_FUSE_ON || s->A.nt);
 }
 
-// p double-buffered, its buffers alternating per iteration: the fused step,
-// and the unfused folded HS step (k_xpay_xf's every-other-iteration x).
+// Buffers alternating per iteration: p for the fused HS step and the
+// unfused folded HS step (k_xpay_xf's every-other-iteration x); r, s, w for
+// the fused CG1 step.
 bool alternating(const cgx_solver *s) {
-  return s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST;
+  return (s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST) || fused(s);
 }
 
 void free_system(cgx_solver *s) {
@@ -181,6 +185,9 @@ void free_system(cgx_solver *s) {
   dev_free(&s->d_s);
   dev_free(&s->d_w);
   dev_free(&s->d_p2);
+  dev_free(&s->d_r2);
+  dev_free(&s->d_s2);
+  dev_free(&s->d_w2);
   dev_free(&s->d_pa);
   dev_free(&s->d_pb);
   dev_free(&s->d_hist);
@@ -201,6 +208,9 @@ int alloc_vectors(cgx_solver *s) {
       (rc = dev_alloc(&s->d_r, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_p, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_s, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_w, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_p2, nv, &s->vec_bytes)) ||
+      (rc = dev_alloc(&s->d_r2, nv, &s->vec_bytes)) ||
+      (rc = dev_alloc(&s->d_s2, nv, &s->vec_bytes)) ||
+      (rc = dev_alloc(&s->d_w2, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pa, (size_t)s->part_cap * 8, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pb, (size_t)s->part_cap * 8, &s->vec_bytes))) {
     free_system(s);
@@ -276,6 +286,21 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = s->A.n;
   T *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p, *sv = (T *)s->d_s, *w = (T *)s->d_w;
   int np = 0;
+  if (fused(s) && s->alg == CGX_ALG_CG1) {
+    // k_cg1_dia_h: p, s, x, r recurrences + w = A r_new with the gamma /
+    // delta partials; k_finalize: the single reduction's scalar step
+    const int q = s->pbuf;
+    T *ro = (T *)(q ? s->d_r2 : s->d_r), *rn = (T *)(q ? s->d_r : s->d_r2);
+    T *so = (T *)(q ? s->d_s2 : s->d_s), *sn = (T *)(q ? s->d_s : s->d_s2);
+    T *wo = (T *)(q ? s->d_w2 : s->d_w), *wn = (T *)(q ? s->d_w : s->d_w2);
+    const SpmvArgs<T> a = s->A.args<T>(nullptr, wn, s->d_pb, &s->d_st->done, s->A.all_items());
+    const Cg1Args<T> f{x, p, ro, so, wo, rn, sn, s->d_st, s->d_pa, 0};
+    np = s->A.partials(s->A.all_items());
+    CGX_HIP(launch_cg1_fused<T>(a, f, st, LaunchEv{ev0, ev1}));
+    CGX_HIP(launch_finalize(FIN_CG1, s->d_pa, np, s->d_pb, np, s->d_st, s->d_hist, nullptr, st));
+    s->pbuf ^= 1;
+    return 0;
+  }
   if (fused(s)) {
     // k_spmv_dia_h: the previous x / p update + s = A p_new (+ p_new.s
     // partials); k_update_rf: alpha, r -= alpha s, r.r partials and their
@@ -446,7 +471,7 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
   if ((rc = enqueue_init<T>(s))) return rc;
   // the fused step does an iteration's x update in the next launch: one
   // more step carries the last one (and finds the stop)
-  const long long total = (long long)maxit + 1 + (fused(s) ? 1 : 0);
+  const long long total = (long long)maxit + 1 + (fused(s) && s->alg == CGX_ALG_HS ? 1 : 0);
   if (tol <= 0.0) {
     if ((rc = enqueue_iters<T>(s, total))) return rc;
     if ((rc = read_state(s))) return rc;
@@ -817,7 +842,10 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   // the fused step also reads r, p_old and writes p_new (the SpMV's own p
   // read becomes the r / p_old reads: +2 vectors); every other launch reads
   // x and p_{k-1}, writes x (+3 / 2): the average launch, +3.5 n vectors
-  if (s->have_matrix && fused(s)) info->spmv_iter_bytes += 3.5 * A.n * sv;
+  if (s->have_matrix && fused(s))
+    // CG1: r, w, s, p, x read and p, s, r, w, x written, the SpMV's own x
+    // read / y write included: + 8 n vectors
+    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : 3.5) * A.n * sv;
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;

@@ -48,7 +48,8 @@ int solve(const struct __mv_sparse *A, const struct __mv_sparse *b,
 void cgx_free_mv_deep(struct __mv_sparse *m);
 
 /* Numerics of the reference-compatible entry points (conj_grad, solve and
- * the mv_ops.h arithmetic), process-wide; the library reads no environment.
+ * the mv_ops.h arithmetic), process-wide; the library is configured only
+ * through these calls.
  *   mode CGX_MODE_FAST (default): two-stage parallel reductions, x within
  *        fp64 rounding of the reference (tests: 1e-12 relative)
  *   mode CGX_MODE_EXACT: the reference's sequential dot-product order, x
@@ -60,9 +61,10 @@ int cgx_ops_set_mode(int mode, int alg);
 int cgx_ops_set_device(int device);
 
 /* Wall-clock split of the last conj_grad / solve call (what cg.c:71-75
- * times around conj_grad): setup = content hash of A + upload and layout
- * encoding when A is not resident (uploaded = 1), solve = device iterations
- * incl. the rhs copy, download = x back to the host. */
+ * times around conj_grad): setup = upload and layout encoding when A was
+ * not resident (uploaded = 1) + hash_ms, the time spent waiting for the
+ * content hash of A (it overlaps the device work when A is resident);
+ * solve = device iterations incl. the rhs copy; download = x to the host. */
 typedef struct {
   double total_ms, setup_ms, hash_ms, solve_ms, download_ms;
   int uploaded, iters;
@@ -70,10 +72,14 @@ typedef struct {
 int cgx_ops_last_timing(cgx_ops_timing *t);
 
 /* Matrix residency of the mv_ops.h / conj_grad / solve entry points: the
- * last matrix stays on the device, keyed by the struct's array pointers,
- * sizes and a 64-bit hash of row_ptr, col_indices and values.  A call with
- * the same (unmodified) matrix reuses it -- a cg.c caller linked at the op
- * level (cg.c:111 -> mv_mult) uploads A once, not once per iteration.
+ * last matrix stays on the device, keyed by the struct's array pointers and
+ * sizes, and checked against a 64-bit content hash of row_ptr, col_indices
+ * and values.  A call with the same struct starts on the resident matrix at
+ * once while the hash runs on host threads beside the device work; if A was
+ * edited in place since its upload the hash differs, A is uploaded again
+ * and the call redone -- the result is always that of the A passed in.  A
+ * cg.c caller linked at the op level (cg.c:111 -> mv_mult) thus uploads A
+ * once, not once per iteration.
  * Counts since process start: uploads performed, reuses. */
 int cgx_ops_counters(long long *uploads, long long *reuses);
 
@@ -102,7 +108,9 @@ enum { CGX_ALG_HS = 0,       /* Hestenes-Stiefel, the reference recurrence    */
 enum { CGX_F64 = 0, CGX_F32 = 1 };
 
 /* Device layout of the matrix the SpMV streams (the C ABI always takes the
- * reference's CSR; the CSR arrays stay resident whatever the layout):
+ * reference's CSR; only the chosen layout's arrays are resident -- DIA keeps
+ * just its per-row codes and value tables, and cgx_solver_get_matrix decodes
+ * them back to CSR):
  *   AUTO     DIA where it applies, else DC, else CSR (PANEL for gathers with
  *            no locality, e.g. random SPD)                       (default)
  *   CSR      plain CSR, int32 columns: SURVEY.md 8d's B_spmv layout
@@ -251,6 +259,13 @@ long long cgx_gen_laplacian3d(int nx, int ny, int nz, int row_begin,
 long long cgx_gen_random_spd(int n, int partners, unsigned long long seed,
                              int row_begin, int row_end, int *row_ptr,
                              int *col, double *val, float *val32);
+/* The 7-point pattern of cgx_gen_laplacian3d with one random coefficient per
+ * grid edge, a_ij = a_ji = -(0.5 + U(0,1]) from a splitmix64 hash of the
+ * pair (seed), diagonal = sum |a_ij| + 0.01: SPD, every off-diagonal value
+ * distinct -- the general-coefficient CSR case at a stencil's shape. */
+long long cgx_gen_varcoef3d(int nx, int ny, int nz, unsigned long long seed,
+                            int row_begin, int row_end, int *row_ptr, int *col,
+                            double *val);
 /* Reader for the reference's 4-line input format (replaces read_input_file,
  * cg.c:23,146-218): col_indices / row_ptr / values / b, comma separated.
  * Fills *A (CSR) and *b (vector) with freshly allocated host arrays.
@@ -336,7 +351,7 @@ int  cgx_dist_create(int device, int nranks, int rank,
  * Run/bench through parts[0]; destroy through parts[0]. */
 int  cgx_dist_create_local(int device, int nparts, cgx_dist **parts);
 void cgx_dist_destroy(cgx_dist *d);
-/* Layout of the local rows for the next set_matrix (AUTO, CSR, DC, VI). */
+/* Layout of the local rows for the next set_matrix (AUTO, CSR, DC, DIA). */
 int  cgx_dist_set_layout(cgx_dist *d, int layout);
 int  cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
                          const int *row_ptr, const int *col_global,

@@ -29,9 +29,9 @@
  * matrices: ascending columns, no empty row, first_col(r+1) <= last_col(r)).
  * mat_get_row expands a row correctly from [row_ptr[r], row_ptr[r+1]); the
  * reference's greedy scan past row_ptr[r+1] is not reproduced.
- * dot_product in libcgx is a parallel two-stage reduction unless
- * CGX_MODE=exact is set in the environment, in which case it is the
- * reference's sequential sum.
+ * dot_product in libcgx is a parallel two-stage reduction by default; after
+ * cgx_ops_set_mode(CGX_MODE_EXACT, CGX_ALG_HS) (cgx.h) it is the reference's
+ * sequential sum.  The library reads no configuration from outside the API.
  */
 #ifndef CGX_MV_OPS_H
 #define CGX_MV_OPS_H

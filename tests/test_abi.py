@@ -250,3 +250,34 @@ def test_null_handles_fail_cleanly():
     L.cgx_part_destroy(null)
     L.cgx_free_mv_deep(null)
     assert d.value == 0.0 and vp is not None
+
+
+def test_headers_match_the_library():
+    """The public headers are the drop-in contract: no
+    configuration by environment variable (the library reads none) and no
+    layout name the library does not have ("VI" was renamed DIA)."""
+    for h in (REPO / "include").glob("*.h"):
+        text = h.read_text()
+        assert "environment" not in text.lower(), h.name
+        assert not re.search(r"(?<!DIA-)\bVI\b", text), h.name
+
+
+def test_gen_varcoef3d_properties():
+    """cgx_gen_varcoef3d: the 7-point Laplacian's pattern, symmetric values,
+    strictly diagonally dominant (SPD), all off-diagonal values distinct,
+    row ranges concatenate to the whole."""
+    nx, ny, nz = 7, 6, 5
+    rp, col, val = cgx.varcoef3d(nx, ny, nz, seed=3)
+    rpl, coll, _ = cgx.laplacian3d(nx, ny, nz)
+    assert np.array_equal(rp, rpl) and np.array_equal(col, coll)
+    n = nx * ny * nz
+    A = np.zeros((n, n))
+    for i in range(n):
+        A[i, col[rp[i]:rp[i + 1]]] = val[rp[i]:rp[i + 1]]
+    assert np.array_equal(A, A.T)
+    off = np.abs(A).sum(axis=1) - np.abs(np.diag(A))
+    assert np.all(np.diag(A) > off)
+    offv = A[np.triu(np.ones((n, n), bool), 1) & (A != 0)]
+    assert np.all((offv < -0.5) & (offv >= -1.5)) and len(np.unique(offv)) == len(offv)
+    parts = [cgx.varcoef3d(nx, ny, nz, 3, n * g // 3, n * (g + 1) // 3) for g in range(3)]
+    assert np.array_equal(np.concatenate([p[2] for p in parts]), val)

@@ -376,6 +376,75 @@ def test_fused_rccl_one_rank_graph_parity():
             assert H.same_bits_or_both_nan(h0, h1), key
 
 
+@pytest.mark.parametrize("shape,P", [((24, 20, 30), 1), ((24, 20, 30), 3), ((24, 20, 30), 8),
+                                     ((40, 30, 16), 2), ((40, 30, 24), 8)])
+def test_fused_cg1_partitions(shape, P):
+    """The fused CG1 step across partitions (halo of r_new = r - alpha (w +
+    beta s) packed at the send rows, k_cg1_dia_h over interior then
+    boundary items, ghost diagonals reading the received r_new, ONE
+    all-reduce of (gamma, delta) per iteration): within 1e-9 of the oracle's
+    CG1 solve, stop iteration within 1, and within 1e-12 of the unfused
+    partitioned CG1 at fixed max_iter."""
+    rp, col, val = cgx.laplacian3d(*shape)
+    b = np.random.default_rng(13).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    res = {}
+    for fused in (True, False):
+        parts = cgx.DistSolver.local_group(0, P)
+        try:
+            parts[0].set_alg(cgx.CGX_ALG_CG1)
+            parts[0].set_fused(fused)
+            for g, d in enumerate(parts):
+                rb, re_ = cgx.partition_rows(n, P, g)
+                d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+                d.set_rhs(b[rb:re_])
+            out = []
+            for maxit, tol in [(0, 0.0), (1, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]:
+                its = parts[0].run(maxit, tol)
+                out.append((its, np.concatenate([d.x() for d in parts])))
+            assert all(d.info()["fused"] == (1 if fused else 0) for d in parts)
+        finally:
+            parts[0].close()
+        res[fused] = out
+    for (i0, x0), (i1, x1) in zip(res[True][:-1], res[False][:-1]):
+        assert i0 == i1
+        assert np.linalg.norm(x0 - x1) <= 1e-12 * np.linalg.norm(x1)
+    its, x = res[True][-1]
+    x_ref, its_ref, _ = H.o_solve(3000, 1e-10, rp, col, val, b, cg1=True)
+    assert abs(its - its_ref) <= 1 and its < 3000
+    assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
+
+
+def test_fused_cg1_rccl_one_rank_graph_parity():
+    """The fused CG1 step through a 1-rank RCCL communicator: replayed graphs
+    of both buffer parities and eager launches bit-identical."""
+    rp, col, val = cgx.laplacian3d(24, 20, 30)
+    b = np.random.default_rng(14).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    res = {}
+    for graph in (True, False):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+        try:
+            d.set_alg(cgx.CGX_ALG_CG1)
+            d.set_fused(True)
+            d.set_graph(graph)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            out = []
+            for maxit in (17, 33, 40):
+                its = d.run(maxit, 0.0)
+                out.append((its, d.x()))
+            its = d.run(3000, 1e-10)
+            out.append((its, d.x()))
+            assert d.info()["fused"] == 1 and d.info()["graph"] == (1 if graph else 0)
+        finally:
+            d.close()
+        res[graph] = out
+    for (i0, x0), (i1, x1) in zip(res[True], res[False]):
+        assert i0 == i1
+        assert H.same_bits_or_both_nan(x0, x1)
+
+
 def test_bench_dist_path_rehearsal(tmp_path):
     """bench.py's N > 1 path at one rank (torch.distributed.run, a 1-rank
     RCCL communicator): the parity gate (HS, fused HS, CG1 against the

@@ -1,0 +1,176 @@
+"""GPU: the headline path and the partitioned path at BASELINE sizes, pinned
+to the oracle.
+
+Bars, stated per test:
+  * C3 (216^3) fast mode, fused DIA-VI step (the path bench.py's `value`
+    comes from), maxit 20: ||x - x_oracle|| <= 1e-12 ||x_oracle|| against
+    oracle_conj_grad(20) (cg.c:88-141 restated, the reference's HS order).
+  * C3 exact mode, maxit 5: x bit-identical to oracle_conj_grad(5).
+  * C4 (400^3, 64 M rows) on one GPU, maxit 5: exact mode bit-identical to
+    the oracle; fast mode within 1e-9 (the oracle's dot products are
+    sequential sums of 64 M terms, whose rounding error bound is n u = 7e-9
+    of the sum of |terms|; the tree sums' is log2(n) u: the measured
+    difference is 6e-11).
+  * C4 row-partitioned into 8 slabs of 50 planes (C4/8's exact shapes) as an
+    in-process group on one GPU, maxit 10, tol 0: fused and unfused HS
+    bit-identical to each other (every value of the fused step is the
+    unfused phases'); both within 1e-12 of the single-GPU solver (the dot
+    products are summed per partition, then across partitions: a different
+    rounding order, so not bit-identical to the single-GPU sums); CG1 within
+    1e-9 of the single-GPU CG1.
+  * C3 grid with a random coefficient per edge (no value indexing applies):
+    the layout picked, SpMV bit-exact against the oracle, CG within 1e-12.
+"""
+import numpy as np
+import pytest
+
+import cgx
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(x, ref):
+    return float(np.linalg.norm(x - ref) / np.linalg.norm(ref))
+
+
+@pytest.fixture(scope="module")
+def c3():
+    rp, col, val = cgx.laplacian3d(216, 216, 216)
+    b = np.random.default_rng(17).standard_normal(len(rp) - 1)
+    return rp, col, val, b
+
+
+def test_c3_fused_fast_path_vs_oracle(c3):
+    """The headline configuration through the fused step, against the
+    oracle's HS iteration (cg.c:88-141), 21 SpMVs."""
+    rp, col, val, b = c3
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["layout_name"] == "dia" and i["fused"] == 1
+        s.set_rhs(b)
+        assert s.run(20) == 21
+        x = s.x()
+        hist = s.history(21)
+    x_ref, h_ref = H.o_conj_grad(20, rp, col, val, b)
+    assert rel(x, x_ref) <= 1e-12
+    # r.r summed over 10 M terms in another order: relative differences ~1e-13
+    assert np.allclose(hist, h_ref[:21], rtol=1e-10, atol=0)
+
+
+def test_c3_exact_mode_bit_identical(c3):
+    """CGX_MODE_EXACT (sequential dots, the reference's summation order) at
+    full C3 size: x bit-identical to the oracle after 6 SpMVs."""
+    rp, col, val, b = c3
+    with cgx.Solver(0, mode=cgx.CGX_MODE_EXACT) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        assert s.run(5) == 6
+        x = s.x()
+    x_ref, _ = H.o_conj_grad(5, rp, col, val, b)
+    assert H.same_bits_or_both_nan(x, x_ref)
+
+
+@pytest.mark.timeout(600)
+def test_c4_one_gpu_vs_oracle():
+    """C4 (400^3, 64,000,000 rows, 447,040,000 nnz) on one GPU from the
+    host CSR, 6 SpMVs, against the oracle: bit-identical in exact mode,
+    within 1e-9 in fast mode (the fused step)."""
+    rp, col, val = cgx.laplacian3d(400, 400, 400)
+    b = np.ones(len(rp) - 1)
+    x_ref, _ = H.o_conj_grad(5, rp, col, val, b)
+    for mode in (cgx.CGX_MODE_EXACT, cgx.CGX_MODE_FAST):
+        with cgx.Solver(0, mode=mode) as s:
+            s.set_matrix(rp, col, val)
+            assert s.info()["layout_name"] == "dia"
+            assert s.info()["fused"] == (1 if mode == cgx.CGX_MODE_FAST else 0)
+            s.set_rhs(b)
+            assert s.run(5) == 6
+            x = s.x()
+        if mode == cgx.CGX_MODE_EXACT:
+            assert H.same_bits_or_both_nan(x, x_ref)
+        else:
+            assert rel(x, x_ref) <= 1e-9
+
+
+def c4_group(alg, fused, maxit, P=8):
+    """C4 row-partitioned into P slabs (cgx_partition_rows: 400^3 / 8 = 50
+    planes each) as an in-process group on GPU 0; x of all rows."""
+    nx = 400
+    n = nx ** 3
+    parts = cgx.DistSolver.local_group(0, P)
+    try:
+        parts[0].set_alg(alg)
+        parts[0].set_fused(fused)
+        for g, d in enumerate(parts):
+            rb, re_ = cgx.partition_rows(n, P, g)
+            rp, col, val = cgx.laplacian3d(nx, nx, nx, rb, re_)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(np.ones(re_ - rb))
+            del rp, col, val
+        its = parts[0].run(maxit, 0.0)
+        x = np.concatenate([d.x() for d in parts])
+        st = [d.info() for d in parts]
+        h = parts[0].history(its)
+    finally:
+        parts[0].close()
+    return its, x, h, st
+
+
+def c4_single(alg, maxit):
+    nx = 400
+    with cgx.Solver(0, alg=alg) as s:
+        s.gen_laplacian(3, nx, nx, nx)
+        s.set_rhs(np.ones(nx ** 3))
+        its = s.run(maxit)
+        return its, s.x()
+
+
+@pytest.mark.timeout(900)
+def test_c4_partitioned_8_slabs_in_process():
+    """C4 as it runs at N = 8 (8 M rows per partition, 9 DIA diagonals incl.
+    the ghost faces, halo = one 400^2 plane per neighbour), all 8 partitions
+    on one GPU: the multi-GPU phase code at the full BASELINE shape."""
+    its_f, x_f, h_f, st_f = c4_group(cgx.CGX_ALG_HS, True, 10)
+    its_u, x_u, h_u, st_u = c4_group(cgx.CGX_ALG_HS, False, 10)
+    assert all(s["fused"] == 1 and s["layout_name"] == "dia" for s in st_f)
+    assert all(s["fused"] == 0 for s in st_u)
+    assert [s["n_loc"] for s in st_f] == [8_000_000] * 8
+    assert [s["n_ghost"] for s in st_f] == [160_000] + [320_000] * 6 + [160_000]
+    assert its_f == its_u == 11
+    assert H.same_bits_or_both_nan(x_f, x_u)
+    assert H.same_bits_or_both_nan(h_f, h_u)
+    its1, x1 = c4_single(cgx.CGX_ALG_HS, 10)
+    assert its1 == 11
+    assert rel(x_f, x1) <= 1e-12
+    its_c, x_c, _, _ = c4_group(cgx.CGX_ALG_CG1, "auto", 10)
+    its_c1, x_c1 = c4_single(cgx.CGX_ALG_CG1, 10)
+    assert its_c == its_c1 == 11
+    assert rel(x_c, x_c1) <= 1e-9
+    assert rel(x_c, x1) <= 1e-9
+
+
+@pytest.fixture(scope="module")
+def varcoef_c3():
+    rp, col, val = cgx.varcoef3d(216, 216, 216, seed=7)
+    b = np.random.default_rng(19).standard_normal(len(rp) - 1)
+    return rp, col, val, b
+
+
+@pytest.mark.parametrize("layout", ["auto", "csr"])
+def test_general_coefficients_c3(varcoef_c3, layout):
+    """A general CSR at the C3 shape (mv_ops.h:17-23 carries arbitrary
+    values): every off-diagonal value distinct, so DIA-VI cannot apply and
+    AUTO stores coded columns + the value stream (DC); the SpMV is bit-exact
+    in both layouts and 20 CG iterations stay within 1e-12 of the oracle."""
+    rp, col, val, b = varcoef_c3
+    with cgx.Solver(0, layout=layout) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == {"auto": "dc"}.get(layout, layout)
+        assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
+        s.set_rhs(b)
+        s.run(20)
+        x = s.x()
+    x_ref, _ = H.o_conj_grad(20, rp, col, val, b)
+    assert rel(x, x_ref) <= 1e-12

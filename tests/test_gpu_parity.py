@@ -462,6 +462,27 @@ def test_mv_mult_matrix_residency():
     u3, r3 = cgx.ops_counters()
     assert (u3 - u2, r3 - r2) == (0, 1)
     assert np.all(np.isfinite(x_cg))
+    # edits that cancelled in the round-2 hash: a symmetric pair
+    # a_ij / a_ji negated in place, then every value negated (even length);
+    # each is detected (one upload, the call redone on the new A)
+    i = 1000
+    k = rp[i]  # first entry of row i (its -nx neighbour, column 960)
+    j = int(col[k])
+    kt = rp[j] + int(np.searchsorted(col[rp[j]:rp[j + 1]], i))
+    assert col[kt] == i
+    A.values[k] = -A.values[k]
+    A.values[kt] = -A.values[kt]
+    y4 = cgx.mv_mult(A, b)
+    u4, r4 = cgx.ops_counters()
+    assert (u4 - u3, r4 - r3) == (1, 0)
+    assert H.same_bits_or_both_nan(y4, H.o_spmv(rp, col, A.values, x))
+    assert len(A.values) % 2 == 0
+    A.values[:] = -A.values
+    x_cg2 = cgx.conj_grad(5, A, b)
+    u5, r5 = cgx.ops_counters()
+    assert (u5 - u4, r5 - r4) == (1, 0)
+    x_ref, _ = H.o_conj_grad(5, rp, col, A.values, x)
+    assert rel(x_cg2, x_ref) <= FAST_RTOL
 
 
 def test_vec_sub_in_place_alias():
@@ -702,6 +723,36 @@ def test_cg1_within_tolerance(name):
         x = s.x()
     x_o, its_o, _ = H.o_solve(500, 1e-10, g["row_ptr"], g["col"], g["val"], g["b"], cg1=True)
     assert abs(its - its_o) <= 1
+    assert rel(x, x_o) <= 1e-9
+
+
+@pytest.mark.parametrize("shape", [(12, 12, 12), (40, 30, 24), (7, 5, 9), (64, 48, 10)])
+def test_fused_cg1_step(shape):
+    """The fused Chronopoulos-Gear step (k_cg1_dia_h: the p / s / x / r
+    recurrences and w = A r_new with both partials in one launch, r / s / w
+    double-buffered, replayed graphs of both parities): within 1e-9 of the
+    oracle's CG1 solve (same iteration count within 1), within 1e-12 of the
+    unfused CG1 iteration at fixed max_iter (the two differ only in how the
+    gamma partials are grouped), every max_iter parity of the graph batches."""
+    rp, col, val = cgx.laplacian3d(*shape)
+    b = np.random.default_rng(8).standard_normal(len(rp) - 1)
+    out = {}
+    for fused in (True, False):
+        with cgx.Solver(0, alg=cgx.CGX_ALG_CG1, layout="dia", fused=fused) as s:
+            s.set_matrix(rp, col, val)
+            assert s.info()["fused"] == (1 if fused else 0)
+            res = []
+            for maxit, tol in [(0, 0.0), (1, 0.0), (16, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]:
+                s.set_rhs(b)
+                its = s.run(maxit, tol)
+                res.append((its, s.x()))
+            out[fused] = res
+    for (i0, x0), (i1, x1) in zip(out[True][:-1], out[False][:-1]):
+        assert i0 == i1
+        assert rel(x0, x1) <= 1e-12
+    its, x = out[True][-1]
+    x_o, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b, cg1=True)
+    assert abs(its - its_o) <= 1 and its < 3000
     assert rel(x, x_o) <= 1e-9
 
 
