@@ -160,8 +160,14 @@ void drop_graph(cgx_dist *d) {
 // The fused HS step (k_spmv_dia_h) runs when every partition's layout
 // takes it (decided once per connection: the ranks' phase sequences match).
 bool fz(const cgx_dist *d) { return d->fz_all && d->alg == CGX_ALG_HS; }
-// The fused CG1 step (k_cg1_dia_h), same rule; not in the prologue.
-bool fz1(const cgx_dist *d) { return d->fz_all && d->alg == CGX_ALG_CG1 && !d->in_init; }
+// The fused CG1 step (k_cg1_dia_h): only when forced on (CGX_FUSE_ON) --
+// on a rank's slab it loses to the unfused CG1 kernels (C4/8's 400 x 400 x
+// 50 slab: 164 vs 144 us per iteration, tools/dist_probe.py: the unfused
+// update's r and the SpMV's w are re-read from the Infinity Cache, the fused
+// launch streams all ten vectors from HBM); not in the prologue.
+bool fz1(const cgx_dist *d) {
+  return d->fz_all && d->alg == CGX_ALG_CG1 && d->fuse == CGX_FUSE_ON && !d->in_init;
+}
 
 // this partition takes the fused step (cgx_solver.cpp fused(): auto needs a
 // working set beyond the Infinity Cache)

@@ -19,6 +19,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "cgx_hash.h"
 #include "cgx_internal.h"
 
 namespace {
@@ -108,14 +109,14 @@ int fill(struct __mv_sparse *A, struct __mv_sparse *b, const std::vector<int> &c
   return (A->values && A->col_indices && A->row_ptr && b->values) ? 0 : -1;
 }
 
-int read_text(const char *path, std::vector<int> &col, std::vector<int> &rp,
-              std::vector<double> &val, std::vector<double> &bv) {
+// The whole text file in memory (-1: it cannot be opened).
+int load_text(const char *path, std::vector<char> &buf) {
   FILE *f = fopen(path, "rb");
   if (!f) {
     fprintf(stderr, "Error: Failed to open input file (%s)\n", path);
     return -1;
   }
-  std::vector<char> buf;
+  buf.clear();
   if (fseek(f, 0, SEEK_END) == 0) {
     const long sz = ftell(f);
     if (sz > 0) buf.resize((size_t)sz);
@@ -129,6 +130,11 @@ int read_text(const char *path, std::vector<int> &col, std::vector<int> &rp,
     while ((m = fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + m);
   }
   fclose(f);
+  return 0;
+}
+
+int parse_text(const char *path, const std::vector<char> &buf, std::vector<int> &col,
+               std::vector<int> &rp, std::vector<double> &val, std::vector<double> &bv) {
   // lines 0-3 (cg.c:146-218 reads four); text after the fourth '\n' is ignored
   const char *x = buf.data(), *end = buf.data() + buf.size();
   auto next_line = [&](bool *term, const char **e) {
@@ -161,30 +167,35 @@ int read_text(const char *path, std::vector<int> &col, std::vector<int> &rp,
   return 0;
 }
 
-// Binary cache: header + the four arrays; valid while the text file has
-// the recorded size and modification time.
-struct CacheHdr {
-  char magic[8];
-  long long src_size, src_mtime_ns;
-  long long ncol, nrp, nval, nb;
-};
-constexpr char kMagic[8] = {'c', 'g', 'x', 'b', 'i', 'n', '0', '1'};
-
-bool src_stat(const char *path, long long *size, long long *mtime_ns) {
-  struct stat st;
-  if (stat(path, &st) != 0) return false;
-  *size = (long long)st.st_size;
-  *mtime_ns = (long long)st.st_mtim.tv_sec * 1000000000LL + st.st_mtim.tv_nsec;
-  return true;
+int read_text(const char *path, std::vector<int> &col, std::vector<int> &rp,
+              std::vector<double> &val, std::vector<double> &bv) {
+  std::vector<char> buf;
+  if (load_text(path, buf)) return -1;
+  return parse_text(path, buf, col, rp, val, bv);
 }
 
-bool read_cache(const char *cache, long long size, long long mtime, std::vector<int> &col,
+// Binary cache: header + the four arrays, keyed on the text's size and a
+// 64-bit content hash of all of it (cgx_hash.h; hashing runs at memory
+// bandwidth on host threads, ~10x faster than parsing).  A cache written for
+// another input, or for an earlier version of this one, never matches --
+// whatever the paths, sizes or timestamps (the size + mtime key
+// of round 2 accepted a rewrite with same-width numbers inside one
+// timestamp tick).
+struct CacheHdr {
+  char magic[8];
+  long long src_size;
+  unsigned long long src_hash;
+  long long ncol, nrp, nval, nb;
+};
+constexpr char kMagic[8] = {'c', 'g', 'x', 'b', 'i', 'n', '0', '2'};
+
+bool read_cache(const char *cache, long long size, unsigned long long hash, std::vector<int> &col,
                 std::vector<int> &rp, std::vector<double> &val, std::vector<double> &bv) {
   FILE *f = fopen(cache, "rb");
   if (!f) return false;
   CacheHdr h;
   bool ok = fread(&h, sizeof h, 1, f) == 1 && memcmp(h.magic, kMagic, 8) == 0 &&
-            h.src_size == size && h.src_mtime_ns == mtime && h.ncol >= 0 && h.nrp >= 1 &&
+            h.src_size == size && h.src_hash == hash && h.ncol >= 0 && h.nrp >= 1 &&
             h.nval >= 0 && h.nb >= 0 && h.nrp <= INT32_MAX && h.ncol <= INT32_MAX &&
             h.nval <= INT32_MAX && h.nb <= INT32_MAX;
   if (ok) {
@@ -201,7 +212,8 @@ bool read_cache(const char *cache, long long size, long long mtime, std::vector<
   return ok;
 }
 
-void write_cache(const char *cache, long long size, long long mtime, const std::vector<int> &col,
+void write_cache(const char *cache, long long size, unsigned long long hash,
+                 const std::vector<int> &col,
                  const std::vector<int> &rp, const std::vector<double> &val,
                  const std::vector<double> &bv) {
   std::vector<char> tmp(strlen(cache) + 8);
@@ -211,7 +223,7 @@ void write_cache(const char *cache, long long size, long long mtime, const std::
   CacheHdr h;
   memcpy(h.magic, kMagic, 8);
   h.src_size = size;
-  h.src_mtime_ns = mtime;
+  h.src_hash = hash;
   h.ncol = (long long)col.size();
   h.nrp = (long long)rp.size();
   h.nval = (long long)val.size();
@@ -249,18 +261,17 @@ extern "C" int cgx_read_input_cached(const char *path, const char *cache_path,
     return -1;
   }
   if (from_cache) *from_cache = 0;
-  long long size = 0, mtime = 0;
-  if (!src_stat(path, &size, &mtime)) {
-    fprintf(stderr, "Error: Failed to open input file (%s)\n", path);
-    return -1;
-  }
+  std::vector<char> buf;
+  if (load_text(path, buf)) return -1;
+  const long long size = (long long)buf.size();
+  const unsigned long long hash = cgx::hash_bytes(buf.data(), buf.size());
   std::vector<int> col, rp;
   std::vector<double> val, bv;
-  if (read_cache(cache_path, size, mtime, col, rp, val, bv)) {
+  if (read_cache(cache_path, size, hash, col, rp, val, bv)) {
     if (from_cache) *from_cache = 1;
     return fill(A, b, col, rp, val, bv);
   }
-  if (read_text(path, col, rp, val, bv)) return -1;
-  write_cache(cache_path, size, mtime, col, rp, val, bv);
+  if (parse_text(path, buf, col, rp, val, bv)) return -1;
+  write_cache(cache_path, size, hash, col, rp, val, bv);
   return fill(A, b, col, rp, val, bv);
 }

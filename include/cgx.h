@@ -272,11 +272,11 @@ long long cgx_gen_varcoef3d(int nx, int ny, int nz, unsigned long long seed,
  * Re-entrant, bounds-safe, accepts a missing final newline.  0 or -1. */
 int cgx_read_input_file(const char *path, struct __mv_sparse *A,
                         struct __mv_sparse *b);
-/* The same with a binary cache at cache_path: valid while path keeps the
- * size and modification time recorded in it, the text is then not parsed;
- * otherwise the text is parsed and the cache (re)written (best effort: an
- * unwritable cache_path only costs the next parse).  *from_cache (may be
- * NULL) = 1 when the cache was used.  0 or -1. */
+/* The same with a binary cache at cache_path, keyed on the text's size and
+ * a 64-bit hash of its whole content: when they match, the text is hashed
+ * but not parsed; otherwise it is parsed and the cache (re)written (best
+ * effort: an unwritable cache_path only costs the next parse).  *from_cache
+ * (may be NULL) = 1 when the cache was used.  0 or -1. */
 int cgx_read_input_cached(const char *path, const char *cache_path,
                           struct __mv_sparse *A, struct __mv_sparse *b,
                           int *from_cache);

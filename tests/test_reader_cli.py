@@ -114,6 +114,32 @@ def test_reader_large_lines_and_cache(tmp_path):
     assert read(tmp_path / "missing.txt", cache=c) is None
 
 
+def test_reader_cache_keyed_on_content(tmp_path):
+    """the cache is keyed on the text's content (a 64-bit hash of
+    every byte), not on size + mtime: a rewrite with same-width numbers and
+    the old timestamp restored, or another file of the same size behind the
+    same cache path, is parsed again."""
+    import os
+    txt, rp, col, val, b = _big_text(20000, 7)
+    p, c = tmp_path / "a.txt", tmp_path / "a.cgxbin"
+    p.write_text(txt)
+    st = os.stat(p)
+    assert read(p, cache=c)["from_cache"] == 0
+    assert read(p, cache=c)["from_cache"] == 1
+    i = txt.index("\n") + 1  # first row_ptr entry "0" -> "1": same size
+    assert txt[i] == "0"
+    txt2 = txt[:i] + "1" + txt[i + 1:]
+    p.write_text(txt2)
+    os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert os.stat(p).st_size == st.st_size and os.stat(p).st_mtime_ns == st.st_mtime_ns
+    r = read(p, cache=c)
+    assert r["from_cache"] == 0 and r["rp"][0] == 1
+    q = tmp_path / "b.txt"  # another input of the same size, same cache path
+    q.write_text(txt)
+    r = read(q, cache=c)
+    assert r["from_cache"] == 0 and r["rp"][0] == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,it", [("kat_tridiag10", 4), ("lap2d_32", 25), ("dense128", 11)])
 def test_cli_output_matches_reference(name, it, tmp_path):
