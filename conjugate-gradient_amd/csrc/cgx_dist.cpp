@@ -9,9 +9,10 @@
 //
 // Recurrences (cgx_dist_set_alg):
 //   HS  (default; the reference's cg.c:88-141): per iteration
-//       st_comm: halo of p (ncclSend/Recv with each neighbour, into p's
-//                ghost tail), created at the device's highest priority so its
-//                kernel is dispatched ahead of the interior SpMV's workgroups
+//       st_comm: (forked from st) pack p[send rows], halo of p
+//                (ncclSend/Recv with each neighbour, into p's ghost tail),
+//                created at the device's highest priority so its kernels
+//                are dispatched ahead of the interior SpMV's workgroups
 //       st:      SpMV s = A p over INTERIOR work items (no ghost columns)
 //                || halo; wait; SpMV over BOUNDARY items; one finalize
 //                workgroup sums the p.s partials (local p.s)
@@ -19,17 +20,18 @@
 //                k_update_rf (alpha, r -= alpha s; its last workgroup sums
 //                the r.r partials) -> ncclAllReduce(r.r)
 //                k_xpay_xf (beta, stop test, x += alpha p, p = r + beta p)
-//                pack p[send rows] for the next halo
 //       fused (DIA layouts k_spmv_dia_h takes on every rank; cgx_dist_set_fused):
-//                pack p_new = r + beta p_old at the send rows (k_pack_pnext)
-//       st_comm: halo of p_new into the p_new buffer's ghost tail
+//       st_comm: pack p_new = r + beta p_old at the send rows (k_pack_pnext),
+//                halo of p_new into the p_new buffer's ghost tail
 //       st:      k_spmv_dia_h over INTERIOR items: beta, p_new, x (every
 //                other iteration), s = A p_new || halo; wait; BOUNDARY items
 //                (ghost diagonals read the received p_new) -> local p.s
 //                ncclAllReduce(p.s); k_update_rf -> ncclAllReduce(r.r)
 //                -- two launches and one pack per iteration instead of four
 //   CG1 (Chronopoulos-Gear): ONE all-reduce of (gamma, delta) per iteration,
-//       rounding-level different from HS, 8 B per row more vector traffic.
+//       rounding-level different from HS, 8 B per row more vector traffic;
+//       fused (CGX_FUSE_ON only): k_cg1_dia_h does the vector recurrences
+//       and w = A r_new in one launch, the halo carries r_new (k_pack_rnext).
 // Every rank derives alpha, beta and the stop test from the same all-reduced
 // sums, so they agree bit for bit.  With RCCL, batches of iterations --
 // halo, all-reduces and kernels -- are captured once as a hipGraph and
@@ -81,7 +83,8 @@ struct cgx_dist {
   ncclComm_t comm = nullptr;
   int cus = 256;
   hipStream_t st = nullptr, st_comm = nullptr;
-  hipEvent_t ev_packed = nullptr, ev_halo = nullptr, ev_sums = nullptr, ev_sums2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_packed = nullptr, ev_halo = nullptr, ev_sums = nullptr,
+             ev_sums2 = nullptr;
   hipEvent_t ev_red = nullptr;  // local transport: this part's last group sum has read d_sums
   cgx_part *part = nullptr;
   long long n_global = 0;
@@ -219,6 +222,7 @@ int init_common(cgx_dist *d, int device) {
     CGX_HIP(hipStreamCreateWithPriority(&d->st_comm, hipStreamNonBlocking, greatest));
   }
   d->A.st = d->st;
+  CGX_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums, hipEventDisableTiming));
@@ -503,27 +507,43 @@ double *spmv_y(cgx_dist *d) {
   return d->alg == CGX_ALG_HS ? d->d_s : fz1(d) ? w_new(d) : d->d_w;
 }
 
-// pack the send rows of the gathered vector (after its update; fused:
-// p_new = r + beta p_old computed at the send rows)
+// A rank with neighbours: ghost rows to receive or rows to send.  Without
+// any (one rank, a rank the matrix does not couple) the halo phases are
+// skipped entirely: no fork of the communication stream, no events.
+bool has_peers(const cgx_dist *d) { return !solo(d) && (d->n_send > 0 || d->n_ghost > 0); }
+
+// pack the send rows of the gathered vector (after its update; fused HS:
+// p_new = r + beta p_old computed at the send rows; fused CG1: r_new) on the
+// communication stream, forked from the iteration's stream here: the pack
+// runs beside the interior SpMV instead of in front of it, and the halo
+// send/recv follow it on the same stream.  The fork is a plain record on st
+// + wait on st_comm; the join is phase_spmv's wait on ev_halo.  (Round 2's
+// variant also waited, on st_comm, for an event recorded on st_comm itself,
+// with nothing captured between: the 1-rank capture of that shape crashed
+// the host process.  Neither a self-wait nor an empty fork remains.)
 int phase_pack(cgx_dist *d) {
-  if (solo(d)) return 0;
+  if (!has_peers(d)) return 0;
+  CGX_HIP(hipSetDevice(d->device));
+  CGX_HIP(hipEventRecord(d->ev_fork, d->st));
+  CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_fork, 0));
   if (fz(d))
     CGX_HIP(launch_pack_pnext<double>(d->n_send, d->d_send_idx, d->d_r, p_old(d), d->d_sendbuf,
-                                      d->d_st, rr_new_src(d), d->st));
+                                      d->d_st, rr_new_src(d), d->st_comm));
   else if (fz1(d))
     CGX_HIP(launch_pack_rnext<double>(d->n_send, d->d_send_idx, r_old(d), w_old(d), s_old(d),
-                                      d->d_sendbuf, d->d_st, d->st));
+                                      d->d_sendbuf, d->d_st, d->st_comm));
   else
-    CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, spmv_x(d), d->d_sendbuf, d->st));
-  CGX_HIP(hipEventRecord(d->ev_packed, d->st));
+    CGX_HIP(launch_gather<double>(d->n_send, d->d_send_idx, spmv_x(d), d->d_sendbuf, d->st_comm));
+  // the local transport's peers copy from d_sendbuf on their own streams
+  if (d->local) CGX_HIP(hipEventRecord(d->ev_packed, d->st_comm));
   return 0;
 }
 
-// halo exchange on the communication stream, straight into the ghost tail
+// halo exchange on the communication stream (after this rank's pack, in
+// stream order), straight into the ghost tail; ev_halo joins it back
 int phase_halo(cgx_dist *d) {
-  if (solo(d)) return 0;
+  if (!has_peers(d)) return 0;
   CGX_HIP(hipSetDevice(d->device));
-  CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_packed, 0));
   double *ghost = spmv_x(d) + d->n_loc;
   if (d->local) {
     for (cgx_dist *o : d->group->parts) {
@@ -533,7 +553,7 @@ int phase_halo(cgx_dist *d) {
                              (size_t)d->recv_count[o->rank] * 8, hipMemcpyDeviceToDevice,
                              d->st_comm));
     }
-  } else if (d->nranks > 1) {
+  } else {
     CGX_NCCL(ncclGroupStart());
     for (int q = 0; q < d->nranks; ++q) {
       if (q == d->rank) continue;
@@ -591,7 +611,7 @@ int phase_spmv(cgx_dist *d) {
     return launch_spmv<double>(a, d->st, ev);
   };
   CGX_HIP(launch(d->it_int, d->d_pb, 0));
-  if (!solo(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
+  if (has_peers(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
   CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, 2));
   if (rec) d->ev_i += 4;
   if (solo(d)) return 0;
@@ -1008,6 +1028,7 @@ void destroy_one(cgx_dist *d) {
   if (d->st_comm) (void)hipStreamSynchronize(d->st_comm);
   free_system(d);
   if (d->comm) ncclCommDestroy(d->comm);
+  if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
   if (d->ev_packed) (void)hipEventDestroy(d->ev_packed);
   if (d->ev_halo) (void)hipEventDestroy(d->ev_halo);
   if (d->ev_sums) (void)hipEventDestroy(d->ev_sums);
