@@ -316,6 +316,32 @@ def solve_e2e(sysm, tol=1e-8, maxit=20000):
     return out
 
 
+def general_coefficients(steps, warmup, device=0):
+    """the C3 grid with one random coefficient per edge
+    (cgx_gen_varcoef3d: every off-diagonal value distinct, so no layout can
+    index the values -- the general CSR case mv_ops.h:17-23 allows): the
+    layout libcgx picks for it (coded columns + the value stream) and the
+    plain CSR, each with its CG it/s and in-iteration SpMV on its own bytes
+    and on the CSR basis (SURVEY.md 8d B_spmv)."""
+    import numpy as np
+    import cgx
+    rp, col, val = cgx.varcoef3d(216, 216, 216, seed=7)
+    sysm = dict(rp=rp, col=col, val=val, b=np.ones(len(rp) - 1))
+    out = dict(matrix="7-point pattern of C3 (216^3), a_ij = a_ji = -(0.5 + U(0,1]) per edge, "
+                      "diagonal = sum |a_ij| + 0.01 (cgx_gen_varcoef3d, seed 7), b = 1")
+    for name, layout in (("auto", "auto"), ("csr", "csr")):
+        leg = solver_leg(sysm, steps, warmup, layout, device, b2b=True)
+        i = leg["info"]
+        own_gbs, own_frac = spmv_roofline(i["spmv_iter_bytes"], leg["spmv_us"] * 1e-3)
+        csr_gbs, csr_frac = spmv_roofline(i["spmv_bytes"], leg["spmv_us"] * 1e-3)
+        out[name] = dict(layout=layout_desc(i), layout_name=i["layout_name"], value=leg["value"],
+                         unit="it/s", spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
+                         own_bytes_gbs=own_gbs, own_bytes_frac=own_frac,
+                         csr_basis_gbs=csr_gbs, csr_basis_frac=csr_frac,
+                         kernel=kernel_name(i))
+    return out
+
+
 def c4_one_gpu(steps, warmup, device=0):
     """The N = 1 point of the C4 strong-scaling curve: 400^3 generated in
     device memory (cgx_solver_gen_laplacian), the layout libcgx picks."""
@@ -445,6 +471,7 @@ def run_single(args, wl_name):
                      "unfused three-launch iteration; NOT an upper bound: the fused DIA step "
                      "of the headline moves fewer bytes per iteration")
         if wl_name == "c3":
+            extra["general_coefficients"] = general_coefficients(args.steps, args.warmup)
             extra["c4_1gpu"] = c4_one_gpu(min(args.steps, 50), args.warmup)
             extra["solve_e2e"] = solve_e2e(sysm)
 

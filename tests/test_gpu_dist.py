@@ -445,6 +445,20 @@ def test_fused_cg1_rccl_one_rank_graph_parity():
         assert H.same_bits_or_both_nan(x0, x1)
 
 
+def test_capture_fork_join_shape():
+    """The multi-rank iteration's stream shape (phase_pack / phase_halo /
+    phase_spmv: fork of the communication stream by an event, pack + copy
+    on it, join by an event before the boundary kernel) captured as a
+    hipGraph with real work on the forked stream -- the shape a 1-rank
+    communicator cannot produce (no peers, no fork) -- replayed bit-identical
+    to eager (tests/native/capture_fork.hip)."""
+    import subprocess
+    exe = H.REPO / "conjugate-gradient_amd" / "bin" / "capture_fork"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bit-identical" in r.stdout
+
+
 def test_bench_dist_path_rehearsal(tmp_path):
     """bench.py's N > 1 path at one rank (torch.distributed.run, a 1-rank
     RCCL communicator): the parity gate (HS, fused HS, CG1 against the
