@@ -55,7 +55,8 @@ class CgxInfo(ctypes.Structure):
                 ("code_bytes_per_row", ctypes.c_int), ("encode_fallback", ctypes.c_int),
                 ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double),
                 ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int),
-                ("fused", ctypes.c_int)]
+                ("fused", ctypes.c_int), ("fuse_status", ctypes.c_int),
+                ("breakdown", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):
@@ -66,7 +67,8 @@ class CgxDistStats(ctypes.Structure):
                 ("iter_bytes", ctypes.c_double), ("halo_bytes", ctypes.c_double),
                 ("device_bytes", ctypes.c_size_t), ("spmv_iter_bytes", ctypes.c_double),
                 ("layout", ctypes.c_int), ("n_dict", ctypes.c_int), ("graph", ctypes.c_int),
-                ("alg", ctypes.c_int), ("fused", ctypes.c_int)]
+                ("alg", ctypes.c_int), ("fused", ctypes.c_int),
+                ("fuse_status", ctypes.c_int), ("breakdown", ctypes.c_int)]
 
 
 _MVP = ctypes.POINTER(MvSparse)
@@ -188,6 +190,10 @@ _lib = None
 
 
 CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON = 0, 1, 2
+# cgx_info.fuse_status / cgx_dist_stats.fuse_status (cgx.h)
+(CGX_FUSE_STATUS_RUNS, CGX_FUSE_STATUS_OFF, CGX_FUSE_STATUS_NOT_DIA, CGX_FUSE_STATUS_WIDE_CODES,
+ CGX_FUSE_STATUS_FAR_DIAGS, CGX_FUSE_STATUS_CACHED, CGX_FUSE_STATUS_EXACT, CGX_FUSE_STATUS_PEER,
+ CGX_FUSE_STATUS_CG1_AUTO) = range(9)
 
 
 def fuse_mode(mode):
@@ -523,7 +529,7 @@ class CgxOpsTiming(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("setup_ms", ctypes.c_double),
                 ("hash_ms", ctypes.c_double), ("solve_ms", ctypes.c_double),
                 ("download_ms", ctypes.c_double), ("uploaded", ctypes.c_int),
-                ("iters", ctypes.c_int)]
+                ("iters", ctypes.c_int), ("breakdown", ctypes.c_int)]
 
 
 def ops_set_mode(mode=CGX_MODE_FAST, alg=CGX_ALG_HS):

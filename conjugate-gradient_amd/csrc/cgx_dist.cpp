@@ -1242,6 +1242,19 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   // fused CG1: + r, w, s, p, x read and p, s, r, w, x written (cgx_info)
   if (d->have_matrix && fz1(d)) s->spmv_iter_bytes += 8.0 * d->n_loc * 8.0;
   s->fused = fz(d) || fz1(d) ? 1 : 0;
+  {
+    const int own = d->fuse == CGX_FUSE_OFF ? CGX_FUSE_STATUS_OFF
+                    : !d->have_matrix      ? CGX_FUSE_STATUS_NOT_DIA
+                    : d->A.fuse_block()    ? d->A.fuse_block()
+                    : (d->fuse == CGX_FUSE_AUTO && !d->A.nt) ? CGX_FUSE_STATUS_CACHED
+                                                             : 0;
+    s->fuse_status = s->fused ? CGX_FUSE_STATUS_RUNS
+                     : own    ? own
+                     : (d->alg == CGX_ALG_CG1 && d->fuse != CGX_FUSE_ON) ? CGX_FUSE_STATUS_CG1_AUTO
+                     : d->group && d->group->fz_known && !d->fz_all ? CGX_FUSE_STATUS_PEER
+                                                                     : CGX_FUSE_STATUS_RUNS;
+  }
+  s->breakdown = d->h_st ? d->h_st->brk : 0;
   s->layout = d->have_matrix ? cgx::public_layout(d->A) : CGX_LAYOUT_AUTO;
   s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_DIA ? d->A.dia.ndiag : 0;
   s->graph = d->graph_state;

@@ -69,7 +69,9 @@ struct CgState {
   // rr_u / k_u (+ alpha), k_xpay_xf writes rr_x / k_x (+ rr, k, beta, done)
   int k_u;
   int k_x;
-  int pad;
+  int brk;        // breakdown: 1 + the first iteration whose p.s (HS) or CG1
+                  // denominator was <= 0 or not finite (the reference then
+                  // yields NaN, cg.c:113, 129); 0 = none.  Diagnostic only.
   double rr_u;
   double rr_x;
   // fused HS step (k_spmv_dia_h): k_update_rf's last workgroup writes the

@@ -191,6 +191,7 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
     case FIN_HS_ALPHA:
       st->ps = sa;
       st->alpha = st->rr / sa;  // cg.c:113
+      if (!(sa > 0.0) && st->brk == 0) st->brk = st->k + 1;
       break;
     case FIN_HS_BETA: {
       const double rr_new = sa;
@@ -209,6 +210,7 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
       st->bb = sa;
       st->rr = sa;
       st->delta = sb;
+      st->brk = sb > 0.0 ? 0 : 1;
       st->tol2bb = st->tol * st->tol * sa;
       st->alpha = sa / sb;
       st->beta = 0.0;
@@ -223,8 +225,10 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
         st->done = 1;
       } else {
         const double beta = g / st->rr;
+        const double den = d - beta * g / st->alpha;
         st->delta = d;
-        st->alpha = g / (d - beta * g / st->alpha);
+        st->alpha = g / den;
+        if (!(den > 0.0) && st->brk == 0) st->brk = k + 2;
         st->beta = beta;
         st->rr = g;
         st->k = k + 1;
@@ -1399,6 +1403,7 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
       st->alpha = alpha;
       st->rr_u = rr;
       st->k_u = st->k_x;
+      if (!(ps > 0.0) && st->brk == 0) st->brk = st->k_x + 1;  // p.s <= 0: NaN follows
     }
   }
   __syncthreads();

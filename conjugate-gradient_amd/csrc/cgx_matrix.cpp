@@ -867,11 +867,14 @@ int DevMatrix::padded_rows() const { return padded_rows_for(n); }
 
 bool DevMatrix::near_diag(int k) const { return std::abs(dia.doff[k]) <= kHaloMax; }
 
-bool DevMatrix::fusable() const {
-  if (layout != L_DIA || dia.cbytes > 4) return false;
+bool DevMatrix::fusable() const { return fuse_block() == 0; }
+
+int DevMatrix::fuse_block() const {
+  if (layout != L_DIA) return CGX_FUSE_STATUS_NOT_DIA;
+  if (dia.cbytes > 4) return CGX_FUSE_STATUS_WIDE_CODES;
   int nfar = 0;
   for (int k = 0; k < dia.ndiag; ++k) nfar += !near_diag(k);
-  return nfar <= 4;
+  return nfar <= 4 ? 0 : CGX_FUSE_STATUS_FAR_DIAGS;
 }
 
 std::vector<int> DevMatrix::item_rows() const {

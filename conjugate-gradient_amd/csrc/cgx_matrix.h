@@ -80,6 +80,8 @@ struct DevMatrix {
   // The fused HS step applies (DIA, <= 4 code bytes per row, at most 4
   // far diagonals, |d| > kHaloMax): k_spmv_dia_h's window and far slots.
   bool fusable() const;
+  // why not: 0 fusable, else CGX_FUSE_STATUS_NOT_DIA / _WIDE_CODES / _FAR_DIAGS
+  int fuse_block() const;
   bool near_diag(int k) const;  // read from k_spmv_dia_h's LDS window
   // rows covered by the items (DIA pads to whole 512-row slices)
   int padded_rows() const;

@@ -292,6 +292,10 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct _
   t.download_ms = now_ms() - t2;
   t.total_ms = now_ms() - t0;
   t.iters = iters;
+  {
+    cgx_info inf;
+    if (cgx_solver_info(s, &inf) == 0) t.breakdown = inf.breakdown;
+  }
   g_timing = t;
   *x = xv;  // cg.c:138 (any previous *x is not freed, as in the reference)
   return iters;

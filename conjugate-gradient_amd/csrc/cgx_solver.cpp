@@ -858,6 +858,13 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->setup_device_ms = A.setup_dev_ms;
   info->encode_fallback = A.encode_fallback;
   info->fused = s->have_matrix && fused(s) ? 1 : 0;
+  info->fuse_status = !s->have_matrix ? CGX_FUSE_STATUS_NOT_DIA
+                      : s->mode == CGX_MODE_EXACT ? CGX_FUSE_STATUS_EXACT
+                      : s->fuse == CGX_FUSE_OFF   ? CGX_FUSE_STATUS_OFF
+                      : A.fuse_block()            ? A.fuse_block()
+                      : (s->fuse == CGX_FUSE_AUTO && !A.nt) ? CGX_FUSE_STATUS_CACHED
+                                                            : CGX_FUSE_STATUS_RUNS;
+  info->breakdown = s->h_st ? s->h_st->brk : 0;
   return 0;
 }
 

@@ -68,6 +68,7 @@ int cgx_ops_set_device(int device);
 typedef struct {
   double total_ms, setup_ms, hash_ms, solve_ms, download_ms;
   int uploaded, iters;
+  int breakdown;  /* as cgx_info.breakdown, for the last conj_grad / solve */
 } cgx_ops_timing;
 int cgx_ops_last_timing(cgx_ops_timing *t);
 
@@ -161,8 +162,31 @@ typedef struct {
   double setup_device_ms; /* set_matrix: device time after the last submit  */
   int n_values;         /* DIA: values over all diagonal tables             */
   int gathers_per_chunk; /* CSR / DC: x gathers issued per row chunk (7|8)  */
-  int fused;            /* 1: the HS iteration runs fused (cgx_solver_set_fused) */
+  int fused;            /* 1: the iteration runs fused (cgx_solver_set_fused) */
+  int fuse_status;      /* CGX_FUSE_STATUS_*: why the fused step does or does
+                           not run for the loaded matrix and settings       */
+  int breakdown;        /* after a run: 1 + the first iteration whose p.s (HS)
+                           or CG1 step denominator was <= 0 or not finite --
+                           the point where the reference's iteration turns to
+                           NaN (cg.c:113, 129) -- or 0.  Diagnostic only: the
+                           iteration itself keeps the reference's IEEE
+                           semantics (failure detection)        */
 } cgx_info;
+
+/* cgx_info.fuse_status / cgx_dist_stats.fuse_status */
+enum { CGX_FUSE_STATUS_RUNS = 0,        /* the fused step runs                   */
+       CGX_FUSE_STATUS_OFF = 1,         /* CGX_FUSE_OFF requested                */
+       CGX_FUSE_STATUS_NOT_DIA = 2,     /* the layout is not DIA                 */
+       CGX_FUSE_STATUS_WIDE_CODES = 3,  /* DIA row words of 8 bytes (> 4)        */
+       CGX_FUSE_STATUS_FAR_DIAGS = 4,   /* more than 4 diagonals with |d| > 1024
+                                           (e.g. a slab not starting on a plane) */
+       CGX_FUSE_STATUS_CACHED = 5,      /* AUTO: the working set fits the
+                                           Infinity Cache (faster unfused)       */
+       CGX_FUSE_STATUS_EXACT = 6,       /* exact mode runs the reference's order */
+       CGX_FUSE_STATUS_PEER = 7,        /* partitioned: another rank's layout
+                                           refused (all ranks or none)           */
+       CGX_FUSE_STATUS_CG1_AUTO = 8 };  /* partitioned CG1: fused only when
+                                           forced on (slower on a rank's slab)   */
 
 int  cgx_solver_create(int device, cgx_solver **out);
 void cgx_solver_destroy(cgx_solver *s);
@@ -339,6 +363,8 @@ typedef struct {
   int alg;                               /* CGX_ALG_* in use              */
   int fused;                             /* 1: the fused HS step runs (set
                                             once the ranks are connected) */
+  int fuse_status;                       /* CGX_FUSE_STATUS_* (cgx_info)  */
+  int breakdown;                         /* as cgx_info.breakdown         */
 } cgx_dist_stats;
 
 /* Rank 0 creates the id and distributes it (e.g. torch.distributed). */

@@ -445,6 +445,40 @@ def test_fused_cg1_rccl_one_rank_graph_parity():
         assert H.same_bits_or_both_nan(x0, x1)
 
 
+def test_fuse_refusal_reported_for_plane_cutting_partitions():
+    """slabs that do not start on a plane boundary add ghost
+    diagonals, so some partition's layout cannot take the fused step and the
+    group runs unfused -- now reported per partition (fuse_status: the
+    partition's own reason, or PEER when another partition refused), and
+    the result still matches the oracle."""
+    rp, col, val = cgx.laplacian3d(40, 30, 16)
+    n = len(rp) - 1
+    b = np.random.default_rng(15).standard_normal(n)
+    P = 7
+    parts = cgx.DistSolver.local_group(0, P)
+    try:
+        parts[0].set_alg(cgx.CGX_ALG_HS)
+        parts[0].set_fused(True)
+        for g, d in enumerate(parts):
+            rb, re_ = cgx.partition_rows(n, P, g)
+            d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+            d.set_rhs(b[rb:re_])
+        its = parts[0].run(3000, 1e-10)
+        x = np.concatenate([d.x() for d in parts])
+        st = [d.info() for d in parts]
+    finally:
+        parts[0].close()
+    assert all(s["fused"] == 0 for s in st)
+    codes = [s["fuse_status"] for s in st]
+    own = {cgx.CGX_FUSE_STATUS_NOT_DIA, cgx.CGX_FUSE_STATUS_WIDE_CODES,
+           cgx.CGX_FUSE_STATUS_FAR_DIAGS}
+    assert any(c in own for c in codes), codes
+    assert all(c in own | {cgx.CGX_FUSE_STATUS_PEER} for c in codes), codes
+    x_ref, its_ref, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+    assert abs(its - its_ref) <= 1
+    assert np.linalg.norm(x - x_ref) <= 1e-9 * np.linalg.norm(x_ref)
+
+
 def test_capture_fork_join_shape():
     """The multi-rank iteration's stream shape (phase_pack / phase_halo /
     phase_spmv: fork of the communication stream by an event, pack + copy

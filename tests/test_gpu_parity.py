@@ -542,7 +542,35 @@ def test_kat_values_on_gpu():
     A = cgx.Mv(g["val"], g["col"], g["row_ptr"])
     b = cgx.Mv(g["b"])
     assert list(cgx.conj_grad(4, A, b)) == [5, 9, 12, 14, 15, 15, 14, 12, 9, 5]
+    assert cgx.ops_last_timing()["breakdown"] == 0
     assert np.all(np.isnan(cgx.conj_grad(5, A, b)))
+    # SURVEY.md 5 (failure detection): r is exactly 0 after the 5th x update,
+    # so p = 0 and p.s = 0 at the 6th: the breakdown the reference turns into
+    # NaN (cg.c:113) is reported, the IEEE result kept
+    assert cgx.ops_last_timing()["breakdown"] == 6
+    with cgx.Solver(0, mode=cgx.CGX_MODE_EXACT) as s:
+        s.set_matrix(g["row_ptr"], g["col"], g["val"])
+        s.set_rhs(g["b"])
+        s.run(5)
+        assert s.info()["breakdown"] == 6 and np.all(np.isnan(s.x()))
+        s.run(3)
+        assert s.info()["breakdown"] == 0
+
+
+def test_fuse_status_reports_why():
+    """cgx_info.fuse_status names why the fused step does or does not run
+    (the refusal was silent)."""
+    rp, col, val = cgx.laplacian3d(40, 30, 24)
+    cases = [(dict(), cgx.CGX_FUSE_STATUS_CACHED), (dict(fused=True), cgx.CGX_FUSE_STATUS_RUNS),
+             (dict(fused=False), cgx.CGX_FUSE_STATUS_OFF),
+             (dict(mode=cgx.CGX_MODE_EXACT), cgx.CGX_FUSE_STATUS_EXACT),
+             (dict(layout="csr", fused=True), cgx.CGX_FUSE_STATUS_NOT_DIA)]
+    for kw, want in cases:
+        with cgx.Solver(0, **kw) as s:
+            s.set_matrix(rp, col, val)
+            i = s.info()
+            assert i["fuse_status"] == want, (kw, i["fuse_status"])
+            assert i["fused"] == (1 if want == cgx.CGX_FUSE_STATUS_RUNS else 0)
 
 
 def test_conj_grad_argument_errors():
