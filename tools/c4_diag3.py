@@ -10,7 +10,7 @@ REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO / "conjugate-gradient_amd"))
 sys.path.insert(0, str(REPO / "tests"))
 import cgx  # noqa: E402
-from test_gpu_fullsize import c4_group  # noqa: E402
+from test_gpu_fullsize import c4_group  # noqa: E402  (the full-size test's group builder)
 
 for tok in sys.argv[1:]:
     kind, rest = tok[0], tok[1:]
