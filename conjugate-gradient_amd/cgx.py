@@ -189,7 +189,7 @@ _SIGS = {
 _lib = None
 
 
-CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON, CGX_FUSE_RS = 0, 1, 2, 3
+CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON = 0, 1, 2
 # cgx_info.fuse_status / cgx_dist_stats.fuse_status (cgx.h)
 (CGX_FUSE_STATUS_RUNS, CGX_FUSE_STATUS_OFF, CGX_FUSE_STATUS_NOT_DIA, CGX_FUSE_STATUS_WIDE_CODES,
  CGX_FUSE_STATUS_FAR_DIAGS, CGX_FUSE_STATUS_CACHED, CGX_FUSE_STATUS_EXACT, CGX_FUSE_STATUS_PEER,
@@ -199,8 +199,7 @@ CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON, CGX_FUSE_RS = 0, 1, 2, 3
 def fuse_mode(mode):
     """cgx_*_set_fused mode from "auto" / True / False (or the constant)."""
     if isinstance(mode, str):
-        return {"auto": CGX_FUSE_AUTO, "on": CGX_FUSE_ON, "off": CGX_FUSE_OFF,
-                "rs": CGX_FUSE_RS}[mode]
+        return {"auto": CGX_FUSE_AUTO, "on": CGX_FUSE_ON, "off": CGX_FUSE_OFF}[mode]
     if isinstance(mode, bool):
         return CGX_FUSE_ON if mode else CGX_FUSE_OFF
     return int(mode)

@@ -93,7 +93,6 @@ enum FinOp {
   FIN_CG1 = 4,       // gamma' = sum(a), delta = sum(b); stop test; alpha, beta
   FIN_SUM = 5,       // out[0] = sum(a) (op-level dot, local sums)
   FIN_SUM2 = 6,      // out[0] = sum(a), out[1] = sum(b)
-  FIN_HS_ALPHA_F = 7,  // fused RS mode: alpha = rr_x / sum(a) with k_update_rf's state writes
 };
 
 constexpr int kVecBS = 256;
@@ -295,13 +294,6 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
 template <typename T>
 hipError_t launch_cg1_fused(const SpmvArgs<T> &a, const Cg1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev = LaunchEv{});
-// Fuse mode RS (single GPU): the fused launch does not store s (a.y ==
-// nullptr in launch_spmv_fused); k_update_rs recomputes it from p_new (a.x)
-// and does r -= alpha s, the r.r partials (rr_part, one per workgroup) and
-// their canonical sum into fin.out (fin.pa == rr_part, fin.na == grid).
-template <typename T>
-hipError_t launch_update_rs(const SpmvArgs<T> &a, T *r, CgState *stt, double *rr_part, int grid,
-                            hipStream_t st, const FinArgs &fin);
 // out[i] = r_new[idx[i]] = r - alpha (w + beta s) (the fused partitioned CG1
 // step's halo send rows)
 template <typename T>

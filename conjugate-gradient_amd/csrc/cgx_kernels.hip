@@ -188,13 +188,6 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
       st->k_u = -1;  // fused step: no previous iteration yet
       st->done = 0;
       break;
-    case FIN_HS_ALPHA_F:  // fused RS mode: k_update_rf's scalar step (cg.c:113)
-      st->ps = sa;
-      st->alpha = st->rr_x / sa;
-      st->rr_u = st->rr_x;
-      st->k_u = st->k_x;
-      if (!(sa > 0.0) && st->brk == 0) st->brk = st->k_x + 1;
-      break;
     case FIN_HS_ALPHA:
       st->ps = sa;
       st->alpha = st->rr / sa;  // cg.c:113
@@ -719,7 +712,7 @@ __device__ __forceinline__ typename Pair<T>::type p_next(typename Pair<T>::type 
 // 8 p_new + 8 s, + 24 (x read and written, p_{k-1} read) every other
 // launch.  Every value is the unfused path's (same roundings): x and the
 // r.r history are bit-identical to SpMV + k_update_rf + k_xpay_xf.
-template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH, bool STS = true>
+template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH>
 __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *win = reinterpret_cast<T *>(dyn_lds);
@@ -851,7 +844,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     }
   }
   const T pn0 = win[rw], pn1 = win[rw + 1];
-  if (STS) st_pair(a.y, r, a.n, a0, a1, NT);  // !STS: k_update_rs recomputes s
+  st_pair(a.y, r, a.n, a0, a1, NT);
   double dot = 0.0;
   if (r < a.n) {
     st_pair(f.pnew, r, a.n, pn0, pn1, false);
@@ -1071,86 +1064,6 @@ __global__ __launch_bounds__(256) void k_pack_pnext(int n_send, const int *__res
       out[i] = r[j] + b;
     }
   }
-}
-
-// The r update of the fused HS step WITHOUT a stored s (fuse mode RS): s =
-// A p_new is recomputed from the p_new the fused launch just stored (the
-// same products in the same diagonal order, so s is bit-identical), then r
-// -= alpha s (cg.c:118-123), r.r partials, and the last-arriving
-// workgroup's canonical sum of them into *fin.out.  alpha comes from
-// CgState (k_finalize FIN_HS_ALPHA_F over the fused launch's p.s
-// partials).  Grid-stride over 512-row slices (a few workgroups per CU, so
-// the last-arriver ticket stays cheap); k_spmv_dia's pair-load gathers.
-// Bytes per row: code + p_new (gathered) + r read + r written = 25, against
-// 16 for s (written by the fused launch, read back by k_update_rf) + 24.
-template <typename T, int KW, bool NT>
-__global__ __launch_bounds__(256) void k_update_rs(SpmvArgs<T> a, T *r, CgState *st, double *rr_part,
-                                                   FinArgs fin) {
-  constexpr int KM = 8 * KW;
-  typedef typename std::conditional<KW == 1, unsigned, unsigned long long>::type C;
-  typedef typename Pair<T>::type P;
-  __shared__ T lv[KM * 16];
-  __shared__ double red[4];
-  const int done = st->done;
-  if (done) {
-    if (done == 1 && blockIdx.x == 0 && threadIdx.x == 0) st->done = 2;
-    return;
-  }
-  const int t = threadIdx.x;
-  const T alpha = (T)st->alpha;
-  if (t < a.ndiag * 16) lv[t] = a.vtab[t];
-  __syncthreads();
-  double acc = 0.0;
-  const int nsl = a.items.count, g = gridDim.x, w = xcd_block();
-  // contiguous slices per workgroup (neighbouring slices share the gathers'
-  // lines in L1/L2)
-  const int sb = (int)((long long)nsl * w / g), se = (int)((long long)nsl * (w + 1) / g);
-  for (int sl = sb; sl < se; ++sl) {
-    const int rw = sl * kDiaSliceRows + 2 * t;
-    const int rs = rw < a.n ? rw : 0;
-    C c0, c1;
-    ld_codes(a.dcode, a.cb, rw, c0, c1);
-    P xv[KM];
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
-      xv[k] = ld_pair(a.x, k < a.ndiag && (n0 != a.cmask[k] || n1 != a.cmask[k]) ? rw + a.doff[k] : rs);
-    }
-    P rv = P();
-    if (rw < a.n) rv = ld_pair((const T *)r, rw);
-    T s0 = T(0), s1 = T(0);
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      if (k < a.ndiag) {
-        const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
-        const T p0 = lv[k * 16 + n0] * xv[k].x, p1 = lv[k * 16 + n1] * xv[k].y;
-        s0 = n0 != a.cmask[k] ? s0 + p0 : s0;
-        s1 = n1 != a.cmask[k] ? s1 + p1 : s1;
-      }
-    }
-    if (rw < a.n) {
-      const T as0 = alpha * s0, as1 = alpha * s1;
-      const T r0 = rv.x - as0, r1 = rv.y - as1;
-      st_pair(r, rw, a.n, r0, r1, false);
-      acc = acc + (double)r0 * (double)r0;
-      if (rw + 1 < a.n) acc = acc + (double)r1 * (double)r1;
-    }
-  }
-  acc = wave_sum(acc);
-  const int lane = t & (kWave - 1), wid = t / kWave;
-  if (lane == 0) red[wid] = acc;
-  __syncthreads();
-  __shared__ int last;
-  if (t == 0) {
-    const double q = ((red[0] + red[1]) + red[2]) + red[3];
-    publish(rr_part + blockIdx.x, q);
-    last = take_ticket(fin.cnt, gridDim.x);
-  }
-  __syncthreads();
-  if (!last) return;
-  __shared__ double red16[16];
-  const double sa = canon_sum<256, true>(fin.pa, fin.na, red16);
-  if (t == 0) fin.out[0] = sa;
 }
 
 // -------------------------------------------------------------- k_stencil
@@ -2082,20 +1995,18 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev)
   return launch_spmv_en<T, false, false>(a, g, st, ev);
 }
 
-template <typename T, int NF, int NFAR, bool GH, bool STS>
+template <typename T, int NF, int NFAR, bool GH>
 static const void *fused_kernel_g(bool nt, bool list) {
-  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true, GH, STS>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, GH, STS>))
-            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true, GH, STS>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, GH, STS>));
+  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, GH>))
+            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, GH>));
 }
 
-// s not stored (fuse mode RS) only on one GPU (no ghost columns)
 template <typename T, int NF, int NFAR>
-static const void *fused_kernel(bool nt, bool list, bool gh, bool sts) {
-  return gh ? fused_kernel_g<T, NF, NFAR, true, true>(nt, list)
-            : sts ? fused_kernel_g<T, NF, NFAR, false, true>(nt, list)
-                  : fused_kernel_g<T, NF, NFAR, false, false>(nt, list);
+static const void *fused_kernel(bool nt, bool list, bool gh) {
+  return gh ? fused_kernel_g<T, NF, NFAR, true>(nt, list)
+            : fused_kernel_g<T, NF, NFAR, false>(nt, list);
 }
 
 template <typename T>
@@ -2110,19 +2021,17 @@ hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStre
   for (int q = 0; q < 4; ++q) nfar += a.fark[q] >= 0;
   if (nf > 5) return hipErrorInvalidValue;
   const bool nt = a.nt != 0, l = a.items.list != nullptr, gh = f.ghost != 0;
-  const bool sts = a.y != nullptr;  // a.y == nullptr: s not stored (fuse mode RS)
-  if (!sts && gh) return hipErrorInvalidValue;
   const void *k = nullptr;
   switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + (nfar == 0 ? 0 : nfar <= 2 ? 2 : 4)) {
-    case 20: k = fused_kernel<T, 2, 0>(nt, l, gh, sts); break;
-    case 22: k = fused_kernel<T, 2, 2>(nt, l, gh, sts); break;
-    case 24: k = fused_kernel<T, 2, 4>(nt, l, gh, sts); break;
-    case 30: k = fused_kernel<T, 3, 0>(nt, l, gh, sts); break;
-    case 32: k = fused_kernel<T, 3, 2>(nt, l, gh, sts); break;
-    case 34: k = fused_kernel<T, 3, 4>(nt, l, gh, sts); break;
-    case 50: k = fused_kernel<T, 5, 0>(nt, l, gh, sts); break;
-    case 52: k = fused_kernel<T, 5, 2>(nt, l, gh, sts); break;
-    case 54: k = fused_kernel<T, 5, 4>(nt, l, gh, sts); break;
+    case 20: k = fused_kernel<T, 2, 0>(nt, l, gh); break;
+    case 22: k = fused_kernel<T, 2, 2>(nt, l, gh); break;
+    case 24: k = fused_kernel<T, 2, 4>(nt, l, gh); break;
+    case 30: k = fused_kernel<T, 3, 0>(nt, l, gh); break;
+    case 32: k = fused_kernel<T, 3, 2>(nt, l, gh); break;
+    case 34: k = fused_kernel<T, 3, 4>(nt, l, gh); break;
+    case 50: k = fused_kernel<T, 5, 0>(nt, l, gh); break;
+    case 52: k = fused_kernel<T, 5, 2>(nt, l, gh); break;
+    case 54: k = fused_kernel<T, 5, 4>(nt, l, gh); break;
     default: return hipErrorInvalidValue;
   }
   void *args[] = {(void *)&a, (void *)&f};
@@ -2178,19 +2087,6 @@ hipError_t launch_cg1_fused(const SpmvArgs<T> &a, const Cg1Args<T> &f, hipStream
     (void)hipExtLaunchKernel(k, dim3(g), dim3(256), args, lds, st, ev.start, ev.stop, 0);
   else
     (void)hipLaunchKernel(k, dim3(g), dim3(256), args, lds, st);
-  return hipGetLastError();
-}
-
-template <typename T>
-hipError_t launch_update_rs(const SpmvArgs<T> &a, T *r, CgState *stt, double *rr_part, int grid,
-                            hipStream_t st, const FinArgs &fin) {
-  if (a.layout != L_DIA || grid <= 0 || !fin.cnt) return hipErrorInvalidValue;
-  if (a.ndiag <= 8)
-    hipLaunchKernelGGL((k_update_rs<T, 1, false>), dim3(grid), dim3(256), 0, st, a, r, stt, rr_part,
-                       fin);
-  else
-    hipLaunchKernelGGL((k_update_rs<T, 2, false>), dim3(grid), dim3(256), 0, st, a, r, stt, rr_part,
-                       fin);
   return hipGetLastError();
 }
 
@@ -2368,8 +2264,6 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                                           const LaunchEv &);                                     \
   template hipError_t launch_pack_rnext<T>(int, const int *, const T *, const T *, const T *,    \
                                            T *, const CgState *, hipStream_t);                   \
-  template hipError_t launch_update_rs<T>(const SpmvArgs<T> &, T *, CgState *, double *, int,    \
-                                          hipStream_t, const FinArgs &);                         \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
                                           double *, int, hipStream_t, const FinArgs *);          \
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \

@@ -165,7 +165,7 @@ void drop_graph(cgx_solver *s) {
 // per HS iteration).
 bool fused(const cgx_solver *s) {
   return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
-         (s->fuse != CGX_FUSE_AUTO || s->A.nt);
+         (s->fuse == CGX_FUSE_ON || s->A.nt);
 }
 
 // Buffers alternating per iteration: p for the fused HS step and the
@@ -307,22 +307,10 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     // canonical sum (last workgroup) into st->rr_new for the next step
     // (cg.c:111-132)
     T *pold = (T *)(s->pbuf ? s->d_p2 : s->d_p), *pnew = (T *)(s->pbuf ? s->d_p : s->d_p2);
-    const bool rs = s->fuse == CGX_FUSE_RS;  // s recomputed by the r update, not stored
-    const SpmvArgs<T> a =
-        s->A.args<T>(nullptr, rs ? nullptr : sv, s->d_pa, &s->d_st->done, s->A.all_items());
+    const SpmvArgs<T> a = s->A.args<T>(nullptr, sv, s->d_pa, &s->d_st->done, s->A.all_items());
     const FuseArgs<T> f{x, pold, pnew, r, s->d_st, s->d_hist, &s->d_st->rr_new, 1, 0};
     np = s->A.partials(s->A.all_items());
     CGX_HIP(launch_spmv_fused<T>(a, f, st, LaunchEv{ev0, ev1}));
-    if (rs) {
-      const int g2 = std::min(s->cus * 4, np);
-      CGX_HIP(launch_finalize(FIN_HS_ALPHA_F, s->d_pa, np, nullptr, 0, s->d_st, s->d_hist, nullptr,
-                              st));
-      const SpmvArgs<T> a2 = s->A.args<T>(pnew, nullptr, nullptr, nullptr, s->A.all_items());
-      const FinArgs fin{s->d_tick, s->d_pb, g2, &s->d_st->rr_new};
-      CGX_HIP(launch_update_rs<T>(a2, r, s->d_st, s->d_pb, g2, st, fin));
-      s->pbuf ^= 1;
-      return 0;
-    }
     const int gf = s->vec_grid / 4;
     const FinArgs fin{s->d_tick, s->d_pb, 4 * gf, &s->d_st->rr_new};
     CGX_HIP(launch_update_rf<T>(n, r, sv, s->d_st, s->d_pa, np, s->d_pb, gf, st, &fin));
@@ -717,7 +705,7 @@ int cgx_solver_set_mode(cgx_solver *s, int mode, int alg) {
 }
 
 int cgx_solver_set_fused(cgx_solver *s, int mode) {
-  if (!s || mode < CGX_FUSE_OFF || mode > CGX_FUSE_RS) return CGX_EINVAL;
+  if (!s || mode < CGX_FUSE_OFF || mode > CGX_FUSE_ON) return CGX_EINVAL;
   s->fuse = mode;
   drop_graph(s);
   return 0;
@@ -857,9 +845,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   if (s->have_matrix && fused(s))
     // CG1: r, w, s, p, x read and p, s, r, w, x written, the SpMV's own x
     // read / y write included: + 8 n vectors
-    // (RS: the fused launch writes no s: 1 vector less)
-    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : s->fuse == CGX_FUSE_RS ? 2.5 : 3.5) *
-                             A.n * sv;
+    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : 3.5) * A.n * sv;
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;

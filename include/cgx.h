@@ -206,11 +206,6 @@ int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
 #define CGX_FUSE_OFF  0
 #define CGX_FUSE_AUTO 1
 #define CGX_FUSE_ON   2
-/* CGX_FUSE_RS (single-GPU solver, HS): as ON, but the fused launch does not
- * store s = A p; the r update recomputes it from the stored p (the same
- * products in the same order, so x stays within rounding of the other
- * modes): 16 B per row of s traffic traded for a gathered p.  (CG1: = ON.) */
-#define CGX_FUSE_RS   3
 int  cgx_solver_set_fused(cgx_solver *s, int mode);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);

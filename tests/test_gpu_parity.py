@@ -784,35 +784,6 @@ def test_fused_cg1_step(shape):
     assert rel(x, x_o) <= 1e-9
 
 
-@pytest.mark.parametrize("shape", [(40, 30, 24), (12, 12, 12), (64, 48, 10)])
-def test_fused_rs_mode(shape):
-    """CGX_FUSE_RS: the fused launch stores no s and the r update recomputes
-    it from p_new (k_update_rs: the same products in the same order); only
-    the r.r partials are grouped differently, so x stays within 1e-12 of the
-    oracle's HS iteration and of the other modes, the stop iteration within
-    1 (graph batches of both parities)."""
-    rp, col, val = cgx.laplacian3d(*shape)
-    b = np.random.default_rng(21).standard_normal(len(rp) - 1)
-    res = {}
-    for mode in ("rs", True):
-        with cgx.Solver(0, fused=mode) as s:
-            s.set_matrix(rp, col, val)
-            assert s.info()["fused"] == 1
-            out = []
-            for maxit, tol in [(0, 0.0), (1, 0.0), (16, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]:
-                s.set_rhs(b)
-                its = s.run(maxit, tol)
-                out.append((its, s.x()))
-            res[mode] = out
-    for (i0, x0), (i1, x1) in zip(res["rs"][:-1], res[True][:-1]):
-        assert i0 == i1 and rel(x0, x1) <= 1e-12
-    x_ref, _ = H.o_conj_grad(40, rp, col, val, b)
-    assert rel(res["rs"][4][1], x_ref) <= FAST_RTOL
-    its, x = res["rs"][-1]
-    _, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
-    assert abs(its - its_o) <= 1 and its < 3000
-
-
 def test_fp32_solve_converges():
     rp, col, val = cgx.random_spd(50000, 16, 5, f32=True)
     b = np.random.default_rng(4).standard_normal(50000).astype(np.float32)
