@@ -1,25 +1,29 @@
 """Fused vs unfused iteration time on one GPU (cgx.Solver, graph-replayed,
 device-generated Laplacian), same box, same build, back to back; HS, or the
 CG1 recurrence with --cg1.
-  python tools/fused_probe.py [--cg1] [dim:nx[:ny:nz] ...]   default 3:216 3:400 (C3, C4); 2:1000 = C2"""
+  python tools/fused_probe.py [--cg1] [--modes=on,off,...] [dim:nx[:ny:nz] ...]   default 3:216 3:400 (C3, C4); 2:1000 = C2"""
 import sys
 sys.path.insert(0, "conjugate-gradient_amd")
 import numpy as np, cgx
 
-args = [a for a in sys.argv[1:] if a != "--cg1"]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
 alg = cgx.CGX_ALG_CG1 if "--cg1" in sys.argv else cgx.CGX_ALG_HS
+modes = [True, False, True, False]
+for a in sys.argv[1:]:
+    if a.startswith("--modes="):  # e.g. --modes=on,off,on,off (cgx.fuse_mode names)
+        modes = a.split("=", 1)[1].split(",")
 for spec in args or ["3:216", "3:400"]:
     v = [int(t) for t in spec.split(":")]
     dim, nx = v[0], v[1]
     ny, nz = (v[2], v[3]) if len(v) > 2 else (nx, nx if dim == 3 else 1)
     n = nx * ny * nz
-    for fused in (True, False, True, False):
+    for fused in modes:
         with cgx.Solver(0, alg=alg, fused=fused) as s:
             s.gen_laplacian(dim, nx, ny, nz)
             s.set_rhs(np.ones(n))
             s.bench_prepare(5)
             ms = s.bench_run(200)[0]
             _, sp = s.bench_run(30, graph=False, spmv_events=True)
-            print("%s %dD nx %d fused %d: %.1f us/iter, spmv launch %.1f us" %
-                  ("cg1" if alg else "hs", dim, nx, s.info()["fused"], 1e3 * ms / 200, 1e3 * sp),
-                  flush=True)
+            print("%s %dD nx %d mode %s fused %d: %.1f us/iter, spmv launch %.1f us" %
+                  ("cg1" if alg else "hs", dim, nx, fused, s.info()["fused"], 1e3 * ms / 200,
+                   1e3 * sp), flush=True)
