@@ -39,13 +39,20 @@ derived = []
 if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
     derived.append(("L2 hit rate", d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1)))
 if "GRBM_GUI_ACTIVE" in d:
-    cyc = d["GRBM_GUI_ACTIVE"]
+    # GRBM_GUI_ACTIVE comes summed over the 8 XCDs (checked on k_stream_read:
+    # 512 MiB in 1.82 M summed = 228 K cycles = 95 us at 2.4 GHz, 5.6 TB/s)
+    cyc = d["GRBM_GUI_ACTIVE"] / 8
+    derived.append(("GPU cycles (GRBM_GUI_ACTIVE / 8 XCDs)", cyc))
+    derived.append(("time at 2.4 GHz (us)", cyc / 2400.0))
     if "TCC_REQ_sum" in d:
-        derived.append(("L2 requests per GPU cycle (all 8 XCDs; 16 per XCD-cycle = 128)", d["TCC_REQ_sum"] / cyc))
+        derived.append(("L2 requests per XCD-cycle (16 channels: peak 16)", d["TCC_REQ_sum"] / 8 / cyc))
     if "TA_TA_BUSY_sum" in d:
-        derived.append(("TA busy fraction (per CU: TA_BUSY_sum / 256 CUs / cycles)", d["TA_TA_BUSY_sum"] / 256 / cyc))
+        derived.append(("TA busy fraction (TA_BUSY_sum / 256 CUs / cycles)", d["TA_TA_BUSY_sum"] / 256 / cyc))
     if "TA_ADDR_STALLED_BY_TC_CYCLES_sum" in d:
-        derived.append(("TA address stalled by TC (per CU fraction)", d["TA_ADDR_STALLED_BY_TC_CYCLES_sum"] / 256 / cyc))
+        derived.append(("TA address path stalled by the TC (fraction of cycles)",
+                        d["TA_ADDR_STALLED_BY_TC_CYCLES_sum"] / 256 / cyc))
+    if "TD_TD_BUSY_sum" in d:
+        derived.append(("TD busy fraction", d["TD_TD_BUSY_sum"] / 256 / cyc))
 if "TCP_TCC_READ_REQ_LATENCY_sum" in d and "TCP_TCC_READ_REQ_sum" in d:
     derived.append(("TCP->TCC read latency (cycles per request)",
                     d["TCP_TCC_READ_REQ_LATENCY_sum"] / max(d["TCP_TCC_READ_REQ_sum"], 1)))
