@@ -7,13 +7,20 @@ products + vector updates) on a synthetic SPD system already resident in HBM.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c4|c2|c5]
 
-N = 1 (default workload C3): the 7-point 3-D Laplacian 216^3 (10,077,696 rows,
-70,263,936 nnz, fp64, b = 1) -- BASELINE.json's HBM roofline configuration --
-in the layout libcgx picks for it, plus, in the same run, the same solve with
-the reference's plain CSR (SURVEY.md 8d's B_spmv: the north-star roofline
-figure), with dictionary-coded columns and matrix-free; C4 (64M rows) on this
-one GPU (the N = 1 point of the C4 strong-scaling curve); the end-to-end
-drop-in call solve(A, b, &x, 1e-8, maxit) through the C ABI; the CPU baseline.
+Every N runs the same workload (default C4), so the driver's per-N values form
+one strong-scaling curve and BASELINE.json's ">= 6x single-GPU CG it/s at 8
+GPUs" reads off it directly.
+
+N = 1 (default workload C4): the 7-point 3-D Laplacian 400^3 (64,000,000 rows,
+447,040,000 nnz, fp64, b = 1) on ONE GPU in the layout libcgx picks for it --
+the base of the curve; in the same run the same solve on the reference's plain
+CSR (SURVEY.md 8d's B_spmv: the roofline figure), with dictionary-coded
+columns and matrix-free; then C3 (216^3, 10,077,696 rows -- BASELINE.json's
+HBM roofline configuration, the north star's ">= 70 % on fp64 CSR SpMV for a
+10M-row 3-D Laplacian") in the picked layout and in plain CSR, C3's pattern
+with general coefficients, and the end-to-end drop-in call solve(A, b, &x,
+1e-8, maxit) through the C ABI; the CPU baseline on a bounded sample of the
+workload.  (--workload c3 makes C3 the timed line, as rounds 1-2 did.)
 
 N > 1 (default workload C4): one process per GPU.  Without WORLD_SIZE in the
 environment this script starts itself under torch.distributed.run as a child
@@ -89,7 +96,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
-                    help="default: c3 at N = 1, c4 at N > 1")
+                    help="default: c4 (every N: one strong-scaling curve)")
     ap.add_argument("--alg", default=None, choices=["hs", "cg1"],
                     help="N > 1: recurrence (default: a timed trial of both)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -98,7 +105,9 @@ def parse_args(argv=None):
                     help="at one rank (under torch.distributed.run --nproc-per-node 1): run the "
                          "N > 1 path -- parity gate, RCCL communicator, C4 -- on one GPU")
     ap.add_argument("--no-legs", action="store_true",
-                    help="N = 1: only the headline solve (no CSR/DC/stencil/C4/e2e legs)")
+                    help="N = 1: only the headline solve (no CSR/DC/stencil/C3/e2e legs)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "csr", "dc", "dia"],
+                    help="N = 1: the headline solve's layout (profiling one kernel)")
     return ap.parse_args(argv)
 
 
@@ -365,8 +374,101 @@ def c4_one_gpu(steps, warmup, device=0):
                      "base of the C4 strong-scaling curve (N > 1 lines run C4 across N ranks)")
 
 
+def headline_solve(sysm, steps, warmup, layout="auto"):
+    """The timed solve: upload (not timed), W warmup iterations, exactly K
+    graph-replayed iterations bracketed by device syncs, then K more with HIP
+    events around every SpMV launch (its average time in the iteration)."""
+    import torch
+    import cgx
+    t_up = time.perf_counter()
+    s = cgx.Solver(0, layout=layout)
+    try:
+        s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+        s.set_rhs(sysm["b"])
+        info = s.info()
+        upload_ms = 1e3 * (time.perf_counter() - t_up)
+        s.bench_prepare(warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev_ms = s.bench_run(steps, graph=True)[0]
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        _, spmv_ms = s.bench_run(steps, graph=False, spmv_events=True)
+    finally:
+        s.close()
+    return dict(info=info, upload_ms=upload_ms, wall=wall, dev_ms=dev_ms, spmv_ms=spmv_ms)
+
+
+def csr_roofline(csr, wl_name):
+    """SURVEY.md 8d's roofline figure: the plain-CSR SpMV on B_spmv = 12 nnz +
+    4 (n+1) + 16 n, in the CG iteration and back to back."""
+    ci = csr["info"]
+    c_gbs, c_frac = spmv_roofline(ci["spmv_bytes"], csr["spmv_us"] * 1e-3)
+    b_gbs, b_frac = spmv_roofline(ci["spmv_bytes"], csr["b2b_spmv_us"] * 1e-3)
+    return dict(
+        bound="hbm", achieved=c_gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=c_frac,
+        traffic=load_traffic(f"{wl_name}_csr"), kernel=KERNELS["csr"] + ", in the CG iteration",
+        basis="SURVEY.md 8d B_spmv = 12 nnz + 4 (n+1) + 16 n (CSR int32 col + fp64 val, "
+              "row_ptr, x read once, y written once)",
+        algorithmic_bytes_per_launch=int(ci["spmv_bytes"]), spmv_us=csr["spmv_us"],
+        csr=dict(frac=c_frac, achieved=c_gbs, spmv_us=csr["spmv_us"],
+                 b2b_spmv_us=csr["b2b_spmv_us"], b2b_achieved=b_gbs, b2b_frac=b_frac,
+                 cg_its=csr["value"], gathers_per_chunk=ci["gathers_per_chunk"],
+                 note="in_cg: average launch inside the CG iteration (HIP events); b2b: "
+                      "back-to-back y = A p launches (the standard SpMV benchmark, "
+                      "k_spmv_csr without the p.s epilogue)"))
+
+
+def layout_roofline(info, spmv_ms, wl_name):
+    """The picked layout's SpMV launch priced on the bytes it moves."""
+    gbs, frac = spmv_roofline(info["spmv_iter_bytes"], spmv_ms)
+    return dict(kernel=kernel_name(info), layout=layout_desc(info),
+                spmv_us=round(spmv_ms * 1e3, 2), achieved=gbs, frac=frac,
+                algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
+                traffic=load_traffic(wl_name),
+                csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
+                note="the SpMV launch of the headline solve, priced on the bytes it moves (its "
+                     "layout; with the fused HS step also r, p_old, x, p_new)")
+
+
+def matrix_free(wl, b, steps, warmup):
+    import cgx
+    dims = wl["dims"]
+    with cgx.Solver(0) as ms:
+        ms.set_stencil(3 if wl["kind"] == "lap3d" else 2, dims[0], dims[1],
+                       dims[2] if len(dims) > 2 else 1)
+        ms.set_rhs(b)
+        ms.bench_prepare(warmup)
+        mf_ms = ms.bench_run(steps, graph=True)[0]
+        _, mf_spmv = ms.bench_run(min(steps, 50), graph=False, spmv_events=True)
+    return dict(value=round(steps / (mf_ms * 1e-3), 2), unit="it/s",
+                spmv_us=round(mf_spmv * 1e3, 2), kernel=KERNELS["stencil"],
+                note="the same operator without a stored matrix (x and y only), run as the "
+                     "unfused three-launch iteration; NOT an upper bound: the fused DIA step "
+                     "of the headline moves fewer bytes per iteration")
+
+
+def c3_legs(steps, warmup):
+    """C3 inside a C4 line: BASELINE.json's HBM roofline configuration in the
+    picked layout and in plain CSR (the north star's 70 % figure), the general
+    coefficient matrix on its grid, and the end-to-end drop-in call."""
+    wl = WORKLOADS["c3"]
+    sysm = make_system(wl)
+    h = headline_solve(sysm, steps, warmup)
+    csr = solver_leg(sysm, steps, warmup, "csr", b2b=True)
+    out = dict(workload=wl["desc"], value=round(steps / h["wall"], 2), unit="it/s",
+               ms_per_step=round(1e3 * h["wall"] / steps, 4), layout=layout_desc(h["info"]),
+               layout_name=h["info"]["layout_name"],
+               default_layout=layout_roofline(h["info"], h["spmv_ms"], "c3"),
+               csr_roofline=csr_roofline(csr, "c3"),
+               csr_plain=dict(value=csr["value"], unit="it/s", spmv_us=csr["spmv_us"],
+                              b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"]))
+    out["general_coefficients"] = general_coefficients(steps, warmup)
+    out["solve_e2e"] = solve_e2e(sysm)
+    return out
+
+
 def run_single(args, wl_name):
-    import numpy as np
     import torch
     import cgx
 
@@ -376,26 +478,9 @@ def run_single(args, wl_name):
     torch.cuda.synchronize()
 
     # ---- headline: the layout libcgx picks (default path of the drop-in)
-    t_up = time.perf_counter()
-    s = cgx.Solver(0)
-    s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
-    s.set_rhs(sysm["b"])
-    info = s.info()
-    upload_ms = 1e3 * (time.perf_counter() - t_up)
-
-    # timed region: exactly K steps, sync on both sides
-    s.bench_prepare(args.warmup)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    dev_ms = s.bench_run(args.steps, graph=True)[0]
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
+    h = headline_solve(sysm, args.steps, args.warmup, args.layout)
+    info, spmv_ms, wall = h["info"], h["spmv_ms"], h["wall"]
     ms_per_step = 1e3 * wall / args.steps
-    # the SpMV's average launch time inside the iteration (HIP events on the
-    # solver's stream), K more iterations
-    _, spmv_ms = s.bench_run(args.steps, graph=False, spmv_events=True)
-    s.close()
-    head_gbs, head_frac = spmv_roofline(info["spmv_iter_bytes"], spmv_ms)
 
     legs = {}
     if not args.no_legs:
@@ -405,39 +490,17 @@ def run_single(args, wl_name):
             legs["dc"] = solver_leg(sysm, args.steps, args.warmup, "dc")
     csr = legs.get("csr")
 
-    # ---- roofline: SURVEY.md 8d's north-star figure, the plain-CSR SpMV on
-    # B_spmv = 12 nnz + 4 (n+1) + 16 n, in the CG iteration; the default
-    # layout's SpMV (its own bytes) beside it
+    # ---- roofline: the plain-CSR SpMV of the workload (SURVEY.md 8d basis),
+    # the picked layout's SpMV (its own bytes) beside it
     if csr is not None:
-        ci = csr["info"]
-        c_gbs, c_frac = spmv_roofline(ci["spmv_bytes"], csr["spmv_us"] * 1e-3)
-        b_gbs, b_frac = spmv_roofline(ci["spmv_bytes"], csr["b2b_spmv_us"] * 1e-3)
-        roofline = dict(
-            bound="hbm", achieved=c_gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=c_frac,
-            traffic=load_traffic(f"{wl_name}_csr"), kernel=KERNELS["csr"] + ", in the CG iteration",
-            basis="SURVEY.md 8d B_spmv = 12 nnz + 4 (n+1) + 16 n (CSR int32 col + fp64 val, "
-                  "row_ptr, x read once, y written once)",
-            algorithmic_bytes_per_launch=int(ci["spmv_bytes"]), spmv_us=csr["spmv_us"],
-            csr=dict(frac=c_frac, achieved=c_gbs, spmv_us=csr["spmv_us"],
-                     b2b_spmv_us=csr["b2b_spmv_us"], b2b_achieved=b_gbs, b2b_frac=b_frac,
-                     cg_its=csr["value"], gathers_per_chunk=ci["gathers_per_chunk"],
-                     note="in_cg: average launch inside the CG iteration (HIP events); b2b: "
-                          "back-to-back y = A p launches (the standard SpMV benchmark, "
-                          "k_spmv_csr without the p.s epilogue)"))
-        roofline["default_layout"] = dict(
-            kernel=kernel_name(info),
-            layout=layout_desc(info), spmv_us=round(spmv_ms * 1e3, 2), achieved=head_gbs,
-            frac=head_frac, algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
-            traffic=load_traffic(wl_name),
-            csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
-            note="the SpMV launch of the headline solve, priced on the bytes it moves (its "
-                 "layout; with the fused HS step also r, p_old, x, p_new)")
+        roofline = csr_roofline(csr, wl_name)
+        roofline["default_layout"] = layout_roofline(info, spmv_ms, wl_name)
     else:
-        roofline = dict(bound="hbm", achieved=head_gbs, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=head_frac, traffic=load_traffic(wl_name),
-                        kernel=kernel_name(info),
-                        algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
-                        spmv_us=round(spmv_ms * 1e3, 2))
+        lr = layout_roofline(info, spmv_ms, wl_name)
+        roofline = dict(bound="hbm", achieved=lr["achieved"], peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=lr["frac"], traffic=lr["traffic"], kernel=lr["kernel"],
+                        algorithmic_bytes_per_launch=lr["algorithmic_bytes_per_launch"],
+                        spmv_us=lr["spmv_us"])
     triad = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)
     rd = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_READ)
     roofline["stream_triad_gbs"] = round(triad, 1)
@@ -456,20 +519,9 @@ def run_single(args, wl_name):
                                       b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"],
                                       note="the same solve on the reference's CSR (layout csr)")
         if wl["kind"] in ("lap3d", "lap2d"):
-            dims = wl["dims"]
-            with cgx.Solver(0) as ms:
-                ms.set_stencil(3 if wl["kind"] == "lap3d" else 2, dims[0], dims[1],
-                               dims[2] if len(dims) > 2 else 1)
-                ms.set_rhs(sysm["b"])
-                ms.bench_prepare(args.warmup)
-                mf_ms = ms.bench_run(args.steps, graph=True)[0]
-                _, mf_spmv = ms.bench_run(min(args.steps, 50), graph=False, spmv_events=True)
-            extra["matrix_free"] = dict(
-                value=round(args.steps / (mf_ms * 1e-3), 2), unit="it/s",
-                spmv_us=round(mf_spmv * 1e3, 2), kernel=KERNELS["stencil"],
-                note="the same operator without a stored matrix (x and y only), run as the "
-                     "unfused three-launch iteration; NOT an upper bound: the fused DIA step "
-                     "of the headline moves fewer bytes per iteration")
+            extra["matrix_free"] = matrix_free(wl, sysm["b"], args.steps, args.warmup)
+        if wl_name == "c4":
+            extra["c3"] = c3_legs(args.steps, args.warmup)
         if wl_name == "c3":
             extra["general_coefficients"] = general_coefficients(args.steps, args.warmup)
             extra["c4_1gpu"] = c4_one_gpu(min(args.steps, 50), args.warmup)
@@ -491,9 +543,11 @@ def run_single(args, wl_name):
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz=int(len(sysm["col"])),
                     alg="hs (the reference recurrence, cg.c:88-141)", graph=True,
                     parallelism="single GPU", layout=layout_desc(info),
-                    layout_name=info["layout_name"]),
-        device_ms_per_step=round(dev_ms / args.steps, 4),
-        upload_ms=round(upload_ms, 1),  # host CSR -> HBM + layout encoding, not in `value`
+                    layout_name=info["layout_name"],
+                    scaling_curve="the same workload at every N (N > 1: row-partitioned "
+                                  "over RCCL), so value(N) / value(1) is the speedup"),
+        device_ms_per_step=round(h["dev_ms"] / args.steps, 4),
+        upload_ms=round(h["upload_ms"], 1),  # host CSR -> HBM + layout encoding, not in `value`
         iter_bytes=int(info["iter_bytes"]),
         roofline=roofline, cpu_baseline=cpu, **extra)
     print(json.dumps(out), flush=True)
@@ -662,9 +716,9 @@ def run_dist(args, wl_name, world, rank, local_rank):
                         nnz_rank0=info["nnz"], alg=alg, alg_trial_ms_per_iter=trial,
                         graph=info["graph"], fused=info["fused"],
                         parallelism=f"row-partition x{world} (RCCL)",
-                        scaling_base="the N = 1 point of this C4 curve is the N = 1 line's "
-                                     "c4_1gpu leg (same solver, one GPU); the N = 1 line's "
-                                     "value is C3",
+                        scaling_curve="the same workload at every N (N = 1: the "
+                                      "single-GPU solver), so value(N) / value(1) is the "
+                                      "speedup",
                         layout=info["layout_name"], halo_bytes_per_iter_max_rank=halo),
             device_ms_per_step=None if dev is None else round(dev, 4),
             upload_ms=round(upload_ms, 1), iter_bytes_rank0=int(info["iter_bytes"]),
@@ -687,7 +741,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist_path = world > 1 or args.dist_rehearsal
-    wl_name = args.workload or ("c4" if dist_path else "c3")
+    wl_name = args.workload or "c4"
     if not dist_path:
         run_single(args, wl_name)
     else:

@@ -60,12 +60,14 @@ def test_default_workloads():
     assert bench.WORKLOADS["c3"]["dims"] == (216, 216, 216)
 
 
-@pytest.mark.parametrize("argv,expect", [(["--gpus", "1"], ("single", "c3")),
+@pytest.mark.parametrize("argv,expect", [(["--gpus", "1"], ("single", "c4")),
+                                         (["--gpus", "1", "--workload", "c3"], ("single", "c3")),
                                          (["--gpus", "1", "--dist-rehearsal"], ("dist", "c4")),
                                          (["--gpus", "1", "--workload", "c2"], ("single", "c2"))])
 def test_rank_path_selection(monkeypatch, argv, expect):
-    """One rank runs the single-GPU line (C3) unless --dist-rehearsal asks for
-    the N > 1 path (C4 over a 1-rank RCCL communicator)."""
+    """Every N runs the same workload (C4: one strong-scaling curve); one rank
+    runs the single-GPU solver unless --dist-rehearsal asks for the N > 1
+    path (C4 over a 1-rank RCCL communicator)."""
     seen = {}
     monkeypatch.setenv("WORLD_SIZE", "1")
     monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
