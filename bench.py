@@ -97,8 +97,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c4 (every N: one strong-scaling curve)")
-    ap.add_argument("--alg", default=None, choices=["hs", "cg1"],
-                    help="N > 1: recurrence (default: a timed trial of both)")
+    ap.add_argument("--alg", default=None, choices=["hs", "sr", "cg1"],
+                    help="N > 1: recurrence (default: a timed trial of all three)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-rehearsal", action="store_true",
@@ -589,14 +589,16 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
         d.set_matrix(n, rp, col, val)
         d.set_rhs(b_full[rb:re_])
         # the fused HS step forced on: the timed C4 run takes it (auto), this
-        # small system would not
-        for name, alg, fused in (("hs", cgx.CGX_ALG_HS, False), ("hs_fused", cgx.CGX_ALG_HS, True),
-                                 ("cg1", cgx.CGX_ALG_CG1, False)):
+        # small system would not; SR is always the fused step
+        for name, alg, fused, want in (("hs", cgx.CGX_ALG_HS, False, 0),
+                                       ("hs_fused", cgx.CGX_ALG_HS, True, 1),
+                                       ("sr", cgx.CGX_ALG_SR, "auto", 1),
+                                       ("cg1", cgx.CGX_ALG_CG1, False, 0)):
             d.set_alg(alg)
             d.set_fused(fused)
             its = d.run(5000, tol)
             i = d.info()
-            res[name] = (its, gather_x(d.x(), n, world, rank), i["graph"], i["fused"] == int(fused))
+            res[name] = (its, gather_x(d.x(), n, world, rank), i["graph"], i["fused"] == want)
         d.set_fused("auto")
     finally:
         d.close()
@@ -661,11 +663,12 @@ def run_dist(args, wl_name, world, rank, local_rank):
     dist.barrier()
     upload_ms = 1e3 * (time.perf_counter() - t_up)
 
-    # ---- recurrence: HS pays two all-reduce latencies per iteration, CG1 one
-    # (and 8 B/row more traffic); a timed trial (max over ranks) picks
+    # ---- recurrence: HS pays two all-reduce latencies per iteration, SR and
+    # CG1 one (CG1 with 8-13 B/row more traffic); a timed trial (max over
+    # ranks) picks
     trial = {}
-    algs = {"hs": cgx.CGX_ALG_HS, "cg1": cgx.CGX_ALG_CG1}
-    for name in ([args.alg] if args.alg else ["hs", "cg1"]):
+    algs = {"hs": cgx.CGX_ALG_HS, "sr": cgx.CGX_ALG_SR, "cg1": cgx.CGX_ALG_CG1}
+    for name in ([args.alg] if args.alg else ["hs", "sr", "cg1"]):
         s.set_alg(algs[name])
         s.bench_prepare(3)
         dist.barrier()

@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ["CGX_LIB"]) if os.environ.get("CGX_LIB") else HERE / 
 
 CGX_EINVAL, CGX_ENODEV, CGX_ENOMEM, CGX_ECOMM = -1, -2, -3, -4
 CGX_MODE_FAST, CGX_MODE_EXACT = 0, 1
-CGX_ALG_HS, CGX_ALG_CG1 = 0, 1
+CGX_ALG_HS, CGX_ALG_CG1, CGX_ALG_SR = 0, 1, 2
 CGX_F64, CGX_F32 = 0, 1
 CGX_BENCH_GRAPH, CGX_BENCH_SPMV_EVENTS, CGX_BENCH_SPMV_ONLY = 1, 2, 4
 (CGX_LAYOUT_AUTO, CGX_LAYOUT_CSR, CGX_LAYOUT_DC, CGX_LAYOUT_DIA, CGX_LAYOUT_PANEL,
@@ -670,7 +670,8 @@ class DistSolver:
         check(lib().cgx_dist_set_rhs(self._h, _p(b, _f64p)), "dist_set_rhs")
 
     def set_alg(self, alg):
-        """CGX_ALG_HS (default, two all-reduces) or CGX_ALG_CG1 (one)."""
+        """CGX_ALG_HS (default, two all-reduces), CGX_ALG_CG1 (one) or
+        CGX_ALG_SR (HS with one all-reduce; needs the fused DIA step)."""
         check(lib().cgx_dist_set_alg(self._h, alg), "dist_set_alg")
 
     def set_layout(self, layout):

@@ -28,6 +28,13 @@
 //                (ghost diagonals read the received p_new) -> local p.s
 //                ncclAllReduce(p.s); k_update_rf -> ncclAllReduce(r.r)
 //                -- two launches and one pack per iteration instead of four
+//   SR  (single reduction; the fused step only): the fused HS iteration with
+//       the s.s partials beside p.s in the fused launch; ONE all-reduce of
+//       (p.s, s.s, r.r) -- r.r the exact local sum of the last r update's
+//       partials -- then k_update_rf takes alpha = r.r / p.s (cg.c:113) and
+//       writes r_new.r_new = alpha^2 s.s - r.r (r.s = p.s) for beta
+//       (cg.c:129) and the stop test: HS's bytes, one all-reduce latency per
+//       iteration instead of two, rounding-level different from HS.
 //   CG1 (Chronopoulos-Gear): ONE all-reduce of (gamma, delta) per iteration,
 //       rounding-level different from HS, 8 B per row more vector traffic;
 //       fused (CGX_FUSE_ON only): k_cg1_dia_h does the vector recurrences
@@ -109,7 +116,8 @@ struct cgx_dist {
   std::vector<int> send_count, send_off, recv_count, recv_off;
   int n_send = 0;
   double *d_pa = nullptr, *d_pb = nullptr;
-  double *d_sums = nullptr, *d_gsums = nullptr;  // [0, 1] local, [2, 3] all-reduced
+  double *d_pss = nullptr;  // SR: the fused launches' s.s partials (d_pb's offsets)
+  double *d_sums = nullptr, *d_gsums = nullptr;  // [0, 4) local, [4, 8) all-reduced
   unsigned *d_tick = nullptr;                    // last-arriver counters
   int vec_grid = 1;
   CgState *d_st = nullptr, *h_st = nullptr;
@@ -162,7 +170,9 @@ void drop_graph(cgx_dist *d) {
 
 // The fused HS step (k_spmv_dia_h) runs when every partition's layout
 // takes it (decided once per connection: the ranks' phase sequences match).
-bool fz(const cgx_dist *d) { return d->fz_all && d->alg == CGX_ALG_HS; }
+// SR is the fused step with one reduction.
+bool fz(const cgx_dist *d) { return d->fz_all && (d->alg == CGX_ALG_HS || d->alg == CGX_ALG_SR); }
+bool sr(const cgx_dist *d) { return d->alg == CGX_ALG_SR; }
 // The fused CG1 step (k_cg1_dia_h): only when forced on (CGX_FUSE_ON) --
 // on a rank's slab it loses to the unfused CG1 kernels (C4/8's 400 x 400 x
 // 50 slab: 164 vs 144 us per iteration, tools/dist_probe.py: the unfused
@@ -173,9 +183,10 @@ bool fz1(const cgx_dist *d) {
 }
 
 // this partition takes the fused step (cgx_solver.cpp fused(): auto needs a
-// working set beyond the Infinity Cache)
+// working set beyond the Infinity Cache; SR has no unfused form)
 bool part_fusable(const cgx_dist *d) {
-  return d->fuse != CGX_FUSE_OFF && d->A.fusable() && (d->fuse == CGX_FUSE_ON || d->A.nt);
+  return d->fuse != CGX_FUSE_OFF && d->A.fusable() &&
+         (d->fuse == CGX_FUSE_ON || d->A.nt || sr(d));
 }
 
 void free_system(cgx_dist *d) {
@@ -197,6 +208,7 @@ void free_system(cgx_dist *d) {
   dev_free(&d->d_sendbuf);
   dev_free(&d->d_pa);
   dev_free(&d->d_pb);
+  dev_free(&d->d_pss);
   dev_free(&d->d_hist);
   d->hist_alloc = 0;
   if (d->part) cgx_part_destroy(d->part);
@@ -229,13 +241,13 @@ int init_common(cgx_dist *d, int device) {
   CGX_HIP(hipEventCreateWithFlags(&d->ev_sums2, hipEventDisableTiming));
   CGX_HIP(hipEventCreateWithFlags(&d->ev_red, hipEventDisableTiming));
   CGX_HIP(hipMalloc((void **)&d->d_st, sizeof(CgState)));
-  CGX_HIP(hipMalloc((void **)&d->d_sums, 4 * sizeof(double)));
-  CGX_HIP(hipMemset(d->d_sums, 0, 4 * sizeof(double)));
+  CGX_HIP(hipMalloc((void **)&d->d_sums, 8 * sizeof(double)));
+  CGX_HIP(hipMemset(d->d_sums, 0, 8 * sizeof(double)));
   // the ticket region of k_update_rf's local r.r sums
   CGX_HIP(hipMalloc((void **)&d->d_tick, kTickRegion * sizeof(unsigned)));
   CGX_HIP(hipMemset(d->d_tick, 0, kTickRegion * sizeof(unsigned)));
   CGX_HIP(hipHostMalloc((void **)&d->h_st, sizeof(CgState), hipHostMallocDefault));
-  d->d_gsums = d->d_sums + 2;
+  d->d_gsums = d->d_sums + 4;
   return 0;
 }
 
@@ -318,7 +330,8 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
       (rc = dev_alloc(&d->d_p2, ng * 8, cb)) || (rc = dev_alloc(&d->d_r2, ng * 8, cb)) ||
       (rc = dev_alloc(&d->d_s2, ng * 8, cb)) || (rc = dev_alloc(&d->d_w2, ng * 8, cb)) ||
       (rc = dev_alloc(&d->d_pa, npa * 8, cb)) ||
-      (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb))) {
+      (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb)) ||
+      (rc = dev_alloc(&d->d_pss, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb))) {
     free_system(d);
     return rc;
   }
@@ -469,7 +482,20 @@ int ensure_fused_known(Group *g) {
   return 0;
 }
 
+int ensure_connected_fz(Group *g);
+
+// connected, the fused step decided, and the recurrence runnable on it
 int ensure_connected(Group *g) {
+  int rc = ensure_connected_fz(g);
+  if (rc) return rc;
+  if (sr(g->parts[0]) && !g->parts[0]->fz_all) {
+    set_error("dist: CGX_ALG_SR needs the fused DIA step on every partition (fuse_status)");
+    return CGX_EINVAL;
+  }
+  return 0;
+}
+
+int ensure_connected_fz(Group *g) {
   if (!g->connected) {
     for (cgx_dist *d : g->parts)
       if (!d->have_matrix) {
@@ -501,8 +527,11 @@ double *spmv_x(cgx_dist *d) {
   if (d->alg != CGX_ALG_HS) return fz1(d) ? r_new(d) : d->d_r;
   return fz(d) ? p_new(d) : d->d_p;
 }
-// r.r of the last r update, as the fused step reads it
-const double *rr_new_src(cgx_dist *d) { return solo(d) ? &d->d_st->rr_new : d->d_gsums + 1; }
+// r.r of the last r update, as the fused step reads it (SR: k_update_rf's
+// alpha^2 s.s - r.r)
+const double *rr_new_src(cgx_dist *d) {
+  return solo(d) || sr(d) ? &d->d_st->rr_new : d->d_gsums + 1;
+}
 double *spmv_y(cgx_dist *d) {
   return d->alg == CGX_ALG_HS ? d->d_s : fz1(d) ? w_new(d) : d->d_w;
 }
@@ -605,7 +634,8 @@ int phase_spmv(cgx_dist *d) {
       // items (e == 2) read ghost columns' p_new from the halo
       const int pub = (e == 0 || d->it_int.count == 0) ? 1 : 0;
       const FuseArgs<double> f{d->d_x, p_old(d), p_new(d), d->d_r, d->d_st, d->d_hist,
-                               rr_new_src(d), pub, e == 2 ? 1 : 0};
+                               rr_new_src(d), pub, e == 2 ? 1 : 0,
+                               sr(d) ? d->d_pss + (part - d->d_pb) : nullptr};
       return launch_spmv_fused<double>(a, f, d->st, ev);
     }
     return launch_spmv<double>(a, d->st, ev);
@@ -614,7 +644,7 @@ int phase_spmv(cgx_dist *d) {
   if (has_peers(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
   CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, 2));
   if (rec) d->ev_i += 4;
-  if (solo(d)) return 0;
+  if (solo(d) && !sr(d)) return 0;
   // local transport: every part's group sum of the last reduction must have
   // read this part's local sums before they are overwritten.  The halo orders
   // this part only after its NEIGHBOURS' packs, so without the wait a part
@@ -624,7 +654,10 @@ int phase_spmv(cgx_dist *d) {
   if (d->local)
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
-  if (d->alg == CGX_ALG_HS)
+  if (sr(d))  // p.s, s.s, and r.r of the last r update (the prologue's b.b at first)
+    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pb, np, d->d_pss, np, d->d_st, d->d_hist, d->d_sums,
+                            d->st, d->d_pa, d->vec_grid));
+  else if (d->alg == CGX_ALG_HS)
     CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
                             d->st));
   else
@@ -679,6 +712,17 @@ int hs_init_reduce(cgx_dist *d) {
 int hs_alpha(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const int gf = d->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
+  if (sr(d)) {
+    // the iteration's one all-reduce: (p.s, s.s, r.r); the r.r partials of
+    // this update stay local until the next iteration's finalize
+    if (!solo(d)) {
+      int rc = allreduce(d, 0, 3);
+      if (rc) return rc;
+    }
+    CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, nullptr, 0, d->d_pa, gf,
+                                     d->st, nullptr, solo(d) ? d->d_sums : d->d_gsums));
+    return 0;
+  }
   if (solo(d)) {
     const FinArgs fin{d->d_tick, d->d_pa, 4 * gf, &d->d_st->rr_new};
     CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, d->d_pb,
@@ -746,7 +790,7 @@ int cg1_reduce(cgx_dist *d, bool init) {
 // fused: the all-reduce of the local r.r (the next iteration's beta), and
 // the p buffers swap roles
 int fz_close(cgx_dist *d) {
-  if (!solo(d)) {
+  if (!solo(d) && !sr(d)) {
     int rc = allreduce(d, 1, 1);
     if (rc) return rc;
   }
@@ -1207,7 +1251,8 @@ int cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms, doub
 }
 
 int cgx_dist_set_alg(cgx_dist *d, int alg) {
-  if (!d || (alg != CGX_ALG_HS && alg != CGX_ALG_CG1) || (d->local && !d->owns_group))
+  if (!d || (alg != CGX_ALG_HS && alg != CGX_ALG_CG1 && alg != CGX_ALG_SR) ||
+      (d->local && !d->owns_group))
     return CGX_EINVAL;
   for (cgx_dist *o : d->group->parts) {
     if (o->alg != alg && o->gexec[0]) {  // a captured graph holds the other recurrence
@@ -1217,6 +1262,7 @@ int cgx_dist_set_alg(cgx_dist *d, int alg) {
     o->alg = alg;
     o->bench_ready = false;
   }
+  d->group->fz_known = false;  // part_fusable depends on the recurrence (SR)
   return 0;
 }
 

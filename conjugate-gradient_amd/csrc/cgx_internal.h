@@ -93,6 +93,7 @@ enum FinOp {
   FIN_CG1 = 4,       // gamma' = sum(a), delta = sum(b); stop test; alpha, beta
   FIN_SUM = 5,       // out[0] = sum(a) (op-level dot, local sums)
   FIN_SUM2 = 6,      // out[0] = sum(a), out[1] = sum(b)
+  FIN_SUM3 = 7,      // out[0..2] = sum(a), sum(b), sum(c) (SR local sums)
 };
 
 constexpr int kVecBS = 256;
@@ -258,6 +259,8 @@ struct FuseArgs {
   const double *rr_new;  // r.r of the last r update (&st->rr_new, or all-reduced)
   int publish;           // this launch's workgroup 0 writes the scalar state back
   int ghost;             // columns >= n are ghosts: p_new from pnew's ghost tail
+  double *ss;            // CGX_ALG_SR: the s.s partials beside a.part's p.s ones
+                         // (same offsets; nullptr: none)
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
@@ -323,10 +326,13 @@ hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
 // folded HS steps (alpha / beta computed inside from the producer's partials)
 // fin (optional): the r.r partials' canonical sum to fin->out[0] by the last
 // workgroup (fin->pa must be rr_part, fin->na = 4 * grid)
+// sr (CGX_ALG_SR): the reduced (p.s, s.s, r.r) -- alpha = r.r / p.s from
+// them instead of ps_part and rr_x, and r_new.r_new = alpha^2 s.s - r.r to
+// st->rr_new for the next fused launch's beta and stop test
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
-                            const FinArgs *fin = nullptr);
+                            const FinArgs *fin = nullptr, const double *sr = nullptr);
 // p -> pn (pn == p: in place, x every iteration; pn != p: x every other
 // iteration, k_xpay_xf)
 template <typename T>
@@ -345,7 +351,8 @@ template <typename T>
 hipError_t launch_dot_part(int n, const T *a, const T *b, double *part, int grid,
                            hipStream_t st);
 hipError_t launch_finalize(int op, const double *pa, int na, const double *pb, int nb,
-                           CgState *stt, double *hist, double *out, hipStream_t st);
+                           CgState *stt, double *hist, double *out, hipStream_t st,
+                           const double *pc = nullptr, int nc = 0);
 // Elementwise ops of the mv_ops API: op 0: r = s*a, 1: r = a+b, 2: r = a-b
 template <typename T>
 hipError_t launch_axpby(int op, int n, double s, const T *a, const T *b, T *r, int grid,

@@ -166,6 +166,28 @@ __device__ __forceinline__ void epi_store(double dot, double *part) {
   }
 }
 
+// Two partials per workgroup (CGX_ALG_SR's fused step: p.s and s.s), each
+// summed exactly as epi_store sums one.
+template <int WPB>
+__device__ __forceinline__ void epi_store2(double dot, double dot2, double *part, double *part2) {
+  __shared__ double red2[2][WPB];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  dot = wave_sum(dot);
+  dot2 = wave_sum(dot2);
+  if (lane == 0) {
+    red2[0][wid] = dot;
+    red2[1][wid] = dot2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const double *rw = red2[threadIdx.x];
+    double s = rw[0];
+#pragma unroll
+    for (int w = 1; w < WPB; ++w) s = s + rw[w];
+    (threadIdx.x == 0 ? part : part2)[blockIdx.x] = s;
+  }
+}
+
 // The scalar lines of the recurrence (cg.c:113, 125-129; CG1 analogues) on
 // the reduced sums sa, sb -- run by ONE thread (k_finalize).
 __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *hist,
@@ -175,6 +197,10 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
       out[0] = sa;
       break;
     case FIN_SUM2:
+      out[0] = sa;
+      out[1] = sb;
+      break;
+    case FIN_SUM3:  // out[2] written by k_finalize
       out[0] = sa;
       out[1] = sb;
       break;
@@ -845,14 +871,21 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   }
   const T pn0 = win[rw], pn1 = win[rw + 1];
   st_pair(a.y, r, a.n, a0, a1, NT);
-  double dot = 0.0;
+  double dot = 0.0, dot2 = 0.0;
   if (r < a.n) {
     st_pair(f.pnew, r, a.n, pn0, pn1, false);
     if (xup) x_update();
     dot = (double)pn0 * (double)a0;
     if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
+    if (f.ss) {
+      dot2 = (double)a0 * (double)a0;
+      if (r + 1 < a.n) dot2 = dot2 + (double)a1 * (double)a1;
+    }
   }
-  epi_store<4>(dot, a.part);
+  if (f.ss)  // uniform
+    epi_store2<4>(dot, dot2, a.part, f.ss);
+  else
+    epi_store<4>(dot, a.part);
 }
 
 // ---------------------------------------- fused CG1 step (DIA-VI)
@@ -1376,7 +1409,7 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
                                                        CgState *__restrict__ st,
                                                        const double *__restrict__ ps_part,
                                                        int nps, double *__restrict__ rr_part,
-                                                       FinArgs fin) {
+                                                       FinArgs fin, const double *sr) {
   __shared__ double red[kFoldBS / kWave];
   __shared__ double bcast;
   const int done = st->done;
@@ -1393,9 +1426,11 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
     rv0 = reinterpret_cast<const V *>(r)[gid];
     sv0 = reinterpret_cast<const V *>(s)[gid];
   }
-  const double ps = sum_parts<kFoldBS>(ps_part, nps, red);
+  // CGX_ALG_SR: p.s, s.s and the exact r.r of the current r come reduced
+  // together (one all-reduce); r_new.r_new = alpha^2 s.s - r.r (r.s = p.s)
+  const double ps = sr ? sr[0] : sum_parts<kFoldBS>(ps_part, nps, red);
   if (threadIdx.x == 0) {
-    const double rr = st->rr_x;
+    const double rr = sr ? sr[2] : st->rr_x;
     const double alpha = rr / ps;  // cg.c:113
     bcast = alpha;
     if (blockIdx.x == 0) {
@@ -1404,6 +1439,11 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
       st->rr_u = rr;
       st->k_u = st->k_x;
       if (!(ps > 0.0) && st->brk == 0) st->brk = st->k_x + 1;  // p.s <= 0: NaN follows
+      if (sr) {
+        const double as = alpha * sr[1];
+        const double e = alpha * as - rr;
+        st->rr_new = e > 0.0 ? e : 0.0;  // cancellation below 0: converged (beta 0)
+      }
     }
   }
   __syncthreads();
@@ -1699,13 +1739,17 @@ __global__ __launch_bounds__(BS) void k_dot_part(int n, const T *__restrict__ a,
 template <int BS>
 __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int na,
                                                  const double *pb, int nb, CgState *st,
-                                                 double *hist, double *out) {
+                                                 double *hist, double *out, const double *pc,
+                                                 int nc) {
   __shared__ double red[BS / kWave];
-  double sa, sb = 0.0;
+  double sa, sb = 0.0, sc = 0.0;
   if (pb) sum_parts2<BS>(pa, na, pb, nb, red, sa, sb);
   else sa = sum_parts<BS>(pa, na, red);
+  if (pc) sc = sum_parts<BS>(pc, nc, red);
   if (threadIdx.x != 0) return;
-  if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_INIT_HS && op != FIN_INIT_CG1 && st->done)
+  if (op == FIN_SUM3) out[2] = sc;
+  if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_SUM3 && op != FIN_INIT_HS &&
+      op != FIN_INIT_CG1 && st->done)
     return;
   apply_fin(op, sa, sb, st, hist, out);
 }
@@ -2143,10 +2187,10 @@ hipError_t launch_pack_pnext(int n_send, const int *idx, const T *r, const T *po
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
-                            const FinArgs *fin) {
+                            const FinArgs *fin, const double *sr) {
   const FinArgs f = fin ? *fin : FinArgs{};
   hipLaunchKernelGGL((k_update_rf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt, ps_part,
-                     nps, rr_part, f);
+                     nps, rr_part, f, sr);
   return hipGetLastError();
 }
 
@@ -2181,9 +2225,10 @@ hipError_t launch_dot_part(int n, const T *a, const T *b, double *part, int grid
 }
 
 hipError_t launch_finalize(int op, const double *pa, int na, const double *pb, int nb,
-                           CgState *stt, double *hist, double *out, hipStream_t st) {
+                           CgState *stt, double *hist, double *out, hipStream_t st,
+                           const double *pc, int nc) {
   hipLaunchKernelGGL((k_finalize<kFinBS>), dim3(1), dim3(kFinBS), 0, st, op, pa, na, pb, nb, stt,
-                     hist, out);
+                     hist, out, pc, nc);
   return hipGetLastError();
 }
 
@@ -2265,7 +2310,8 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template hipError_t launch_pack_rnext<T>(int, const int *, const T *, const T *, const T *,    \
                                            T *, const CgState *, hipStream_t);                   \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
-                                          double *, int, hipStream_t, const FinArgs *);          \
+                                          double *, int, hipStream_t, const FinArgs *,           \
+                                          const double *);                                       \
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \
                                         const double *, int, double *, int, hipStream_t);        \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *, const T *, const CgState *,  \

@@ -308,7 +308,7 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     // (cg.c:111-132)
     T *pold = (T *)(s->pbuf ? s->d_p2 : s->d_p), *pnew = (T *)(s->pbuf ? s->d_p : s->d_p2);
     const SpmvArgs<T> a = s->A.args<T>(nullptr, sv, s->d_pa, &s->d_st->done, s->A.all_items());
-    const FuseArgs<T> f{x, pold, pnew, r, s->d_st, s->d_hist, &s->d_st->rr_new, 1, 0};
+    const FuseArgs<T> f{x, pold, pnew, r, s->d_st, s->d_hist, &s->d_st->rr_new, 1, 0, nullptr};
     np = s->A.partials(s->A.all_items());
     CGX_HIP(launch_spmv_fused<T>(a, f, st, LaunchEv{ev0, ev1}));
     const int gf = s->vec_grid / 4;

@@ -105,7 +105,8 @@ typedef struct cgx_solver cgx_solver;
 enum { CGX_MODE_FAST = 0,    /* two-stage parallel reductions (default)      */
        CGX_MODE_EXACT = 1 }; /* sequential dots: reference bit order          */
 enum { CGX_ALG_HS = 0,       /* Hestenes-Stiefel, the reference recurrence    */
-       CGX_ALG_CG1 = 1 };    /* Chronopoulos-Gear, one fused reduction/iter   */
+       CGX_ALG_CG1 = 1,      /* Chronopoulos-Gear, one fused reduction/iter   */
+       CGX_ALG_SR = 2 };     /* HS with one reduction/iter (cgx_dist only)   */
 enum { CGX_F64 = 0, CGX_F32 = 1 };
 
 /* Device layout of the matrix the SpMV streams (the C ABI always takes the
@@ -385,10 +386,16 @@ int  cgx_dist_set_matrix(cgx_dist *d, long long n_global, int n_loc, int nnz,
 int  cgx_dist_set_rhs(cgx_dist *d, const double *b_local);
 /* Recurrence: CGX_ALG_HS (default; the reference's cg.c:88-141 recurrence:
  * two all-reduces of one double per iteration, bit-identical to the
- * single-GPU solver at one rank) or CGX_ALG_CG1 (Chronopoulos-Gear: ONE
- * all-reduce of two doubles, 8 bytes per row more vector traffic).  Every
- * rank (every part of a local group) must use the same one; on a local
- * group, setting it on part 0 sets the group. */
+ * single-GPU solver at one rank), CGX_ALG_CG1 (Chronopoulos-Gear: ONE
+ * all-reduce of two doubles, 8 bytes per row more vector traffic) or
+ * CGX_ALG_SR (the HS recurrence with ONE all-reduce of three doubles and HS's
+ * bytes: p.s, s.s and the exact r.r of the last r update are reduced
+ * together; alpha = r.r / p.s as in cg.c:113, while beta (cg.c:129) and the
+ * stop test use r_new.r_new = alpha^2 s.s - r.r, exact in exact arithmetic
+ * since r.s = p.s; rounding-level different from HS, tolerance parity.
+ * Needs the fused DIA step on every partition: run / bench_prepare return
+ * CGX_EINVAL otherwise).  Every rank (every part of a local group) must use
+ * the same one; on a local group, setting it on part 0 sets the group. */
 int  cgx_dist_set_alg(cgx_dist *d, int alg);
 /* The fused HS step (cgx_solver_set_fused modes) on all ranks or none --
  * agreed collectively at the next run / bench_prepare: the halo carries

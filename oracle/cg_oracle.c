@@ -212,6 +212,64 @@ int oracle_solve_cg1(int maxit, double tol, int n, const int *row_ptr,
   return k + 1;
 }
 
+/* The single-reduction HS variant of the partitioned solver (CGX_ALG_SR):
+ * cg.c:88-141's recurrence with p.s, s.s and r.r computed together (one
+ * all-reduce on the GPUs).  alpha = r.r / p.s exactly as cg.c:113; beta
+ * (cg.c:129) and the stop test (cg.c:125 position) use
+ * r_new.r_new = alpha (alpha s.s) - r.r (clamped at 0), which equals the
+ * exact r_new.r_new in exact arithmetic because r.s = p.s; the exact r_new.r_new
+ * becomes the next alpha's numerator.  rr_hist records the estimate (what the
+ * stop test saw), as the GPU solver's history does. */
+int oracle_solve_sr(int maxit, double tol, int n, const int *row_ptr,
+                    const int *col, const double *val, const double *b,
+                    double *x, double *rr_hist)
+{
+  size_t bytes = (size_t)(n > 0 ? n : 1) * sizeof(double);
+  double *r = (double *)malloc(bytes), *p = (double *)malloc(bytes);
+  double *s = (double *)malloc(bytes);
+  if (!r || !p || !s) {
+    free(r); free(p); free(s);
+    return -1;
+  }
+  memset(x, 0, (size_t)n * sizeof(double));
+  memcpy(r, b, (size_t)n * sizeof(double));
+  memcpy(p, r, (size_t)n * sizeof(double));
+  double bb = oracle_dot(n, b, b);
+  double rr = bb;
+  double tol2bb = tol * tol * bb;
+  int k = 0;
+  for (;;) {
+    oracle_spmv_csr(n, row_ptr, col, val, p, s);
+    double ps = oracle_dot(n, p, s), ss = oracle_dot(n, s, s);
+    double alpha = rr / ps;
+    for (int i = 0; i < n; i++) {
+      double ap = alpha * p[i];
+      x[i] = x[i] + ap;
+      double as = alpha * s[i];
+      r[i] = r[i] - as;
+    }
+    double as2 = alpha * ss;
+    double est = alpha * as2 - rr;
+    if (!(est > 0.0))
+      est = 0.0;
+    if (rr_hist)
+      rr_hist[k] = est;
+    if (k == maxit)
+      break;
+    if (tol > 0.0 && est <= tol2bb)
+      break;
+    double beta = est / rr;
+    for (int i = 0; i < n; i++) {
+      double bp = beta * p[i];
+      p[i] = r[i] + bp;
+    }
+    rr = oracle_dot(n, r, r);
+    k++;
+  }
+  free(r); free(p); free(s);
+  return k + 1;
+}
+
 int oracle_spmv_csr_f32(int n, const int *row_ptr, const int *col,
                         const float *val, const float *x, float *y)
 {

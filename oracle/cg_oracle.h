@@ -73,6 +73,13 @@ int oracle_solve_cg1(int maxit, double tol, int n, const int *row_ptr,
                      const int *col, const double *val, const double *b,
                      double *x, double *rr_hist);
 
+/* The partitioned solver's single-reduction HS variant (CGX_ALG_SR): alpha
+ * as cg.c:113, beta and the stop test from alpha^2 s.s - r.r.  Same stopping
+ * rule as oracle_solve; rounding-level different from it. */
+int oracle_solve_sr(int maxit, double tol, int n, const int *row_ptr,
+                    const int *col, const double *val, const double *b,
+                    double *x, double *rr_hist);
+
 /* Same CSR SpMV with fp32 values and vectors, fp32 products and row sums
  * (the C5 fp32 configuration; the reference itself is fp64 only,
  * mv_ops.h:20). */

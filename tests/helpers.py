@@ -254,6 +254,7 @@ def oracle():
     lib.oracle_solve.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                  _i32p, _i32p, _f64p, _f64p, _f64p, _f64p]
     lib.oracle_solve_cg1.argtypes = lib.oracle_solve.argtypes
+    lib.oracle_solve_sr.argtypes = lib.oracle_solve.argtypes
     lib.oracle_spmv_csr_f32.argtypes = [ctypes.c_int, _i32p, _i32p, _f32p,
                                         _f32p, _f32p]
     lib.oracle_solve_mt.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int,
@@ -312,11 +313,12 @@ def o_conj_grad(max_iter, rp, col, val, b, dense_expand=False):
     return x, hist
 
 
-def o_solve(maxit, tol, rp, col, val, b, cg1=False):
+def o_solve(maxit, tol, rp, col, val, b, cg1=False, sr=False):
     n = len(rp) - 1
     x = np.empty(n, np.float64)
     hist = np.zeros(maxit + 1, np.float64)
-    fn = oracle().oracle_solve_cg1 if cg1 else oracle().oracle_solve
+    fn = (oracle().oracle_solve_cg1 if cg1 else oracle().oracle_solve_sr if sr
+          else oracle().oracle_solve)
     its = fn(maxit, tol, n, _p(rp, _i32p), _p(col, _i32p), _p(val, _f64p),
              _p(b, _f64p), _p(x, _f64p), _p(hist, _f64p))
     return x, its, hist[:its]

@@ -4,8 +4,10 @@ then runs the distributed recurrence with the same communication pattern as
 the GPU solver -- Chronopoulos-Gear: halo of r point-to-point, ONE all-reduce
 of (gamma, delta) per iteration; HS: halo of p, one all-reduce of p.s and one
 of r.r; fused HS: the halo carries p_new = r + beta p_old computed at the send
-rows, x updated in pairs -- and the gathered x is checked against the serial
-oracle (fused HS: bit-identical to the HS protocol's)."""
+rows, x updated in pairs; SR: the fused HS protocol with ONE all-reduce of
+(p.s, s.s, r.r) per iteration, beta and the stop test from alpha^2 s.s - r.r --
+and the gathered x is checked against the serial oracle (fused HS:
+bit-identical to the HS protocol's; SR: against oracle_solve_sr)."""
 import os
 import socket
 
@@ -109,6 +111,44 @@ def _worker(rank, world, port, kind, out_path, alg="cg1"):
         return np.concatenate([own, ext])
 
     maxit, tol = 500, 1e-10
+    if alg == "sr":  # cgx_dist.cpp's CGX_ALG_SR: one all-reduce per iteration
+        def allreduce3(a, c, e):
+            t = torch.tensor([a, c, e], dtype=torch.float64)
+            dist.all_reduce(t)
+            return float(t[0]), float(t[1]), float(t[2])
+        x = np.zeros(n_loc)
+        r = b.copy()
+        rr_loc = float(np.dot(r, r))      # the prologue's local b.b
+        t = torch.tensor([rr_loc], dtype=torch.float64)
+        dist.all_reduce(t)
+        bb = float(t[0])
+        k, beta, first, p_old = 0, 0.0, True, None
+        while True:
+            if first:
+                p_new = r.copy()
+                ext = halo_vals(lambda idx: r[idx], p_new)
+            else:
+                p_new = r + beta * p_old
+                ext = halo_vals(lambda idx: r[idx] + beta * p_old[idx], p_new)
+            s = H.o_spmv(rp, lcol, val, ext)
+            ps, ss, rr = allreduce3(float(np.dot(p_new, s)), float(np.dot(s, s)), rr_loc)
+            alpha = rr / ps
+            x = x + alpha * p_new
+            r = r - alpha * s
+            rr_loc = float(np.dot(r, r))  # reduced with the next p.s, s.s
+            est = max(alpha * (alpha * ss) - rr, 0.0)
+            if k == maxit or est <= tol * tol * bb:
+                break
+            beta, first = est / rr, False
+            p_old = p_new
+            k += 1
+        xs = [None] * world
+        dist.all_gather_object(xs, x.tolist())
+        if rank == 0:
+            np.save(out_path, np.array(sum(xs, [])))
+            np.save(out_path + ".its.npy", np.array([k + 1]))
+        dist.destroy_process_group()
+        return
     if alg == "hs_fused":  # cgx_dist.cpp's fused step: pack p_new, x in pairs
         def allreduce1(a):
             t = torch.tensor([a], dtype=torch.float64)
@@ -207,7 +247,7 @@ def _worker(rank, world, port, kind, out_path, alg="cg1"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("alg", ["cg1", "hs", "hs_fused"])
+@pytest.mark.parametrize("alg", ["cg1", "hs", "hs_fused", "sr"])
 @pytest.mark.parametrize("kind", ["lap3d", "rand"])
 def test_distributed_world2_gloo(kind, alg, tmp_path):
     import helpers as H
@@ -223,7 +263,7 @@ def test_distributed_world2_gloo(kind, alg, tmp_path):
     else:
         rp, col, val = cgx.random_spd(1200, 6, 3)
         b = np.random.default_rng(9).standard_normal(1200)
-    x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=alg == "cg1")
+    x_ref, its_ref, _ = H.o_solve(500, 1e-10, rp, col, val, b, cg1=alg == "cg1", sr=alg == "sr")
     if alg == "hs_fused":  # the same values as the HS protocol's, bit for bit
         out2 = str(tmp_path / "x_hs.npy")
         mp.start_processes(_worker, args=(2, _free_port(), kind, out2, "hs"), nprocs=2,

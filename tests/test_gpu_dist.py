@@ -445,6 +445,102 @@ def test_fused_cg1_rccl_one_rank_graph_parity():
         assert H.same_bits_or_both_nan(x0, x1)
 
 
+def _sr_group(rp, col, val, b, P, runs, alg=cgx.CGX_ALG_SR, fused="auto", layout="auto"):
+    n = len(rp) - 1
+    parts = cgx.DistSolver.local_group(0, P)
+    out = []
+    try:
+        parts[0].set_alg(alg)
+        parts[0].set_fused(fused)
+        for g, d in enumerate(parts):
+            d.set_layout(layout)
+            rb, re_ = cgx.partition_rows(n, P, g)
+            d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+            d.set_rhs(b[rb:re_])
+        for maxit, tol in runs:
+            its = parts[0].run(maxit, tol)
+            out.append((its, np.concatenate([d.x() for d in parts]), parts[0].history(its)))
+        stats = [d.info() for d in parts]
+    finally:
+        parts[0].close()
+    return out, stats
+
+
+@pytest.mark.parametrize("shape,P", [((24, 20, 30), 1), ((24, 20, 30), 2), ((24, 20, 30), 3),
+                                     ((24, 20, 30), 8), ((40, 30, 16), 2), ((40, 30, 16), 4),
+                                     ((40, 30, 24), 8)])
+def test_sr_partitions(shape, P):
+    """CGX_ALG_SR, the fused HS step with ONE reduction of (p.s, s.s, r.r)
+    per iteration (beta and the stop test from alpha^2 s.s - r.r): the fused
+    step runs under AUTO even on these cache-resident sizes (SR has no
+    unfused form); within 1e-9 of oracle_solve_sr (the restated variant) and
+    of the HS oracle, stop iteration within 1 of both, true residual below
+    the tolerance; at fixed max_iter within 1e-10 of the fused HS group (the
+    recurrences differ only in how r_new.r_new is formed)."""
+    rp, col, val = cgx.laplacian3d(*shape)
+    b = np.random.default_rng(23).standard_normal(len(rp) - 1)
+    runs = [(0, 0.0), (1, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]
+    sr, st = _sr_group(rp, col, val, b, P, runs)
+    hs, _ = _sr_group(rp, col, val, b, P, runs, alg=cgx.CGX_ALG_HS, fused="on")
+    assert all(s["fused"] == 1 and s["alg"] == cgx.CGX_ALG_SR for s in st)
+    for (i0, x0, _), (i1, x1, _) in zip(sr[:-1], hs[:-1]):
+        assert i0 == i1
+        assert np.linalg.norm(x0 - x1) <= 1e-10 * np.linalg.norm(x1)
+    its, x, hist = sr[-1]
+    x_sr, its_sr, hist_sr = H.o_solve(3000, 1e-10, rp, col, val, b, sr=True)
+    x_hs, its_hs, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+    assert abs(its - its_sr) <= 1 and abs(its - its_hs) <= 1 and its < 3000
+    assert np.linalg.norm(x - x_sr) <= 1e-9 * np.linalg.norm(x_sr)
+    assert np.linalg.norm(x - x_hs) <= 1e-9 * np.linalg.norm(x_hs)
+    m = min(len(hist), len(hist_sr)) - 2
+    assert np.allclose(hist[:m], hist_sr[:m], rtol=1e-6, atol=0)
+    assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
+
+
+def test_sr_rccl_one_rank_graph_parity():
+    """SR through a 1-rank RCCL communicator (the all-reduce of three doubles
+    in the replayed graphs), eager, and without a communicator (local sums
+    straight into k_update_rf): bit-identical x, iteration counts and
+    histories."""
+    rp, col, val = cgx.laplacian3d(24, 20, 30)
+    b = np.random.default_rng(24).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    res = {}
+    for key in (("rccl", True), ("rccl", False), ("solo", True)):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id() if key[0] == "rccl" else None)
+        try:
+            d.set_alg(cgx.CGX_ALG_SR)
+            d.set_graph(key[1])
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            out = []
+            for maxit in (17, 33, 40):
+                its = d.run(maxit, 0.0)
+                out.append((its, d.x(), d.history(its)))
+            its = d.run(3000, 1e-10)
+            out.append((its, d.x(), d.history(its)))
+            i = d.info()
+            assert i["fused"] == 1 and i["alg"] == cgx.CGX_ALG_SR
+        finally:
+            d.close()
+        res[key] = out
+    for key in (("rccl", False), ("solo", True)):
+        for (i0, x0, h0), (i1, x1, h1) in zip(res[("rccl", True)], res[key]):
+            assert i0 == i1
+            assert H.same_bits_or_both_nan(x0, x1), key
+            assert H.same_bits_or_both_nan(h0, h1), key
+
+
+def test_sr_refused_without_fused_step():
+    """SR has no unfused form: a CSR layout (or CGX_FUSE_OFF) makes run()
+    fail with CGX_EINVAL and a message, not run another recurrence."""
+    rp, col, val = cgx.laplacian3d(12, 10, 8)
+    b = np.ones(len(rp) - 1)
+    for layout, fused in (("csr", "auto"), ("auto", "off")):
+        with pytest.raises(cgx.CgxError, match="CGX_ALG_SR"):
+            _sr_group(rp, col, val, b, 2, [(5, 0.0)], layout=layout, fused=fused)
+
+
 def test_fuse_refusal_reported_for_plane_cutting_partitions():
     """slabs that do not start on a plane boundary add ghost
     diagonals, so some partition's layout cannot take the fused step and the
@@ -513,5 +609,5 @@ def test_bench_dist_path_rehearsal(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert line["parity"]["ok"] and set(line["parity"]) >= {"hs", "hs_fused", "cg1"}
+    assert line["parity"]["ok"] and set(line["parity"]) >= {"hs", "hs_fused", "sr", "cg1"}
     assert line["n_gpus"] == 1 and line["value"] > 0 and line["config"]["fused"] in (0, 1)

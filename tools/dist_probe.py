@@ -1,8 +1,8 @@
 """Per-rank iteration time of the partitioned solver on ONE GPU: a 1-rank
 RCCL communicator (the multi-GPU phase code: pack, halo loop with no peers,
 ncclAllReduce) on a slab of C4 (400 x 400 x nz planes, 8M rows at nz = 50 =
-C4's slab at N = 8), HS and CG1, fused and unfused, graph-replayed (the
-fused ones twice, alternating)."""
+C4's slab at N = 8), HS, SR (HS with one all-reduce) and CG1, fused and
+unfused, graph-replayed (HS fused and SR twice, alternating)."""
 import sys, time
 sys.path.insert(0, "conjugate-gradient_amd")
 import numpy as np, cgx
@@ -11,9 +11,9 @@ nz = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 rp, col, val = cgx.laplacian3d(400, 400, nz)
 n = len(rp) - 1
 b = np.ones(n)
-for name, alg, fused in (("hs_fused", cgx.CGX_ALG_HS, True), ("hs", cgx.CGX_ALG_HS, False),
-                         ("cg1_fused", cgx.CGX_ALG_CG1, True), ("cg1", cgx.CGX_ALG_CG1, False),
-                         ("hs_fused", cgx.CGX_ALG_HS, True), ("cg1_fused", cgx.CGX_ALG_CG1, True)):
+for name, alg, fused in (("hs_fused", cgx.CGX_ALG_HS, True), ("sr", cgx.CGX_ALG_SR, "auto"),
+                         ("hs", cgx.CGX_ALG_HS, False), ("cg1", cgx.CGX_ALG_CG1, False),
+                         ("hs_fused", cgx.CGX_ALG_HS, True), ("sr", cgx.CGX_ALG_SR, "auto")):
     d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
     try:
         d.set_alg(alg)
