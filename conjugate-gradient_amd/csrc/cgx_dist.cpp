@@ -171,7 +171,9 @@ void drop_graph(cgx_dist *d) {
 // The fused HS step (k_spmv_dia_h) runs when every partition's layout
 // takes it (decided once per connection: the ranks' phase sequences match).
 // SR is the fused step with one reduction.
-bool fz(const cgx_dist *d) { return d->fz_all && (d->alg == CGX_ALG_HS || d->alg == CGX_ALG_SR); }
+// HS-shaped recurrences (HS, SR): s = A p, r -= alpha s, p = r + beta p
+bool hs_like(const cgx_dist *d) { return d->alg == CGX_ALG_HS || d->alg == CGX_ALG_SR; }
+bool fz(const cgx_dist *d) { return d->fz_all && hs_like(d); }
 bool sr(const cgx_dist *d) { return d->alg == CGX_ALG_SR; }
 // The fused CG1 step (k_cg1_dia_h): only when forced on (CGX_FUSE_ON) --
 // on a rank's slab it loses to the unfused CG1 kernels (C4/8's 400 x 400 x
@@ -524,7 +526,7 @@ double *s_new(cgx_dist *d) { return d->pbuf ? d->d_s : d->d_s2; }
 double *w_old(cgx_dist *d) { return d->pbuf ? d->d_w2 : d->d_w; }
 double *w_new(cgx_dist *d) { return d->pbuf ? d->d_w : d->d_w2; }
 double *spmv_x(cgx_dist *d) {
-  if (d->alg != CGX_ALG_HS) return fz1(d) ? r_new(d) : d->d_r;
+  if (!hs_like(d)) return fz1(d) ? r_new(d) : d->d_r;
   return fz(d) ? p_new(d) : d->d_p;
 }
 // r.r of the last r update, as the fused step reads it (SR: k_update_rf's
@@ -533,7 +535,7 @@ const double *rr_new_src(cgx_dist *d) {
   return solo(d) || sr(d) ? &d->d_st->rr_new : d->d_gsums + 1;
 }
 double *spmv_y(cgx_dist *d) {
-  return d->alg == CGX_ALG_HS ? d->d_s : fz1(d) ? w_new(d) : d->d_w;
+  return hs_like(d) ? d->d_s : fz1(d) ? w_new(d) : d->d_w;
 }
 
 // A rank with neighbours: ghost rows to receive or rows to send.  Without
@@ -801,7 +803,7 @@ int fz_close(cgx_dist *d) {
 int run_phases_eager(Group *g, bool init, long long iters) {
   auto &P = g->parts;
   int rc;
-  if (P[0]->alg == CGX_ALG_HS) {
+  if (hs_like(P[0])) {
     if (init) {
       for (cgx_dist *d : P) d->pbuf = 0;  // the prologue writes p into d_p
       for (cgx_dist *d : P) if ((rc = hs_init(d))) return rc;
