@@ -116,7 +116,7 @@ struct cgx_dist {
   std::vector<int> send_count, send_off, recv_count, recv_off;
   int n_send = 0;
   double *d_pa = nullptr, *d_pb = nullptr;
-  double *d_pss = nullptr;  // SR: the fused launches' s.s partials (d_pb's offsets)
+  double *d_pss = nullptr;  // SR: the fused launches' (p.s, s.s) partial pairs (2x d_pb's offsets)
   double *d_sums = nullptr, *d_gsums = nullptr;  // [0, 4) local, [4, 8) all-reduced
   unsigned *d_tick = nullptr;                    // last-arriver counters
   int vec_grid = 1;
@@ -333,7 +333,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
       (rc = dev_alloc(&d->d_s2, ng * 8, cb)) || (rc = dev_alloc(&d->d_w2, ng * 8, cb)) ||
       (rc = dev_alloc(&d->d_pa, npa * 8, cb)) ||
       (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb)) ||
-      (rc = dev_alloc(&d->d_pss, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb))) {
+      (rc = dev_alloc(&d->d_pss, ((size_t)d->g_int + d->g_bnd + 8) * 16, cb))) {
     free_system(d);
     return rc;
   }
@@ -637,7 +637,7 @@ int phase_spmv(cgx_dist *d) {
       const int pub = (e == 0 || d->it_int.count == 0) ? 1 : 0;
       const FuseArgs<double> f{d->d_x, p_old(d), p_new(d), d->d_r, d->d_st, d->d_hist,
                                rr_new_src(d), pub, e == 2 ? 1 : 0,
-                               sr(d) ? d->d_pss + (part - d->d_pb) : nullptr};
+                               sr(d) ? d->d_pss + 2 * (part - d->d_pb) : nullptr};
       return launch_spmv_fused<double>(a, f, d->st, ev);
     }
     return launch_spmv<double>(a, d->st, ev);
@@ -657,7 +657,7 @@ int phase_spmv(cgx_dist *d) {
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
   if (sr(d))  // p.s, s.s, and r.r of the last r update (the prologue's b.b at first)
-    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pb, np, d->d_pss, np, d->d_st, d->d_hist, d->d_sums,
+    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pss, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
                             d->st, d->d_pa, d->vec_grid));
   else if (d->alg == CGX_ALG_HS)
     CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,

@@ -93,7 +93,7 @@ enum FinOp {
   FIN_CG1 = 4,       // gamma' = sum(a), delta = sum(b); stop test; alpha, beta
   FIN_SUM = 5,       // out[0] = sum(a) (op-level dot, local sums)
   FIN_SUM2 = 6,      // out[0] = sum(a), out[1] = sum(b)
-  FIN_SUM3 = 7,      // out[0..2] = sum(a), sum(b), sum(c) (SR local sums)
+  FIN_SUM3 = 7,      // out[0..2] = sums of a's (x, y) pairs and of c (SR local sums)
 };
 
 constexpr int kVecBS = 256;
@@ -259,8 +259,8 @@ struct FuseArgs {
   const double *rr_new;  // r.r of the last r update (&st->rr_new, or all-reduced)
   int publish;           // this launch's workgroup 0 writes the scalar state back
   int ghost;             // columns >= n are ghosts: p_new from pnew's ghost tail
-  double *ss;            // CGX_ALG_SR: the s.s partials beside a.part's p.s ones
-                         // (same offsets; nullptr: none)
+  double *ss;            // CGX_ALG_SR: (p.s, s.s) partial pairs, ss[2 b], ss[2 b + 1],
+                         // instead of a.part (nullptr: none)
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one

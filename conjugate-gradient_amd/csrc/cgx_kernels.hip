@@ -167,9 +167,10 @@ __device__ __forceinline__ void epi_store(double dot, double *part) {
 }
 
 // Two partials per workgroup (CGX_ALG_SR's fused step: p.s and s.s), each
-// summed exactly as epi_store sums one.
+// summed exactly as epi_store sums one, stored as one (p.s, s.s) pair:
+// pair[2 b], pair[2 b + 1] -- one 16-byte load per workgroup for k_finalize.
 template <int WPB>
-__device__ __forceinline__ void epi_store2(double dot, double dot2, double *part, double *part2) {
+__device__ __forceinline__ void epi_store2(double dot, double dot2, double *pair) {
   __shared__ double red2[2][WPB];
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   dot = wave_sum(dot);
@@ -179,12 +180,14 @@ __device__ __forceinline__ void epi_store2(double dot, double dot2, double *part
     red2[1][wid] = dot2;
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    const double *rw = red2[threadIdx.x];
-    double s = rw[0];
+  if (threadIdx.x == 0) {
+    double s = red2[0][0], q = red2[1][0];
 #pragma unroll
-    for (int w = 1; w < WPB; ++w) s = s + rw[w];
-    (threadIdx.x == 0 ? part : part2)[blockIdx.x] = s;
+    for (int w = 1; w < WPB; ++w) {
+      s = s + red2[0][w];
+      q = q + red2[1][w];
+    }
+    reinterpret_cast<double2 *>(pair)[blockIdx.x] = make_double2(s, q);
   }
 }
 
@@ -883,7 +886,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
     }
   }
   if (f.ss)  // uniform
-    epi_store2<4>(dot, dot2, a.part, f.ss);
+    epi_store2<4>(dot, dot2, f.ss);
   else
     epi_store<4>(dot, a.part);
 }
@@ -1388,6 +1391,47 @@ __device__ __forceinline__ void sum_parts2(const double *pa, int na, const doubl
   __syncthreads();
 }
 
+// CGX_ALG_SR's local sums in one pass: (p.s, s.s) pairs pq[0, na) -- one
+// 16-byte load each -- and the r.r partials pc[0, nc), all loads of a pass in
+// flight together; each sum in sum_parts' order (thread t: index order, then
+// the block tree).
+template <int BS>
+__device__ __forceinline__ void sum_parts_sr(const double *pq, int na, const double *pc, int nc,
+                                             double *red, double &sa, double &sb, double &sc) {
+  constexpr int U = 16;
+  const double2 *q2 = reinterpret_cast<const double2 *>(pq);
+  double a = 0.0, b = 0.0, c = 0.0;
+  bool fa = true, fc = true;
+  const int nmax = na > nc ? na : nc;
+  for (int i = threadIdx.x; i < nmax; i += U * BS) {
+    double2 v[U];
+    double w[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      v[j] = i + j * BS < na ? q2[i + j * BS] : make_double2(0.0, 0.0);
+      w[j] = i + j * BS < nc ? pc[i + j * BS] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (i + j * BS < na) {
+        a = fa ? v[j].x : a + v[j].x;
+        b = fa ? v[j].y : b + v[j].y;
+        fa = false;
+      }
+      if (i + j * BS < nc) {
+        c = fc ? w[j] : c + w[j];
+        fc = false;
+      }
+    }
+  }
+  sa = block_sum<BS>(a, red);
+  __syncthreads();
+  sb = block_sum<BS>(b, red);
+  __syncthreads();
+  sc = block_sum<BS>(c, red);
+  __syncthreads();
+}
+
 // Folded HS (the default fast path): no finalize kernels.  Every workgroup
 // of the vector kernels sums the previous kernel's partials itself -- the
 // same sum_parts<1024> order as k_finalize<1024>, so alpha, beta and the
@@ -1743,9 +1787,9 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
                                                  int nc) {
   __shared__ double red[BS / kWave];
   double sa, sb = 0.0, sc = 0.0;
-  if (pb) sum_parts2<BS>(pa, na, pb, nb, red, sa, sb);
+  if (op == FIN_SUM3) sum_parts_sr<BS>(pa, na, pc, nc, red, sa, sb, sc);  // pa: (p.s, s.s) pairs
+  else if (pb) sum_parts2<BS>(pa, na, pb, nb, red, sa, sb);
   else sa = sum_parts<BS>(pa, na, red);
-  if (pc) sc = sum_parts<BS>(pc, nc, red);
   if (threadIdx.x != 0) return;
   if (op == FIN_SUM3) out[2] = sc;
   if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_SUM3 && op != FIN_INIT_HS &&

@@ -451,6 +451,7 @@ void DevMatrix::release() {
   panel_first.clear();
   panel_count.clear();
   n = nnz = ncols = nblk = ndict = tile_bands = 0;
+  csr_reach = 0;
   memset(&dia, 0, sizeof dia);
   kdiag = -1;
   gath = 8;
@@ -772,6 +773,18 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     }
   }
   (void)hipFree(d_err);
+  // plain CSR of a banded matrix (<= 256 distinct col - row offsets in the
+  // sampled rows, or a generated stencil): its reach, for the L2-tiled order
+  csr_reach = 0;
+  if (layout == L_CSR && npanel == 1 && n > 0 && nnz > 0) {
+    std::vector<int> off = doff;
+    std::vector<T> dummy;
+    if (off.empty()) {
+      if (gen) off = lap_offsets(*gen);
+      else if (!find_pairs(n, rp, col, val, false, 256, true, off, dummy)) off.clear();
+    }
+    for (int v : off) csr_reach = std::max(csr_reach, (long long)std::abs(v));
+  }
   return finish_upload(t0);
 }
 
@@ -792,12 +805,12 @@ int DevMatrix::finish_upload(double t0) {
     doff = dd;
   }
 
-  // ---- L2-tiled item order for wide stencils (DC / DIA)
-  if (layout == L_DC || layout == L_DIA) {
-    long long P = 0;
+  // ---- L2-tiled item order for wide stencils (DC / DIA / banded CSR)
+  if (layout == L_DC || layout == L_DIA || (layout == L_CSR && csr_reach > 0)) {
+    long long P = csr_reach;
     if (layout == L_DIA)
       for (int k = 0; k < dia.ndiag; ++k) P = std::max(P, (long long)std::abs(dia.doff[k]));
-    else
+    else if (layout == L_DC)
       for (int v : doff) P = std::max(P, (long long)std::abs(v));
     const std::vector<int> ir = item_rows();
     order = tile_order(ir, P, ts, tile_bands);

@@ -51,10 +51,12 @@ struct DevMatrix {
   DiaCand dia{};
   int kdiag = -1;               // main diagonal's index, -1: none
   int gath = 8;                 // CSR / DC: gathers per row chunk
-  // L2-tiled order of the work items (DC / DIA, wide stencils; nullptr: natural)
+  // L2-tiled order of the work items (DC / DIA / banded CSR, wide stencils;
+  // nullptr: natural)
   int *d_order = nullptr;
   std::vector<int> order;    // host copy of the tiled order (empty: natural)
   int tile_bands = 0;
+  long long csr_reach = 0;   // CSR: largest |col - row| of a banded matrix (0: not banded)
   // stencil
   LapSpec lap{};
   // setup record

@@ -997,11 +997,11 @@ def test_matrix_free_stencil_bit_exact(dim, shape):
         assert abs(its - its_o) <= 1
 
 
-@pytest.mark.parametrize("layout", ["dia", "dc"])
+@pytest.mark.parametrize("layout", ["dia", "dc", "csr"])
 def test_tiled_item_order_bit_exact(layout):
     """L2-tiled work-item order for a stencil whose plane exceeds the L2
-    budget (600 x 600 planes: 3 planes of x = 8.6 MB > 1.5 MiB per XCD): only
-    the order changes, so the SpMV is bit-identical to the oracle and a CG run
+    budget (600 x 600 planes: 3 planes of x = 8.6 MB > 1.5 MiB per XCD; plain
+    CSR too, its reach taken from the sampled offsets): only the order changes, so the SpMV is bit-identical to the oracle and a CG run
     stays within the fast-mode tolerance."""
     rp, col, val = cgx.laplacian3d(600, 600, 5)
     n = len(rp) - 1
@@ -1027,6 +1027,22 @@ def test_c4_full_size_spmv_device_generated():
         s.gen_laplacian(3, 400, 400, 400)
         assert s.info()["nnz"] == 447_040_000
         assert s.info()["layout_name"] == "dia" and s.info()["tile_bands"] > 0
+        y = s.spmv(x)
+    with cgx.Solver(0) as s:
+        s.set_stencil(3, 400, 400, 400)
+        y2 = s.spmv(x)
+    assert H.same_bits_or_both_nan(y, y2)
+
+
+def test_c4_full_size_csr_tiled_spmv():
+    """C4 at full size in the reference's plain CSR (the roofline layout,
+    SURVEY.md 8d): the generated CSR runs in the L2-tiled block order and its
+    SpMV equals the matrix-free stencil bit for bit."""
+    x = np.random.default_rng(12).standard_normal(400 ** 3)
+    with cgx.Solver(0, layout="csr") as s:
+        s.gen_laplacian(3, 400, 400, 400)
+        i = s.info()
+        assert i["layout_name"] == "csr" and i["tile_bands"] > 0
         y = s.spmv(x)
     with cgx.Solver(0) as s:
         s.set_stencil(3, 400, 400, 400)
