@@ -45,6 +45,11 @@ template <> struct Vec16<float> {
   static constexpr int W = 4;
 };
 
+// Kernel experiments (A/B builds only: tools/ab_build.sh; 0 in the product)
+#ifndef CGX_EXP
+#define CGX_EXP 0
+#endif
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_down(v, off, kWave);
@@ -849,6 +854,10 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   // s = A p_new in diagonal order: near diagonals from the window, far ones
   // from their slot (the number of far diagonals before k)
   const int rw = r - w0;
+  const T pn0 = win[rw], pn1 = win[rw + 1];
+  constexpr bool kPnNt = (CGX_EXP & 1) != 0;
+  if constexpr ((CGX_EXP & 2) != 0)
+    if (r < a.n) st_pair(f.pnew, r, a.n, pn0, pn1, kPnNt && NT);
   T a0 = T(0), a1 = T(0);
 #pragma unroll
   for (int kk = 0; kk < kDiaMax; ++kk) {
@@ -872,11 +881,10 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
       a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
     }
   }
-  const T pn0 = win[rw], pn1 = win[rw + 1];
   st_pair(a.y, r, a.n, a0, a1, NT);
   double dot = 0.0, dot2 = 0.0;
   if (r < a.n) {
-    st_pair(f.pnew, r, a.n, pn0, pn1, false);
+    if constexpr ((CGX_EXP & 2) == 0) st_pair(f.pnew, r, a.n, pn0, pn1, kPnNt && NT);
     if (xup) x_update();
     dot = (double)pn0 * (double)a0;
     if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
