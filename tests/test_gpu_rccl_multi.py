@@ -1,6 +1,6 @@
 """GPU, >= 2 devices: the partitioned solver over a real multi-rank RCCL
 communicator -- ncclSend/Recv halos between ranks and ncclAllReduce of both
-recurrences, fused and unfused HS, graph-replayed -- one fresh child process
+recurrences, fused and unfused HS and SR (one all-reduce), graph-replayed -- one fresh child process
 per GPU (spawned; the children initialise their own device).  Every rank's x
 must be bit-identical to the in-process group of the same partitions (the
 same phase code with device copies and a fixed-order sum).  Skipped on a
@@ -19,7 +19,12 @@ torch = pytest.importorskip("torch")
 import torch.multiprocessing as mp  # noqa: E402
 
 SHAPE = (40, 30, 24)  # plane-aligned slabs at 2 ranks: the fused step applies
-CASES = [("hs", True), ("hs", False), ("cg1", False)]
+CASES = [("hs", True), ("hs", False), ("sr", "auto"), ("cg1", False)]
+ALGS = {"hs": cgx.CGX_ALG_HS, "sr": cgx.CGX_ALG_SR, "cg1": cgx.CGX_ALG_CG1}
+
+
+def _fused_expected(alg, fused):
+    return 1 if alg == "sr" or fused is True else 0
 
 
 def _system():
@@ -43,11 +48,11 @@ def _worker(rank, world, uid, out_dir):
         d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
         d.set_rhs(b[rb:re_])
         for alg, fused in CASES:
-            d.set_alg(c.CGX_ALG_HS if alg == "hs" else c.CGX_ALG_CG1)
+            d.set_alg({"hs": c.CGX_ALG_HS, "sr": c.CGX_ALG_SR, "cg1": c.CGX_ALG_CG1}[alg])
             d.set_fused(fused)
             its = d.run(3000, 1e-10)
-            np.save(os.path.join(out_dir, f"x_{alg}_{int(fused)}_{rank}.npy"), d.x())
-            np.save(os.path.join(out_dir, f"its_{alg}_{int(fused)}_{rank}.npy"),
+            np.save(os.path.join(out_dir, f"x_{alg}_{fused}_{rank}.npy"), d.x())
+            np.save(os.path.join(out_dir, f"its_{alg}_{fused}_{rank}.npy"),
                     np.array([its, d.info()["fused"], d.info()["graph"]]))
     finally:
         d.close()
@@ -58,7 +63,7 @@ def _local(alg, fused, world):
     n = len(rp) - 1
     parts = cgx.DistSolver.local_group(0, world)
     try:
-        parts[0].set_alg(cgx.CGX_ALG_HS if alg == "hs" else cgx.CGX_ALG_CG1)
+        parts[0].set_alg(ALGS[alg])
         parts[0].set_fused(fused)
         for g, d in enumerate(parts):
             rb, re_ = cgx.partition_rows(n, world, g)
@@ -80,8 +85,8 @@ def test_two_rank_rccl_bit_identical_to_local_group(tmp_path):
     for alg, fused in CASES:
         its_l, xs_l = _local(alg, fused, world)
         for rank in range(world):
-            its, fz, graph = np.load(tmp_path / f"its_{alg}_{int(fused)}_{rank}.npy")
+            its, fz, graph = np.load(tmp_path / f"its_{alg}_{fused}_{rank}.npy")
             assert its == its_l, (alg, fused)
-            assert fz == (1 if fused else 0) and graph == 1
-            x = np.load(tmp_path / f"x_{alg}_{int(fused)}_{rank}.npy")
+            assert fz == _fused_expected(alg, fused) and graph == 1
+            x = np.load(tmp_path / f"x_{alg}_{fused}_{rank}.npy")
             assert np.array_equal(x.view(np.uint64), xs_l[rank].view(np.uint64)), (alg, fused)
