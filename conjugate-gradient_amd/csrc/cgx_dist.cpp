@@ -101,6 +101,7 @@ struct cgx_dist {
   DevMatrix A;
   cgx::Items it_int{}, it_bnd{};
   int *d_list_int = nullptr, *d_list_bnd = nullptr;
+  int *d_pairs_int = nullptr, *d_pairs_bnd = nullptr;  // the fused step's super-items of a list
   int g_int = 0, g_bnd = 0;  // SpMV partials of each launch
   double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
          *d_w = nullptr;
@@ -196,6 +197,8 @@ void free_system(cgx_dist *d) {
   d->A.release();
   dev_free(&d->d_list_int);
   dev_free(&d->d_list_bnd);
+  dev_free(&d->d_pairs_int);
+  dev_free(&d->d_pairs_bnd);
   dev_free(&d->d_b);
   dev_free(&d->d_x);
   dev_free(&d->d_r);
@@ -270,7 +273,7 @@ int split_items(cgx_dist *d, const int *rp, const std::vector<int> &col_local) {
     const int i = d->A.order.empty() ? j : d->A.order[(size_t)j];
     (ghost[(size_t)i] ? lbnd : lint).push_back(i);
   }
-  auto make = [&](const std::vector<int> &l, int **dl, Items &it) -> int {
+  auto make = [&](const std::vector<int> &l, int **dl, int **dp, Items &it) -> int {
     const bool run = !l.empty() && l.back() - l.front() + 1 == (int)l.size() &&
                      std::is_sorted(l.begin(), l.end());
     it = Items{nullptr, l.empty() ? 0 : l.front(), (int)l.size()};
@@ -280,10 +283,18 @@ int split_items(cgx_dist *d, const int *rp, const std::vector<int> &col_local) {
     CGX_HIP(hipMemcpy(*dl, l.data(), l.size() * 4, hipMemcpyHostToDevice));
     it.list = *dl;
     it.first = 0;
+    if (d->A.layout == L_DIA) {  // the fused step's super-items of the list
+      const std::vector<int> fp = fuse_pairs(l);
+      if ((rc = dev_alloc(dp, fp.size() * 4, &d->vec_bytes))) return rc;
+      CGX_HIP(hipMemcpy(*dp, fp.data(), fp.size() * 4, hipMemcpyHostToDevice));
+      it.pairs = *dp;
+      it.npairs = (int)fp.size() / 2;
+    }
     return 0;
   };
   int rc;
-  if ((rc = make(lint, &d->d_list_int, d->it_int)) || (rc = make(lbnd, &d->d_list_bnd, d->it_bnd)))
+  if ((rc = make(lint, &d->d_list_int, &d->d_pairs_int, d->it_int)) ||
+      (rc = make(lbnd, &d->d_list_bnd, &d->d_pairs_bnd, d->it_bnd)))
     return rc;
   d->g_int = d->it_int.count ? d->A.partials(d->it_int) : 0;
   d->g_bnd = d->it_bnd.count ? d->A.partials(d->it_bnd) : 0;

@@ -156,11 +156,20 @@ enum Layout : int { L_CSR = 0, L_DC = 1, L_DIA = 2, L_STENCIL = 3 };
 
 // Work items of one launch (CSR/DC: row blocks; DIA: 512-row slices): list[0, count)
 // when list != nullptr, else first, first+1, ..., first+count-1.
+// The fused HS step (k_spmv_dia_h) with two slices per workgroup (wide
+// halos, cgx_kernels.hip fuse_slices) runs super-items of <= 2 ADJACENT slices: pairs[2 w], pairs[2 w + 1] = (list position, 1 or 2) of
+// super-item w (npairs of them); pairs == nullptr: the natural pairing
+// (positions 2w, 2w + 1) -- a contiguous run, or a list of adjacent pairs.
 struct Items {
   const int *list;
   int first;
   int count;
+  const int *pairs = nullptr;
+  int npairs = 0;
 };
+// Super-items of a list of slices on the host: greedy adjacent pairs, as
+// Items::pairs (2 ints each).
+std::vector<int> fuse_pairs(const std::vector<int> &slices);
 
 // In-kernel local sums of k_update_rf ("last arriver"): every workgroup
 // publishes its partials and takes a ticket on *cnt; the last one sums

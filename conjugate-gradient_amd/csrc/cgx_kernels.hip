@@ -171,31 +171,6 @@ __device__ __forceinline__ void epi_store(double dot, double *part) {
   }
 }
 
-// Two partials per workgroup (CGX_ALG_SR's fused step: p.s and s.s), each
-// summed exactly as epi_store sums one, stored as one (p.s, s.s) pair:
-// pair[2 b], pair[2 b + 1] -- one 16-byte load per workgroup for k_finalize.
-template <int WPB>
-__device__ __forceinline__ void epi_store2(double dot, double dot2, double *pair) {
-  __shared__ double red2[2][WPB];
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  dot = wave_sum(dot);
-  dot2 = wave_sum(dot2);
-  if (lane == 0) {
-    red2[0][wid] = dot;
-    red2[1][wid] = dot2;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = red2[0][0], q = red2[1][0];
-#pragma unroll
-    for (int w = 1; w < WPB; ++w) {
-      s = s + red2[0][w];
-      q = q + red2[1][w];
-    }
-    reinterpret_cast<double2 *>(pair)[blockIdx.x] = make_double2(s, q);
-  }
-}
-
 // The scalar lines of the recurrence (cg.c:113, 125-129; CG1 analogues) on
 // the reduced sums sa, sb -- run by ONE thread (k_finalize).
 __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *hist,
@@ -283,6 +258,47 @@ __device__ __forceinline__ int xcd_block() {
   if (G < 16) return b;
   const int x = b & 7, i = b >> 3, q = G >> 3, rem = G & 7;
   return x * q + min(x, rem) + i;
+}
+
+// The workgroup index whose xcd_block() is logical index L (grid G): where a
+// one-workgroup-per-item launch writes item L's partial.
+__device__ __forceinline__ int xcd_slot(int L, int G) {
+  if (G < 16) return L;
+  const int q = G >> 3, rem = G & 7;
+  const int x = L < rem * (q + 1) ? L / (q + 1) : rem + (L - rem * (q + 1)) / q;
+  const int i = L - (x * q + min(x, rem));
+  return 8 * i + x;
+}
+
+// The fused step's epilogue (SB slices of 256 threads): per slice the p.s
+// partial (and with ss the (p.s, s.s) pair) summed over its four waves in
+// order -- epi_store<4> of a 256-thread workgroup -- written at
+// xcd_slot(pos + h, G), the unfused k_spmv_dia's slot for it.
+template <int SB>
+__device__ __forceinline__ void epi_store_slices(double dot, double dot2, double *ss, double *part,
+                                                 int pos, int cnt, int G) {
+  constexpr int NW = 4 * SB;
+  __shared__ double red[2][NW];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  dot = wave_sum(dot);
+  if (ss) dot2 = wave_sum(dot2);
+  if (lane == 0) {
+    red[0][wid] = dot;
+    red[1][wid] = dot2;
+  }
+  __syncthreads();
+  const int h = threadIdx.x / kWave;  // thread 0 of wave h sums slice h
+  if (lane == 0 && h < cnt) {
+    double sa = red[0][4 * h], sb = red[1][4 * h];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) {
+      sa = sa + red[0][4 * h + v];
+      sb = sb + red[1][4 * h + v];
+    }
+    const int slot = xcd_slot(pos + h, G);
+    if (ss) reinterpret_cast<double2 *>(ss)[slot] = make_double2(sa, sb);
+    else part[slot] = sa;
+  }
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -746,19 +762,39 @@ __device__ __forceinline__ typename Pair<T>::type p_next(typename Pair<T>::type 
 // 8 p_new + 8 s, + 24 (x read and written, p_{k-1} read) every other
 // launch.  Every value is the unfused path's (same roundings): x and the
 // r.r history are bit-identical to SpMV + k_update_rf + k_xpay_xf.
-template <typename T, int NF, int NFAR, bool NT, bool LIST, bool GH>
-__global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
+template <typename T, int SB, int NF, int NFAR, bool NT, bool LIST, bool GH>
+__global__ __launch_bounds__(256 * SB) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f) {
+  constexpr int BS = 256 * SB;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *win = reinterpret_cast<T *>(dyn_lds);
   __shared__ T lv[kDiaMax * 16];
   typedef typename Pair<T>::type P;
   const int t = threadIdx.x;
-  const int wi = xcd_block();
-  const int s = LIST ? a.items.list[wi] : a.items.first + wi;
+  // this workgroup's super-item: list positions [pos, pos + cnt), cnt <= SB
+  // adjacent slices (SB = 2: Items::pairs, or the natural pairing of a
+  // contiguous run; SB = 1: one slice, the k_spmv_dia shape)
+  const int w = xcd_block();
+  int pos, cnt;
+  if (SB == 1) {
+    pos = w;
+    cnt = 1;
+  } else if (a.items.pairs) {
+    pos = a.items.pairs[2 * w];
+    cnt = a.items.pairs[2 * w + 1];
+  } else {
+    pos = 2 * w;
+    cnt = min(2, a.items.count - pos);
+  }
+  const int s = LIST ? a.items.list[pos] : a.items.first + pos;
   if (f.st->done > 1) return;  // uniform
   const FuseStep fs = fuse_step(f.st, f.hist, f.rr_new, f.publish != 0);
   const T alpha = (T)fs.alpha, beta = (T)fs.beta;
   const int s0 = s * kDiaSliceRows, r = s0 + 2 * t;
+  // act: the row pair lies in the super-item's slices (rows >= n there are
+  // padding: no entries); own: it holds a row of the matrix
+  const int sx = s0 + kDiaSliceRows * cnt, rend = min(a.n, sx);
+  const bool act = r < sx;
+  const int ra = act ? r : s0;
   const int rs = r < a.n ? r : 0;
   // x (cg.c:115-116) is updated every other iteration: an even iteration k
   // defers x += alpha_k p_k, the odd k + 1 applies both terms in order (the
@@ -786,15 +822,15 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
       x1 = x1 + d1;
     }
     const T a0 = alpha * po.x, a1 = alpha * po.y;
-    st_pair(f.x, r, a.n, x0 + a0, x1 + a1, false);
+    st_pair(f.x, r, rend, x0 + a0, x1 + a1, false);
   };
   if (fs.stop) {  // the pending x updates only (then the cg.c:125 break)
     load_x();
-    if (xup && r < a.n) x_update();
+    if (xup && r < rend) x_update();
     return;
   }
-  unsigned c0, c1;  // the code words of row r / r + 1 (<= 4 bytes: fusable())
-  ld_codes(a.dcode, a.cb, r, c0, c1);
+  unsigned c0, c1;  // the code words of row ra / ra + 1 (<= 4 bytes: fusable())
+  ld_codes(a.dcode, a.cb, ra, c0, c1);
   const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
   // far diagonals: slot q holds diagonal a.fark[q] (-1: an unused slot)
   constexpr int NS = NFAR > 0 ? NFAR : 1;
@@ -804,7 +840,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   for (int q = 0; q < NFAR; ++q) {
     const int kq = a.fark[q];
     int b = rs;
-    if (kq >= 0) {
+    if (kq >= 0 && act) {
       const unsigned n0 = fld(a, c0, kq), n1 = fld(a, c1, kq);
       if (n0 != a.cmask[kq] || n1 != a.cmask[kq]) b = r + a.doff[kq];
     }
@@ -815,12 +851,12 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   }
   // the window: p_new of rows w0 + i, i < wn (pairs; rows outside [0, ncols)
   // are loaded from a clamped address and never read)
-  const int w0 = s0 - a.hl, wn = kDiaSliceRows + a.hl + a.hr;
+  const int w0 = s0 - a.hl, wn = kDiaSliceRows * cnt + a.hl + a.hr;
   P wr[NF], wp[NF], wg[NF];
   int wj[NF];
 #pragma unroll
   for (int q = 0; q < NF; ++q) {
-    const int j = min(max(w0 + 2 * t + q * 2 * 256, -1), a.ncols - 1);
+    const int j = min(max(w0 + 2 * t + q * 2 * BS, -1), a.ncols - 1);
     wj[q] = j;
     wr[q] = ld_pair(f.r, j);
     wp[q] = ld_pair(f.pold, j);
@@ -838,7 +874,7 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   };
 #pragma unroll
   for (int q = 0; q < NF; ++q) {
-    const int i = 2 * t + q * 2 * 256;
+    const int i = 2 * t + q * 2 * BS;
     const P pn = pnext_at(wr[q], wp[q], wg[q], wj[q]);
     if (i < wn) win[i] = pn.x;
     if (i + 1 < wn) win[i + 1] = pn.y;
@@ -852,12 +888,9 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
   // slots' load registers are dead (70 -> fewer VGPRs over the launch)
   load_x();
   // s = A p_new in diagonal order: near diagonals from the window, far ones
-  // from their slot (the number of far diagonals before k)
+  // from their slot (the number of far diagonals before k); an inactive pair
+  // reads inside the window's allocation and stores nothing
   const int rw = r - w0;
-  const T pn0 = win[rw], pn1 = win[rw + 1];
-  constexpr bool kPnNt = (CGX_EXP & 1) != 0;
-  if constexpr ((CGX_EXP & 2) != 0)
-    if (r < a.n) st_pair(f.pnew, r, a.n, pn0, pn1, kPnNt && NT);
   T a0 = T(0), a1 = T(0);
 #pragma unroll
   for (int kk = 0; kk < kDiaMax; ++kk) {
@@ -881,22 +914,22 @@ __global__ __launch_bounds__(256) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs<T> f
       a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
     }
   }
-  st_pair(a.y, r, a.n, a0, a1, NT);
+  const T pn0 = win[rw], pn1 = win[rw + 1];
+  st_pair(a.y, r, rend, a0, a1, NT);
   double dot = 0.0, dot2 = 0.0;
-  if (r < a.n) {
-    if constexpr ((CGX_EXP & 2) == 0) st_pair(f.pnew, r, a.n, pn0, pn1, kPnNt && NT);
+  if (r < rend) {
+    st_pair(f.pnew, r, rend, pn0, pn1, false);
     if (xup) x_update();
     dot = (double)pn0 * (double)a0;
-    if (r + 1 < a.n) dot = dot + (double)pn1 * (double)a1;
+    if (r + 1 < rend) dot = dot + (double)pn1 * (double)a1;
     if (f.ss) {
       dot2 = (double)a0 * (double)a0;
-      if (r + 1 < a.n) dot2 = dot2 + (double)a1 * (double)a1;
+      if (r + 1 < rend) dot2 = dot2 + (double)a1 * (double)a1;
     }
   }
-  if (f.ss)  // uniform
-    epi_store2<4>(dot, dot2, f.ss);
-  else
-    epi_store<4>(dot, a.part);
+  // one partial per slice, at the slot the unfused launch (one workgroup per
+  // slice, k_spmv_dia) writes it: the same four wave sums in the same order
+  epi_store_slices<SB>(dot, dot2, f.ss, a.part, pos, cnt, a.items.count);
 }
 
 // ---------------------------------------- fused CG1 step (DIA-VI)
@@ -2091,51 +2124,69 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev)
   return launch_spmv_en<T, false, false>(a, g, st, ev);
 }
 
-template <typename T, int NF, int NFAR, bool GH>
+template <typename T, int SB, int NF, int NFAR, bool GH>
 static const void *fused_kernel_g(bool nt, bool list) {
-  return nt ? (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, true, true, GH>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, true, false, GH>))
-            : (list ? CGX_K(k_spmv_dia_h<T, NF, NFAR, false, true, GH>)
-                    : CGX_K(k_spmv_dia_h<T, NF, NFAR, false, false, GH>));
+  return nt ? (list ? CGX_K(k_spmv_dia_h<T, SB, NF, NFAR, true, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, SB, NF, NFAR, true, false, GH>))
+            : (list ? CGX_K(k_spmv_dia_h<T, SB, NF, NFAR, false, true, GH>)
+                    : CGX_K(k_spmv_dia_h<T, SB, NF, NFAR, false, false, GH>));
 }
 
-template <typename T, int NF, int NFAR>
+template <typename T, int SB, int NF, int NFAR>
 static const void *fused_kernel(bool nt, bool list, bool gh) {
-  return gh ? fused_kernel_g<T, NF, NFAR, true>(nt, list)
-            : fused_kernel_g<T, NF, NFAR, false>(nt, list);
+  return gh ? fused_kernel_g<T, SB, NF, NFAR, true>(nt, list)
+            : fused_kernel_g<T, SB, NF, NFAR, false>(nt, list);
 }
+
+// Slices per fused workgroup: two (512 threads, one window for both) when
+// the halo rows exceed a slice -- C4 and its slabs (hl + hr = 800): the
+// window re-reads 1.78x instead of 2.56x the rows, 672-681 vs 702 us per
+// launch; at C3 (432) one slice per workgroup stays faster (106-107 vs
+// 109-110 us; tools/ab_probe.sh, same box, alternating).
+static int fuse_slices(int hl, int hr) { return hl + hr > kDiaSliceRows ? 2 : 1; }
 
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev) {
-  const int g = spmv_grid(a);
-  if (g <= 0) return hipSuccess;
-  if (a.layout != L_DIA || a.cb > 4) return hipErrorInvalidValue;
-  const int wn = kDiaSliceRows + a.hl + a.hr;
-  const int nf = (wn + 511) / 512;
+  if (a.items.count <= 0) return hipSuccess;
+  const int sb = fuse_slices(a.hl, a.hr);
+  const int g = sb == 1 ? a.items.count
+                        : a.items.pairs ? a.items.npairs : (a.items.count + 1) / 2;  // super-items
+  if (a.layout != L_DIA || a.cb > 4 || g <= 0) return hipErrorInvalidValue;
+  const int wn = sb * kDiaSliceRows + a.hl + a.hr;  // the widest window
+  const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
   int nfar = 0;
   for (int q = 0; q < 4; ++q) nfar += a.fark[q] >= 0;
-  if (nf > 5) return hipErrorInvalidValue;
+  if (nf > (sb == 1 ? 5 : 3)) return hipErrorInvalidValue;
   const bool nt = a.nt != 0, l = a.items.list != nullptr, gh = f.ghost != 0;
   const void *k = nullptr;
-  switch ((nf <= 2 ? 2 : nf <= 3 ? 3 : 5) * 10 + (nfar == 0 ? 0 : nfar <= 2 ? 2 : 4)) {
-    case 20: k = fused_kernel<T, 2, 0>(nt, l, gh); break;
-    case 22: k = fused_kernel<T, 2, 2>(nt, l, gh); break;
-    case 24: k = fused_kernel<T, 2, 4>(nt, l, gh); break;
-    case 30: k = fused_kernel<T, 3, 0>(nt, l, gh); break;
-    case 32: k = fused_kernel<T, 3, 2>(nt, l, gh); break;
-    case 34: k = fused_kernel<T, 3, 4>(nt, l, gh); break;
-    case 50: k = fused_kernel<T, 5, 0>(nt, l, gh); break;
-    case 52: k = fused_kernel<T, 5, 2>(nt, l, gh); break;
-    case 54: k = fused_kernel<T, 5, 4>(nt, l, gh); break;
+  const int nfc = nf <= 2 ? 2 : nf <= 3 ? 3 : 5;
+  switch (sb * 100 + nfc * 10 + (nfar == 0 ? 0 : nfar <= 2 ? 2 : 4)) {
+    case 120: k = fused_kernel<T, 1, 2, 0>(nt, l, gh); break;
+    case 122: k = fused_kernel<T, 1, 2, 2>(nt, l, gh); break;
+    case 124: k = fused_kernel<T, 1, 2, 4>(nt, l, gh); break;
+    case 130: k = fused_kernel<T, 1, 3, 0>(nt, l, gh); break;
+    case 132: k = fused_kernel<T, 1, 3, 2>(nt, l, gh); break;
+    case 134: k = fused_kernel<T, 1, 3, 4>(nt, l, gh); break;
+    case 150: k = fused_kernel<T, 1, 5, 0>(nt, l, gh); break;
+    case 152: k = fused_kernel<T, 1, 5, 2>(nt, l, gh); break;
+    case 154: k = fused_kernel<T, 1, 5, 4>(nt, l, gh); break;
+    case 220: k = fused_kernel<T, 2, 2, 0>(nt, l, gh); break;
+    case 222: k = fused_kernel<T, 2, 2, 2>(nt, l, gh); break;
+    case 224: k = fused_kernel<T, 2, 2, 4>(nt, l, gh); break;
+    case 230: k = fused_kernel<T, 2, 3, 0>(nt, l, gh); break;
+    case 232: k = fused_kernel<T, 2, 3, 2>(nt, l, gh); break;
+    case 234: k = fused_kernel<T, 2, 3, 4>(nt, l, gh); break;
     default: return hipErrorInvalidValue;
   }
   void *args[] = {(void *)&a, (void *)&f};
-  const size_t lds = (size_t)wn * sizeof(T) + 16;
+  // the window's allocation, plus the pair an inactive thread of a one-slice
+  // super-item reads past it
+  const size_t lds = (size_t)(wn + 2) * sizeof(T) + 16;
   if (ev.start || ev.stop)
-    (void)hipExtLaunchKernel(k, dim3(g), dim3(256), args, lds, st, ev.start, ev.stop, 0);
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st, ev.start, ev.stop, 0);
   else
-    (void)hipLaunchKernel(k, dim3(g), dim3(256), args, lds, st);
+    (void)hipLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st);
   return hipGetLastError();
 }
 

@@ -406,6 +406,18 @@ std::vector<int> tile_order(const std::vector<int> &item_row, long long P, size_
 
 }  // namespace
 
+std::vector<int> fuse_pairs(const std::vector<int> &slices) {
+  std::vector<int> p;
+  const int m = (int)slices.size();
+  for (int i = 0; i < m;) {
+    const int c = i + 1 < m && slices[(size_t)i + 1] == slices[(size_t)i] + 1 ? 2 : 1;
+    p.push_back(i);
+    p.push_back(c);
+    i += c;
+  }
+  return p;
+}
+
 std::vector<int> plan_rowblocks(int n, const int *rp, int rows, int cap) {
   std::vector<int> blk;
   blk.reserve((size_t)n / 48 + 2);
@@ -446,6 +458,8 @@ void DevMatrix::release() {
   dev_free(&d_dcode);
   dev_free(&d_vtab);
   dev_free(&d_order);
+  dev_free(&d_fpairs);
+  n_fpairs = 0;
   order.clear();
   blk_row.clear();
   panel_first.clear();
@@ -818,11 +832,17 @@ int DevMatrix::finish_upload(double t0) {
     const std::vector<int> ir = item_rows();
     order = tile_order(ir, P, ts, tile_bands);
     if (!order.empty()) {
-      if ((rc = dev_alloc(&d_order, order.size() * 4, &dev_bytes))) {
+      // DIA: the fused step's super-items (adjacent slices of the order)
+      const std::vector<int> fp = layout == L_DIA ? fuse_pairs(order) : std::vector<int>{};
+      if ((rc = dev_alloc(&d_order, order.size() * 4, &dev_bytes)) ||
+          (!fp.empty() && (rc = dev_alloc(&d_fpairs, fp.size() * 4, &dev_bytes)))) {
         release();
         return rc;
       }
       CGX_HIP(hipMemcpyAsync(d_order, order.data(), order.size() * 4, hipMemcpyHostToDevice, st));
+      if (!fp.empty())
+        CGX_HIP(hipMemcpyAsync(d_fpairs, fp.data(), fp.size() * 4, hipMemcpyHostToDevice, st));
+      n_fpairs = (int)fp.size() / 2;
       CGX_HIP(hipStreamSynchronize(st));
     }
   }

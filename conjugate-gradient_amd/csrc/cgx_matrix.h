@@ -94,7 +94,10 @@ struct DevMatrix {
 
   template <typename T>
   SpmvArgs<T> args(const T *x, T *y, double *part, const int *done, Items it) const;
-  Items all_items() const { return Items{d_order, 0, items()}; }
+  // the fused step's super-items of the tiled order (d_order's adjacent pairs)
+  int *d_fpairs = nullptr;
+  int n_fpairs = 0;
+  Items all_items() const { return Items{d_order, 0, items(), d_fpairs, n_fpairs}; }
   // One SpMV (panels: one launch per panel, rows continuing their sums;
   // the epilogue partials on the last panel).  Returns the partial count.
   // ev: timing events around the whole SpMV (start on its first launch,
