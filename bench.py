@@ -668,9 +668,14 @@ def run_dist(args, wl_name, world, rank, local_rank):
     # ranks) picks
     trial = {}
     algs = {"hs": cgx.CGX_ALG_HS, "sr": cgx.CGX_ALG_SR, "cg1": cgx.CGX_ALG_CG1}
+    refused = {}
     for name in ([args.alg] if args.alg else ["hs", "sr", "cg1"]):
         s.set_alg(algs[name])
-        s.bench_prepare(3)
+        try:
+            s.bench_prepare(3)  # collective: every rank refuses SR alike (no fused step)
+        except cgx.CgxError as e:
+            refused[name] = str(e)
+            continue
         dist.barrier()
         trial[name] = round(allmax(s.bench_run(20)[0] / 20), 4)
     alg = min(trial, key=trial.get)
@@ -717,6 +722,7 @@ def run_dist(args, wl_name, world, rank, local_rank):
             data="synthetic",
             config=dict(workload=wl["desc"], n=sysm["n_global"], rows_per_rank=info["n_loc"],
                         nnz_rank0=info["nnz"], alg=alg, alg_trial_ms_per_iter=trial,
+                        alg_refused=refused or None, fuse_status=info["fuse_status"],
                         graph=info["graph"], fused=info["fused"],
                         parallelism=f"row-partition x{world} (RCCL)",
                         scaling_curve="the same workload at every N (N = 1: the "
