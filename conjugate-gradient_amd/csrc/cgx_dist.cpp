@@ -117,7 +117,7 @@ struct cgx_dist {
   std::vector<int> send_count, send_off, recv_count, recv_off;
   int n_send = 0;
   double *d_pa = nullptr, *d_pb = nullptr;
-  double *d_pss = nullptr;  // SR: the fused launches' (p.s, s.s) partial pairs (2x d_pb's offsets)
+  double *d_pss = nullptr;  // SR: the fused launches' (p.s, s.s) pairs, one per workgroup
   double *d_sums = nullptr, *d_gsums = nullptr;  // [0, 4) local, [4, 8) all-reduced
   unsigned *d_tick = nullptr;                    // last-arriver counters
   int vec_grid = 1;
@@ -622,6 +622,11 @@ int phase_spmv(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
   const int np = d->g_int + d->g_bnd;
+  // SR: the fused launches write one (p.s, s.s) pair per workgroup
+  auto fgrid = [&](const Items &it) {
+    return it.count ? fused_grid(d->A.args<double>(nullptr, nullptr, nullptr, nullptr, it)) : 0;
+  };
+  const int gi = sr(d) ? fgrid(d->it_int) : 0, gb = sr(d) ? fgrid(d->it_bnd) : 0;
   // rec: kernel timing events (hipExtLaunchKernel) of the two launches; an
   // empty launch records both of its events on the stream instead
   auto launch = [&](const Items &it, double *part, int e) -> hipError_t {
@@ -648,7 +653,7 @@ int phase_spmv(cgx_dist *d) {
       const int pub = (e == 0 || d->it_int.count == 0) ? 1 : 0;
       const FuseArgs<double> f{d->d_x, p_old(d), p_new(d), d->d_r, d->d_st, d->d_hist,
                                rr_new_src(d), pub, e == 2 ? 1 : 0,
-                               sr(d) ? d->d_pss + 2 * (part - d->d_pb) : nullptr};
+                               sr(d) ? d->d_pss + (e == 2 ? 2 * gi : 0) : nullptr};
       return launch_spmv_fused<double>(a, f, d->st, ev);
     }
     return launch_spmv<double>(a, d->st, ev);
@@ -668,8 +673,8 @@ int phase_spmv(cgx_dist *d) {
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
   if (sr(d))  // p.s, s.s, and r.r of the last r update (the prologue's b.b at first)
-    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pss, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
-                            d->st, d->d_pa, d->vec_grid));
+    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pss, gi + gb, nullptr, 0, d->d_st, d->d_hist,
+                            d->d_sums, d->st, d->d_pa, d->vec_grid));
   else if (d->alg == CGX_ALG_HS)
     CGX_HIP(launch_finalize(FIN_SUM, d->d_pb, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
                             d->st));

@@ -268,8 +268,8 @@ struct FuseArgs {
   const double *rr_new;  // r.r of the last r update (&st->rr_new, or all-reduced)
   int publish;           // this launch's workgroup 0 writes the scalar state back
   int ghost;             // columns >= n are ghosts: p_new from pnew's ghost tail
-  double *ss;            // CGX_ALG_SR: (p.s, s.s) partial pairs, ss[2 b], ss[2 b + 1],
-                         // instead of a.part (nullptr: none)
+  double *ss;            // CGX_ALG_SR: one (p.s, s.s) pair per workgroup, ss[2 b],
+                         // ss[2 b + 1], instead of a.part (nullptr: none)
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
@@ -300,6 +300,9 @@ template <typename T>
 hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev = LaunchEv{});
 // The fused HS step on a DIA layout (a.x unused, a.y = s, a.part the
 // p_new.s partials).
+// Workgroups of the fused launch (= SR (p.s, s.s) pairs it writes)
+template <typename T>
+int fused_grid(const SpmvArgs<T> &a);
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev = LaunchEv{});

@@ -271,9 +271,10 @@ __device__ __forceinline__ int xcd_slot(int L, int G) {
 }
 
 // The fused step's epilogue (SB slices of 256 threads): per slice the p.s
-// partial (and with ss the (p.s, s.s) pair) summed over its four waves in
-// order -- epi_store<4> of a 256-thread workgroup -- written at
-// xcd_slot(pos + h, G), the unfused k_spmv_dia's slot for it.
+// partial summed over its four waves in order -- epi_store<4> of a
+// 256-thread workgroup -- written at xcd_slot(pos + h, G), the unfused
+// k_spmv_dia's slot for it.  With ss (CGX_ALG_SR): one (p.s, s.s) pair per
+// workgroup at blockIdx (fused_grid(a) pairs per launch).
 template <int SB>
 __device__ __forceinline__ void epi_store_slices(double dot, double dot2, double *ss, double *part,
                                                  int pos, int cnt, int G) {
@@ -287,17 +288,24 @@ __device__ __forceinline__ void epi_store_slices(double dot, double dot2, double
     red[1][wid] = dot2;
   }
   __syncthreads();
+  if (ss) {  // SR (no unfused twin to match): ONE pair per workgroup, at blockIdx
+    if (threadIdx.x == 0) {
+      double sa = red[0][0], sb = red[1][0];
+#pragma unroll
+      for (int v = 1; v < NW; ++v) {
+        sa = sa + red[0][v];
+        sb = sb + red[1][v];
+      }
+      reinterpret_cast<double2 *>(ss)[blockIdx.x] = make_double2(sa, sb);
+    }
+    return;
+  }
   const int h = threadIdx.x / kWave;  // thread 0 of wave h sums slice h
   if (lane == 0 && h < cnt) {
-    double sa = red[0][4 * h], sb = red[1][4 * h];
+    double sa = red[0][4 * h];
 #pragma unroll
-    for (int v = 1; v < 4; ++v) {
-      sa = sa + red[0][4 * h + v];
-      sb = sb + red[1][4 * h + v];
-    }
-    const int slot = xcd_slot(pos + h, G);
-    if (ss) reinterpret_cast<double2 *>(ss)[slot] = make_double2(sa, sb);
-    else part[slot] = sa;
+    for (int v = 1; v < 4; ++v) sa = sa + red[0][4 * h + v];
+    part[xcd_slot(pos + h, G)] = sa;
   }
 }
 
@@ -2146,12 +2154,18 @@ static const void *fused_kernel(bool nt, bool list, bool gh) {
 static int fuse_slices(int hl, int hr) { return hl + hr > kDiaSliceRows ? 2 : 1; }
 
 template <typename T>
+int fused_grid(const SpmvArgs<T> &a) {
+  if (a.items.count <= 0) return 0;
+  if (fuse_slices(a.hl, a.hr) == 1) return a.items.count;
+  return a.items.pairs ? a.items.npairs : (a.items.count + 1) / 2;  // super-items
+}
+
+template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev) {
   if (a.items.count <= 0) return hipSuccess;
   const int sb = fuse_slices(a.hl, a.hr);
-  const int g = sb == 1 ? a.items.count
-                        : a.items.pairs ? a.items.npairs : (a.items.count + 1) / 2;  // super-items
+  const int g = fused_grid(a);
   if (a.layout != L_DIA || a.cb > 4 || g <= 0) return hipErrorInvalidValue;
   const int wn = sb * kDiaSliceRows + a.hl + a.hr;  // the widest window
   const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
@@ -2397,6 +2411,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
 #define CGX_INSTANTIATE(T)                                                                       \
   template int spmv_grid<T>(const SpmvArgs<T> &);                                                \
   template hipError_t launch_spmv<T>(const SpmvArgs<T> &, hipStream_t, const LaunchEv &);      \
+  template int fused_grid<T>(const SpmvArgs<T> &);                                               \
   template hipError_t launch_spmv_fused<T>(const SpmvArgs<T> &, const FuseArgs<T> &, hipStream_t, \
                                            const LaunchEv &);                                    \
   template hipError_t launch_init_hs<T>(int, const T *, T *, T *, T *, double *, int,            \
