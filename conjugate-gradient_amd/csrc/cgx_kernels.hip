@@ -45,11 +45,6 @@ template <> struct Vec16<float> {
   static constexpr int W = 4;
 };
 
-// Kernel experiments (A/B builds only: tools/ab_build.sh; 0 in the product)
-#ifndef CGX_EXP
-#define CGX_EXP 0
-#endif
-
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_down(v, off, kWave);

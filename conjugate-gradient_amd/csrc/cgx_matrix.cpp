@@ -799,9 +799,6 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     }
     for (int v : off) csr_reach = std::max(csr_reach, (long long)std::abs(v));
   }
-#if defined(CGX_EXP) && (CGX_EXP & 4)
-  csr_reach = 0;  // A/B: natural block order for plain CSR
-#endif
   return finish_upload(t0);
 }
 

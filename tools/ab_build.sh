@@ -1,8 +1,11 @@
 #!/bin/bash
 # tools/ab_build.sh <exp> -- a variant libcgx.so for same-box A/B timing:
-# every source compiled with -DCGX_EXP=<exp> (the product builds CGX_EXP=0:
-# kernel and host experiments behind that mask); output ab/<exp>/libcgx.so.
-# Use it through cgx.py's CGX_LIB, or tools/ab_probe.sh.
+# every source compiled with -DCGX_EXP=<exp>; an experiment puts its variant
+# behind `#if CGX_EXP & bit` while it is measured (the product never defines
+# CGX_EXP; round 3's experiments -- p_new stores, CSR tiling -- were removed
+# after their A/B); output ab/<exp>/libcgx.so.  Use it through
+# cgx.py's CGX_LIB, or tools/ab_probe.sh.  To compare against the last commit:
+# copy its libcgx.so to ab/0/ before rebuilding.
 set -eu
 cd "$(dirname "$0")/../conjugate-gradient_amd"
 exp=$1
