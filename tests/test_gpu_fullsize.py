@@ -131,7 +131,9 @@ def c4_single(alg, maxit):
 def test_c4_partitioned_8_slabs_in_process():
     """C4 as it runs at N = 8 (8 M rows per partition, 9 DIA diagonals incl.
     the ghost faces, halo = one 400^2 plane per neighbour), all 8 partitions
-    on one GPU: the multi-GPU phase code at the full BASELINE shape."""
+    on one GPU: the multi-GPU phase code at the full BASELINE shape -- fused
+    and unfused HS bit-identical, within 1e-12 of the single-GPU solver; CG1
+    within 1e-9; SR within 1e-10."""
     its_f, x_f, h_f, st_f = c4_group(cgx.CGX_ALG_HS, True, 10)
     its_u, x_u, h_u, st_u = c4_group(cgx.CGX_ALG_HS, False, 10)
     assert all(s["fused"] == 1 and s["layout_name"] == "dia" for s in st_f)
@@ -149,6 +151,12 @@ def test_c4_partitioned_8_slabs_in_process():
     assert its_c == its_c1 == 11
     assert rel(x_c, x_c1) <= 1e-9
     assert rel(x_c, x1) <= 1e-9
+    # SR (one all-reduce per iteration; two-slice fused workgroups at this
+    # halo): the HS recurrence up to how r_new.r_new is formed
+    its_s, x_s, _, st_s = c4_group(cgx.CGX_ALG_SR, "auto", 10)
+    assert all(s["fused"] == 1 and s["alg"] == cgx.CGX_ALG_SR for s in st_s)
+    assert its_s == 11
+    assert rel(x_s, x1) <= 1e-10
 
 
 @pytest.fixture(scope="module")
