@@ -153,6 +153,9 @@ KERNELS = {
     "dia": "k_spmv_dia (DIA-VI: value-indexed diagonal codes, two rows per thread, pair loads of x)",
     "dia_fused": "k_spmv_dia_h (fused HS step on DIA-VI: x / p update of the previous iteration, "
                  "p of the slice + halo in an LDS window, s = A p, p.s partials)",
+    "dia_march": "k_spmv_dia_m (fused HS step on DIA-VI as a plane march: a workgroup walks "
+                 "slices nx*ny apart, p of three consecutive slices + halos in an LDS ring, "
+                 "x / p update, s = A p, p.s partials)",
     "dc": "k_spmv_dc (LDS-DMA code window + value window per 64-row block, dictionary-coded columns)",
     "csr": "k_spmv_csr (LDS-DMA val/col window per 64-row block, lane-per-row sums from LDS)",
     "panel": "k_spmv_csr over column panels",
@@ -162,7 +165,7 @@ KERNELS = {
 
 def kernel_name(info):
     if info["layout_name"] == "dia" and info.get("fused"):
-        return KERNELS["dia_fused"]
+        return KERNELS["dia_march" if info.get("fuse_march") else "dia_fused"]
     return KERNELS.get(info["layout_name"], info["layout_name"])
 
 

@@ -56,7 +56,7 @@ class CgxInfo(ctypes.Structure):
                 ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double),
                 ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int),
                 ("fused", ctypes.c_int), ("fuse_status", ctypes.c_int),
-                ("breakdown", ctypes.c_int)]
+                ("breakdown", ctypes.c_int), ("fuse_march", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):
@@ -105,6 +105,7 @@ _SIGS = {
     "cgx_solver_set_mode": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "cgx_solver_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_solver_set_march": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_matrix": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                              _i32p, _i32p, _f64p]),
     "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
@@ -352,6 +353,11 @@ class Solver:
         """Fused HS step on DIA layouts (cgx_solver_set_fused): "auto",
         True (wherever the layout takes it) or False."""
         check(lib().cgx_solver_set_fused(self._h, fuse_mode(mode)), "set_fused")
+
+    def set_march(self, steps=-1):
+        """Plane march of the fused HS step (cgx_solver_set_march): -1 auto,
+        0 off (the per-slice fused kernel), > 0 slices of a chain per workgroup."""
+        check(lib().cgx_solver_set_march(self._h, int(steps)), "set_march")
 
     def set_layout(self, layout):
         """CGX_LAYOUT_* (or its name) for the next set_matrix / gen_laplacian."""

@@ -246,6 +246,13 @@ struct SpmvArgs {
   int hl, hr;
   unsigned near;
   int fark[4];      // the far (not near) diagonals, -1: unused slot
+  // plane march of the fused step (k_spmv_dia_m; DevMatrix::plan_march):
+  // every far diagonal is +-F, F within the halo of mq slices; chains of
+  // msb-slice super-items j0, j0 + mq, ... (mchains of them, j0 = msb c);
+  // mws: LDS ring slot stride (entries); mpos: slice -> position in mlist
+  // (the item order its partial slots follow; nullptr: natural order)
+  int mq, msb, mchains, mslices, mws, mlen;
+  const int *mpos, *mlist;
   // stencil
   LapSpec lap;
   double inv_nx, inv_pl;  // 1 / nx, 1 / (nx ny): exact floor divisions (fdiv)
@@ -270,6 +277,7 @@ struct FuseArgs {
   int ghost;             // columns >= n are ghosts: p_new from pnew's ghost tail
   double *ss;            // CGX_ALG_SR: one (p.s, s.s) pair per workgroup, ss[2 b],
                          // ss[2 b + 1], instead of a.part (nullptr: none)
+  int march = 0;         // plane march (k_spmv_dia_m): steps per segment, 0: off
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one

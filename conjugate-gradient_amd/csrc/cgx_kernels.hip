@@ -935,6 +935,222 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs
   epi_store_slices<SB>(dot, dot2, f.ss, a.part, pos, cnt, a.items.count);
 }
 
+// ------------------------------------- fused HS step, plane march (DIA-VI)
+// k_spmv_dia_h's iteration with its far diagonals read from LDS instead of
+// gathered.  When every far diagonal is +F or -F and F = Q * 512 + e with
+// |e| <= the window's halo (C3: F = 46,656 = 91 * 512 + 64, halo 216; C4:
+// 160,000 = 312 * 512 + 256, halo 400), the rows F away from super-item j
+// lie inside the WINDOW of super-item j +- Q.  A workgroup therefore walks a
+// chain of super-items j0, j0 + Q, j0 + 2Q, ... (a column of the grid for a
+// 3-D stencil), keeping three windows of p_new in an LDS ring: step m reads
+// its near diagonals from window m and the -F / +F ones from windows m - 1
+// and m + 1, so each p_new of the chain is computed once and no r / p_old
+// gather is issued for the far diagonals (the unit profile of k_spmv_dia_h,
+// profiles/r03_c4_units.md: vector-memory-instruction-bound, the far slots
+// ~40 % of its loads).  The loads of window m + 2 are in flight while step m
+// computes.  A chain is cut into segments of a.mlen steps (a workgroup each;
+// a segment computes its two neighbouring windows as well).  Every value is
+// k_spmv_dia_h's -- same roundings, the row's diagonal order -- and each
+// slice's p.s partial is the sum of its four waves in order at the slot the
+// one-workgroup-per-slice launch writes it (a.mpos: slice -> list position),
+// so x and the r.r history stay bit-identical to the unfused path.  Single
+// GPU only (no ghosts, no SR pairs): launch_spmv_fused checks.
+// The two rows' code words as loaded (CB bytes each), split by code_split
+// only where they are used: ALU work on a loaded value before a later load
+// would make the wave wait for the value right there (k_spmv_dia_m).
+template <int CB>
+struct CodeRaw {
+  typedef typename std::conditional<CB == 4, uint2, unsigned>::type type;
+};
+
+template <int CB>
+__device__ __forceinline__ typename CodeRaw<CB>::type ld_code_raw(const unsigned char *code, int r) {
+  const unsigned char *p = code + (long long)r * CB;
+  if constexpr (CB == 1) return *reinterpret_cast<const unsigned short *>(p);
+  else if constexpr (CB == 2) return *reinterpret_cast<const unsigned *>(p);
+  else return *reinterpret_cast<const uint2 *>(p);
+}
+
+template <int CB>
+__device__ __forceinline__ void code_split(typename CodeRaw<CB>::type w, unsigned &c0,
+                                           unsigned &c1) {
+  if constexpr (CB == 1) {
+    c0 = w & 0xffu;
+    c1 = w >> 8;
+  } else if constexpr (CB == 2) {
+    c0 = w & 0xffffu;
+    c1 = w >> 16;
+  } else {
+    c0 = w.x;
+    c1 = w.y;
+  }
+}
+
+template <typename T, int SB, int NF, int CB>
+__global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs<T> f) {
+  constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  T *ring = reinterpret_cast<T *>(dyn_lds);
+  __shared__ T lv[kDiaMax * 16];
+  __shared__ double red[4 * SB];
+  typedef typename Pair<T>::type P;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int w = xcd_block();
+  const int chain = w % a.mchains, seg = w / a.mchains;
+  const int j0 = chain * SB;
+  const int msteps = (a.mslices - j0 + a.mq - 1) / a.mq;
+  const int m0 = seg * f.march, m1 = min(m0 + f.march, msteps);
+  if (f.st->done > 1) return;  // uniform
+  const FuseStep fs = fuse_step(f.st, f.hist, f.rr_new, f.publish != 0);
+  const T alpha = (T)fs.alpha, beta = (T)fs.beta;
+  const int k = f.st->k_u;
+  const bool odd = (k & 1) != 0;
+  const bool xup = !fs.first && (odd || fs.stop);
+  const T alpha_d = (T)f.st->alpha_def;
+  if (f.publish && !fs.first && !odd && !fs.stop && blockIdx.x == 0 && t == 0)
+    f.st->alpha_def = fs.alpha;
+  if (m0 >= m1) return;  // uniform (workgroup 0 always has steps: it publishes above)
+  const int QR = a.mq * kDiaSliceRows;  // rows between the steps of a chain
+  const int padn = a.mslices * kDiaSliceRows;
+  const bool nt = a.nt != 0;
+  const int wn = SR + a.hl + a.hr, ws = a.mws;
+  auto base_of = [&](int m) { return (j0 + m * a.mq) * kDiaSliceRows; };
+  auto slot = [&](int m) { return ring + ((m + 3) % 3) * ws; };
+  P wr[NF], wp[NF];
+  auto load_win = [&](int m) {
+    const int w0 = base_of(m) - a.hl;
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int j = min(max(w0 + 2 * t + q * 2 * BS, -1), a.ncols - 1);
+      wr[q] = ld_pair(f.r, j);
+      wp[q] = ld_pair(f.pold, j);
+    }
+  };
+  auto store_win = [&](int m) {
+    T *win = slot(m);
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int i = 2 * t + q * 2 * BS;
+      const P pn = fs.first ? wr[q] : p_next<T>(wr[q], wp[q], beta);
+      if (i < wn) win[i] = pn.x;
+      if (i + 1 < wn) win[i + 1] = pn.y;
+    }
+  };
+  // the x update's operands of step m's rows (p_old, x, and on odd launches
+  // p_{k-1} from the p_new buffer)
+  struct XOps {
+    P po, xo, pd;
+  };
+  auto load_x = [&](int m, XOps &o) {
+    const int r = base_of(m) + 2 * t, rs = r < a.n ? r : 0;
+    o.po = ld_pair(f.pold, rs);
+    o.xo = ld_pair(f.x, rs);
+    if (odd) o.pd = ld_pair((const T *)f.pnew, rs);
+  };
+  auto x_update = [&](const XOps &o, int r, int rend) {
+    T x0 = o.xo.x, x1 = o.xo.y;
+    if (odd) {
+      const T d0 = alpha_d * o.pd.x, d1 = alpha_d * o.pd.y;
+      x0 = x0 + d0;
+      x1 = x1 + d1;
+    }
+    const T a0 = alpha * o.po.x, a1 = alpha * o.po.y;
+    st_pair(f.x, r, rend, x0 + a0, x1 + a1, false);
+  };
+  XOps xc{}, xn{};
+  if (fs.stop) {  // the pending x updates only (then the cg.c:125 break)
+    if (xup)
+      for (int m = m0; m < m1; ++m) {
+        const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + SR);
+        load_x(m, xc);
+        if (r < rend) x_update(xc, r, rend);
+      }
+    return;
+  }
+  // Issue order matters: vector-memory operations retire in order (s_waitcnt
+  // vmcnt), so a value is waited for together with everything issued before
+  // it.  The codes, slot position and x operands of step m + 1 are therefore
+  // issued during step m BEFORE window m + 2's loads, and used in step m + 1,
+  // after window m + 1's wait has covered them: no step waits on the window
+  // prefetch in flight.
+  typedef typename CodeRaw<CB>::type CR;
+  auto codes_at = [&](int m, CR &cw, int &ps) {
+    const int r = base_of(m) + 2 * t;
+    cw = ld_code_raw<CB>(a.dcode, r < padn ? r : base_of(m));  // past the last slice: none
+    const int js = min(j0 + m * a.mq + min(wid, SB - 1), a.mslices - 1);
+    ps = a.mpos ? a.mpos[js] : js;
+  };
+  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
+  CR cw, cwn{};
+  int ps, psn = 0;
+  codes_at(m0, cw, ps);
+  if (xup) load_x(m0, xc);
+  load_win(m0 - 1);
+  store_win(m0 - 1);
+  load_win(m0);
+  store_win(m0);
+  load_win(m0 + 1);
+  if (t < a.ndiag * 16) lv[t] = tv;
+  const int G = a.items.count;
+  // One step; its operands (codes, slot position, x operands) arrive in the
+  // "cur" set and the next step's are loaded into the "nxt" set.  The loop
+  // below alternates the two register sets (no copies: a copy of a value
+  // still in flight would wait for the window prefetch behind it).
+  auto step = [&](int m, const CR &ccw, int &cps, XOps &cx, CR &ncw, int &nps, XOps &nx) {
+    store_win(m + 1);
+    // unconditional (past the segment: a reload of its last step / window,
+    // L2 hits): a load under a branch leaves a merge that the compiler
+    // resolves right away, i.e. a wait on everything in flight
+    codes_at(min(m + 1, m1 - 1), ncw, nps);
+    load_win(min(m + 2, m1));  // in flight during step m
+    if (xup && m + 1 < m1) load_x(m + 1, nx);
+    __syncthreads();
+    const int base = base_of(m), r = base + 2 * t;
+    const int rend = min(a.n, base + SR);
+    const T *cur = slot(m), *prv = slot(m - 1), *nxt = slot(m + 1);
+    const int rw = 2 * t + a.hl;
+    unsigned cc0, cc1;
+    code_split<CB>(ccw, cc0, cc1);
+    T a0 = T(0), a1 = T(0);
+#pragma unroll
+    for (int kk = 0; kk < kDiaMax; ++kk) {
+      if (kk < a.ndiag) {
+        const int d = a.doff[kk];
+        const T *src = (a.near >> kk) & 1u ? cur : d < 0 ? prv : nxt;
+        const int i = (a.near >> kk) & 1u ? rw + d : d < 0 ? rw + d + QR : rw + d - QR;
+        const T v0 = src[i], v1 = src[i + 1];
+        const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
+        const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
+        a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
+        a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
+      }
+    }
+    const T pn0 = cur[rw], pn1 = cur[rw + 1];
+    double dot = 0.0;
+    if (r < rend) {
+      st_pair(a.y, r, rend, a0, a1, nt);
+      st_pair(f.pnew, r, rend, pn0, pn1, false);
+      if (xup) x_update(cx, r, rend);
+      dot = (double)pn0 * (double)a0;
+      if (r + 1 < rend) dot = dot + (double)pn1 * (double)a1;
+    }
+    // per slice: its four waves' sums in order, at the slice's slot
+    dot = wave_sum(dot);
+    if (lane == 0) red[wid] = dot;
+    __syncthreads();  // also: every read of window m - 1's slot is done before step m + 1 refills it
+    if (lane == 0 && wid < SB && j0 + m * a.mq + wid < a.mslices) {
+      double sa = red[4 * wid];
+#pragma unroll
+      for (int v = 1; v < 4; ++v) sa = sa + red[4 * wid + v];
+      a.part[xcd_slot(cps, G)] = sa;
+    }
+  };
+  for (int m = m0; m < m1; m += 2) {
+    step(m, cw, ps, xc, cwn, psn, xn);
+    if (m + 1 < m1) step(m + 1, cwn, psn, xn, cw, ps, xc);
+  }
+}
+
 // ---------------------------------------- fused CG1 step (DIA-VI)
 // The Chronopoulos-Gear iteration in ONE launch: k_cg1_update's vector
 // recurrences (p = r + beta p; s = w + beta s; x += alpha p; r -= alpha s)
@@ -2155,10 +2371,62 @@ int fused_grid(const SpmvArgs<T> &a) {
   return a.items.pairs ? a.items.npairs : (a.items.count + 1) / 2;  // super-items
 }
 
+// The plane march applies: a planned chain structure (DevMatrix::plan_march),
+// the launch covers the matrix's own item order in full, no ghosts, no SR
+// pairs, and the caller allows it (FuseArgs::march = steps per segment).
+template <typename T>
+static bool march_applies(const SpmvArgs<T> &a, const FuseArgs<T> &f) {
+  return f.march > 0 && a.mq > 0 && !f.ghost && !f.ss && a.items.first == 0 &&
+         a.items.list == a.mlist && a.items.count == a.mslices;
+}
+
+template <typename T>
+int march_grid(const SpmvArgs<T> &a, int len) {
+  const int steps = (a.mslices + a.mq - 1) / a.mq;  // chain 0's, the longest
+  return a.mchains * ((steps + len - 1) / len);
+}
+
+template <typename T, int SB, int NF>
+static const void *march_kernel(int cb) {
+  return cb == 1 ? CGX_K(k_spmv_dia_m<T, SB, NF, 1>)
+                 : cb == 2 ? CGX_K(k_spmv_dia_m<T, SB, NF, 2>) : CGX_K(k_spmv_dia_m<T, SB, NF, 4>);
+}
+
+template <typename T>
+static hipError_t launch_march(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
+                               const LaunchEv &ev) {
+  const int sb = a.msb;
+  const int wn = sb * kDiaSliceRows + a.hl + a.hr;
+  const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
+  if (a.mws < wn + 2 || (sb != 1 && sb != 2) || nf > (sb == 1 ? 5 : 3))
+    return hipErrorInvalidValue;
+  const int nfc = nf <= 2 ? 2 : nf <= 3 ? 3 : 5;
+  const int cb = a.cb;
+  if (cb != 1 && cb != 2 && cb != 4) return hipErrorInvalidValue;
+  const void *k = nullptr;
+  switch (sb * 10 + nfc) {
+    case 12: k = march_kernel<T, 1, 2>(cb); break;
+    case 13: k = march_kernel<T, 1, 3>(cb); break;
+    case 15: k = march_kernel<T, 1, 5>(cb); break;
+    case 22: k = march_kernel<T, 2, 2>(cb); break;
+    case 23: k = march_kernel<T, 2, 3>(cb); break;
+    default: return hipErrorInvalidValue;
+  }
+  const int g = march_grid(a, f.march);
+  void *args[] = {(void *)&a, (void *)&f};
+  const size_t lds = (size_t)3 * a.mws * sizeof(T) + 16;  // the three-window ring
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st, ev.start, ev.stop, 0);
+  else
+    (void)hipLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev) {
   if (a.items.count <= 0) return hipSuccess;
+  if (march_applies(a, f)) return launch_march(a, f, st, ev);
   const int sb = fuse_slices(a.hl, a.hr);
   const int g = fused_grid(a);
   if (a.layout != L_DIA || a.cb > 4 || g <= 0) return hipErrorInvalidValue;

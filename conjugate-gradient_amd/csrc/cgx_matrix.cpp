@@ -459,7 +459,10 @@ void DevMatrix::release() {
   dev_free(&d_vtab);
   dev_free(&d_order);
   dev_free(&d_fpairs);
+  dev_free(&d_mpos);
   n_fpairs = 0;
+  mq = mchains = mws = mlen = 0;
+  msb = 1;
   order.clear();
   blk_row.clear();
   panel_first.clear();
@@ -843,6 +846,10 @@ int DevMatrix::finish_upload(double t0) {
       CGX_HIP(hipStreamSynchronize(st));
     }
   }
+  if ((rc = plan_march())) {
+    release();
+    return rc;
+  }
   // the matrix stream and y bypass the caches when the iteration's working
   // set (this layout's stream + five vectors) cannot stay in the 256 MiB
   // Infinity Cache anyway: the vectors then keep what residency there is
@@ -897,6 +904,67 @@ int DevMatrix::items() const {
 }
 
 int DevMatrix::padded_rows() const { return padded_rows_for(n); }
+
+// The plane march (k_spmv_dia_m, cgx_kernels.hip): every far diagonal is +F
+// or -F, and F = Q * 512 + e with e inside the window's halo on the side the
+// neighbour rows fall (+F: -hl <= e <= hr; -F: -hr <= e <= hl), so the rows F
+// away from a super-item lie in the window of the super-item Q slices away.
+// Two-slice super-items (wide halos, the fused step's rule) need Q even: the
+// chains j0 = 2c, c < Q / 2, then cover every slice once.  Segment length:
+// about 2,048 workgroups per launch (8 per CU), fewer than 1 in 8 windows
+// recomputed at a segment's ends at C3 / C4.
+int DevMatrix::plan_march() {
+  dev_free(&d_mpos);
+  mq = mchains = mws = mlen = 0;
+  msb = 1;
+  if (layout != L_DIA || dia.cbytes > 4 || n == 0) return 0;
+  int hl = 0, hr = 0, F = 0;
+  bool neg = false, pos = false;
+  for (int k = 0; k < dia.ndiag; ++k) {
+    const int d = dia.doff[k];
+    if (near_diag(k)) {
+      hl = std::max(hl, -d);
+      hr = std::max(hr, d);
+    } else {
+      if (F != 0 && std::abs(d) != F) return 0;
+      F = std::abs(d);
+      (d < 0 ? neg : pos) = true;
+    }
+  }
+  hl = (hl + 1) & ~1;  // as args()
+  if (F == 0) return 0;
+  const int sb = hl + hr > kDiaSliceRows ? 2 : 1;
+  auto fits = [&](long long q) {
+    const long long e = F - q * kDiaSliceRows;
+    if (q < 1) return false;
+    if (pos && (e < -hl || e > hr)) return false;
+    if (neg && (e < -hr || e > hl)) return false;
+    return true;
+  };
+  const long long q0 = F / kDiaSliceRows;
+  int Q = 0;
+  for (long long q : {q0, q0 + 1})
+    if (!Q && fits(q) && (sb == 1 || q % 2 == 0)) Q = (int)q;
+  if (!Q) return 0;
+  const int ns = items();
+  const int wn = sb * kDiaSliceRows + hl + hr;
+  if ((wn + 2 * 256 * sb - 1) / (2 * 256 * sb) > (sb == 1 ? 5 : 3)) return 0;
+  mq = Q;
+  msb = sb;
+  mchains = Q / sb;
+  mws = (wn + 3) & ~1;
+  const int steps = (ns + Q - 1) / Q;
+  const int nseg = std::max(1, std::min(steps, (2048 + mchains / 2) / mchains));
+  mlen = (steps + nseg - 1) / nseg;
+  if (!order.empty()) {
+    std::vector<int> p((size_t)ns);
+    for (int i = 0; i < ns; ++i) p[(size_t)order[(size_t)i]] = i;
+    int rc;
+    if ((rc = dev_alloc(&d_mpos, p.size() * 4, &dev_bytes))) return rc;
+    CGX_HIP(hipMemcpy(d_mpos, p.data(), p.size() * 4, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
 
 bool DevMatrix::near_diag(int k) const { return std::abs(dia.doff[k]) <= kHaloMax; }
 
@@ -981,6 +1049,14 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
       a.fark[nf++] = k;
     }
   a.hl = (a.hl + 1) & ~1;  // an even window start: aligned pair loads
+  a.mq = mq;
+  a.msb = msb;
+  a.mchains = mchains;
+  a.mslices = items();
+  a.mws = mws;
+  a.mlen = mlen;
+  a.mpos = d_mpos;
+  a.mlist = d_order;
   a.n = n;
   a.lap = lap;
   if (layout == L_STENCIL) {

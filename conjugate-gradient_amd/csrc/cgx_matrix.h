@@ -97,6 +97,13 @@ struct DevMatrix {
   // the fused step's super-items of the tiled order (d_order's adjacent pairs)
   int *d_fpairs = nullptr;
   int n_fpairs = 0;
+  // plane march of the fused step (k_spmv_dia_m): chain stride mq slices
+  // (0: no march), msb slices per super-item, mchains chains, LDS ring slot
+  // stride mws, mlen steps per segment (the default), d_mpos: slice ->
+  // position in d_order (nullptr: natural order)
+  int mq = 0, msb = 1, mchains = 0, mws = 0, mlen = 0;
+  int *d_mpos = nullptr;
+  int plan_march();
   Items all_items() const { return Items{d_order, 0, items(), d_fpairs, n_fpairs}; }
   // One SpMV (panels: one launch per panel, rows continuing their sums;
   // the epilogue partials on the last panel).  Returns the partial count.

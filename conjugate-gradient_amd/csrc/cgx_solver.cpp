@@ -128,6 +128,7 @@ struct cgx_solver {
   void *d_r2 = nullptr, *d_s2 = nullptr, *d_w2 = nullptr;
   int pbuf = 0;          // fused step: which buffer holds p_old (0: d_p) / r, s, w_old
   int fuse = CGX_FUSE_AUTO;  // cgx_solver_set_fused
+  int march = -1;            // cgx_solver_set_march: -1 auto, 0 off, > 0 steps per segment
   unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
   int part_cap = 0;
@@ -166,6 +167,14 @@ void drop_graph(cgx_solver *s) {
 bool fused(const cgx_solver *s) {
   return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
          (s->fuse == CGX_FUSE_ON || s->A.nt);
+}
+
+// Steps per segment of the fused HS step's plane march (k_spmv_dia_m), 0
+// when it does not run: the matrix plans one (DevMatrix::plan_march) and
+// cgx_solver_set_march has not turned it off.
+int march_len(const cgx_solver *s) {
+  if (!fused(s) || s->alg != CGX_ALG_HS || s->A.mq == 0 || s->march == 0) return 0;
+  return s->march > 0 ? s->march : s->A.mlen;
 }
 
 // Buffers alternating per iteration: p for the fused HS step and the
@@ -308,7 +317,8 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     // (cg.c:111-132)
     T *pold = (T *)(s->pbuf ? s->d_p2 : s->d_p), *pnew = (T *)(s->pbuf ? s->d_p : s->d_p2);
     const SpmvArgs<T> a = s->A.args<T>(nullptr, sv, s->d_pa, &s->d_st->done, s->A.all_items());
-    const FuseArgs<T> f{x, pold, pnew, r, s->d_st, s->d_hist, &s->d_st->rr_new, 1, 0, nullptr};
+    FuseArgs<T> f{x, pold, pnew, r, s->d_st, s->d_hist, &s->d_st->rr_new, 1, 0, nullptr};
+    f.march = march_len(s);
     np = s->A.partials(s->A.all_items());
     CGX_HIP(launch_spmv_fused<T>(a, f, st, LaunchEv{ev0, ev1}));
     const int gf = s->vec_grid / 4;
@@ -711,6 +721,13 @@ int cgx_solver_set_fused(cgx_solver *s, int mode) {
   return 0;
 }
 
+int cgx_solver_set_march(cgx_solver *s, int steps) {
+  if (!s || steps < -1) return CGX_EINVAL;
+  s->march = steps;
+  drop_graph(s);
+  return 0;
+}
+
 int cgx_solver_set_layout(cgx_solver *s, int layout) {
   if (!s || layout < CGX_LAYOUT_AUTO || layout > CGX_LAYOUT_PANEL) {
     cgx::set_error("set_layout: bad arguments");
@@ -865,6 +882,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                       : (s->fuse == CGX_FUSE_AUTO && !A.nt) ? CGX_FUSE_STATUS_CACHED
                                                             : CGX_FUSE_STATUS_RUNS;
   info->breakdown = s->h_st ? s->h_st->brk : 0;
+  info->fuse_march = s->have_matrix ? march_len(s) : 0;
   return 0;
 }
 

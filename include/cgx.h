@@ -172,6 +172,9 @@ typedef struct {
                            NaN (cg.c:113, 129) -- or 0.  Diagnostic only: the
                            iteration itself keeps the reference's IEEE
                            semantics (failure detection)        */
+  int fuse_march;       /* > 0: the fused HS step runs as a plane march
+                           (cgx_solver_set_march), this many steps per
+                           workgroup; 0: it does not                         */
 } cgx_info;
 
 /* cgx_info.fuse_status / cgx_dist_stats.fuse_status */
@@ -208,6 +211,16 @@ int  cgx_solver_set_mode(cgx_solver *s, int mode, int alg);
 #define CGX_FUSE_AUTO 1
 #define CGX_FUSE_ON   2
 int  cgx_solver_set_fused(cgx_solver *s, int mode);
+/* The fused HS step as a plane march: where every diagonal with |d| > 1024 is
+ * +F or -F and F lies within the in-plane halo of a multiple of 512 rows (a
+ * 3-D stencil's +-nx*ny planes: C3, C4), a workgroup walks a chain of slices
+ * F apart, keeping p of three consecutive slices (and their halos) in LDS, so
+ * the +-F neighbours are read from LDS instead of recomputed from r / p
+ * gathers.  Same values, same order: x and the r.r history are bit-identical
+ * to the unfused path.  steps: -1 auto (default; about 2,048 workgroups per
+ * launch), 0 off (the per-slice fused kernel), > 0 slices of a chain per
+ * workgroup.  cgx_info.fuse_march reports what runs. */
+int  cgx_solver_set_march(cgx_solver *s, int steps);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);
 /* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.

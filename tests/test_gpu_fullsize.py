@@ -59,6 +59,26 @@ def test_c3_fused_fast_path_vs_oracle(c3):
     assert np.allclose(hist, h_ref[:21], rtol=1e-10, atol=0)
 
 
+def test_c3_march_bit_identical_to_unfused(c3):
+    """The headline kernel at full C3 size: the plane-marching fused step
+    (chains of slices 91 apart over the L2-tiled item order's partial
+    slots) against the unfused three-launch iteration, 20 iterations: x and
+    the r.r history bit-identical."""
+    rp, col, val, b = c3
+    out = []
+    for fused in (True, False):
+        with cgx.Solver(0, fused=fused) as s:
+            s.set_matrix(rp, col, val)
+            i = s.info()
+            assert i["layout_name"] == "dia" and i["fused"] == int(fused)
+            assert (i["fuse_march"] > 0) == fused
+            s.set_rhs(b)
+            assert s.run(20) == 21
+            out.append((s.x(), s.history(21)))
+    assert H.same_bits_or_both_nan(out[0][0], out[1][0])
+    assert H.same_bits_or_both_nan(out[0][1], out[1][1])
+
+
 def test_c3_exact_mode_bit_identical(c3):
     """CGX_MODE_EXACT (sequential dots, the reference's summation order) at
     full C3 size: x bit-identical to the oracle after 6 SpMVs."""

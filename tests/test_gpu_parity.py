@@ -741,6 +741,57 @@ def test_fused_step_bit_identical_to_unfused(case):
     assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 1.01e-9 * np.linalg.norm(b)
 
 
+def march_cases():
+    # (name, system, two-slice super-items)
+    yield "lap3d_32x48x20", (*H.laplacian3d(32, 48, 20), None), False   # F 1536 = 3 slices
+    yield "lap3d_64x64x10", (*H.laplacian3d(64, 64, 10), None), False   # F 4096 = 8 slices
+    yield "lap3d_300x7x20", (*H.laplacian3d(300, 7, 20), None), True    # F 2100 = 4 * 512 + 52
+    yield "band_1_200_1100", band_sym_rhs(20000, [1, 200, 1100], 8), False  # 2 * 512 + 76
+
+
+@pytest.mark.parametrize("case", list(march_cases()), ids=lambda c: c[0])
+def test_fused_march_bit_identical_to_unfused(case):
+    """The plane march of the fused step (k_spmv_dia_m: a workgroup walks
+    slices F apart, the +-F neighbours read from an LDS ring of windows)
+    computes every value of the unfused iteration with the same roundings
+    and writes each slice's p.s partial at the unfused slot: x, iteration
+    counts and the r.r history bit-identical to the unfused path for every
+    segment length (1 step, a few, the auto length, whole chains), with
+    ragged last slices and chains of unequal length."""
+    _, (rp, col, val, b), two = case
+    n = len(rp) - 1
+    if b is None:
+        b = np.random.default_rng(11).standard_normal(n)
+    runs = [(0, 0.0), (1, 0.0), (16, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-9)]
+
+    def solve(fused, march):
+        res = []
+        with cgx.Solver(0, layout="dia", fused=fused) as s:
+            s.set_march(march)
+            s.set_matrix(rp, col, val)
+            info = s.info()
+            for maxit, tol in runs:
+                s.set_rhs(b)
+                its = s.run(maxit, tol)
+                res.append((its, s.x(), s.history(its)))
+            s.set_rhs(b)
+            s.bench_prepare(0)
+            s.bench_run(35 if fused else 34)
+            res.append((34, s.x(), None))
+        return info, res
+
+    _, ref = solve(False, -1)
+    for march in (-1, 1, 3, 100000, 0):
+        info, res = solve(True, march)
+        assert info["fused"] == 1
+        assert (info["fuse_march"] > 0) == (march != 0), (march, info["fuse_march"])
+        for j, ((i0, x0, h0), (i1, x1, h1)) in enumerate(zip(res, ref)):
+            assert i0 == i1, (march, j)
+            assert H.same_bits_or_both_nan(x0, x1), (march, j)
+            if h0 is not None:
+                assert H.same_bits_or_both_nan(h0, h1), (march, j)
+
+
 @pytest.mark.parametrize("name", ["lap2d_32", "lap3d_12", "rand_spd_2000", "dense128"])
 def test_cg1_within_tolerance(name):
     g = H.load_golden(name)
