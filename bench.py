@@ -98,7 +98,8 @@ def parse_args(argv=None):
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
                     help="default: c4 (every N: one strong-scaling curve)")
     ap.add_argument("--alg", default=None, choices=["hs", "sr", "cg1"],
-                    help="N > 1: recurrence (default: a timed trial of all three)")
+                    help="recurrence (default: a timed trial after a parity gate -- N > 1: HS, "
+                         "SR, CG1; N = 1: HS and SR, SR only where the one-launch march runs)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-rehearsal", action="store_true",
@@ -156,6 +157,9 @@ KERNELS = {
     "dia_march": "k_spmv_dia_m (fused HS step on DIA-VI as a plane march: a workgroup walks "
                  "slices nx*ny apart, p of three consecutive slices + halos in an LDS ring, "
                  "x / p update, s = A p, p.s partials)",
+    "sr1": "k_sr1_dia_m (one-launch SR iteration on DIA-VI as a plane march: r = r - alpha s "
+           "and p = r + beta p of the previous iteration for each window row, x update, "
+           "s = A p from an LDS ring of three windows, (p.s, s.s, r.r) per workgroup)",
     "dc": "k_spmv_dc (LDS-DMA code window + value window per 64-row block, dictionary-coded columns)",
     "csr": "k_spmv_csr (LDS-DMA val/col window per 64-row block, lane-per-row sums from LDS)",
     "panel": "k_spmv_csr over column panels",
@@ -165,6 +169,8 @@ KERNELS = {
 
 def kernel_name(info):
     if info["layout_name"] == "dia" and info.get("fused"):
+        if info.get("alg") == 2:
+            return KERNELS["sr1"]
         return KERNELS["dia_march" if info.get("fuse_march") else "dia_fused"]
     return KERNELS.get(info["layout_name"], info["layout_name"])
 
@@ -377,14 +383,54 @@ def c4_one_gpu(steps, warmup, device=0):
                      "base of the C4 strong-scaling curve (N > 1 lines run C4 across N ranks)")
 
 
-def headline_solve(sysm, steps, warmup, layout="auto"):
+ALGS = {"hs": 0, "cg1": 1, "sr": 2}  # cgx.CGX_ALG_*
+ALG_DESC = {"hs": "hs (the reference recurrence, cg.c:88-141)",
+            "sr": "sr (cg.c:88-141's recurrence with ONE reduction of (p.s, s.s, r.r) per "
+                  "iteration, beta from r_new.r_new = alpha (alpha s.s) - r.r; on one GPU the "
+                  "r update of iteration k runs inside the SpMV launch of k + 1: one launch per "
+                  "iteration, k_sr1_dia_m; oracle_solve_sr)",
+            "cg1": "cg1 (Chronopoulos-Gear)"}
+
+
+def alg_trial(sysm, warmup, layout="auto", maxit=20, its=30):
+    """N = 1: the recurrence of the headline, as the N > 1 path picks it --
+    a parity gate (HS and SR solves of `maxit` iterations: x within 1e-10 of
+    each other), then a timed trial of `its` graph-replayed iterations each;
+    the faster passing one.  SR runs on one GPU only where the plane-marched
+    DIA step applies (cgx_info.fuse_march)."""
+    import numpy as np
+    import cgx
+    res, trial, xs = {}, {}, {}
+    with cgx.Solver(0, layout=layout) as s:
+        s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+        for name in ("hs", "sr"):
+            s.set_mode(cgx.CGX_MODE_FAST, ALGS[name])
+            if name == "sr" and not s.info()["fuse_march"]:
+                res[name] = "refused: no plane-marched DIA step for this matrix"
+                continue
+            s.set_rhs(sysm["b"])
+            s.run(maxit)
+            xs[name] = s.x()
+            s.set_rhs(sysm["b"])
+            s.bench_prepare(warmup)
+            trial[name] = round(s.bench_run(its, graph=True)[0] / its, 4)
+    if "sr" in xs:
+        rel = float(np.linalg.norm(xs["sr"] - xs["hs"]) / np.linalg.norm(xs["hs"]))
+        res["sr_vs_hs_rel"] = rel
+        if not rel <= 1e-10:
+            res["sr"] = f"parity gate failed: {rel:.3e}"
+            trial.pop("sr", None)
+    return min(trial, key=trial.get), dict(gate=res, ms_per_iter=trial, gate_maxit=maxit)
+
+
+def headline_solve(sysm, steps, warmup, layout="auto", alg="hs"):
     """The timed solve: upload (not timed), W warmup iterations, exactly K
     graph-replayed iterations bracketed by device syncs, then K more with HIP
     events around every SpMV launch (its average time in the iteration)."""
     import torch
     import cgx
     t_up = time.perf_counter()
-    s = cgx.Solver(0, layout=layout)
+    s = cgx.Solver(0, layout=layout, alg=ALGS[alg])
     try:
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
         s.set_rhs(sysm["b"])
@@ -431,7 +477,8 @@ def layout_roofline(info, spmv_ms, wl_name):
                 traffic=load_traffic(wl_name),
                 csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
                 note="the SpMV launch of the headline solve, priced on the bytes it moves (its "
-                     "layout; with the fused HS step also r, p_old, x, p_new)")
+                     "layout; with the fused HS step also r, p_old, x, p_new; with the one-launch "
+                     "SR step r, s, p read and written, x every other launch)")
 
 
 def matrix_free(wl, b, steps, warmup):
@@ -480,12 +527,23 @@ def run_single(args, wl_name):
     sysm = make_system(wl)
     torch.cuda.synchronize()
 
-    # ---- headline: the layout libcgx picks (default path of the drop-in)
-    h = headline_solve(sysm, args.steps, args.warmup, args.layout)
+    # ---- headline: the layout libcgx picks (default path of the drop-in), the
+    # recurrence a parity-gated trial picks (HS or SR)
+    if args.alg in ("hs", "sr"):
+        alg, trial = args.alg, None
+    else:
+        alg, trial = alg_trial(sysm, args.warmup, args.layout)
+    h = headline_solve(sysm, args.steps, args.warmup, args.layout, alg)
     info, spmv_ms, wall = h["info"], h["spmv_ms"], h["wall"]
     ms_per_step = 1e3 * wall / args.steps
 
     legs = {}
+    if alg != "hs" and not args.no_legs:  # the reference recurrence's own figure beside it
+        hh = headline_solve(sysm, args.steps, args.warmup, args.layout, "hs")
+        legs["hs"] = dict(value=round(args.steps / hh["wall"], 2), unit="it/s",
+                          ms_per_step=round(1e3 * hh["wall"] / args.steps, 4),
+                          alg=ALG_DESC["hs"], kernel=kernel_name(hh["info"]),
+                          default_layout=layout_roofline(hh["info"], hh["spmv_ms"], wl_name))
     if not args.no_legs:
         if info["layout_name"] != "csr":
             legs["csr"] = solver_leg(sysm, args.steps, args.warmup, "csr", b2b=True)
@@ -510,6 +568,8 @@ def run_single(args, wl_name):
     roofline["stream_read_gbs"] = round(rd, 1)
 
     extra = {}
+    if "hs" in legs:
+        extra["hs_recurrence"] = legs["hs"]
     if not args.no_legs:
         if "dc" in legs:
             d = legs["dc"]
@@ -544,7 +604,7 @@ def run_single(args, wl_name):
         higher_is_better=True, scaling="strong", vs_baseline=None, dtype=wl["dtype"],
         data="synthetic",
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz=int(len(sysm["col"])),
-                    alg="hs (the reference recurrence, cg.c:88-141)", graph=True,
+                    alg=ALG_DESC[alg], alg_trial=trial, graph=True,
                     parallelism="single GPU", layout=layout_desc(info),
                     layout_name=info["layout_name"],
                     scaling_curve="the same workload at every N (N > 1: row-partitioned "

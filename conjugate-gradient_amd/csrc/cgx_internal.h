@@ -94,6 +94,8 @@ enum FinOp {
   FIN_SUM = 5,       // out[0] = sum(a) (op-level dot, local sums)
   FIN_SUM2 = 6,      // out[0] = sum(a), out[1] = sum(b)
   FIN_SUM3 = 7,      // out[0..2] = sums of a's (x, y) pairs and of c (SR local sums)
+  FIN_SR1 = 8,       // single-GPU SR step: (p.s, s.s) pairs + r.r -> alpha, estimate,
+                     // stop test, beta (k_sr1_dia_m's partials)
 };
 
 constexpr int kVecBS = 256;
@@ -280,6 +282,25 @@ struct FuseArgs {
   int march = 0;         // plane march (k_spmv_dia_m): steps per segment, 0: off
 };
 
+// The single-GPU SR iteration in ONE launch (k_sr1_dia_m, plane march): the
+// previous iteration's r = r - alpha s and p = r + beta p (the window rows:
+// r, s, p read from the _o buffers) and x += alpha p, then s = A p; the
+// (p.s, s.s) pairs (pq[2 b], pq[2 b + 1]) and r.r (pc[b]) per workgroup b for
+// k_finalize(FIN_SR1).  r, s, p are double-buffered (read _o, write _n; s_n
+// = SpmvArgs::y).
+template <typename T>
+struct Sr1Args {
+  T *x;
+  const T *pold;
+  T *pnew;
+  const T *rold;
+  T *rnew;
+  const T *sold;
+  const CgState *st;
+  double *pq, *pc;
+  int march;  // steps per segment
+};
+
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
 // launch does k_cg1_update's p / s / x / r recurrences (alpha, beta and the
 // stop flag from CgState) and w = A r_new, writing the gamma = r.r (pg) and
@@ -311,6 +332,12 @@ hipError_t launch_spmv(const SpmvArgs<T> &a, hipStream_t st, const LaunchEv &ev 
 // Workgroups of the fused launch (= SR (p.s, s.s) pairs it writes)
 template <typename T>
 int fused_grid(const SpmvArgs<T> &a);
+template <typename T>
+hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
+                            const LaunchEv &ev);
+// workgroups (= partial pairs) of the plane march at `len` steps per segment
+template <typename T>
+int march_grid(const SpmvArgs<T> &a, int len);
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev = LaunchEv{});

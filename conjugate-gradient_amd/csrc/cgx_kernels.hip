@@ -242,6 +242,32 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
   }
 }
 
+// CGX_ALG_SR on one GPU (k_sr1_dia_m's sums of iteration k = k_u + 1):
+// alpha = r.r / p.s (cg.c:113), the estimate r_new.r_new = alpha (alpha s.s)
+// - r.r clamped at 0 (oracle_solve_sr) for the history, the stop test (the
+// cg.c:125 position) and beta (cg.c:129).  done = 1: the next launch applies
+// the pending x updates, whose finalize marks the solve complete (2).
+__device__ void fin_sr1(double ps, double ss, double rr, CgState *st, double *hist) {
+  if (st->done) {
+    st->done = 2;
+    return;
+  }
+  const int k = st->k_u + 1;
+  const double alpha = rr / ps;
+  const double as2 = alpha * ss;
+  double est = alpha * as2 - rr;
+  if (!(est > 0.0)) est = 0.0;
+  if (k < st->hist_cap) hist[k] = est;
+  if (!(ps > 0.0) && st->brk == 0) st->brk = k + 1;
+  st->ps = ps;
+  st->alpha = alpha;
+  st->k_u = k;
+  st->k = k;
+  st->rr = est;
+  if (k >= st->max_iter || (st->use_tol && est <= st->tol2bb)) st->done = 1;
+  else st->beta = est / rr;
+}
+
 // XCD-contiguous workgroup order (speed only, never correctness): the
 // hardware deals workgroups round-robin over the 8 XCDs, so workgroups b,
 // b+8, b+16, ... share one XCD's L2.  Give XCD x the contiguous range of
@@ -1151,6 +1177,206 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
   }
 }
 
+// ------------------------------ single-GPU SR iteration, plane march (DIA-VI)
+// CGX_ALG_SR on one GPU in ONE launch per iteration (+ k_finalize FIN_SR1):
+// the partitioned solver's SR recurrence (oracle_solve_sr: alpha = r.r / p.s
+// as cg.c:113, beta from the estimate r_new.r_new = alpha (alpha s.s) - r.r)
+// needs only the (p.s, s.s, r.r) of the launch that computes s = A p, so the
+// r update of the next iteration moves into the next launch instead of a
+// separate pass: per window row r_k = r_{k-1} - alpha s_{k-1} and
+// p_k = r_k + beta p_{k-1} (the same two roundings each as the oracle), then
+// s_k = A p_k from the three-window ring (k_spmv_dia_m's march), and per own
+// row r_k, p_k, s_k stored and x += alpha p_{k-1} (every other launch for
+// two iterations, as the HS step).  Bytes per row: code + r, s, p read, r, p,
+// s written + x / p_{k-2} every other launch = 61 against the HS step's 69
+// (fused launch 45 + r update 24).  r_k of the own rows is kept in an LDS
+// buffer (two slots) when the window is built.  One (p.s, s.s) pair and one
+// r.r per workgroup: each thread sums its rows in step order, then the wave
+// tree and the waves in order -- deterministic.
+template <typename T, int SB, int NF, int CB>
+__global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
+  constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
+  T *ring = reinterpret_cast<T *>(dyn_lds);
+  T *rbuf = ring + 3 * a.mws;  // r_k of the own rows, two slots of SR
+  __shared__ T lv[kDiaMax * 16];
+  __shared__ double red[3][4 * SB];
+  typedef typename Pair<T>::type P;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int w = xcd_block();
+  const int chain = w % a.mchains, seg = w / a.mchains;
+  const int j0 = chain * SB;
+  const int msteps = (a.mslices - j0 + a.mq - 1) / a.mq;
+  const int m0 = seg * f.march, m1 = min(m0 + f.march, msteps);
+  if (f.st->done > 1) return;  // uniform
+  const int k = f.st->k_u;  // the last finalized iteration (-1: none)
+  const bool first = k < 0, stop = f.st->done == 1;
+  const bool odd = (k & 1) != 0;
+  const bool xup = !first && (odd || stop);
+  const T alpha = (T)f.st->alpha, beta = (T)f.st->beta, alpha_d = (T)f.st->alpha_def;
+  if (!first && !odd && !stop && blockIdx.x == 0 && t == 0)
+    const_cast<CgState *>(f.st)->alpha_def = f.st->alpha;
+  const int QR = a.mq * kDiaSliceRows;
+  const int padn = a.mslices * kDiaSliceRows;
+  const bool nt = a.nt != 0;
+  const int wn = SR + a.hl + a.hr, ws = a.mws;
+  auto base_of = [&](int m) { return (j0 + m * a.mq) * kDiaSliceRows; };
+  auto slot = [&](int m) { return ring + ((m + 3) % 3) * ws; };
+  struct XOps {
+    P po, xo, pd;
+  };
+  auto load_x = [&](int m, XOps &o) {
+    const int r = base_of(m) + 2 * t, rs = r < a.n ? r : 0;
+    o.po = ld_pair(f.pold, rs);
+    o.xo = ld_pair(f.x, rs);
+    if (odd) o.pd = ld_pair((const T *)f.pnew, rs);
+  };
+  auto x_update = [&](const XOps &o, int r, int rend) {
+    T x0 = o.xo.x, x1 = o.xo.y;
+    if (odd) {
+      const T d0 = alpha_d * o.pd.x, d1 = alpha_d * o.pd.y;
+      x0 = x0 + d0;
+      x1 = x1 + d1;
+    }
+    const T a0 = alpha * o.po.x, a1 = alpha * o.po.y;
+    st_pair(f.x, r, rend, x0 + a0, x1 + a1, false);
+  };
+  XOps xc{}, xn{};
+  double sps = 0.0, sss = 0.0, srr = 0.0;
+  auto publish = [&]() {
+    sps = wave_sum(sps);
+    sss = wave_sum(sss);
+    srr = wave_sum(srr);
+    if (lane == 0) {
+      red[0][wid] = sps;
+      red[1][wid] = sss;
+      red[2][wid] = srr;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double p0 = red[0][0], p1 = red[1][0], p2 = red[2][0];
+#pragma unroll
+      for (int v = 1; v < 4 * SB; ++v) {
+        p0 = p0 + red[0][v];
+        p1 = p1 + red[1][v];
+        p2 = p2 + red[2][v];
+      }
+      reinterpret_cast<double2 *>(f.pq)[blockIdx.x] = make_double2(p0, p1);
+      f.pc[blockIdx.x] = p2;
+    }
+  };
+  if (stop) {  // the pending x updates only (then the stop of oracle_solve_sr)
+    if (xup)
+      for (int m = m0; m < m1; ++m) {
+        const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + SR);
+        load_x(m, xc);
+        if (r < rend) x_update(xc, r, rend);
+      }
+    return;
+  }
+  if (m0 >= m1) {  // no steps: zero sums (k_finalize adds every workgroup's)
+    publish();
+    return;
+  }
+  P wr[NF], wp[NF], wsv[NF];
+  auto load_win = [&](int m) {
+    const int w0 = base_of(m) - a.hl;
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int j = min(max(w0 + 2 * t + q * 2 * BS, -1), a.ncols - 1);
+      wr[q] = ld_pair(f.rold, j);
+      wp[q] = ld_pair(f.pold, j);
+      wsv[q] = ld_pair(f.sold, j);
+    }
+  };
+  auto store_win = [&](int m) {
+    T *win = slot(m), *rb = rbuf + (m & 1) * SR;
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int i = 2 * t + q * 2 * BS;
+      P rk = wr[q], pk = wr[q];
+      if (!first) {
+        const T as0 = alpha * wsv[q].x, as1 = alpha * wsv[q].y;
+        rk.x = wr[q].x - as0;
+        rk.y = wr[q].y - as1;
+        pk = p_next<T>(rk, wp[q], beta);
+      }
+      if (i < wn) win[i] = pk.x;
+      if (i + 1 < wn) win[i + 1] = pk.y;
+      const int o = i - a.hl;  // hl even: a pair is in the own rows or not
+      if (o >= 0 && o < SR) {
+        rb[o] = rk.x;
+        rb[o + 1] = rk.y;
+      }
+    }
+  };
+  typedef typename CodeRaw<CB>::type CR;
+  auto codes_at = [&](int m, CR &cw) {
+    const int r = base_of(m) + 2 * t;
+    cw = ld_code_raw<CB>(a.dcode, r < padn ? r : base_of(m));
+  };
+  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
+  CR cw, cwn{};
+  codes_at(m0, cw);
+  if (xup) load_x(m0, xc);
+  load_win(m0 - 1);
+  store_win(m0 - 1);
+  load_win(m0);
+  store_win(m0);
+  load_win(m0 + 1);
+  if (t < a.ndiag * 16) lv[t] = tv;
+  auto step = [&](int m, const CR &ccw, XOps &cx, CR &ncw, XOps &nx) {
+    store_win(m + 1);
+    codes_at(min(m + 1, m1 - 1), ncw);
+    load_win(min(m + 2, m1));  // in flight during step m
+    if (xup && m + 1 < m1) load_x(m + 1, nx);
+    __syncthreads();
+    const int base = base_of(m), r = base + 2 * t;
+    const int rend = min(a.n, base + SR);
+    const T *cur = slot(m), *prv = slot(m - 1), *nxt = slot(m + 1);
+    const T *rb = rbuf + (m & 1) * SR;
+    const int rw = 2 * t + a.hl;
+    unsigned cc0, cc1;
+    code_split<CB>(ccw, cc0, cc1);
+    T a0 = T(0), a1 = T(0);
+#pragma unroll
+    for (int kk = 0; kk < kDiaMax; ++kk) {
+      if (kk < a.ndiag) {
+        const int d = a.doff[kk];
+        const T *src = (a.near >> kk) & 1u ? cur : d < 0 ? prv : nxt;
+        const int i = (a.near >> kk) & 1u ? rw + d : d < 0 ? rw + d + QR : rw + d - QR;
+        const T v0 = src[i], v1 = src[i + 1];
+        const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
+        const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
+        a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
+        a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
+      }
+    }
+    const T pn0 = cur[rw], pn1 = cur[rw + 1];
+    const T rk0 = rb[2 * t], rk1 = rb[2 * t + 1];
+    if (r < rend) {
+      st_pair(a.y, r, rend, a0, a1, nt);
+      st_pair(f.pnew, r, rend, pn0, pn1, false);
+      st_pair(f.rnew, r, rend, rk0, rk1, false);
+      if (xup) x_update(cx, r, rend);
+      sps = sps + (double)pn0 * (double)a0;
+      sss = sss + (double)a0 * (double)a0;
+      srr = srr + (double)rk0 * (double)rk0;
+      if (r + 1 < rend) {
+        sps = sps + (double)pn1 * (double)a1;
+        sss = sss + (double)a1 * (double)a1;
+        srr = srr + (double)rk1 * (double)rk1;
+      }
+    }
+    __syncthreads();  // every read of window m - 1's slot (and r slot m) is done before step m + 1 refills it
+  };
+  for (int m = m0; m < m1; m += 2) {
+    step(m, cw, xc, cwn, xn);
+    if (m + 1 < m1) step(m + 1, cwn, xn, cw, xc);
+  }
+  publish();
+}
+
 // ---------------------------------------- fused CG1 step (DIA-VI)
 // The Chronopoulos-Gear iteration in ONE launch: k_cg1_update's vector
 // recurrences (p = r + beta p; s = w + beta s; x += alpha p; r -= alpha s)
@@ -2047,11 +2273,16 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
                                                  int nc) {
   __shared__ double red[BS / kWave];
   double sa, sb = 0.0, sc = 0.0;
-  if (op == FIN_SUM3) sum_parts_sr<BS>(pa, na, pc, nc, red, sa, sb, sc);  // pa: (p.s, s.s) pairs
+  if (op == FIN_SUM3 || op == FIN_SR1)
+    sum_parts_sr<BS>(pa, na, pc, nc, red, sa, sb, sc);  // pa: (p.s, s.s) pairs
   else if (pb) sum_parts2<BS>(pa, na, pb, nb, red, sa, sb);
   else sa = sum_parts<BS>(pa, na, red);
   if (threadIdx.x != 0) return;
   if (op == FIN_SUM3) out[2] = sc;
+  if (op == FIN_SR1) {
+    fin_sr1(sa, sb, sc, st, hist);
+    return;
+  }
   if (op != FIN_SUM && op != FIN_SUM2 && op != FIN_SUM3 && op != FIN_INIT_HS &&
       op != FIN_INIT_CG1 && st->done)
     return;
@@ -2422,6 +2653,44 @@ static hipError_t launch_march(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipSt
   return hipGetLastError();
 }
 
+template <typename T, int SB, int NF>
+static const void *sr1_kernel(int cb) {
+  return cb == 1 ? CGX_K(k_sr1_dia_m<T, SB, NF, 1>)
+                 : cb == 2 ? CGX_K(k_sr1_dia_m<T, SB, NF, 2>) : CGX_K(k_sr1_dia_m<T, SB, NF, 4>);
+}
+
+template <typename T>
+hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
+                            const LaunchEv &ev) {
+  if (a.mq <= 0 || f.march <= 0 || a.items.count != a.mslices || a.layout != L_DIA)
+    return hipErrorInvalidValue;
+  const int sb = a.msb;
+  const int wn = sb * kDiaSliceRows + a.hl + a.hr;
+  const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
+  if (a.mws < wn + 2 || (sb != 1 && sb != 2) || nf > (sb == 1 ? 5 : 3)) return hipErrorInvalidValue;
+  const int nfc = nf <= 2 ? 2 : nf <= 3 ? 3 : 5;
+  const int cb = a.cb;
+  if (cb != 1 && cb != 2 && cb != 4) return hipErrorInvalidValue;
+  const void *k = nullptr;
+  switch (sb * 10 + nfc) {
+    case 12: k = sr1_kernel<T, 1, 2>(cb); break;
+    case 13: k = sr1_kernel<T, 1, 3>(cb); break;
+    case 15: k = sr1_kernel<T, 1, 5>(cb); break;
+    case 22: k = sr1_kernel<T, 2, 2>(cb); break;
+    case 23: k = sr1_kernel<T, 2, 3>(cb); break;
+    default: return hipErrorInvalidValue;
+  }
+  const int g = march_grid(a, f.march);
+  void *args[] = {(void *)&a, (void *)&f};
+  // the three-window ring and two slots of own-row r
+  const size_t lds = ((size_t)3 * a.mws + 2 * sb * kDiaSliceRows) * sizeof(T) + 16;
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st, ev.start, ev.stop, 0);
+  else
+    (void)hipLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev) {
@@ -2675,6 +2944,9 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int spmv_grid<T>(const SpmvArgs<T> &);                                                \
   template hipError_t launch_spmv<T>(const SpmvArgs<T> &, hipStream_t, const LaunchEv &);      \
   template int fused_grid<T>(const SpmvArgs<T> &);                                               \
+  template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
+  template hipError_t launch_sr1_march<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,  \
+                                          const LaunchEv &);                                     \
   template hipError_t launch_spmv_fused<T>(const SpmvArgs<T> &, const FuseArgs<T> &, hipStream_t, \
                                            const LaunchEv &);                                    \
   template hipError_t launch_init_hs<T>(int, const T *, T *, T *, T *, double *, int,            \

@@ -164,7 +164,12 @@ void drop_graph(cgx_solver *s) {
 // working set beyond the Infinity Cache (cache-resident systems are launch-
 // and latency-bound: the heavier fused workgroup loses, C2 29.1 vs 26.8 us
 // per HS iteration).
+// CGX_ALG_SR on one GPU exists only as the single-launch plane march
+// (k_sr1_dia_m): it needs a march plan, whatever the cache rule says.
 bool fused(const cgx_solver *s) {
+  if (s->alg == CGX_ALG_SR)
+    return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
+           s->A.mq > 0 && s->march != 0;
   return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
          (s->fuse == CGX_FUSE_ON || s->A.nt);
 }
@@ -173,7 +178,7 @@ bool fused(const cgx_solver *s) {
 // when it does not run: the matrix plans one (DevMatrix::plan_march) and
 // cgx_solver_set_march has not turned it off.
 int march_len(const cgx_solver *s) {
-  if (!fused(s) || s->alg != CGX_ALG_HS || s->A.mq == 0 || s->march == 0) return 0;
+  if (!fused(s) || s->alg == CGX_ALG_CG1 || s->A.mq == 0 || s->march == 0) return 0;
   return s->march > 0 ? s->march : s->A.mlen;
 }
 
@@ -181,7 +186,7 @@ int march_len(const cgx_solver *s) {
 // unfused folded HS step (k_xpay_xf's every-other-iteration x); r, s, w for
 // the fused CG1 step.
 bool alternating(const cgx_solver *s) {
-  return (s->alg == CGX_ALG_HS && s->mode == CGX_MODE_FAST) || fused(s);
+  return (s->alg != CGX_ALG_CG1 && s->mode == CGX_MODE_FAST) || fused(s);
 }
 
 void free_system(cgx_solver *s) {
@@ -212,6 +217,9 @@ int alloc_vectors(cgx_solver *s) {
   s->vec_grid = vec_grid_for(n, s->cus);
   s->vec_grid = (std::max(s->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
   s->part_cap = std::max(s->A.partials(s->A.all_items()), s->vec_grid) + 1;
+  // CGX_ALG_SR: one (p.s, s.s) pair per march workgroup, at most one
+  // workgroup per slice and chain (segments of one step)
+  if (s->A.mq > 0) s->part_cap = std::max(s->part_cap, 2 * (s->A.items() + s->A.mchains) + 2);
   int rc;
   if ((rc = dev_alloc(&s->d_b, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_x, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_r, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_p, nv, &s->vec_bytes)) ||
@@ -268,7 +276,7 @@ int enqueue_init(cgx_solver *s) {
   const int n = s->A.n;
   T *b = (T *)s->d_b, *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p;
   s->pbuf = 0;  // the prologue writes p into d_p
-  if (s->alg == CGX_ALG_HS) {
+  if (s->alg != CGX_ALG_CG1) {  // HS, SR: x = 0, r = p = b
     if (s->mode == CGX_MODE_EXACT) {
       CGX_HIP(launch_init_hs<T>(n, b, x, r, p, nullptr, s->vec_grid, st));
       CGX_HIP(launch_dot_seq<T>(n, b, b, s->d_pa, nullptr, st));
@@ -295,6 +303,24 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = s->A.n;
   T *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p, *sv = (T *)s->d_s, *w = (T *)s->d_w;
   int np = 0;
+  if (s->alg == CGX_ALG_SR) {
+    // k_sr1_dia_m: r = r - alpha s, p = r + beta p (window rows), x update,
+    // s = A p, (p.s, s.s) pairs + r.r per workgroup; k_finalize FIN_SR1: the
+    // scalar step (oracle_solve_sr's recurrence, one reduction)
+    const int q = s->pbuf;
+    T *po = (T *)(q ? s->d_p2 : s->d_p), *pn = (T *)(q ? s->d_p : s->d_p2);
+    T *ro = (T *)(q ? s->d_r2 : s->d_r), *rn = (T *)(q ? s->d_r : s->d_r2);
+    T *so = (T *)(q ? s->d_s2 : s->d_s), *sn = (T *)(q ? s->d_s : s->d_s2);
+    const SpmvArgs<T> a = s->A.args<T>(nullptr, sn, nullptr, &s->d_st->done, s->A.all_items());
+    const Sr1Args<T> f{x, po, pn, ro, rn, so, s->d_st, s->d_pa, s->d_pb, march_len(s)};
+    const int g = march_grid(a, f.march);
+    if (2 * g > s->part_cap) return CGX_EINVAL;
+    CGX_HIP(launch_sr1_march<T>(a, f, st, LaunchEv{ev0, ev1}));
+    CGX_HIP(launch_finalize(FIN_SR1, s->d_pa, g, nullptr, 0, s->d_st, s->d_hist, nullptr, st,
+                            s->d_pb, g));
+    s->pbuf ^= 1;
+    return 0;
+  }
   if (fused(s) && s->alg == CGX_ALG_CG1) {
     // k_cg1_dia_h: p, s, x, r recurrences + w = A r_new with the gamma /
     // delta partials; k_finalize: the single reduction's scalar step
@@ -481,7 +507,14 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
   if ((rc = enqueue_init<T>(s))) return rc;
   // the fused step does an iteration's x update in the next launch: one
   // more step carries the last one (and finds the stop)
-  const long long total = (long long)maxit + 1 + (fused(s) && s->alg == CGX_ALG_HS ? 1 : 0);
+  if (s->alg == CGX_ALG_SR && !fused(s)) {
+    set_error("CGX_ALG_SR on one GPU needs the plane-marched DIA step (cgx_info.fuse_march)");
+    return CGX_EINVAL;
+  }
+  const long long total = (long long)maxit + 1 + (fused(s) && s->alg != CGX_ALG_CG1 ? 1 : 0);
+  // SR decides the stop in the finalize before the launch that applies the
+  // last x update: complete once that launch's finalize marks done = 2
+  const int fin_done = s->alg == CGX_ALG_SR ? 2 : 1;
   if (tol <= 0.0) {
     if ((rc = enqueue_iters<T>(s, total))) return rc;
     if ((rc = read_state(s))) return rc;
@@ -498,7 +531,7 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
       if ((rc = enqueue_iters<T>(s, b))) return rc;
       done_iters += b;
       if ((rc = read_state(s))) return rc;
-      if (s->h_st->done || done_iters >= total) break;
+      if (s->h_st->done >= fin_done || done_iters >= total) break;
       batch = next_batch(s->h_st->rr, s->h_st->tol2bb, s->h_st->k, rr_prev, k_prev, batch);
       rr_prev = s->h_st->rr;
       k_prev = s->h_st->k;
@@ -516,6 +549,10 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
 template <typename T>
 int bench_prepare_t(cgx_solver *s, int warmup) {
   int rc;
+  if (s->alg == CGX_ALG_SR && !fused(s)) {
+    set_error("CGX_ALG_SR on one GPU needs the plane-marched DIA step (cgx_info.fuse_march)");
+    return CGX_EINVAL;
+  }
   if ((rc = prepare_state(s, INT_MAX - 1, 0.0, 0))) return rc;
   if ((rc = enqueue_init<T>(s))) return rc;
   if ((rc = ensure_graphs<T>(s))) return rc;  // captured here, not in a timed region
@@ -700,7 +737,7 @@ void cgx_solver_destroy(cgx_solver *s) {
 
 int cgx_solver_set_mode(cgx_solver *s, int mode, int alg) {
   if (!s || (mode != CGX_MODE_FAST && mode != CGX_MODE_EXACT) ||
-      (alg != CGX_ALG_HS && alg != CGX_ALG_CG1)) {
+      (alg != CGX_ALG_HS && alg != CGX_ALG_CG1 && alg != CGX_ALG_SR)) {
     cgx::set_error("set_mode: bad arguments");
     return CGX_EINVAL;
   }
@@ -862,7 +899,9 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   if (s->have_matrix && fused(s))
     // CG1: r, w, s, p, x read and p, s, r, w, x written, the SpMV's own x
     // read / y write included: + 8 n vectors
-    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : 3.5) * A.n * sv;
+    // SR (one launch): r, s, p read and written, x / p_{k-2} every other
+    // launch: + 5.5 n vectors
+    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : s->alg == CGX_ALG_SR ? 5.5 : 3.5) * A.n * sv;
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;

@@ -106,7 +106,9 @@ enum { CGX_MODE_FAST = 0,    /* two-stage parallel reductions (default)      */
        CGX_MODE_EXACT = 1 }; /* sequential dots: reference bit order          */
 enum { CGX_ALG_HS = 0,       /* Hestenes-Stiefel, the reference recurrence    */
        CGX_ALG_CG1 = 1,      /* Chronopoulos-Gear, one fused reduction/iter   */
-       CGX_ALG_SR = 2 };     /* HS with one reduction/iter (cgx_dist only)   */
+       CGX_ALG_SR = 2 };     /* HS with one reduction/iter: cgx_dist, and one
+                                GPU where the plane-marched DIA step applies
+                                (one launch per iteration, cgx_solver_set_march) */
 enum { CGX_F64 = 0, CGX_F32 = 1 };
 
 /* Device layout of the matrix the SpMV streams (the C ABI always takes the

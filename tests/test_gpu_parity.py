@@ -792,6 +792,50 @@ def test_fused_march_bit_identical_to_unfused(case):
                 assert H.same_bits_or_both_nan(h0, h1), (march, j)
 
 
+@pytest.mark.parametrize("case", list(march_cases()), ids=lambda c: c[0])
+def test_sr_single_launch_vs_oracle(case):
+    """CGX_ALG_SR on one GPU (k_sr1_dia_m: the r update of the previous
+    iteration, the p update and s = A p in ONE plane-marched launch, one
+    reduction of (p.s, s.s, r.r)) against oracle_solve_sr, the recurrence it
+    restates, and the HS oracle: same iteration counts at fixed maxit (+-1 at
+    a tolerance stop), x within 1e-10 (fixed maxit; only the dot products'
+    summation order differs), the r.r estimates within 1e-6, segment lengths
+    1 / auto / whole chains, and graph vs eager replays bit-identical."""
+    _, (rp, col, val, b), _ = case
+    n = len(rp) - 1
+    if b is None:
+        b = np.random.default_rng(13).standard_normal(n)
+    for march in (-1, 1, 100000):
+        with cgx.Solver(0, alg=cgx.CGX_ALG_SR, layout="dia") as s:
+            s.set_march(march)
+            s.set_matrix(rp, col, val)
+            info = s.info()
+            assert info["fused"] == 1 and info["fuse_march"] > 0
+            for maxit in (0, 1, 16, 17, 40):
+                s.set_rhs(b)
+                its = s.run(maxit)
+                x, h = s.x(), s.history(its)
+                x_ref, its_ref, h_ref = H.o_solve(maxit, 0.0, rp, col, val, b, sr=True)
+                assert its == its_ref == maxit + 1, (march, maxit)
+                assert rel(x, x_ref) <= 1e-10, (march, maxit)
+                assert np.allclose(h, h_ref, rtol=1e-6, atol=0), (march, maxit)
+            s.set_rhs(b)
+            its = s.run(3000, 1e-10)
+            x = s.x()
+            x_sr, its_sr, _ = H.o_solve(3000, 1e-10, rp, col, val, b, sr=True)
+            x_hs, its_hs, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+            assert abs(its - its_sr) <= 1 and abs(its - its_hs) <= 1 and its < 3000
+            assert rel(x, x_sr) <= 1e-9 and rel(x, x_hs) <= 1e-9
+            assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
+            out = []
+            for graph in (True, False):
+                s.set_rhs(b)
+                s.bench_prepare(0)
+                s.bench_run(35, graph=graph)
+                out.append(s.x())
+            assert H.same_bits_or_both_nan(out[0], out[1])
+
+
 @pytest.mark.parametrize("name", ["lap2d_32", "lap3d_12", "rand_spd_2000", "dense128"])
 def test_cg1_within_tolerance(name):
     g = H.load_golden(name)

@@ -1,7 +1,7 @@
 """Fused vs unfused iteration time on one GPU (cgx.Solver, graph-replayed,
 device-generated Laplacian), same box, same build, back to back; HS, or the
 CG1 recurrence with --cg1.
-  python tools/fused_probe.py [--cg1] [--modes=on,off,...] [--march=-1,0,...] [dim:nx[:ny:nz] ...]
+  python tools/fused_probe.py [--cg1|--sr] [--modes=on,off,...] [--march=-1,0,...] [dim:nx[:ny:nz] ...]
 default 3:216 3:400 (C3, C4); 2:1000 = C2.  --march: cgx_solver_set_march values tried
 for each mode (-1 auto, 0 off, > 0 steps per segment)."""
 import sys
@@ -9,7 +9,8 @@ sys.path.insert(0, "conjugate-gradient_amd")
 import numpy as np, cgx
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
-alg = cgx.CGX_ALG_CG1 if "--cg1" in sys.argv else cgx.CGX_ALG_HS
+alg = (cgx.CGX_ALG_CG1 if "--cg1" in sys.argv else cgx.CGX_ALG_SR if "--sr" in sys.argv
+       else cgx.CGX_ALG_HS)
 modes = [True, False, True, False]
 for a in sys.argv[1:]:
     if a.startswith("--modes="):  # e.g. --modes=on,off,on,off (cgx.fuse_mode names)
@@ -33,5 +34,5 @@ for spec in args or ["3:216", "3:400"]:
             _, sp = s.bench_run(30, graph=False, spmv_events=True)
             i = s.info()
             print("%s %dD nx %d mode %s march %d (runs %d) fused %d: %.1f us/iter, spmv launch %.1f us" %
-                  ("cg1" if alg else "hs", dim, nx, fused, march, i["fuse_march"], i["fused"],
+                  (["hs", "cg1", "sr"][alg], dim, nx, fused, march, i["fuse_march"], i["fused"],
                    1e3 * ms / 200, 1e3 * sp), flush=True)
