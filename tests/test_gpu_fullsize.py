@@ -114,6 +114,28 @@ def test_c4_one_gpu_vs_oracle():
             assert rel(x, x_ref) <= 1e-9
 
 
+@pytest.mark.timeout(600)
+def test_c4_sr_one_gpu_vs_oracle():
+    """The N = 1 headline path at full C4 size: CGX_ALG_SR as one
+    plane-marched launch per iteration (k_sr1_dia_m), 6 SpMVs: within 1e-10
+    of oracle_solve_sr (only the grouping of the dot products differs), its
+    r.r estimates within 1e-8, and within 1e-9 of the HS oracle."""
+    nx = 400
+    rp, col, val = cgx.laplacian3d(nx, nx, nx)
+    b = np.ones(len(rp) - 1)
+    x_sr, its_sr, h_sr = H.o_solve(5, 0.0, rp, col, val, b, sr=True)
+    x_hs, _ = H.o_conj_grad(5, rp, col, val, b)
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["fuse_march"] > 0
+        s.set_rhs(b)
+        assert s.run(5) == its_sr == 6
+        x = s.x()
+        assert np.allclose(s.history(6), h_sr, rtol=1e-8, atol=0)
+    assert rel(x, x_sr) <= 1e-10
+    assert rel(x, x_hs) <= 1e-9
+
+
 def c4_group(alg, fused, maxit, P=8):
     """C4 row-partitioned into P slabs (cgx_partition_rows: 400^3 / 8 = 50
     planes each) as an in-process group on GPU 0; x of all rows."""
