@@ -644,6 +644,29 @@ __device__ __forceinline__ void st_pair(T *y, int r, int n, T a0, T a1, bool nt)
   }
 }
 
+// LDS pair access at an EVEN index of a window whose base is 16-B aligned:
+// one ds_read_b128 / ds_write_b128 (fp64) instead of two 8-B accesses at a
+// 16-B lane stride (the plane-march kernels: slot strides even, halos even;
+// same-box A/B at C4 / C3 within the noise: 748-750 vs 755-803 / 134-138 vs
+// 133 us per SR iteration -- kept for the halved LDS instruction count).
+template <typename T>
+struct PairA {
+  typedef T type __attribute__((ext_vector_type(2), aligned(2 * sizeof(T))));
+};
+template <typename T>
+__device__ __forceinline__ void lds_ld2(const T *w, int i, T &v0, T &v1) {
+  const typename PairA<T>::type v = *reinterpret_cast<const typename PairA<T>::type *>(w + i);
+  v0 = v.x;
+  v1 = v.y;
+}
+template <typename T>
+__device__ __forceinline__ void lds_st2(T *w, int i, T v0, T v1) {
+  typename PairA<T>::type v;
+  v.x = v0;
+  v.y = v1;
+  *reinterpret_cast<typename PairA<T>::type *>(w + i) = v;
+}
+
 // The code words of rows r, r + 1 (r even): one load of 2 cb bytes (cb is
 // uniform: a scalar branch).  C = unsigned holds words of <= 4 bytes.
 template <typename C>
@@ -1058,8 +1081,8 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
     for (int q = 0; q < NF; ++q) {
       const int i = 2 * t + q * 2 * BS;
       const P pn = fs.first ? wr[q] : p_next<T>(wr[q], wp[q], beta);
-      if (i < wn) win[i] = pn.x;
-      if (i + 1 < wn) win[i + 1] = pn.y;
+      if (i + 1 < wn) lds_st2(win, i, pn.x, pn.y);  // wn even (march plan)
+      else if (i < wn) win[i] = pn.x;
     }
   };
   // the x update's operands of step m's rows (p_old, x, and on odd launches
@@ -1144,14 +1167,20 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
         const int d = a.doff[kk];
         const T *src = (a.near >> kk) & 1u ? cur : d < 0 ? prv : nxt;
         const int i = (a.near >> kk) & 1u ? rw + d : d < 0 ? rw + d + QR : rw + d - QR;
-        const T v0 = src[i], v1 = src[i + 1];
+        T v0, v1;
+        if ((d & 1) == 0) lds_ld2(src, i, v0, v1);  // rw, QR even: an aligned pair
+        else {
+          v0 = src[i];
+          v1 = src[i + 1];
+        }
         const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
         const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
         a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
         a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
       }
     }
-    const T pn0 = cur[rw], pn1 = cur[rw + 1];
+    T pn0, pn1;
+    lds_ld2(cur, rw, pn0, pn1);
     double dot = 0.0;
     if (r < rend) {
       st_pair(a.y, r, rend, a0, a1, nt);
@@ -1301,13 +1330,10 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
         rk.y = wr[q].y - as1;
         pk = p_next<T>(rk, wp[q], beta);
       }
-      if (i < wn) win[i] = pk.x;
-      if (i + 1 < wn) win[i + 1] = pk.y;
+      if (i + 1 < wn) lds_st2(win, i, pk.x, pk.y);  // wn even (march plan)
+      else if (i < wn) win[i] = pk.x;
       const int o = i - a.hl;  // hl even: a pair is in the own rows or not
-      if (o >= 0 && o < SR) {
-        rb[o] = rk.x;
-        rb[o + 1] = rk.y;
-      }
+      if (o >= 0 && o < SR) lds_st2(rb, o, rk.x, rk.y);
     }
   };
   typedef typename CodeRaw<CB>::type CR;
@@ -1345,15 +1371,21 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
         const int d = a.doff[kk];
         const T *src = (a.near >> kk) & 1u ? cur : d < 0 ? prv : nxt;
         const int i = (a.near >> kk) & 1u ? rw + d : d < 0 ? rw + d + QR : rw + d - QR;
-        const T v0 = src[i], v1 = src[i + 1];
+        T v0, v1;
+        if ((d & 1) == 0) lds_ld2(src, i, v0, v1);  // rw, QR even: an aligned pair
+        else {
+          v0 = src[i];
+          v1 = src[i + 1];
+        }
         const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
         const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
         a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
         a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
       }
     }
-    const T pn0 = cur[rw], pn1 = cur[rw + 1];
-    const T rk0 = rb[2 * t], rk1 = rb[2 * t + 1];
+    T pn0, pn1, rk0, rk1;
+    lds_ld2(cur, rw, pn0, pn1);
+    lds_ld2(rb, 2 * t, rk0, rk1);
     if (r < rend) {
       st_pair(a.y, r, rend, a0, a1, nt);
       st_pair(f.pnew, r, rend, pn0, pn1, false);
