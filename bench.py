@@ -504,9 +504,11 @@ def c3_legs(steps, warmup):
     coefficient matrix on its grid, and the end-to-end drop-in call."""
     wl = WORKLOADS["c3"]
     sysm = make_system(wl)
-    h = headline_solve(sysm, steps, warmup)
+    alg, trial = alg_trial(sysm, warmup)
+    h = headline_solve(sysm, steps, warmup, alg=alg)
     csr = solver_leg(sysm, steps, warmup, "csr", b2b=True)
     out = dict(workload=wl["desc"], value=round(steps / h["wall"], 2), unit="it/s",
+               alg=ALG_DESC[alg], alg_trial=trial,
                ms_per_step=round(1e3 * h["wall"] / steps, 4), layout=layout_desc(h["info"]),
                layout_name=h["info"]["layout_name"],
                default_layout=layout_roofline(h["info"], h["spmv_ms"], "c3"),
