@@ -138,16 +138,37 @@ def make_system(wl, rank=0, world=1):
                 row_end=re_)
 
 
-def load_traffic(tag):
-    """L2->fabric bytes per SpMV launch from the committed rocprofv3 PMC
-    summary (profiles/pmc_<tag>.json, tools/pmc_summary.py), or None."""
-    p = REPO / "profiles" / f"pmc_{tag}.json"
+# kernel key -> the name prefix its rocprofv3 PMC summary must carry
+KERNEL_PREFIX = {"sr1": "k_sr1_dia_m<", "dia_march": "k_spmv_dia_m<", "dia_fused": "k_spmv_dia_h<",
+                 "dia": "k_spmv_dia<", "dc": "k_spmv_dc<", "csr": "k_spmv_csr<",
+                 "panel": "k_spmv_csr<", "stencil": "k_stencil<"}
+
+
+def load_traffic(wl_name, key):
+    """L2->fabric bytes per launch of kernel `key` (KERNEL_PREFIX) at workload
+    wl_name from the committed rocprofv3 PMC summary
+    profiles/pmc_<wl_name>_<key>.json (tools/pmc_summary.py) -- only when the
+    file's `kernel` IS that kernel (traffic was attributed by
+    workload name, to another kernel).  (bytes, source) or (None, reason)."""
+    p = REPO / "profiles" / f"pmc_{wl_name}_{key}.json"
     if not p.exists():
-        return None
+        return None, f"no profiles/{p.name}"
     try:
-        return json.loads(p.read_text()).get("spmv_hbm_bytes_per_launch")
-    except Exception:
-        return None
+        d = json.loads(p.read_text())
+    except Exception as e:  # a malformed summary prices nothing
+        return None, f"profiles/{p.name}: {e}"
+    kern = str(d.get("kernel", ""))
+    if not kern.startswith(KERNEL_PREFIX[key]):
+        return None, f"profiles/{p.name} is {kern}, not {KERNEL_PREFIX[key]}...>"
+    return d.get("spmv_hbm_bytes_per_launch"), f"profiles/{p.name} ({kern}, {d.get('source', '')})"
+
+
+def traffic_fields(wl_name, key, alg_bytes):
+    """`traffic` (HBM bytes per launch, PMC) beside `achieved`, its source and
+    its ratio to the algorithmic bytes of the same kernel."""
+    t, src = load_traffic(wl_name, key)
+    return dict(traffic=None if t is None else int(t), traffic_source=src,
+                traffic_ratio=None if t is None else round(t / alg_bytes, 4))
 
 
 KERNELS = {
@@ -167,12 +188,16 @@ KERNELS = {
 }
 
 
-def kernel_name(info):
+def kernel_key(info):
     if info["layout_name"] == "dia" and info.get("fused"):
         if info.get("alg") == 2:
-            return KERNELS["sr1"]
-        return KERNELS["dia_march" if info.get("fuse_march") else "dia_fused"]
-    return KERNELS.get(info["layout_name"], info["layout_name"])
+            return "sr1"
+        return "dia_march" if info.get("fuse_march") else "dia_fused"
+    return info["layout_name"]
+
+
+def kernel_name(info):
+    return KERNELS.get(kernel_key(info), info["layout_name"])
 
 
 def layout_desc(info):
@@ -302,20 +327,22 @@ def solver_leg(sysm, steps, warmup, layout, device=0, b2b=False):
     return out
 
 
-def solve_e2e(sysm, tol=1e-8, maxit=20000):
+def solve_e2e(sysm, tol=1e-8, maxit=20000, alg="hs", legs=("cold", "warm")):
     """What cg.c:71-75 times: the drop-in call solve(A, b, &x, tol, maxit)
     through the C ABI on host structs -- content hash of A, upload + layout
     encoding (first call), the device iterations, x back to the host -- cold
     (A not yet resident) and warm (A resident, the second call on the same
-    struct).  The true residual is computed here on the host (scipy)."""
+    struct).  The true residual is computed here on the host (scipy).
+    alg "sr": cgx_ops_set_mode(FAST, SR) -- the one-launch SR step where the
+    matrix takes it, HS otherwise (`alg_ran`, cgx_ops_last_timing)."""
     import numpy as np
     import scipy.sparse as sp
     import cgx
     A = cgx.Mv(sysm["val"], sysm["col"], sysm["rp"])
     b = cgx.Mv(sysm["b"])
-    cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST, ALGS[alg])
     out = {}
-    for leg in ("cold", "warm"):
+    for leg in legs:
         t0 = time.perf_counter()
         x, its = cgx.solve(A, b, tol, maxit)
         wall = 1e3 * (time.perf_counter() - t0)
@@ -327,10 +354,12 @@ def solve_e2e(sysm, tol=1e-8, maxit=20000):
                         setup_ms=round(t["setup_ms"], 1), hash_ms=round(t["hash_ms"], 1),
                         solve_ms=round(t["solve_ms"], 1), download_ms=round(t["download_ms"], 1),
                         uploaded=bool(t["uploaded"]),
-                        setup_frac=round(t["setup_ms"] / max(wall, 1e-9), 3))
+                        setup_frac=round(t["setup_ms"] / max(wall, 1e-9), 3),
+                        alg_ran={v: k for k, v in ALGS.items()}[t["alg"]])
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
     out["note"] = (f"solve(A,b,&x,{tol:g},{maxit}) through the C ABI on host structs "
-                   "(include/cgx.h), wall time incl. ctypes; cold = A uploaded and encoded, "
-                   "warm = A resident (op-level residency)")
+                   f"(include/cgx.h), cgx_ops_set_mode(FAST, {alg.upper()}), wall time incl. "
+                   "ctypes; cold = A uploaded and encoded, warm = A resident (op-level residency)")
     return out
 
 
@@ -392,15 +421,51 @@ ALG_DESC = {"hs": "hs (the reference recurrence, cg.c:88-141)",
             "cg1": "cg1 (Chronopoulos-Gear)"}
 
 
-def alg_trial(sysm, warmup, layout="auto", maxit=20, its=30):
-    """N = 1: the recurrence of the headline, as the N > 1 path picks it --
-    a parity gate (HS and SR solves of `maxit` iterations: x within 1e-10 of
-    each other), then a timed trial of `its` graph-replayed iterations each;
-    the faster passing one.  SR runs on one GPU only where the plane-marched
-    DIA step applies (cgx_info.fuse_march)."""
+_ORACLE_GATE = {}
+
+
+def oracle_gate(maxit=20):
+    """the N = 1 parity gate against the ORACLE -- C3 (216^3,
+    b = 1, the bench's system) solved for maxit + 1 SpMVs on the GPU with HS
+    and with SR (the one-launch plane-marched step), each x within 1e-10 of
+    oracle_conj_grad(maxit) (cg.c:88-141 restated, bit-exact to the
+    reference).  Computed once per process."""
+    if _ORACLE_GATE:
+        return _ORACLE_GATE
     import numpy as np
     import cgx
-    res, trial, xs = {}, {}, {}
+    import helpers as H
+    sysm = make_system(WORKLOADS["c3"])
+    t0 = time.perf_counter()
+    x_ref, _ = H.o_conj_grad(maxit, sysm["rp"], sysm["col"], sysm["val"], sysm["b"])
+    out = dict(system="C3 216^3, b = 1", maxit=maxit,
+               oracle="oracle_conj_grad (cg.c:88-141, the reference's HS order)",
+               oracle_s=round(time.perf_counter() - t0, 2))
+    with cgx.Solver(0) as s:
+        s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+        for name in ("hs", "sr"):
+            s.set_mode(cgx.CGX_MODE_FAST, ALGS[name])
+            if name == "sr" and not s.info()["fuse_march"]:
+                out[name] = dict(ok=False, note="no plane-marched DIA step")
+                continue
+            s.set_rhs(sysm["b"])
+            s.run(maxit)
+            rel = float(np.linalg.norm(s.x() - x_ref) / np.linalg.norm(x_ref))
+            out[name] = dict(rel_vs_oracle=rel, ok=rel <= 1e-10)
+    _ORACLE_GATE.update(out)
+    return out
+
+
+def alg_trial(sysm, warmup, layout="auto", maxit=20, its=30):
+    """N = 1: the recurrence of the headline, as the N > 1 path picks it --
+    a parity gate (the oracle gate above at C3: HS and SR within 1e-10 of
+    oracle_conj_grad(20); on this workload HS and SR solves of `maxit`
+    iterations within 1e-10 of each other), then a timed trial of `its`
+    graph-replayed iterations each; the faster passing one.  SR runs on one
+    GPU only where the plane-marched DIA step applies (cgx_info.fuse_march)."""
+    import numpy as np
+    import cgx
+    res, trial, xs = {"oracle_gate": oracle_gate()}, {}, {}
     with cgx.Solver(0, layout=layout) as s:
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
         for name in ("hs", "sr"):
@@ -417,9 +482,11 @@ def alg_trial(sysm, warmup, layout="auto", maxit=20, its=30):
     if "sr" in xs:
         rel = float(np.linalg.norm(xs["sr"] - xs["hs"]) / np.linalg.norm(xs["hs"]))
         res["sr_vs_hs_rel"] = rel
-        if not rel <= 1e-10:
-            res["sr"] = f"parity gate failed: {rel:.3e}"
+        if not (rel <= 1e-10 and res["oracle_gate"]["sr"]["ok"]):
+            res["sr"] = f"parity gate failed: {rel:.3e} vs HS, oracle gate {res['oracle_gate']['sr']}"
             trial.pop("sr", None)
+    if not res["oracle_gate"]["hs"]["ok"]:
+        raise SystemExit(f"bench: HS failed the oracle gate: {res['oracle_gate']['hs']}")
     return min(trial, key=trial.get), dict(gate=res, ms_per_iter=trial, gate_maxit=maxit)
 
 
@@ -456,7 +523,8 @@ def csr_roofline(csr, wl_name):
     b_gbs, b_frac = spmv_roofline(ci["spmv_bytes"], csr["b2b_spmv_us"] * 1e-3)
     return dict(
         bound="hbm", achieved=c_gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=c_frac,
-        traffic=load_traffic(f"{wl_name}_csr"), kernel=KERNELS["csr"] + ", in the CG iteration",
+        **traffic_fields(wl_name, "csr", ci["spmv_bytes"]),
+        kernel=KERNELS["csr"] + ", in the CG iteration",
         basis="SURVEY.md 8d B_spmv = 12 nnz + 4 (n+1) + 16 n (CSR int32 col + fp64 val, "
               "row_ptr, x read once, y written once)",
         algorithmic_bytes_per_launch=int(ci["spmv_bytes"]), spmv_us=csr["spmv_us"],
@@ -474,7 +542,7 @@ def layout_roofline(info, spmv_ms, wl_name):
     return dict(kernel=kernel_name(info), layout=layout_desc(info),
                 spmv_us=round(spmv_ms * 1e3, 2), achieved=gbs, frac=frac,
                 algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
-                traffic=load_traffic(wl_name),
+                **traffic_fields(wl_name, kernel_key(info), info["spmv_iter_bytes"]),
                 csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
                 note="the SpMV launch of the headline solve, priced on the bytes it moves (its "
                      "layout; with the fused HS step also r, p_old, x, p_new; with the one-launch "
@@ -517,7 +585,29 @@ def c3_legs(steps, warmup):
                               b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"]))
     out["general_coefficients"] = general_coefficients(steps, warmup)
     out["solve_e2e"] = solve_e2e(sysm)
+    out["solve_e2e_sr"] = solve_e2e(sysm, alg="sr", legs=("warm",))
     return out
+
+
+def c5_leg(steps, warmup):
+    """C5 (random SPD, 5 M rows, ~64 nnz/row, fp32) inside the
+    default line -- CG it/s in the layout libcgx picks (column panels) and its
+    SpMV in the iteration on its own bytes and on SURVEY.md 8d's CSR basis."""
+    t0 = time.perf_counter()
+    sysm = make_system(WORKLOADS["c5"])
+    gen_s = time.perf_counter() - t0
+    leg = solver_leg(sysm, steps, warmup, "auto", b2b=True)
+    i = leg["info"]
+    own_gbs, own_frac = spmv_roofline(i["spmv_iter_bytes"], leg["spmv_us"] * 1e-3)
+    csr_gbs, csr_frac = spmv_roofline(i["spmv_bytes"], leg["spmv_us"] * 1e-3)
+    return dict(workload=WORKLOADS["c5"]["desc"], n=i["n"], nnz=i["nnz"], value=leg["value"],
+                unit="it/s", dtype="f32", layout=layout_desc(i), kernel=kernel_name(i),
+                spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
+                own_bytes=int(i["spmv_iter_bytes"]), own_bytes_gbs=own_gbs,
+                own_bytes_frac=own_frac, csr_basis_bytes=int(i["spmv_bytes"]),
+                csr_basis_gbs=csr_gbs, csr_basis_frac=csr_frac,
+                **traffic_fields("c5", kernel_key(i), i["spmv_iter_bytes"]),
+                host_gen_s=round(gen_s, 1), setup_ms=leg["setup_ms"])
 
 
 def run_single(args, wl_name):
@@ -562,8 +652,18 @@ def run_single(args, wl_name):
         lr = layout_roofline(info, spmv_ms, wl_name)
         roofline = dict(bound="hbm", achieved=lr["achieved"], peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=lr["frac"], traffic=lr["traffic"], kernel=lr["kernel"],
+                        traffic_source=lr["traffic_source"], traffic_ratio=lr["traffic_ratio"],
                         algorithmic_bytes_per_launch=lr["algorithmic_bytes_per_launch"],
                         spmv_us=lr["spmv_us"])
+    # the headline's own launch (the kernel `value` runs) beside the 8d CSR
+    # figure, with its bytes, duration, roofline fraction and PMC traffic
+    hk = layout_roofline(info, spmv_ms, wl_name)
+    headline_kernel = dict(bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
+                           **{k: hk[k] for k in ("kernel", "spmv_us", "achieved", "frac",
+                                                  "algorithmic_bytes_per_launch", "traffic",
+                                                  "traffic_source", "traffic_ratio")},
+                           timing="HIP events (hipExtLaunchKernel) around every launch of "
+                                  f"{args.steps} eager iterations on the solver's stream")
     triad = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)
     rd = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_READ)
     roofline["stream_triad_gbs"] = round(triad, 1)
@@ -587,6 +687,7 @@ def run_single(args, wl_name):
             extra["matrix_free"] = matrix_free(wl, sysm["b"], args.steps, args.warmup)
         if wl_name == "c4":
             extra["c3"] = c3_legs(args.steps, args.warmup)
+            extra["c5"] = c5_leg(args.steps, args.warmup)
         if wl_name == "c3":
             extra["general_coefficients"] = general_coefficients(args.steps, args.warmup)
             extra["c4_1gpu"] = c4_one_gpu(min(args.steps, 50), args.warmup)
@@ -614,7 +715,7 @@ def run_single(args, wl_name):
         device_ms_per_step=round(h["dev_ms"] / args.steps, 4),
         upload_ms=round(h["upload_ms"], 1),  # host CSR -> HBM + layout encoding, not in `value`
         iter_bytes=int(info["iter_bytes"]),
-        roofline=roofline, cpu_baseline=cpu, **extra)
+        roofline=roofline, headline_kernel=headline_kernel, cpu_baseline=cpu, **extra)
     print(json.dumps(out), flush=True)
 
 

@@ -194,7 +194,7 @@ CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON = 0, 1, 2
 # cgx_info.fuse_status / cgx_dist_stats.fuse_status (cgx.h)
 (CGX_FUSE_STATUS_RUNS, CGX_FUSE_STATUS_OFF, CGX_FUSE_STATUS_NOT_DIA, CGX_FUSE_STATUS_WIDE_CODES,
  CGX_FUSE_STATUS_FAR_DIAGS, CGX_FUSE_STATUS_CACHED, CGX_FUSE_STATUS_EXACT, CGX_FUSE_STATUS_PEER,
- CGX_FUSE_STATUS_CG1_AUTO) = range(9)
+ CGX_FUSE_STATUS_CG1_AUTO, CGX_FUSE_STATUS_NO_MARCH) = range(10)
 
 
 def fuse_mode(mode):
@@ -535,7 +535,8 @@ class CgxOpsTiming(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("setup_ms", ctypes.c_double),
                 ("hash_ms", ctypes.c_double), ("solve_ms", ctypes.c_double),
                 ("download_ms", ctypes.c_double), ("uploaded", ctypes.c_int),
-                ("iters", ctypes.c_int), ("breakdown", ctypes.c_int)]
+                ("iters", ctypes.c_int), ("breakdown", ctypes.c_int),
+                ("alg", ctypes.c_int)]
 
 
 def ops_set_mode(mode=CGX_MODE_FAST, alg=CGX_ALG_HS):

@@ -738,7 +738,8 @@ int hs_alpha(cgx_dist *d) {
       if (rc) return rc;
     }
     CGX_HIP(launch_update_rf<double>(d->n_loc, d->d_r, d->d_s, d->d_st, nullptr, 0, d->d_pa, gf,
-                                     d->st, nullptr, solo(d) ? d->d_sums : d->d_gsums));
+                                     d->st, nullptr, solo(d) ? d->d_sums : d->d_gsums,
+                                     d->d_hist));
     return 0;
   }
   if (solo(d)) {
@@ -978,8 +979,13 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
   if ((rc = prepare_states(g, maxit, tol, maxit + 1))) return rc;
   if ((rc = run_phases(g, true, 1))) return rc;
   // the fused step does an iteration's x update in the next launch: one
-  // more step carries the last one (and finds the stop)
-  const long long total = (long long)maxit + 1 + (fz(g->parts[0]) ? 1 : 0);
+  // more step carries the last one (and finds the stop); SR tests iteration
+  // k's stop on the exact r.r of the next reduction: one more, and it is
+  // complete at done = 2 (an even stop iteration's x update still pending
+  // at 1)
+  const bool sr0 = sr(g->parts[0]);
+  const long long total = (long long)maxit + 1 + (fz(g->parts[0]) ? 1 : 0) + (sr0 ? 1 : 0);
+  const int fin_done = sr0 ? 2 : 1;
   if (tol <= 0.0) {
     if ((rc = run_phases(g, false, total))) return rc;
     if ((rc = read_states(g))) return rc;
@@ -993,7 +999,7 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
       done += b;
       if ((rc = read_states(g))) return rc;
       const CgState *h = g->parts[0]->h_st;
-      if (h->done || done >= total) break;
+      if (h->done >= fin_done || done >= total) break;
       // every rank sees the same all-reduced r.r: the same batches everywhere
       batch = next_batch(h->rr, h->tol2bb, h->k, rr_prev, k_prev, batch);
       rr_prev = h->rr;

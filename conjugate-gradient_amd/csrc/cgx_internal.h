@@ -373,13 +373,16 @@ hipError_t launch_xpay(int n, T *p, const T *r, const CgState *stt, int grid,
 // folded HS steps (alpha / beta computed inside from the producer's partials)
 // fin (optional): the r.r partials' canonical sum to fin->out[0] by the last
 // workgroup (fin->pa must be rr_part, fin->na = 4 * grid)
-// sr (CGX_ALG_SR): the reduced (p.s, s.s, r.r) -- alpha = r.r / p.s from
-// them instead of ps_part and rr_x, and r_new.r_new = alpha^2 s.s - r.r to
-// st->rr_new for the next fused launch's beta and stop test
+// sr (CGX_ALG_SR): the reduced (p.s, s.s, r.r) -- first the previous
+// iteration's stop test on the exact r.r (its history entry to hist), then
+// alpha = r.r / p.s from them instead of ps_part and rr_x, and the estimate
+// r_new.r_new = alpha^2 s.s - r.r to st->rr_new for the next fused launch's
+// beta
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
-                            const FinArgs *fin = nullptr, const double *sr = nullptr);
+                            const FinArgs *fin = nullptr, const double *sr = nullptr,
+                            double *hist = nullptr);
 // p -> pn (pn == p: in place, x every iteration; pn != p: x every other
 // iteration, k_xpay_xf)
 template <typename T>

@@ -242,30 +242,41 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
   }
 }
 
-// CGX_ALG_SR on one GPU (k_sr1_dia_m's sums of iteration k = k_u + 1):
-// alpha = r.r / p.s (cg.c:113), the estimate r_new.r_new = alpha (alpha s.s)
-// - r.r clamped at 0 (oracle_solve_sr) for the history, the stop test (the
-// cg.c:125 position) and beta (cg.c:129).  done = 1: the next launch applies
-// the pending x updates, whose finalize marks the solve complete (2).
+// CGX_ALG_SR on one GPU (k_sr1_dia_m's sums of launch j = k_u + 1: p_j.s_j,
+// s_j.s_j and the EXACT r_j.r_j of the r_j it computed).  First the stop
+// test of iteration j - 1 (cg.c:125's position) on the exact r_j.r_j --
+// the reference's own rule, one launch late; the estimate never stops a
+// solve -- and its history entry.  Otherwise iteration j's
+// scalars: alpha = r.r / p.s (cg.c:113), the estimate r_new.r_new = alpha
+// (alpha s.s) - r.r clamped at 0 for beta (cg.c:129) only (oracle_solve_sr).
+// A stop at an odd j - 1: launch j completed x (done = 2); at an even one
+// x += alpha_{j-1} p_{j-1} is pending (done = 1): the next launch applies
+// it, and its finalize marks the solve complete (2).
 __device__ void fin_sr1(double ps, double ss, double rr, CgState *st, double *hist) {
   if (st->done) {
     st->done = 2;
     return;
   }
-  const int k = st->k_u + 1;
+  const int j = st->k_u + 1;
+  if (j >= 1) {
+    const int k = j - 1;
+    if (k < st->hist_cap) hist[k] = rr;
+    st->rr = rr;
+    st->k = k;
+    if (k >= st->max_iter || (st->use_tol && rr <= st->tol2bb)) {
+      st->done = (k & 1) ? 2 : 1;
+      return;
+    }
+  }
   const double alpha = rr / ps;
   const double as2 = alpha * ss;
   double est = alpha * as2 - rr;
   if (!(est > 0.0)) est = 0.0;
-  if (k < st->hist_cap) hist[k] = est;
-  if (!(ps > 0.0) && st->brk == 0) st->brk = k + 1;
+  if (!(ps > 0.0) && st->brk == 0) st->brk = j + 1;
   st->ps = ps;
   st->alpha = alpha;
-  st->k_u = k;
-  st->k = k;
-  st->rr = est;
-  if (k >= st->max_iter || (st->use_tol && est <= st->tol2bb)) st->done = 1;
-  else st->beta = est / rr;
+  st->k_u = j;
+  st->beta = est / rr;
 }
 
 // XCD-contiguous workgroup order (speed only, never correctness): the
@@ -759,14 +770,28 @@ struct FuseStep {
   double alpha, beta;
 };
 
+// CGX_ALG_SR (sr): *rr_new_p is k_update_rf's estimate alpha^2 s.s - r.r,
+// for beta only; the stop test is k_update_rf's, on the exact r.r one
+// launch later (oracle_solve_sr), which sets done = 1 when an even
+// iteration's deferred x update is pending: stop here means "apply it".
 __device__ __forceinline__ FuseStep fuse_step(CgState *st, double *hist, const double *rr_new_p,
-                                              bool publish) {
+                                              bool publish, bool sr = false) {
   FuseStep f;
   const int k = st->k_u;
   f.first = k < 0;
   f.alpha = st->alpha;
   f.beta = 0.0;
   f.stop = false;
+  if (sr) {
+    f.stop = st->done == 1;
+    if (!f.first) f.beta = *rr_new_p / st->rr_u;  // cg.c:129
+    if (!f.first && !f.stop && publish && blockIdx.x == 0 && threadIdx.x == 0) {
+      st->beta = f.beta;
+      st->k = k + 1;
+      st->k_x = k + 1;
+    }
+    return f;
+  }
   if (!f.first) {
     const double rr_new = *rr_new_p;
     f.stop = k >= st->max_iter || (st->use_tol && rr_new <= st->tol2bb);
@@ -839,7 +864,7 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs
   }
   const int s = LIST ? a.items.list[pos] : a.items.first + pos;
   if (f.st->done > 1) return;  // uniform
-  const FuseStep fs = fuse_step(f.st, f.hist, f.rr_new, f.publish != 0);
+  const FuseStep fs = fuse_step(f.st, f.hist, f.rr_new, f.publish != 0, f.ss != nullptr);
   const T alpha = (T)fs.alpha, beta = (T)fs.beta;
   const int s0 = s * kDiaSliceRows, r = s0 + 2 * t;
   // act: the row pair lies in the super-item's slices (rows >= n there are
@@ -855,6 +880,9 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs
   const int k = f.st->k_u;
   const bool odd = (k & 1) != 0;
   const bool xup = !fs.first && (odd || fs.stop);
+  // SR's stop (fuse_step): only the deferred x += alpha_k p_k of the even
+  // stop iteration k, p_k in the p_new buffer
+  const bool xdef = f.ss != nullptr && fs.stop;
   const T alpha_d = (T)f.st->alpha_def;
   if (f.publish && !fs.first && !odd && !fs.stop && blockIdx.x == 0 && t == 0)
     f.st->alpha_def = fs.alpha;
@@ -863,18 +891,22 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_h(SpmvArgs<T> a, FuseArgs
     if (xup) {
       po = ld_pair(f.pold, rs);
       xo = ld_pair(f.x, rs);
-      if (odd) pd = ld_pair((const T *)f.pnew, rs);
+      if (odd || xdef) pd = ld_pair((const T *)f.pnew, rs);
     }
   };
   auto x_update = [&]() {
     T x0 = xo.x, x1 = xo.y;
-    if (odd) {
+    if (odd || xdef) {
       const T d0 = alpha_d * pd.x, d1 = alpha_d * pd.y;
       x0 = x0 + d0;
       x1 = x1 + d1;
     }
-    const T a0 = alpha * po.x, a1 = alpha * po.y;
-    st_pair(f.x, r, rend, x0 + a0, x1 + a1, false);
+    if (!xdef) {
+      const T a0 = alpha * po.x, a1 = alpha * po.y;
+      x0 = x0 + a0;
+      x1 = x1 + a1;
+    }
+    st_pair(f.x, r, rend, x0, x1, false);
   };
   if (fs.stop) {  // the pending x updates only (then the cg.c:125 break)
     load_x();
@@ -1241,7 +1273,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   const int k = f.st->k_u;  // the last finalized iteration (-1: none)
   const bool first = k < 0, stop = f.st->done == 1;
   const bool odd = (k & 1) != 0;
-  const bool xup = !first && (odd || stop);
+  const bool xup = !first && odd;
   const T alpha = (T)f.st->alpha, beta = (T)f.st->beta, alpha_d = (T)f.st->alpha_def;
   if (!first && !odd && !stop && blockIdx.x == 0 && t == 0)
     const_cast<CgState *>(f.st)->alpha_def = f.st->alpha;
@@ -1294,13 +1326,15 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       f.pc[blockIdx.x] = p2;
     }
   };
-  if (stop) {  // the pending x updates only (then the stop of oracle_solve_sr)
-    if (xup)
-      for (int m = m0; m < m1; ++m) {
-        const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + SR);
-        load_x(m, xc);
-        if (r < rend) x_update(xc, r, rend);
-      }
+  if (stop) {
+    // fin_sr1 stopped at an even iteration k (k_u): its deferred x +=
+    // alpha_k p_k only, p_k in the p_new buffer of this launch
+    for (int m = m0; m < m1; ++m) {
+      const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + SR), rs = r < a.n ? r : 0;
+      const P pd = ld_pair((const T *)f.pnew, rs), xo = ld_pair(f.x, rs);
+      const T d0 = alpha_d * pd.x, d1 = alpha_d * pd.y;
+      if (r < rend) st_pair(f.x, r, rend, xo.x + d0, xo.y + d1, false);
+    }
     return;
   }
   if (m0 >= m1) {  // no steps: zero sums (k_finalize adds every workgroup's)
@@ -1971,7 +2005,8 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
                                                        CgState *__restrict__ st,
                                                        const double *__restrict__ ps_part,
                                                        int nps, double *__restrict__ rr_part,
-                                                       FinArgs fin, const double *sr) {
+                                                       FinArgs fin, const double *sr,
+                                                       double *hist) {
   __shared__ double red[kFoldBS / kWave];
   __shared__ double bcast;
   const int done = st->done;
@@ -1990,6 +2025,24 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
   }
   // CGX_ALG_SR: p.s, s.s and the exact r.r of the current r come reduced
   // together (one all-reduce); r_new.r_new = alpha^2 s.s - r.r (r.s = p.s)
+  // for the next beta.  First the stop test of the PREVIOUS iteration
+  // (cg.c:125's position) on that exact r.r (oracle_solve_sr): uniform over
+  // the grid (every workgroup reads the same values); r stays as it is.  An
+  // odd stop iteration's x is complete (done = 2), an even one's deferred x
+  // update is applied by the next fused launch (done = 1; fuse_step).
+  if (sr) {
+    const int kp = st->k_x - 1;
+    const bool stop = kp >= 0 && (kp >= st->max_iter || (st->use_tol && sr[2] <= st->tol2bb));
+    if (kp >= 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+      if (kp < st->hist_cap) hist[kp] = sr[2];
+      st->rr = sr[2];
+      if (stop) {
+        st->k = kp;
+        st->done = (kp & 1) ? 2 : 1;
+      }
+    }
+    if (stop) return;
+  }
   const double ps = sr ? sr[0] : sum_parts<kFoldBS>(ps_part, nps, red);
   if (threadIdx.x == 0) {
     const double rr = sr ? sr[2] : st->rr_x;
@@ -2868,10 +2921,10 @@ hipError_t launch_pack_pnext(int n_send, const int *idx, const T *r, const T *po
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
-                            const FinArgs *fin, const double *sr) {
+                            const FinArgs *fin, const double *sr, double *hist) {
   const FinArgs f = fin ? *fin : FinArgs{};
   hipLaunchKernelGGL((k_update_rf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt, ps_part,
-                     nps, rr_part, f, sr);
+                     nps, rr_part, f, sr, hist);
   return hipGetLastError();
 }
 
@@ -2996,7 +3049,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                                            T *, const CgState *, hipStream_t);                   \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
                                           double *, int, hipStream_t, const FinArgs *,           \
-                                          const double *);                                       \
+                                          const double *, double *);                             \
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \
                                         const double *, int, double *, int, hipStream_t);        \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *, const T *, const CgState *,  \

@@ -268,12 +268,20 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct _
   cgx_solver *s = nullptr;
   int rc = default_solver(&s);
   if (rc) return rc;
-  if ((rc = cgx_solver_set_mode(s, g_mode, g_mode == CGX_MODE_EXACT ? CGX_ALG_HS : g_alg)))
-    return rc;
-  int iters = maxit + 1;
+  int iters = maxit + 1, ran = g_alg;
   MatTiming mt;
   rc = with_matrix(s, A, [&] {
-    int r = cgx_solver_set_rhs(s, b->values);
+    // CGX_ALG_SR only where the matrix takes its one-launch step (the plane-
+    // marched DIA layout); otherwise the reference's HS -- reported in
+    // cgx_ops_last_timing().alg
+    ran = g_alg;
+    int r = cgx_solver_set_mode(s, g_mode, ran);
+    if (r == 0 && ran == CGX_ALG_SR) {
+      cgx_info inf;
+      r = cgx_solver_info(s, &inf);
+      if (r == 0 && !inf.fused) r = cgx_solver_set_mode(s, g_mode, ran = CGX_ALG_HS);
+    }
+    if (r == 0) r = cgx_solver_set_rhs(s, b->values);
     if (r == 0 && A->size > 0) r = cgx_solver_run(s, maxit, tol, &iters);
     return r;
   }, &mt);
@@ -292,6 +300,7 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct _
   t.download_ms = now_ms() - t2;
   t.total_ms = now_ms() - t0;
   t.iters = iters;
+  t.alg = ran;
   {
     cgx_info inf;
     if (cgx_solver_info(s, &inf) == 0) t.breakdown = inf.breakdown;
@@ -450,7 +459,8 @@ int mv_mult(struct __mv_sparse *A, struct __mv_sparse *b, struct __mv_sparse **r
 }
 
 int cgx_ops_set_mode(int mode, int alg) {
-  if ((mode != CGX_MODE_FAST && mode != CGX_MODE_EXACT) || (alg != CGX_ALG_HS && alg != CGX_ALG_CG1) ||
+  if ((mode != CGX_MODE_FAST && mode != CGX_MODE_EXACT) ||
+      (alg != CGX_ALG_HS && alg != CGX_ALG_CG1 && alg != CGX_ALG_SR) ||
       (mode == CGX_MODE_EXACT && alg != CGX_ALG_HS)) {
     set_error("cgx_ops_set_mode: bad mode/alg (exact mode is HS only)");
     return CGX_EINVAL;

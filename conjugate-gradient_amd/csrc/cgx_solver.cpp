@@ -225,9 +225,6 @@ int alloc_vectors(cgx_solver *s) {
       (rc = dev_alloc(&s->d_r, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_p, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_s, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_w, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_p2, nv, &s->vec_bytes)) ||
-      (rc = dev_alloc(&s->d_r2, nv, &s->vec_bytes)) ||
-      (rc = dev_alloc(&s->d_s2, nv, &s->vec_bytes)) ||
-      (rc = dev_alloc(&s->d_w2, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pa, (size_t)s->part_cap * 8, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pb, (size_t)s->part_cap * 8, &s->vec_bytes))) {
     free_system(s);
@@ -239,6 +236,39 @@ int alloc_vectors(cgx_solver *s) {
   CGX_HIP(hipMemsetAsync(s->d_p2, 0, nv, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
   s->have_matrix = true;
+  return 0;
+}
+
+// The second r, s (and w) buffers exist only while a recurrence that reads
+// one set and writes the other runs (SR's one launch, the fused CG1 step):
+// 3 n vectors HS never touches (1.5 GB at C4).  Allocated before
+// the prologue and the graph capture of such a run.
+bool needs_rsw2(const cgx_solver *s) {
+  return fused(s) && (s->alg == CGX_ALG_SR || s->alg == CGX_ALG_CG1);
+}
+
+int ensure_rsw2(cgx_solver *s) {
+  if (!needs_rsw2(s) || s->d_r2) return 0;
+  const size_t nv = ((size_t)s->A.n + kPad) * tsize(s->A.dtype);
+  int rc;
+  if ((rc = dev_alloc(&s->d_r2, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_s2, nv, &s->vec_bytes)) ||
+      (rc = dev_alloc(&s->d_w2, nv, &s->vec_bytes))) {
+    dev_free(&s->d_r2);
+    dev_free(&s->d_s2);
+    dev_free(&s->d_w2);
+    return rc;
+  }
+  for (void *v : {s->d_r2, s->d_s2, s->d_w2}) CGX_HIP(hipMemsetAsync(v, 0, nv, s->stream));
+  return 0;
+}
+
+// A recurrence the loaded matrix cannot run (SR without the plane-marched
+// DIA step) is refused before anything is enqueued.
+int check_runnable(const cgx_solver *s) {
+  if (s->alg == CGX_ALG_SR && !fused(s)) {
+    set_error("CGX_ALG_SR on one GPU needs the plane-marched DIA step (cgx_info.fuse_march)");
+    return CGX_EINVAL;
+  }
   return 0;
 }
 
@@ -503,17 +533,15 @@ template <typename T>
 int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
   int rc;
   s->bench_ready = false;
+  if ((rc = check_runnable(s)) || (rc = ensure_rsw2(s))) return rc;
   if ((rc = prepare_state(s, maxit, tol, maxit + 1))) return rc;
   if ((rc = enqueue_init<T>(s))) return rc;
   // the fused step does an iteration's x update in the next launch: one
-  // more step carries the last one (and finds the stop)
-  if (s->alg == CGX_ALG_SR && !fused(s)) {
-    set_error("CGX_ALG_SR on one GPU needs the plane-marched DIA step (cgx_info.fuse_march)");
-    return CGX_EINVAL;
-  }
-  const long long total = (long long)maxit + 1 + (fused(s) && s->alg != CGX_ALG_CG1 ? 1 : 0);
-  // SR decides the stop in the finalize before the launch that applies the
-  // last x update: complete once that launch's finalize marks done = 2
+  // more step carries the last one (and finds the stop); SR tests the stop
+  // of iteration k on the exact r.r that launch k + 1 computes: one more
+  const long long total = (long long)maxit + 1 + (fused(s) && s->alg != CGX_ALG_CG1 ? 1 : 0) +
+                          (s->alg == CGX_ALG_SR ? 1 : 0);
+  // SR: complete once the finalize after the last x update marks done = 2
   const int fin_done = s->alg == CGX_ALG_SR ? 2 : 1;
   if (tol <= 0.0) {
     if ((rc = enqueue_iters<T>(s, total))) return rc;
@@ -549,10 +577,7 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
 template <typename T>
 int bench_prepare_t(cgx_solver *s, int warmup) {
   int rc;
-  if (s->alg == CGX_ALG_SR && !fused(s)) {
-    set_error("CGX_ALG_SR on one GPU needs the plane-marched DIA step (cgx_info.fuse_march)");
-    return CGX_EINVAL;
-  }
+  if ((rc = check_runnable(s)) || (rc = ensure_rsw2(s))) return rc;
   if ((rc = prepare_state(s, INT_MAX - 1, 0.0, 0))) return rc;
   if ((rc = enqueue_init<T>(s))) return rc;
   if ((rc = ensure_graphs<T>(s))) return rc;  // captured here, not in a timed region
@@ -745,6 +770,7 @@ int cgx_solver_set_mode(cgx_solver *s, int mode, int alg) {
     cgx::set_error("exact mode is defined for the HS recurrence only");
     return CGX_EINVAL;
   }
+  if (s->mode == mode && s->alg == alg) return 0;  // keeps the captured graphs
   s->mode = mode;
   s->alg = alg;
   drop_graph(s);
@@ -914,12 +940,16 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->setup_device_ms = A.setup_dev_ms;
   info->encode_fallback = A.encode_fallback;
   info->fused = s->have_matrix && fused(s) ? 1 : 0;
+  // the conditions of fused(): SR needs the march plan and ignores the
+  // Infinity Cache rule
+  const bool sr = s->alg == CGX_ALG_SR;
   info->fuse_status = !s->have_matrix ? CGX_FUSE_STATUS_NOT_DIA
                       : s->mode == CGX_MODE_EXACT ? CGX_FUSE_STATUS_EXACT
                       : s->fuse == CGX_FUSE_OFF   ? CGX_FUSE_STATUS_OFF
                       : A.fuse_block()            ? A.fuse_block()
-                      : (s->fuse == CGX_FUSE_AUTO && !A.nt) ? CGX_FUSE_STATUS_CACHED
-                                                            : CGX_FUSE_STATUS_RUNS;
+                      : sr && (A.mq == 0 || s->march == 0) ? CGX_FUSE_STATUS_NO_MARCH
+                      : (!sr && s->fuse == CGX_FUSE_AUTO && !A.nt) ? CGX_FUSE_STATUS_CACHED
+                                                                   : CGX_FUSE_STATUS_RUNS;
   info->breakdown = s->h_st ? s->h_st->brk : 0;
   info->fuse_march = s->have_matrix ? march_len(s) : 0;
   return 0;

@@ -10,7 +10,9 @@
  *
  * Environment (read here, not by the library): CGX_MODE=exact -> the
  * reference's sequential dot-product order (bit-identical x), CGX_ALG=cg1 ->
- * Chronopoulos-Gear, CGX_DEVICE=<ordinal> -> the GPU, CGX_INPUT_CACHE=<path>
+ * Chronopoulos-Gear, CGX_ALG=sr -> the single-reduction recurrence where the
+ * matrix takes its one-launch step (HS otherwise), CGX_DEVICE=<ordinal> ->
+ * the GPU, CGX_INPUT_CACHE=<path>
  * -> read the input through the binary cache at <path>
  * (cgx_read_input_cached: the text is parsed once per input version). */
 #include <stdio.h>
@@ -33,8 +35,10 @@ int main(int argc, char **argv)
 
   const char *mode = getenv("CGX_MODE"), *alg = getenv("CGX_ALG"), *dev = getenv("CGX_DEVICE");
   const int exact = mode && strcmp(mode, "exact") == 0;
-  if (cgx_ops_set_mode(exact ? CGX_MODE_EXACT : CGX_MODE_FAST,
-                       !exact && alg && strcmp(alg, "cg1") == 0 ? CGX_ALG_CG1 : CGX_ALG_HS) != 0 ||
+  int a = CGX_ALG_HS;
+  if (!exact && alg && strcmp(alg, "cg1") == 0) a = CGX_ALG_CG1;
+  if (!exact && alg && strcmp(alg, "sr") == 0) a = CGX_ALG_SR;
+  if (cgx_ops_set_mode(exact ? CGX_MODE_EXACT : CGX_MODE_FAST, a) != 0 ||
       (dev && *dev && cgx_ops_set_device(atoi(dev)) != 0)) {
     fprintf(stderr, "cg: %s\n", cgx_last_error());
     return 1;

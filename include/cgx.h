@@ -54,8 +54,12 @@ void cgx_free_mv_deep(struct __mv_sparse *m);
  *        fp64 rounding of the reference (tests: 1e-12 relative)
  *   mode CGX_MODE_EXACT: the reference's sequential dot-product order, x
  *        bit-identical to cg.c on chained matrices (HS only)
- *   alg  CGX_ALG_HS (the reference recurrence, default) or CGX_ALG_CG1
- * The drop-in CLI maps CGX_MODE=exact / CGX_ALG=cg1 onto this call. */
+ *   alg  CGX_ALG_HS (the reference recurrence, default), CGX_ALG_CG1, or
+ *        CGX_ALG_SR (fast mode only: the one-launch single-reduction step
+ *        where the matrix takes the plane-marched DIA step -- the bench's
+ *        N = 1 recurrence; any other matrix runs HS instead, and
+ *        cgx_ops_last_timing().alg reports which one ran)
+ * The drop-in CLI maps CGX_MODE=exact / CGX_ALG=cg1|sr onto this call. */
 int cgx_ops_set_mode(int mode, int alg);
 /* GPU of those entry points (default 0); before their first call only. */
 int cgx_ops_set_device(int device);
@@ -69,6 +73,8 @@ typedef struct {
   double total_ms, setup_ms, hash_ms, solve_ms, download_ms;
   int uploaded, iters;
   int breakdown;  /* as cgx_info.breakdown, for the last conj_grad / solve */
+  int alg;        /* CGX_ALG_* that ran: CGX_ALG_SR was requested but the
+                     matrix has no plane-marched DIA step -> CGX_ALG_HS */
 } cgx_ops_timing;
 int cgx_ops_last_timing(cgx_ops_timing *t);
 
@@ -191,8 +197,11 @@ enum { CGX_FUSE_STATUS_RUNS = 0,        /* the fused step runs                  
        CGX_FUSE_STATUS_EXACT = 6,       /* exact mode runs the reference's order */
        CGX_FUSE_STATUS_PEER = 7,        /* partitioned: another rank's layout
                                            refused (all ranks or none)           */
-       CGX_FUSE_STATUS_CG1_AUTO = 8 };  /* partitioned CG1: fused only when
+       CGX_FUSE_STATUS_CG1_AUTO = 8,    /* partitioned CG1: fused only when
                                            forced on (slower on a rank's slab)   */
+       CGX_FUSE_STATUS_NO_MARCH = 9 };  /* CGX_ALG_SR on one GPU: the matrix has
+                                           no plane-march plan, or
+                                           cgx_solver_set_march(0)               */
 
 int  cgx_solver_create(int device, cgx_solver **out);
 void cgx_solver_destroy(cgx_solver *s);

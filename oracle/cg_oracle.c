@@ -212,14 +212,16 @@ int oracle_solve_cg1(int maxit, double tol, int n, const int *row_ptr,
   return k + 1;
 }
 
-/* The single-reduction HS variant of the partitioned solver (CGX_ALG_SR):
- * cg.c:88-141's recurrence with p.s, s.s and r.r computed together (one
- * all-reduce on the GPUs).  alpha = r.r / p.s exactly as cg.c:113; beta
- * (cg.c:129) and the stop test (cg.c:125 position) use
+/* The single-reduction HS variant (CGX_ALG_SR, the N = 1 bench recurrence
+ * and the partitioned solver's): cg.c:88-141's recurrence with p.s, s.s and
+ * r.r computed together (one reduction / all-reduce on the GPUs).
+ * alpha = r.r / p.s exactly as cg.c:113; beta (cg.c:129) uses
  * r_new.r_new = alpha (alpha s.s) - r.r (clamped at 0), which equals the
- * exact r_new.r_new in exact arithmetic because r.s = p.s; the exact r_new.r_new
- * becomes the next alpha's numerator.  rr_hist records the estimate (what the
- * stop test saw), as the GPU solver's history does. */
+ * exact r_new.r_new in exact arithmetic because r.s = p.s.  The stop test
+ * (cg.c:125 position) reads the EXACT r_new.r_new -- the reference's rule;
+ * the GPUs get it from the next launch's reduction, one launch late -- and
+ * the exact r_new.r_new is the next alpha's numerator.  rr_hist records the
+ * exact r_new.r_new, as oracle_solve's. */
 int oracle_solve_sr(int maxit, double tol, int n, const int *row_ptr,
                     const int *col, const double *val, const double *b,
                     double *x, double *rr_hist)
@@ -252,18 +254,19 @@ int oracle_solve_sr(int maxit, double tol, int n, const int *row_ptr,
     double est = alpha * as2 - rr;
     if (!(est > 0.0))
       est = 0.0;
+    double rr_new = oracle_dot(n, r, r);
     if (rr_hist)
-      rr_hist[k] = est;
+      rr_hist[k] = rr_new;
     if (k == maxit)
       break;
-    if (tol > 0.0 && est <= tol2bb)
+    if (tol > 0.0 && rr_new <= tol2bb)
       break;
     double beta = est / rr;
     for (int i = 0; i < n; i++) {
       double bp = beta * p[i];
       p[i] = r[i] + bp;
     }
-    rr = oracle_dot(n, r, r);
+    rr = rr_new;
     k++;
   }
   free(r); free(p); free(s);
@@ -282,6 +285,67 @@ int oracle_spmv_csr_f32(int n, const int *row_ptr, const int *col,
     y[i] = acc;
   }
   return 0;
+}
+
+/* C5's iteration: cg.c:88-141 with fp32 matrix and vectors, as libcgx runs
+ * it (the reference itself is fp64 only, mv_ops.h:20).
+ * Row sums and products in float (oracle_spmv_csr_f32); every dot product
+ * sums the EXACT double products of the float operands, sequentially from
+ * 0.0 (the kernels' partials do the same in another grouping); alpha and
+ * beta are formed in double (cg.c:113, 129) and rounded to float once for
+ * the float vector updates, each a float product then a float add
+ * (cg.c:115-132's two roundings). */
+static double dot_f32(int n, const float *a, const float *b)
+{
+  double acc = 0.0;
+  for (int i = 0; i < n; i++)
+    acc = acc + (double)a[i] * (double)b[i];
+  return acc;
+}
+
+int oracle_solve_f32(int maxit, double tol, int n, const int *row_ptr,
+                     const int *col, const float *val, const float *b,
+                     float *x, double *rr_hist)
+{
+  size_t bytes = (size_t)(n > 0 ? n : 1) * sizeof(float);
+  float *r = (float *)malloc(bytes), *p = (float *)malloc(bytes);
+  float *s = (float *)malloc(bytes);
+  if (!r || !p || !s) {
+    free(r); free(p); free(s);
+    return -1;
+  }
+  memset(x, 0, (size_t)n * sizeof(float));          /* cg.c:104 */
+  memcpy(r, b, (size_t)n * sizeof(float));          /* cg.c:107 */
+  memcpy(p, b, (size_t)n * sizeof(float));          /* cg.c:108 */
+  double bb = dot_f32(n, b, b), rr = bb, tol2bb = tol * tol * bb;
+  int k = 0;
+  for (;;) {
+    oracle_spmv_csr_f32(n, row_ptr, col, val, p, s);          /* cg.c:111 */
+    double alpha = rr / dot_f32(n, p, s);                     /* cg.c:113 */
+    float af = (float)alpha;
+    for (int i = 0; i < n; i++) {
+      float ap = af * p[i];
+      x[i] = x[i] + ap;                                       /* cg.c:115-118 */
+      float as = af * s[i];
+      r[i] = r[i] - as;                                       /* cg.c:122-123 */
+    }
+    double rr_new = dot_f32(n, r, r);
+    if (rr_hist)
+      rr_hist[k] = rr_new;
+    if (k == maxit)                                           /* cg.c:125 */
+      break;
+    if (tol > 0.0 && rr_new <= tol2bb)
+      break;
+    float bf = (float)(rr_new / rr);                          /* cg.c:129 */
+    for (int i = 0; i < n; i++) {
+      float bp = bf * p[i];
+      p[i] = r[i] + bp;                                       /* cg.c:131-132 */
+    }
+    rr = rr_new;
+    k++;
+  }
+  free(r); free(p); free(s);
+  return k + 1;
 }
 
 /* ---------------- multithreaded CPU baseline (pthreads) ---------------- */

@@ -73,9 +73,9 @@ int oracle_solve_cg1(int maxit, double tol, int n, const int *row_ptr,
                      const int *col, const double *val, const double *b,
                      double *x, double *rr_hist);
 
-/* The partitioned solver's single-reduction HS variant (CGX_ALG_SR): alpha
- * as cg.c:113, beta and the stop test from alpha^2 s.s - r.r.  Same stopping
- * rule as oracle_solve; rounding-level different from it. */
+/* The single-reduction HS variant (CGX_ALG_SR): alpha as cg.c:113, beta
+ * from alpha^2 s.s - r.r; the stop test on the exact r.r, the same stopping
+ * rule as oracle_solve.  Rounding-level different from it. */
 int oracle_solve_sr(int maxit, double tol, int n, const int *row_ptr,
                     const int *col, const double *val, const double *b,
                     double *x, double *rr_hist);
@@ -85,6 +85,15 @@ int oracle_solve_sr(int maxit, double tol, int n, const int *row_ptr,
  * mv_ops.h:20). */
 int oracle_spmv_csr_f32(int n, const int *row_ptr, const int *col,
                         const float *val, const float *x, float *y);
+
+/* C5's HS-CG in fp32 (cg.c:88-141 with float matrix and vectors, as libcgx
+ * runs it): float products and row sums in the SpMV, dot products as
+ * sequential sums of the exact double products, alpha / beta in double
+ * rounded once to float, float vector updates with two roundings each.
+ * Same stopping rule as oracle_solve.  Returns SpMVs performed. */
+int oracle_solve_f32(int maxit, double tol, int n, const int *row_ptr,
+                     const int *col, const float *val, const float *b,
+                     float *x, double *rr_hist);
 
 /* Multithreaded CSR SpMV + HS-CG on `threads` host threads (pthreads) --
  * the "all host cores" CPU baseline mode of BASELINE.md.  Per-row sums are

@@ -257,6 +257,8 @@ def oracle():
     lib.oracle_solve_sr.argtypes = lib.oracle_solve.argtypes
     lib.oracle_spmv_csr_f32.argtypes = [ctypes.c_int, _i32p, _i32p, _f32p,
                                         _f32p, _f32p]
+    lib.oracle_solve_f32.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                     _i32p, _i32p, _f32p, _f32p, _f32p, _f64p]
     lib.oracle_solve_mt.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                     _i32p, _i32p, _f64p, _f64p, _f64p,
                                     ctypes.c_int]
@@ -321,6 +323,22 @@ def o_solve(maxit, tol, rp, col, val, b, cg1=False, sr=False):
           else oracle().oracle_solve)
     its = fn(maxit, tol, n, _p(rp, _i32p), _p(col, _i32p), _p(val, _f64p),
              _p(b, _f64p), _p(x, _f64p), _p(hist, _f64p))
+    return x, its, hist[:its]
+
+
+def o_solve_f32(maxit, tol, rp, col, val, b):
+    """oracle_solve_f32: C5's fp32 HS-CG (float vectors, exact double dot
+    products, alpha / beta rounded to float once)."""
+    rp = np.ascontiguousarray(rp, np.int32)
+    col = np.ascontiguousarray(col, np.int32)
+    val = np.ascontiguousarray(val, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    n = len(rp) - 1
+    x = np.empty(n, np.float32)
+    hist = np.zeros(maxit + 1, np.float64)
+    its = oracle().oracle_solve_f32(maxit, tol, n, _p(rp, _i32p), _p(col, _i32p),
+                                    _p(val, _f32p), _p(b, _f32p), _p(x, _f32p),
+                                    _p(hist, _f64p))
     return x, its, hist[:its]
 
 

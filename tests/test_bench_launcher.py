@@ -75,3 +75,33 @@ def test_rank_path_selection(monkeypatch, argv, expect):
     monkeypatch.setattr(bench, "run_dist", lambda a, w, *r: seen.update(path="dist", wl=w))
     bench.main()
     assert (seen["path"], seen["wl"]) == expect
+
+
+def test_traffic_is_keyed_on_the_kernel(tmp_path, monkeypatch):
+    """a PMC summary prices only the kernel it was collected
+    on -- a file naming another kernel yields no `traffic` (and says why)."""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "REPO", tmp_path)
+    (prof / "pmc_c4_sr1.json").write_text(json.dumps(
+        {"kernel": "k_sr1_dia_m<double, 2, 2, 1>", "spmv_hbm_bytes_per_launch": 4.1e9}))
+    (prof / "pmc_c4_dia_march.json").write_text(json.dumps(
+        {"kernel": "k_sr1_dia_m<double, 2, 2, 1>", "spmv_hbm_bytes_per_launch": 4.1e9}))
+    t = bench.traffic_fields("c4", "sr1", 3.904e9)
+    assert t["traffic"] == 4_100_000_000 and t["traffic_ratio"] == round(4.1 / 3.904, 4)
+    t = bench.traffic_fields("c4", "dia_march", 2.88e9)
+    assert t["traffic"] is None and "not k_spmv_dia_m<" in t["traffic_source"]
+    assert bench.traffic_fields("c3", "sr1", 1.0)["traffic"] is None
+
+
+def test_committed_pmc_summaries_name_their_kernel():
+    """Every committed profiles/pmc_<workload>_<key>.json is a summary of the
+    kernel its key names."""
+    import json
+    files = sorted((REPO / "profiles").glob("pmc_*_*.json"))
+    assert files
+    for f in files:
+        key = f.stem.split("_", 2)[2]
+        if key in bench.KERNEL_PREFIX:
+            assert json.loads(f.read_text())["kernel"].startswith(bench.KERNEL_PREFIX[key]), f.name

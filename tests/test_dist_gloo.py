@@ -132,21 +132,23 @@ def _worker(rank, world, port, kind, out_path, alg="cg1"):
                 ext = halo_vals(lambda idx: r[idx] + beta * p_old[idx], p_new)
             s = H.o_spmv(rp, lcol, val, ext)
             ps, ss, rr = allreduce3(float(np.dot(p_new, s)), float(np.dot(s, s)), rr_loc)
+            # the previous iteration's stop test on the exact r.r, one
+            # reduction late (cg.c:125's rule; oracle_solve_sr)
+            if k >= 1 and (k - 1 == maxit or rr <= tol * tol * bb):
+                break
             alpha = rr / ps
             x = x + alpha * p_new
             r = r - alpha * s
             rr_loc = float(np.dot(r, r))  # reduced with the next p.s, s.s
             est = max(alpha * (alpha * ss) - rr, 0.0)
-            if k == maxit or est <= tol * tol * bb:
-                break
-            beta, first = est / rr, False
+            beta, first = est / rr, False  # the estimate: beta only
             p_old = p_new
             k += 1
         xs = [None] * world
         dist.all_gather_object(xs, x.tolist())
         if rank == 0:
             np.save(out_path, np.array(sum(xs, [])))
-            np.save(out_path + ".its.npy", np.array([k + 1]))
+            np.save(out_path + ".its.npy", np.array([k]))
         dist.destroy_process_group()
         return
     if alg == "hs_fused":  # cgx_dist.cpp's fused step: pack p_new, x in pairs

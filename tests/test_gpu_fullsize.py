@@ -20,6 +20,27 @@ Bars, stated per test:
     1e-9 of the single-GPU CG1.
   * C3 grid with a random coefficient per edge (no value indexing applies):
     the layout picked, SpMV bit-exact against the oracle, CG within 1e-12.
+  * The N = 1 headline recurrence (CGX_ALG_SR, one plane-marched launch per
+    iteration; a recurrence the reference does not have: beta from
+    alpha^2 s.s - r.r instead of cg.c:129's direct dot) pinned to the oracle
+    at size and to convergence:
+      - C3, b ~ N(0,1), fixed maxit 100: x within 1e-10 of
+        oracle_conj_grad(100) (the reference's HS) and of oracle_solve_sr;
+        the r.r history within 1e-8 of the HS oracle's;
+      - C3 solve(1e-8) against the HS oracle's solve(1e-8): iteration count
+        within max(2, 1 %), true relative residual <= 1.5e-8, x within
+        1e-6 of the oracle's;
+      - C4 solve(1e-8) against the GPU HS solve of the same system: the same
+        iteration bar, the true residual on the host <= 1.5e-8;
+      - C5 (random SPD, 5 M rows, ~64 nnz/row, fp32, column panels) for 21
+        SpMVs against oracle_solve_f32: x within 1e-6
+        (the SpMV is bit-exact and the float updates are elementwise; only
+        the double dot products' grouping differs, which can move a float
+        rounding of alpha or beta -- measured: bit-identical), the r.r
+        history within 1e-10 (5 M-term double sums in another order);
+      - an anisotropic, less well-conditioned DIA system: the
+        stop test reads the exact r.r, so ||b - A x|| <= tol ||b|| (1.5x for
+        the residual gap) and the HS oracle's iteration count.
 """
 import numpy as np
 import pytest
@@ -224,3 +245,154 @@ def test_general_coefficients_c3(varcoef_c3, layout):
         x = s.x()
     x_ref, _ = H.o_conj_grad(20, rp, col, val, b)
     assert rel(x, x_ref) <= 1e-12
+
+
+def its_close(a, b):
+    """The iteration bar of the SR pins: within 1 % and at most 2 apart."""
+    return abs(a - b) <= max(2, 0.01 * b)
+
+
+def true_rel_residual(rp, col, val, b, x):
+    return float(np.linalg.norm(b - H.o_spmv(rp, col, val, x)) / np.linalg.norm(b))
+
+
+def test_c3_sr_fixed_maxit_vs_oracle(c3):
+    """The headline recurrence at full C3 size for 101 SpMVs against the
+    reference's HS iteration (oracle_conj_grad, cg.c:88-141) and against
+    oracle_solve_sr (the recurrence SR restates: only the dot products'
+    grouping differs)."""
+    rp, col, val, b = c3
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["fuse_march"] > 0
+        s.set_rhs(b)
+        assert s.run(100) == 101
+        x, h = s.x(), s.history(101)
+    x_hs, h_hs = H.o_conj_grad(100, rp, col, val, b)
+    x_sr, its_sr, _ = H.o_solve(100, 0.0, rp, col, val, b, sr=True)
+    assert its_sr == 101
+    d_hs, d_sr = rel(x, x_hs), rel(x, x_sr)
+    print(f"C3 SR maxit 100: |x - x_hs| {d_hs:.3e}, |x - x_sr| {d_sr:.3e}")
+    assert d_hs <= 1e-10 and d_sr <= 1e-10
+    assert np.allclose(h, h_hs[:101], rtol=1e-8, atol=0)
+
+
+@pytest.mark.timeout(300)
+def test_c3_sr_solve_vs_hs_oracle(c3):
+    """C3 solve(1e-8) with the headline recurrence against the HS oracle's
+    solve(1e-8) (what bench.py's solve_e2e leg times, b ~ N(0,1))."""
+    rp, col, val, b = c3
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        its = s.run(20000, 1e-8)
+        x = s.x()
+    x_o, its_o, _ = H.o_solve(20000, 1e-8, rp, col, val, b)
+    res = true_rel_residual(rp, col, val, b, x)
+    print(f"C3 SR solve(1e-8): {its} its (HS oracle {its_o}), true residual {res:.3e}, "
+          f"|x - x_o| {rel(x, x_o):.3e}")
+    assert its < 20000 and its_close(its, its_o)
+    assert res <= 1.5e-8
+    assert rel(x, x_o) <= 1e-6
+
+
+@pytest.mark.timeout(600)
+def test_c4_sr_solve_vs_gpu_hs():
+    """C4 (64 M rows) solve(1e-8): SR against the GPU HS solve of the same
+    system (the oracle's HS at this size takes ~10 min on one core), true
+    residual checked on the host."""
+    nx = 400
+    b = np.random.default_rng(29).standard_normal(nx ** 3)
+    out = {}
+    for alg in (cgx.CGX_ALG_HS, cgx.CGX_ALG_SR):
+        with cgx.Solver(0, alg=alg) as s:
+            s.gen_laplacian(3, nx, nx, nx)
+            if alg == cgx.CGX_ALG_SR:
+                assert s.info()["fuse_march"] > 0
+            s.set_rhs(b)
+            its = s.run(20000, 1e-8)
+            out[alg] = (its, s.x())
+    (its_h, x_h), (its_s, x_s) = out[cgx.CGX_ALG_HS], out[cgx.CGX_ALG_SR]
+    rp, col, val = cgx.laplacian3d(nx, nx, nx)
+    res_s = true_rel_residual(rp, col, val, b, x_s)
+    res_h = true_rel_residual(rp, col, val, b, x_h)
+    print(f"C4 solve(1e-8): SR {its_s} its (res {res_s:.3e}), HS {its_h} its (res {res_h:.3e}), "
+          f"|x_sr - x_hs| {rel(x_s, x_h):.3e}")
+    assert its_s < 20000 and its_close(its_s, its_h)
+    assert res_s <= 1.5e-8 and res_h <= 1.5e-8
+    assert rel(x_s, x_h) <= 1e-6
+
+
+def aniso3d(nx, ny, nz, cx=1.0, cy=1e-2, cz=1e2, shift=1e-2):
+    """A 7-point operator with anisotropic coefficients (-cx, -cy, -cz per
+    direction) and diagonal sum|a_ij| + shift (Neumann-like: the constant
+    vector has eigenvalue `shift`): SPD, condition number ~4 (cx + cy + cz)
+    / shift = 4e4, at most 8 distinct diagonal values (DIA-VI applies)."""
+    n = nx * ny * nz
+    rows, cols, vals = [], [], []
+    idx = np.arange(n)
+    xi, yi, zi = idx % nx, (idx // nx) % ny, idx // (nx * ny)
+    diag = np.full(n, shift)
+    for off, c, ok in ((-nx * ny, cz, zi > 0), (-nx, cy, yi > 0), (-1, cx, xi > 0),
+                       (1, cx, xi < nx - 1), (nx, cy, yi < ny - 1), (nx * ny, cz, zi < nz - 1)):
+        r = idx[ok]
+        rows.append(r)
+        cols.append(r + off)
+        vals.append(np.full(len(r), -c))
+        diag[ok] += c
+    rows.append(idx)
+    cols.append(idx)
+    vals.append(diag)
+    r, c, v = (np.concatenate(a) for a in (rows, cols, vals))
+    o = np.lexsort((c, r))
+    rp = np.zeros(n + 1, np.int32)
+    np.add.at(rp, r + 1, 1)
+    return np.cumsum(rp).astype(np.int32), c[o].astype(np.int32), v[o]
+
+
+def test_sr_tolerance_stop_ill_conditioned():
+    """SR's stop test on a less well-conditioned DIA system.  The
+    estimate alpha^2 s.s - r.r only forms beta; the stop reads the exact r.r
+    the next launch computes, so the iteration count is the HS oracle's
+    (within the SR bar) and the true residual meets the tolerance."""
+    rp, col, val = aniso3d(32, 48, 40)  # planes 3 slices apart: the march applies
+    b = np.random.default_rng(31).standard_normal(len(rp) - 1)
+    tol = 1e-8
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["layout_name"] == "dia" and i["fuse_march"] > 0
+        s.set_rhs(b)
+        its = s.run(50000, tol)
+        x = s.x()
+    x_sr, its_sr, _ = H.o_solve(50000, tol, rp, col, val, b, sr=True)
+    x_hs, its_hs, _ = H.o_solve(50000, tol, rp, col, val, b)
+    res, res_hs = true_rel_residual(rp, col, val, b, x), true_rel_residual(rp, col, val, b, x_hs)
+    print(f"aniso SR: {its} its (oracle SR {its_sr}, HS {its_hs}), true residual {res:.3e} "
+          f"(HS oracle {res_hs:.3e})")
+    assert its < 50000 and its_close(its, its_hs) and its_close(its, its_sr)
+    # the recurrence's r meets tol exactly; b - A x drifts from it by
+    # rounding (the residual gap), as much in the reference's HS
+    assert res <= max(1.5 * tol, 1.5 * res_hs)
+
+
+@pytest.mark.timeout(600)
+def test_c5_fp32_iteration_vs_oracle():
+    """C5 at full size through the solver's fp32 path (column panels, the
+    unfused three-launch iteration) against oracle_solve_f32, cg.c:88-141 in
+    float vectors with the kernels' dot-product accumulation."""
+    n = 5_000_000
+    rp, col, val = cgx.random_spd(n, 32, 42, f32=True)
+    b = np.random.default_rng(1).standard_normal(n).astype(np.float32)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == "panel"
+        s.set_rhs(b)
+        assert s.run(20) == 21
+        x, h = s.x(), s.history(21)
+    x_o, its_o, h_o = H.o_solve_f32(20, 0.0, rp, col, val, b)
+    assert its_o == 21
+    d = rel(x.astype(np.float64), x_o.astype(np.float64))
+    print(f"C5 fp32 maxit 20: bit-identical {np.array_equal(x, x_o)}, rel {d:.3e}")
+    assert np.array_equal(x, x_o) or d <= 1e-6
+    assert np.allclose(h, h_o, rtol=1e-10, atol=0)

@@ -573,6 +573,58 @@ def test_fuse_status_reports_why():
             assert i["fused"] == (1 if want == cgx.CGX_FUSE_STATUS_RUNS else 0)
 
 
+def test_dropin_sr_falls_back_to_hs():
+    """cgx_ops_set_mode(FAST, SR) through the drop-in
+    solve() (cg.c:72's caller): a matrix without the plane-marched DIA step
+    (the random-pattern CSR fixture) runs the reference's HS recurrence and
+    cgx_ops_last_timing() says so, against oracle_solve; a 3-D Laplacian
+    whose planes are 8 slices apart runs the one-launch SR step, against
+    oracle_solve_sr and the HS oracle (the bars of test_sr_single_launch_vs_oracle)."""
+    cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_SR)
+    try:
+        g = H.load_golden("rand_spd_2000")
+        A = cgx.Mv(g["val"], g["col"], g["row_ptr"])
+        b = cgx.Mv(g["b"])
+        x, its = cgx.solve(A, b, 1e-10, 1000)
+        assert cgx.ops_last_timing()["alg"] == cgx.CGX_ALG_HS
+        x_o, its_o, _ = H.o_solve(1000, 1e-10, g["row_ptr"], g["col"], g["val"], g["b"])
+        assert its == its_o
+        assert rel(x, x_o) <= FAST_RTOL
+        rp, col, val = H.laplacian3d(64, 64, 40)
+        bv = np.random.default_rng(23).standard_normal(len(rp) - 1)
+        A, b = cgx.Mv(val, col, rp), cgx.Mv(bv)
+        for tol, maxit in ((0.0, 30), (1e-9, 3000)):
+            x, its = cgx.solve(A, b, tol, maxit)
+            assert cgx.ops_last_timing()["alg"] == cgx.CGX_ALG_SR
+            x_sr, its_sr, _ = H.o_solve(maxit, tol, rp, col, val, bv, sr=True)
+            x_hs, its_hs, _ = H.o_solve(maxit, tol, rp, col, val, bv)
+            assert its == its_sr and abs(its - its_hs) <= 1, (tol, its, its_sr, its_hs)
+            assert rel(x, x_sr) <= 1e-10 and rel(x, x_hs) <= 1e-9, tol
+    finally:
+        cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
+
+
+def test_sr_fuse_status():
+    """cgx_info.fuse_status follows fused()'s SR rules -- SR
+    ignores the Infinity Cache rule (a cache-resident system runs it) and
+    needs the march plan (NO_MARCH after set_march(0) or without a plan)."""
+    rp, col, val = H.laplacian3d(64, 64, 10)
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["fused"] == 1 and i["fuse_status"] == cgx.CGX_FUSE_STATUS_RUNS
+        s.set_march(0)
+        i = s.info()
+        assert i["fused"] == 0 and i["fuse_status"] == cgx.CGX_FUSE_STATUS_NO_MARCH
+        s.set_rhs(np.ones(len(rp) - 1))
+        with pytest.raises(cgx.CgxError, match="plane-marched"):
+            s.run(5)
+    rp, col, val = H.laplacian2d(300, 200)
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["fuse_status"] == cgx.CGX_FUSE_STATUS_NO_MARCH
+
+
 def test_conj_grad_argument_errors():
     L = cgx.lib()
     g = H.load_golden("kat_tridiag10")

@@ -109,3 +109,37 @@ def test_oracle_mt_matches_serial():
     x2, its2 = H.o_solve_mt(50, 0.0, rp, col, val, b, 4)
     assert its1 == its2 == 51
     assert np.linalg.norm(x1 - x2) <= 1e-10 * np.linalg.norm(x1)
+
+
+def test_oracle_f32_pinned_on_the_kats():
+    """oracle_solve_f32 (C5's fp32 iteration; the reference is fp64 only,
+    mv_ops.h:20) against the reference's own golden KATs: on the n = 10
+    tridiagonal system every alpha, beta and iterate is a small dyadic or
+    integer value, exact in float, so the fp32 iteration reproduces the
+    reference's x bit for bit (as floats) for max_iter 0..4."""
+    g = H.load_golden("kat_tridiag10")
+    rp, col = g["row_ptr"], g["col"]
+    val, b = g["val"].astype(np.float32), g["b"].astype(np.float32)
+    for it in range(5):
+        x, its, _ = H.o_solve_f32(it, 0.0, rp, col, val, b)
+        assert its == it + 1
+        assert np.array_equal(x, g["iters"][it].astype(np.float32)), it
+
+
+@pytest.mark.parametrize("name", ["lap2d_32", "lap3d_12", "rand_spd_2000", "dense128"])
+def test_oracle_f32_tracks_the_reference(name):
+    """On the other fixtures the fp32 iteration stays within fp32 rounding of
+    the reference's fp64 x (the golden vectors) for its first iterations,
+    and stops at a tolerance within 1 iteration of the fp64 oracle."""
+    g = H.load_golden(name)
+    rp, col = g["row_ptr"], g["col"]
+    val, b = g["val"].astype(np.float32), g["b"].astype(np.float32)
+    for it, want in g["iters"].items():
+        if it > 10:
+            continue
+        x, _, _ = H.o_solve_f32(it, 0.0, rp, col, val, b)
+        assert np.linalg.norm(x - want) <= 1e-4 * np.linalg.norm(want), (name, it)
+    x, its, hist = H.o_solve_f32(500, 1e-4, rp, col, val, b)
+    _, its64, _ = H.o_solve(500, 1e-4, rp, col, g["val"], g["b"])
+    assert abs(its - its64) <= 1
+    assert hist[-1] <= 1e-8 * H.o_dot(g["b"], g["b"]) * 1.0001
