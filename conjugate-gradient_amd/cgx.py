@@ -68,7 +68,8 @@ class CgxDistStats(ctypes.Structure):
                 ("device_bytes", ctypes.c_size_t), ("spmv_iter_bytes", ctypes.c_double),
                 ("layout", ctypes.c_int), ("n_dict", ctypes.c_int), ("graph", ctypes.c_int),
                 ("alg", ctypes.c_int), ("fused", ctypes.c_int),
-                ("fuse_status", ctypes.c_int), ("breakdown", ctypes.c_int)]
+                ("fuse_status", ctypes.c_int), ("breakdown", ctypes.c_int),
+                ("march", ctypes.c_int), ("inplace", ctypes.c_int)]
 
 
 _MVP = ctypes.POINTER(MvSparse)
@@ -177,6 +178,7 @@ _SIGS = {
     "cgx_dist_set_alg": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_graph": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_set_march": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
                                     ctypes.POINTER(ctypes.c_int)]),
@@ -688,6 +690,12 @@ class DistSolver:
 
     def set_graph(self, on):
         check(lib().cgx_dist_set_graph(self._h, 1 if on else 0), "dist_set_graph")
+
+    def set_march(self, steps):
+        """CGX_ALG_SR as one k_sr1_dia_m step per iteration on the in-place
+        numbering (cgx_dist_set_march): -1 auto, 0 off (two-launch fused SR),
+        > 0 interior steps per workgroup."""
+        check(lib().cgx_dist_set_march(self._h, int(steps)), "dist_set_march")
 
     def set_fused(self, mode):
         """The fused HS step on all ranks or none: "auto", True, False."""

@@ -35,6 +35,18 @@
 //       writes r_new.r_new = alpha^2 s.s - r.r (r.s = p.s) for beta
 //       (cg.c:129) and the stop test: HS's bytes, one all-reduce latency per
 //       iteration instead of two, rounding-level different from HS.
+//       One launch per iteration (round 4; where every rank's rows take it,
+//       cgx_dist_set_march): the single-GPU k_sr1_dia_m step on an IN-PLACE
+//       numbering of the rank's rows -- columns = global - row_begin, the
+//       neighbours' boundary planes at [-g_lo, 0) and [n_loc, n_loc + g_hi)
+//       of every vector -- so the plane march runs across the slab edges:
+//       st_comm: k_pack_sr (p_k = (r - alpha s) + beta p at the send rows),
+//                halo into the p_new buffer's ghost rows
+//       st:      k_sr1_dia_m over the INTERIOR steps (no window reaches a
+//                ghost row) || halo; wait; the BOUNDARY steps (ghost rows'
+//                p_k from the halo) -> local (p.s, s.s, r.r)
+//                ncclAllReduce(3 doubles); k_finalize(FIN_SR1)
+//       61 B/row instead of 69, no separate r-update launch.
 //   CG1 (Chronopoulos-Gear): ONE all-reduce of (gamma, delta) per iteration,
 //       rounding-level different from HS, 8 B per row more vector traffic;
 //       fused (CGX_FUSE_ON only): k_cg1_dia_h does the vector recurrences
@@ -118,6 +130,16 @@ struct cgx_dist {
   int n_send = 0;
   double *d_pa = nullptr, *d_pb = nullptr;
   double *d_pss = nullptr;  // SR: the fused launches' (p.s, s.s) pairs, one per workgroup
+  // the one-launch SR step (k_sr1_dia_m) on the in-place numbering
+  DevMatrix Ai;              // columns = global - row_begin (DIA-VI, march plan)
+  bool ai_ok = false;        // Ai built: contiguous ghost ranges, DIA, march plan
+  int g_lo = 0, g_hi = 0;    // ghost rows below / above the own rows
+  std::vector<int> recv_pos; // in-place position of each owner's first ghost row
+  size_t vfront = 0;         // entries before element 0 of the ghosted vectors
+  int march = -1;            // cgx_dist_set_march: -1 auto, 0 off, > 0 interior steps/segment
+  bool mi_all = false;       // every partition runs the one-launch SR step (agreed)
+  double *d_pq = nullptr, *d_pc = nullptr;  // its (p.s, s.s) pairs and r.r partials
+  int gi1 = 0, gb1 = 0;      // workgroups of its interior / boundary launch
   double *d_sums = nullptr, *d_gsums = nullptr;  // [0, 4) local, [4, 8) all-reduced
   unsigned *d_tick = nullptr;                    // last-arriver counters
   int vec_grid = 1;
@@ -174,8 +196,10 @@ void drop_graph(cgx_dist *d) {
 // SR is the fused step with one reduction.
 // HS-shaped recurrences (HS, SR): s = A p, r -= alpha s, p = r + beta p
 bool hs_like(const cgx_dist *d) { return d->alg == CGX_ALG_HS || d->alg == CGX_ALG_SR; }
-bool fz(const cgx_dist *d) { return d->fz_all && hs_like(d); }
 bool sr(const cgx_dist *d) { return d->alg == CGX_ALG_SR; }
+// SR as ONE k_sr1_dia_m launch pair per iteration on the in-place numbering
+bool sr1(const cgx_dist *d) { return sr(d) && d->mi_all; }
+bool fz(const cgx_dist *d) { return d->fz_all && hs_like(d) && !sr1(d); }
 // The fused CG1 step (k_cg1_dia_h): only when forced on (CGX_FUSE_ON) --
 // on a rank's slab it loses to the unfused CG1 kernels (C4/8's 400 x 400 x
 // 50 slab: 164 vs 144 us per iteration, tools/dist_probe.py: the unfused
@@ -192,23 +216,64 @@ bool part_fusable(const cgx_dist *d) {
          (d->fuse == CGX_FUSE_ON || d->A.nt || sr(d));
 }
 
+// this partition can run the one-launch SR step (its in-place layout exists
+// and the march is not switched off)
+bool part_marchable(const cgx_dist *d) {
+  return d->ai_ok && d->march != 0 && d->fuse != CGX_FUSE_OFF;
+}
+
+// The one-launch SR step's launch shapes: boundary steps [0, blo) and
+// [ms - bhi, ms) of every chain -- the steps one of whose three windows
+// reaches a ghost row -- and the interior steps' segment length.
+struct Sr1Plan {
+  int blo, bhi, len;
+};
+
+Sr1Plan sr1_plan(const cgx_dist *d) {
+  const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
+  const long long QR = (long long)a.mq * kDiaSliceRows, SR = (long long)a.msb * kDiaSliceRows;
+  Sr1Plan p;
+  p.blo = 1 + (int)((a.hl + QR - 1) / QR);
+  p.bhi = 1 + (int)((SR + a.hr - 1 + QR - 1) / QR);
+  const int steps = (a.mslices + a.mq - 1) / a.mq;
+  const int inner = std::max(1, steps - p.blo - p.bhi);
+  if (d->march > 0) {
+    p.len = d->march;
+  } else {
+    // about two resident workgroups per CU (the ring's LDS) in one wave
+    const int nseg = std::max(1, (2 * d->cus + a.mchains / 2) / std::max(1, a.mchains));
+    p.len = (inner + nseg - 1) / nseg;
+  }
+  p.len = std::max(1, p.len);
+  return p;
+}
+
+// the ghosted vectors start vfront entries into their allocation (the
+// in-place numbering's ghost rows below element 0)
+void free_ghosted(cgx_dist *d, double **p) {
+  if (*p) dev_free_raw(*p - d->vfront);
+  *p = nullptr;
+}
+
 void free_system(cgx_dist *d) {
   drop_graph(d);
   d->A.release();
+  d->Ai.release();
+  d->ai_ok = false;
+  d->g_lo = d->g_hi = 0;
+  d->recv_pos.clear();
+  dev_free(&d->d_pq);
+  dev_free(&d->d_pc);
+  d->gi1 = d->gb1 = 0;
   dev_free(&d->d_list_int);
   dev_free(&d->d_list_bnd);
   dev_free(&d->d_pairs_int);
   dev_free(&d->d_pairs_bnd);
   dev_free(&d->d_b);
   dev_free(&d->d_x);
-  dev_free(&d->d_r);
-  dev_free(&d->d_p);
-  dev_free(&d->d_s);
-  dev_free(&d->d_w);
-  dev_free(&d->d_p2);
-  dev_free(&d->d_r2);
-  dev_free(&d->d_s2);
-  dev_free(&d->d_w2);
+  for (double **v : {&d->d_r, &d->d_p, &d->d_s, &d->d_w, &d->d_p2, &d->d_r2, &d->d_s2, &d->d_w2})
+    free_ghosted(d, v);
+  d->vfront = 0;
   dev_free(&d->d_send_idx);
   dev_free(&d->d_sendbuf);
   dev_free(&d->d_pa);
@@ -301,6 +366,45 @@ int split_items(cgx_dist *d, const int *rp, const std::vector<int> &col_local) {
   return 0;
 }
 
+// The in-place numbering of this rank's rows for the one-launch SR step:
+// when its ghost columns are exactly the rows [row_begin - g_lo, row_begin)
+// and [row_end, row_end + g_hi) (a banded matrix's neighbouring planes), the
+// columns global - row_begin give a DIA-VI layout whose plane march runs
+// across the slab edges (ghost rows in place, below 0 and from n_loc).
+// Not applicable (scattered ghosts, no DIA, no march plan): ai_ok = false,
+// and SR runs the two-launch fused step.
+int build_inplace(cgx_dist *d, int n_loc, int nnz, const int *rp, const int *col_global,
+                  const double *val) {
+  d->ai_ok = false;
+  if (d->A.layout != L_DIA || n_loc == 0) return 0;
+  std::vector<int> gh((size_t)d->n_ghost);
+  cgx_part_ghosts(d->part, gh.data());
+  const long long rb = d->row_begin, re = rb + n_loc;
+  int nb = 0;
+  while (nb < d->n_ghost && gh[(size_t)nb] < rb) ++nb;
+  for (int i = 0; i < d->n_ghost; ++i) {
+    const long long want = i < nb ? rb - nb + i : re + (i - nb);
+    if (gh[(size_t)i] != want) return 0;
+  }
+  std::vector<int> ci((size_t)nnz);
+  for (size_t k = 0; k < (size_t)nnz; ++k) ci[k] = (int)(col_global[k] - rb);
+  const int g_hi = d->n_ghost - nb;
+  const int rc = d->Ai.upload<double>(n_loc, n_loc + g_hi, nnz, rp, ci.data(), val,
+                                      CGX_LAYOUT_DIA, false, nullptr, -nb);
+  if (rc || d->Ai.layout != L_DIA || d->Ai.mq == 0) {
+    d->Ai.release();
+    set_error("%s", "");
+    return 0;
+  }
+  d->g_lo = nb;
+  d->g_hi = g_hi;
+  d->recv_pos.assign((size_t)d->nranks, 0);
+  for (int q = 0; q < d->nranks; ++q)
+    if (d->recv_count[(size_t)q]) d->recv_pos[(size_t)q] = (int)(gh[(size_t)d->recv_off[q]] - rb);
+  d->ai_ok = true;
+  return 0;
+}
+
 int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int *rp,
                  const int *col_global, const double *val) {
   CGX_HIP(hipSetDevice(d->device));
@@ -329,27 +433,57 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
     free_system(d);
     return rc;
   }
+  if ((rc = build_inplace(d, n_loc, nnz, rp, col_global, val))) {
+    free_system(d);
+    return rc;
+  }
   d->vec_grid = vec_grid_for(n_loc, d->cus);
   d->vec_grid = (std::max(d->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
-  const size_t nv = (size_t)n_loc + kPad, ng = nv + (size_t)d->n_ghost;
+  const size_t nv = (size_t)n_loc + kPad;
+  const size_t ng = nv + (size_t)std::max(d->n_ghost, d->g_hi + 2 * kPad);
+  // the in-place numbering's ghost rows below element 0 (the windows may load
+  // one pair below them, clamped: DevMatrix::col_lo - 1)
+  d->vfront = d->ai_ok ? ((size_t)d->g_lo + 2 * kPad + 7) / 8 * 8 : 0;
   // d_pa: the vector kernels' partials, or the fused CG1 step's gamma partials
   const size_t npa = (size_t)std::max(d->vec_grid, d->g_int + d->g_bnd) + 8;
   size_t *cb = &d->vec_bytes;
-  // r, p, s, w and their second buffers carry the ghost tail (s, w: the fused
-  // CG1 step's window / far-slot loads reach it; only zeros are read there)
+  auto ghosted = [&](double **p) -> int {
+    void *raw = nullptr;
+    const int r = dev_alloc(&raw, (d->vfront + ng) * 8, cb);
+    *p = r ? nullptr : (double *)raw + d->vfront;
+    return r;
+  };
+  // r, p, s, w and their second buffers carry the ghost rows (s, w: the fused
+  // CG1 step's window / far-slot loads reach them; only zeros are read there)
   if ((rc = dev_alloc(&d->d_b, nv * 8, cb)) || (rc = dev_alloc(&d->d_x, nv * 8, cb)) ||
-      (rc = dev_alloc(&d->d_r, ng * 8, cb)) || (rc = dev_alloc(&d->d_p, ng * 8, cb)) ||
-      (rc = dev_alloc(&d->d_s, ng * 8, cb)) || (rc = dev_alloc(&d->d_w, ng * 8, cb)) ||
-      (rc = dev_alloc(&d->d_p2, ng * 8, cb)) || (rc = dev_alloc(&d->d_r2, ng * 8, cb)) ||
-      (rc = dev_alloc(&d->d_s2, ng * 8, cb)) || (rc = dev_alloc(&d->d_w2, ng * 8, cb)) ||
+      (rc = ghosted(&d->d_r)) || (rc = ghosted(&d->d_p)) || (rc = ghosted(&d->d_s)) ||
+      (rc = ghosted(&d->d_w)) || (rc = ghosted(&d->d_p2)) || (rc = ghosted(&d->d_r2)) ||
+      (rc = ghosted(&d->d_s2)) || (rc = ghosted(&d->d_w2)) ||
       (rc = dev_alloc(&d->d_pa, npa * 8, cb)) ||
       (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb)) ||
       (rc = dev_alloc(&d->d_pss, ((size_t)d->g_int + d->g_bnd + 8) * 16, cb))) {
     free_system(d);
     return rc;
   }
+  if (d->ai_ok) {
+    // the one-launch SR step's partials: one (p.s, s.s) pair and one r.r per
+    // workgroup of its two launches (the widest segmentation: length 1)
+    Sr1Plan pl = sr1_plan(d);
+    pl.len = 1;
+    const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
+    Sr1Args<double> f{};
+    f.march = 1;
+    f.blo = pl.blo;
+    f.bhi = pl.bhi;
+    f.seg = 1;
+    const int cap = sr1_grid(a, f) + a.mchains * (pl.blo + pl.bhi) + 8;
+    if ((rc = dev_alloc(&d->d_pq, (size_t)cap * 16, cb)) || (rc = dev_alloc(&d->d_pc, (size_t)cap * 8, cb))) {
+      free_system(d);
+      return rc;
+    }
+  }
   for (double *v : {d->d_r, d->d_p, d->d_p2, d->d_s, d->d_w, d->d_r2, d->d_s2, d->d_w2})
-    CGX_HIP(hipMemsetAsync(v, 0, ng * 8, d->st));
+    CGX_HIP(hipMemsetAsync(v - d->vfront, 0, (d->vfront + ng) * 8, d->st));
   CGX_HIP(hipMemsetAsync(d->d_x, 0, nv * 8, d->st));
   CGX_HIP(hipStreamSynchronize(d->st));
   d->have_matrix = true;
@@ -481,15 +615,23 @@ int agree_fusable(cgx_dist *d, int mine, int *all) {
 int ensure_fused_known(Group *g) {
   if (g->fz_known) return 0;
   if (g->parts[0]->local) {
-    bool all = true;
-    for (cgx_dist *d : g->parts) all = all && part_fusable(d);
-    for (cgx_dist *d : g->parts) d->fz_all = all;
+    bool all = true, mall = true;
+    for (cgx_dist *d : g->parts) {
+      all = all && part_fusable(d);
+      mall = mall && part_marchable(d);
+    }
+    for (cgx_dist *d : g->parts) {
+      d->fz_all = all;
+      d->mi_all = mall;
+    }
   } else {
     cgx_dist *d = g->parts[0];
-    int all = 0;
+    int all = 0, mall = 0;
     int rc = agree_fusable(d, part_fusable(d) ? 1 : 0, &all);
+    if (rc == 0) rc = agree_fusable(d, part_marchable(d) ? 1 : 0, &mall);
     if (rc) return rc;
     d->fz_all = all != 0;
+    d->mi_all = mall != 0;
   }
   g->fz_known = true;
   return 0;
@@ -501,7 +643,7 @@ int ensure_connected_fz(Group *g);
 int ensure_connected(Group *g) {
   int rc = ensure_connected_fz(g);
   if (rc) return rc;
-  if (sr(g->parts[0]) && !g->parts[0]->fz_all) {
+  if (sr(g->parts[0]) && !g->parts[0]->fz_all && !g->parts[0]->mi_all) {
     set_error("dist: CGX_ALG_SR needs the fused DIA step on every partition (fuse_status)");
     return CGX_EINVAL;
   }
@@ -568,7 +710,10 @@ int phase_pack(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   CGX_HIP(hipEventRecord(d->ev_fork, d->st));
   CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_fork, 0));
-  if (fz(d))
+  if (sr1(d))
+    CGX_HIP(launch_pack_sr<double>(d->n_send, d->d_send_idx, r_old(d), p_old(d), s_old(d),
+                                   d->d_sendbuf, d->d_st, d->st_comm));
+  else if (fz(d))
     CGX_HIP(launch_pack_pnext<double>(d->n_send, d->d_send_idx, d->d_r, p_old(d), d->d_sendbuf,
                                       d->d_st, rr_new_src(d), d->st_comm));
   else if (fz1(d))
@@ -586,12 +731,16 @@ int phase_pack(cgx_dist *d) {
 int phase_halo(cgx_dist *d) {
   if (!has_peers(d)) return 0;
   CGX_HIP(hipSetDevice(d->device));
-  double *ghost = spmv_x(d) + d->n_loc;
+  // owner q's ghost rows: the gathered vector's tail at recv_off[q], or (the
+  // one-launch SR step's in-place numbering) p_new at recv_pos[q]
+  const bool ip = sr1(d);
+  double *ghost = ip ? p_new(d) : spmv_x(d) + d->n_loc;
+  auto dst = [&](int q) { return ghost + (ip ? d->recv_pos[(size_t)q] : d->recv_off[q]); };
   if (d->local) {
     for (cgx_dist *o : d->group->parts) {
       if (o == d || d->recv_count[o->rank] == 0) continue;
       CGX_HIP(hipStreamWaitEvent(d->st_comm, o->ev_packed, 0));
-      CGX_HIP(hipMemcpyAsync(ghost + d->recv_off[o->rank], o->d_sendbuf + o->send_off[d->rank],
+      CGX_HIP(hipMemcpyAsync(dst(o->rank), o->d_sendbuf + o->send_off[d->rank],
                              (size_t)d->recv_count[o->rank] * 8, hipMemcpyDeviceToDevice,
                              d->st_comm));
     }
@@ -600,8 +749,7 @@ int phase_halo(cgx_dist *d) {
     for (int q = 0; q < d->nranks; ++q) {
       if (q == d->rank) continue;
       if (d->recv_count[q])
-        CGX_NCCL(ncclRecv(ghost + d->recv_off[q], d->recv_count[q], ncclFloat64, q, d->comm,
-                          d->st_comm));
+        CGX_NCCL(ncclRecv(dst(q), d->recv_count[q], ncclFloat64, q, d->comm, d->st_comm));
       if (d->send_count[q])
         CGX_NCCL(ncclSend(d->d_sendbuf + d->send_off[q], d->send_count[q], ncclFloat64, q,
                           d->comm, d->st_comm));
@@ -618,7 +766,68 @@ int phase_halo(cgx_dist *d) {
 // sums[0..1]).  (An in-kernel last-arriver sum costs every one of the
 // SpMV's ~15 K workgroups a drained store and a device-scope atomic before
 // it may retire: 70 us on an 8 M-row slab, against ~5 us for the launch.)
+int allreduce(cgx_dist *d, int i, int count);
+
+// The one-launch SR step (k_sr1_dia_m on the in-place numbering): interior
+// steps while the halo is in flight, then the boundary steps; the local
+// (p.s, s.s, r.r) (FIN_SUM3), or with no transport the scalar step itself
+// (FIN_SR1, as the single-GPU solver).
+int phase_sr1(cgx_dist *d) {
+  CGX_HIP(hipSetDevice(d->device));
+  const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
+  const Sr1Plan pl = sr1_plan(d);
+  const SpmvArgs<double> a =
+      d->Ai.args<double>(nullptr, s_new(d), nullptr, &d->d_st->done, d->Ai.all_items());
+  Sr1Args<double> f{d->d_x, p_old(d), p_new(d), r_old(d), r_new(d), s_old(d), d->d_st,
+                    d->d_pq, d->d_pc, pl.len};
+  f.blo = pl.blo;
+  f.bhi = pl.bhi;
+  f.seg = 1;
+  const int gi = sr1_grid(a, f);
+  Sr1Args<double> fb = f;
+  fb.seg = 2;
+  fb.pq = d->d_pq + 2 * (size_t)gi;
+  fb.pc = d->d_pc + gi;
+  const int gb = sr1_grid(a, fb);
+  d->gi1 = gi;
+  d->gb1 = gb;
+  auto ev = [&](int e) {
+    return rec ? LaunchEv{d->spmv_ev[d->ev_i + e], d->spmv_ev[d->ev_i + e + 1]} : LaunchEv{};
+  };
+  CGX_HIP(launch_sr1_march<double>(a, f, d->st, ev(0)));
+  if (has_peers(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
+  CGX_HIP(launch_sr1_march<double>(a, fb, d->st, ev(2)));
+  if (rec) d->ev_i += 4;
+  if (solo(d)) {
+    CGX_HIP(launch_finalize(FIN_SR1, d->d_pq, gi + gb, nullptr, 0, d->d_st, d->d_hist, nullptr,
+                            d->st, d->d_pc, gi + gb));
+    return 0;
+  }
+  if (d->local)  // as phase_spmv: every part's last group sum has read d_sums
+    for (cgx_dist *o : d->group->parts)
+      if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
+  CGX_HIP(launch_finalize(FIN_SUM3, d->d_pq, gi + gb, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
+                          d->st, d->d_pc, gi + gb));
+  CGX_HIP(hipEventRecord(d->ev_sums, d->st));
+  return 0;
+}
+
+// the iteration's one all-reduce of (p.s, s.s, r.r), then FIN_SR1 on it
+// (the stop test of the previous iteration, alpha, the estimate, beta);
+// the r, p, s buffers swap roles
+int sr1_reduce(cgx_dist *d) {
+  if (!solo(d)) {
+    int rc = allreduce(d, 0, 3);
+    if (rc) return rc;
+    CGX_HIP(launch_finalize(FIN_SR1, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist, nullptr,
+                            d->st, d->d_gsums + 2, 1));
+  }
+  d->pbuf ^= 1;
+  return 0;
+}
+
 int phase_spmv(cgx_dist *d) {
+  if (sr1(d)) return phase_sr1(d);
   CGX_HIP(hipSetDevice(d->device));
   const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
   const int np = d->g_int + d->g_bnd;
@@ -827,6 +1036,15 @@ int run_phases_eager(Group *g, bool init, long long iters) {
       for (cgx_dist *d : P) if ((rc = hs_init_reduce(d))) return rc;
       return 0;
     }
+    if (sr1(P[0])) {
+      for (long long it = 0; it < iters; ++it) {
+        for (cgx_dist *d : P) if ((rc = phase_pack(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = phase_sr1(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = sr1_reduce(d))) return rc;
+      }
+      return 0;
+    }
     if (fz(P[0])) {
       for (long long it = 0; it < iters; ++it) {
         for (cgx_dist *d : P) if ((rc = phase_pack(d))) return rc;
@@ -897,10 +1115,10 @@ bool graphs_on(const cgx_dist *d) {
 int ensure_graphs(Group *g) {
   cgx_dist *d = g->parts[0];
   if (!graphs_on(d)) return 0;
-  const int key = d->alg * 2 + (fz(d) || fz1(d) ? 1 : 0);
+  const int key = d->alg * 8 + (fz(d) || fz1(d) ? 1 : 0) + (sr1(d) ? 2 : 0);
   if (d->gexec[0] && d->gexec1[0] && d->gexec_alg == key) return 0;
   drop_graph(d);
-  const int nq = fz(d) || fz1(d) ? 2 : 1;
+  const int nq = fz(d) || fz1(d) || sr1(d) ? 2 : 1;
   for (int q = 0; q < nq; ++q)
     if (capture(d, g, d->graph_batch, q, &d->gexec[q]) || capture(d, g, 1, q, &d->gexec1[q])) {
       drop_graph(d);
@@ -918,7 +1136,8 @@ int run_phases(Group *g, bool init, long long iters) {
     int rc = ensure_graphs(g);
     if (rc) return rc;
     if (d->gexec[0] && d->gexec1[0]) {
-      const bool alt = fz(d) || fz1(d);  // an even batch keeps the parity, one iteration flips it
+      // an even batch keeps the parity, one iteration flips it
+      const bool alt = fz(d) || fz1(d) || sr1(d);
       for (; iters >= d->graph_batch; iters -= d->graph_batch) {
         CGX_HIP(hipGraphLaunch(d->gexec[alt ? d->pbuf : 0], d->st));
         if (alt && (d->graph_batch & 1)) d->pbuf ^= 1;
@@ -984,7 +1203,8 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
   // complete at done = 2 (an even stop iteration's x update still pending
   // at 1)
   const bool sr0 = sr(g->parts[0]);
-  const long long total = (long long)maxit + 1 + (fz(g->parts[0]) ? 1 : 0) + (sr0 ? 1 : 0);
+  const long long total =
+      (long long)maxit + 1 + (fz(g->parts[0]) || sr1(g->parts[0]) ? 1 : 0) + (sr0 ? 1 : 0);
   const int fin_done = sr0 ? 2 : 1;
   if (tol <= 0.0) {
     if ((rc = run_phases(g, false, total))) return rc;
@@ -1218,6 +1438,20 @@ int cgx_dist_set_fused(cgx_dist *d, int mode) {
   return 0;
 }
 
+int cgx_dist_set_march(cgx_dist *d, int steps) {
+  if (!d || (d->local && !d->owns_group) || steps < -1) return CGX_EINVAL;
+  for (cgx_dist *o : d->group->parts) {
+    if (o->gexec[0]) {
+      (void)hipStreamSynchronize(o->st);
+      drop_graph(o);
+    }
+    o->march = steps;
+    o->bench_ready = false;
+  }
+  d->group->fz_known = false;
+  return 0;
+}
+
 int cgx_dist_set_graph(cgx_dist *d, int on) {
   if (!d) return CGX_EINVAL;
   d->use_graph = on != 0;
@@ -1304,14 +1538,19 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   s->spmv_bytes = (double)d->nnz * 12.0 + 4.0 * (d->n_loc + 1) + 16.0 * d->n_loc;
   s->iter_bytes = s->spmv_bytes + 72.0 * d->n_loc;
   s->halo_bytes = 8.0 * (d->n_ghost + d->n_send);
-  s->device_bytes = d->A.dev_bytes + d->vec_bytes;
+  s->device_bytes = d->A.dev_bytes + d->Ai.dev_bytes + d->vec_bytes;
   s->spmv_iter_bytes = d->have_matrix ? d->A.layout_bytes() : 0.0;
+  // the one-launch SR step: its layout, + r, s, p read and written, x /
+  // p_{k-2} every other launch (cgx_info)
+  if (d->have_matrix && sr1(d)) s->spmv_iter_bytes = d->Ai.layout_bytes() + 5.5 * d->n_loc * 8.0;
   // fused: + r, p_old read and p_new written, x / p_{k-1} read and x
   // written every other launch (cgx_info)
   if (d->have_matrix && fz(d)) s->spmv_iter_bytes += 3.5 * d->n_loc * 8.0;
   // fused CG1: + r, w, s, p, x read and p, s, r, w, x written (cgx_info)
   if (d->have_matrix && fz1(d)) s->spmv_iter_bytes += 8.0 * d->n_loc * 8.0;
-  s->fused = fz(d) || fz1(d) ? 1 : 0;
+  s->fused = fz(d) || fz1(d) || sr1(d) ? 1 : 0;
+  s->march = d->have_matrix && sr1(d) ? sr1_plan(d).len : 0;
+  s->inplace = d->ai_ok ? 1 : 0;
   {
     const int own = d->fuse == CGX_FUSE_OFF ? CGX_FUSE_STATUS_OFF
                     : !d->have_matrix      ? CGX_FUSE_STATUS_NOT_DIA

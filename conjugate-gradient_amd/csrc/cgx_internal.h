@@ -243,6 +243,9 @@ struct SpmvArgs {
   int doff[kDiaMax];      // diagonal offsets col - row, ascending
   int n;                  // rows (DIA, stencil)
   int ncols;              // entries of x (DIA pair loads stay inside)
+  int xlo;                // lowest pair start the windows may load: -1 (the guard
+                          // entry x[-1]), or below a partition's in-place ghost
+                          // rows [col_lo, 0) (DevMatrix::col_lo)
   // fused step (k_spmv_dia_h): the slice's LDS window covers rows
   // [s0 - hl, s0 + 512 + hr); diagonal k is read from it when near bit k
   int hl, hr;
@@ -288,6 +291,13 @@ struct FuseArgs {
 // (p.s, s.s) pairs (pq[2 b], pq[2 b + 1]) and r.r (pc[b]) per workgroup b for
 // k_finalize(FIN_SR1).  r, s, p are double-buffered (read _o, write _n; s_n
 // = SpmvArgs::y).
+// Partitioned (in-place ghost rows, DevMatrix::col_lo): the steps of each
+// chain split into two launches -- seg 1, the interior steps [blo, ms - bhi)
+// (no window reaches a ghost row) in segments of `march`, run while the halo
+// is in flight; seg 2, the boundary steps [0, blo) and [ms - bhi, ms), one
+// workgroup per step, after it (GH: window rows outside [0, n) take p from
+// the p_new buffer's ghost rows, where the halo put the neighbours' p).
+// seg 0: every step (single GPU).
 template <typename T>
 struct Sr1Args {
   T *x;
@@ -299,6 +309,7 @@ struct Sr1Args {
   const CgState *st;
   double *pq, *pc;
   int march;  // steps per segment
+  int seg = 0, blo = 0, bhi = 0;
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
@@ -338,6 +349,15 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream
 // workgroups (= partial pairs) of the plane march at `len` steps per segment
 template <typename T>
 int march_grid(const SpmvArgs<T> &a, int len);
+// the same for one launch of the partitioned split (Sr1Args::seg 1 / 2)
+template <typename T>
+int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
+// out[i] = p_k[idx[i]] = (r - alpha s) + beta p of the last iteration's
+// buffers (the one-launch SR step's halo send rows; r itself on the first
+// iteration) -- the roundings k_sr1_dia_m uses for its window rows
+template <typename T>
+hipError_t launch_pack_sr(int n_send, const int *idx, const T *rold, const T *pold,
+                          const T *sold, T *out, const CgState *stt, hipStream_t st);
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev = LaunchEv{});

@@ -1254,7 +1254,14 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
 // buffer (two slots) when the window is built.  One (p.s, s.s) pair and one
 // r.r per workgroup: each thread sums its rows in step order, then the wave
 // tree and the waves in order -- deterministic.
-template <typename T, int SB, int NF, int CB>
+// Partitioned ranks (in-place ghost rows: columns = global - row_begin, the
+// rows of the neighbours' boundary planes at [col_lo, 0) and [n, ncols)):
+// the same step, split by Sr1Args::seg into the interior steps (no window
+// reaches a ghost row; launched while the halo is in flight) and the boundary
+// steps (GH: p_k of a window row outside [0, n) is the neighbour's, received
+// into the p_new buffer's ghost rows by the halo exchange; k_pack_sr computed
+// it there with these roundings).
+template <typename T, int SB, int NF, int CB, bool GH>
 __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
@@ -1268,7 +1275,21 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   const int chain = w % a.mchains, seg = w / a.mchains;
   const int j0 = chain * SB;
   const int msteps = (a.mslices - j0 + a.mq - 1) / a.mq;
-  const int m0 = seg * f.march, m1 = min(m0 + f.march, msteps);
+  int m0, m1;
+  if (f.seg == 0) {  // every step, in segments of f.march
+    m0 = seg * f.march;
+    m1 = min(m0 + f.march, msteps);
+  } else {
+    const int lo_end = min(f.blo, msteps), hi0 = max(lo_end, msteps - f.bhi);
+    if (f.seg == 1) {  // interior steps [lo_end, hi0) in segments of f.march
+      m0 = lo_end + seg * f.march;
+      m1 = min(m0 + f.march, hi0);
+    } else {  // boundary steps, one per workgroup: [0, lo_end), then [hi0, msteps)
+      const int m = seg < f.blo ? (seg < lo_end ? seg : msteps) : hi0 + (seg - f.blo);
+      m0 = m;
+      m1 = m < msteps ? m + 1 : m;
+    }
+  }
   if (f.st->done > 1) return;  // uniform
   const int k = f.st->k_u;  // the last finalized iteration (-1: none)
   const bool first = k < 0, stop = f.st->done == 1;
@@ -1341,15 +1362,21 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     publish();
     return;
   }
-  P wr[NF], wp[NF], wsv[NF];
+  constexpr int NG = GH ? NF : 1;
+  P wr[NF], wp[NF], wsv[NF], wg[NG];
+  int wj[NG];
   auto load_win = [&](int m) {
     const int w0 = base_of(m) - a.hl;
 #pragma unroll
     for (int q = 0; q < NF; ++q) {
-      const int j = min(max(w0 + 2 * t + q * 2 * BS, -1), a.ncols - 1);
+      const int j = min(max(w0 + 2 * t + q * 2 * BS, a.xlo), a.ncols - 1);
       wr[q] = ld_pair(f.rold, j);
       wp[q] = ld_pair(f.pold, j);
       wsv[q] = ld_pair(f.sold, j);
+      if constexpr (GH) {
+        wj[q] = j;
+        wg[q] = ld_pair((const T *)f.pnew, j);
+      }
     }
   };
   auto store_win = [&](int m) {
@@ -1363,6 +1390,11 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
         rk.x = wr[q].x - as0;
         rk.y = wr[q].y - as1;
         pk = p_next<T>(rk, wp[q], beta);
+      }
+      if constexpr (GH) {  // a ghost row: the neighbour's p_k from the halo
+        const int j = wj[q];
+        if (j < 0 || j >= a.n) pk.x = wg[q].x;
+        if (j + 1 < 0 || j + 1 >= a.n) pk.y = wg[q].y;
       }
       if (i + 1 < wn) lds_st2(win, i, pk.x, pk.y);  // wn even (march plan)
       else if (i < wn) win[i] = pk.x;
@@ -1650,6 +1682,33 @@ __global__ __launch_bounds__(256) void k_pack_pnext(int n_send, const int *__res
     } else {
       const T b = beta * pold[j];
       out[i] = r[j] + b;
+    }
+  }
+}
+
+// The send rows of p_k for the one-launch SR step on partitioned ranks
+// (k_sr1_dia_m): r_k = r - alpha s, p_k = r_k + beta p of the last
+// iteration's buffers at the rows the neighbours need, the roundings of the
+// kernel's window rows; r (= b = p_0) on the first iteration.  alpha, beta
+// from k_finalize(FIN_SR1) of the all-reduced sums.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack_sr(int n_send, const int *__restrict__ idx,
+                                                 const T *__restrict__ rold,
+                                                 const T *__restrict__ pold,
+                                                 const T *__restrict__ sold, T *__restrict__ out,
+                                                 const CgState *st) {
+  if (st->done > 1) return;
+  const bool first = st->k_u < 0;
+  const T alpha = (T)st->alpha, beta = (T)st->beta;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n_send; i += gridDim.x * 256) {
+    const int j = idx[i];
+    if (first) {
+      out[i] = rold[j];
+    } else {
+      const T as = alpha * sold[j];
+      const T rk = rold[j] - as;
+      const T bp = beta * pold[j];
+      out[i] = rk + bp;
     }
   }
 }
@@ -2738,16 +2797,32 @@ static hipError_t launch_march(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipSt
   return hipGetLastError();
 }
 
+template <typename T, int SB, int NF, bool GH>
+static const void *sr1_kernel_g(int cb) {
+  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, GH>))
+         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2, GH>))
+                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4, GH>));
+}
+
 template <typename T, int SB, int NF>
-static const void *sr1_kernel(int cb) {
-  return cb == 1 ? CGX_K(k_sr1_dia_m<T, SB, NF, 1>)
-                 : cb == 2 ? CGX_K(k_sr1_dia_m<T, SB, NF, 2>) : CGX_K(k_sr1_dia_m<T, SB, NF, 4>);
+static const void *sr1_kernel(int cb, bool gh) {
+  return gh ? sr1_kernel_g<T, SB, NF, true>(cb) : sr1_kernel_g<T, SB, NF, false>(cb);
+}
+
+template <typename T>
+int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f) {
+  if (f.seg == 0) return march_grid(a, f.march);
+  if (f.seg == 2) return a.mchains * (f.blo + f.bhi);
+  const int steps = (a.mslices + a.mq - 1) / a.mq;  // chain 0's, the longest
+  const int inner = std::max(0, steps - std::min(f.blo, steps) - f.bhi);
+  return a.mchains * ((inner + f.march - 1) / f.march);
 }
 
 template <typename T>
 hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev) {
-  if (a.mq <= 0 || f.march <= 0 || a.items.count != a.mslices || a.layout != L_DIA)
+  if (a.mq <= 0 || f.march <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
+      f.seg < 0 || f.seg > 2 || (f.seg != 0 && (f.blo < 1 || f.bhi < 1)))
     return hipErrorInvalidValue;
   const int sb = a.msb;
   const int wn = sb * kDiaSliceRows + a.hl + a.hr;
@@ -2757,15 +2832,21 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream
   const int cb = a.cb;
   if (cb != 1 && cb != 2 && cb != 4) return hipErrorInvalidValue;
   const void *k = nullptr;
+  const bool gh = f.seg == 2;
   switch (sb * 10 + nfc) {
-    case 12: k = sr1_kernel<T, 1, 2>(cb); break;
-    case 13: k = sr1_kernel<T, 1, 3>(cb); break;
-    case 15: k = sr1_kernel<T, 1, 5>(cb); break;
-    case 22: k = sr1_kernel<T, 2, 2>(cb); break;
-    case 23: k = sr1_kernel<T, 2, 3>(cb); break;
+    case 12: k = sr1_kernel<T, 1, 2>(cb, gh); break;
+    case 13: k = sr1_kernel<T, 1, 3>(cb, gh); break;
+    case 15: k = sr1_kernel<T, 1, 5>(cb, gh); break;
+    case 22: k = sr1_kernel<T, 2, 2>(cb, gh); break;
+    case 23: k = sr1_kernel<T, 2, 3>(cb, gh); break;
     default: return hipErrorInvalidValue;
   }
-  const int g = march_grid(a, f.march);
+  const int g = sr1_grid(a, f);
+  if (g <= 0) {  // nothing to run: the launch's events still bracket it
+    if (ev.start) (void)hipEventRecord(ev.start, st);
+    if (ev.stop) (void)hipEventRecord(ev.stop, st);
+    return hipGetLastError();
+  }
   void *args[] = {(void *)&a, (void *)&f};
   // the three-window ring and two slots of own-row r
   const size_t lds = ((size_t)3 * a.mws + 2 * sb * kDiaSliceRows) * sizeof(T) + 16;
@@ -2919,6 +3000,16 @@ hipError_t launch_pack_pnext(int n_send, const int *idx, const T *r, const T *po
 }
 
 template <typename T>
+hipError_t launch_pack_sr(int n_send, const int *idx, const T *rold, const T *pold,
+                          const T *sold, T *out, const CgState *stt, hipStream_t st) {
+  if (n_send <= 0) return hipSuccess;
+  const int grid = std::min((n_send + 255) / 256, 1024);
+  hipLaunchKernelGGL((k_pack_sr<T>), dim3(grid), dim3(256), 0, st, n_send, idx, rold, pold, sold,
+                     out, stt);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
                             const FinArgs *fin, const double *sr, double *hist) {
@@ -3030,6 +3121,9 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template hipError_t launch_spmv<T>(const SpmvArgs<T> &, hipStream_t, const LaunchEv &);      \
   template int fused_grid<T>(const SpmvArgs<T> &);                                               \
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
+  template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
+  template hipError_t launch_pack_sr<T>(int, const int *, const T *, const T *, const T *, T *,  \
+                                        const CgState *, hipStream_t);                            \
   template hipError_t launch_sr1_march<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,  \
                                           const LaunchEv &);                                     \
   template hipError_t launch_spmv_fused<T>(const SpmvArgs<T> &, const FuseArgs<T> &, hipStream_t, \

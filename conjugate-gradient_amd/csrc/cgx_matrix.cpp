@@ -296,8 +296,9 @@ bool group_dia(int n, const int *rp, const int *col, bool sample, const std::vec
 // A row's entries follow the diagonal order, so the search for the next
 // entry's diagonal starts after the previous one's.
 template <typename T>
-int dia_encode_host(int n, int npad, int ncols, const int *rp, const int *col, const T *val,
-                    const DiaCand &c, const std::vector<T> &vt, std::vector<unsigned char> &code) {
+int dia_encode_host(int n, int npad, int col_lo, int ncols, const int *rp, const int *col,
+                    const T *val, const DiaCand &c, const std::vector<T> &vt,
+                    std::vector<unsigned char> &code) {
   const int cb = c.cbytes;
   unsigned long long empty = 0;
   for (int q = 0; q < c.ndiag; ++q) empty |= ((1ull << c.cbits[q]) - 1ull) << c.csh[q];
@@ -317,7 +318,7 @@ int dia_encode_host(int n, int npad, int ncols, const int *rp, const int *col, c
       fm[q] = ((1ull << c.cbits[q]) - 1ull) << c.csh[q];
       for (int v = 0; v < nval[q]; ++v) vb[q * 16 + v] = bits_of(vt[(size_t)q * 16 + v]);
     }
-    const unsigned nc = (unsigned)ncols;
+    const unsigned nc = (unsigned)(ncols - col_lo);
     const unsigned long long e0 = empty;
     int err = 0;
     for (long long r = lo; r < hi && !err; ++r) {
@@ -326,7 +327,7 @@ int dia_encode_host(int n, int npad, int ncols, const int *rp, const int *col, c
       const int k1 = rp[r + 1];
       for (int k = rp[r]; k < k1; ++k) {
         const int cl = col[k];
-        if ((unsigned)cl >= nc) {
+        if ((unsigned)(cl - col_lo) >= nc) {
           err = 2;
           break;
         }
@@ -468,6 +469,7 @@ void DevMatrix::release() {
   panel_first.clear();
   panel_count.clear();
   n = nnz = ncols = nblk = ndict = tile_bands = 0;
+  col_lo = 0;
   csr_reach = 0;
   memset(&dia, 0, sizeof dia);
   kdiag = -1;
@@ -499,9 +501,9 @@ int DevMatrix::set_stencil(const LapSpec &g) {
 
 template <typename T>
 int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *col, const T *val,
-                      int want, bool allow_panels, const LapSpec *gen) {
+                      int want, bool allow_panels, const LapSpec *gen, int col_lo_) {
   const double t0 = now_ms();
-  if (n_ < 0 || nnz_ < 0 || ncols_ < n_ ||
+  if (n_ < 0 || nnz_ < 0 || ncols_ < n_ || col_lo_ > 0 || (col_lo_ < 0 && (gen || !col)) ||
       (n_ > 0 && (!rp || (nnz_ > 0 && !gen && (!col || !val))))) {
     set_error("set_matrix: invalid arguments");
     return CGX_EINVAL;
@@ -538,13 +540,14 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     }
   }
   auto bad_column = [&]() {
-    set_error("set_matrix: a column index is outside [0, %d)", ncols_);
+    set_error("set_matrix: a column index is outside [%d, %d)", col_lo_, ncols_);
     return CGX_EINVAL;
   };
   release();
   dtype = sizeof(T) == 4 ? CGX_F32 : CGX_F64;
   n = n_;
   ncols = ncols_;
+  col_lo = col_lo_;
   nnz = nnz_;
   const size_t ts = sizeof(T);
   const size_t nnz_pad = ((size_t)nnz + kPad - 1) / kPad * kPad + kWindowPad;
@@ -552,7 +555,7 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
 
   // ---- which layout: candidates from a sample (or the generator's stencil)
   const bool want_dia = want == CGX_LAYOUT_AUTO || want == CGX_LAYOUT_DIA;
-  const bool want_dc = want_dia || want == CGX_LAYOUT_DC;
+  const bool want_dc = (want_dia || want == CGX_LAYOUT_DC) && col_lo == 0;
   std::vector<int> poff;  // (offset, value) keys, sorted
   std::vector<T> pval, vt;
   bool dia_ok = false, dc_ok = false;
@@ -573,12 +576,12 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
   const int npad = padded_rows_for(n);
   if (dia_ok && !gen) {
     std::vector<unsigned char> hcode;
-    int e = dia_encode_host(n, npad, ncols, rp, col, val, dia, vt, hcode);
+    int e = dia_encode_host(n, npad, col_lo, ncols, rp, col, val, dia, vt, hcode);
     if (e == 1) {  // the sample missed a diagonal or a value: exact scan
       encode_fallback = 1;
       dia_ok = find_pairs(n, rp, col, val, true, kDiaMax * kDiaVals, false, poff, pval) &&
                group_dia(n, rp, col, false, poff, pval, dia, vt);
-      if (dia_ok) e = dia_encode_host(n, npad, ncols, rp, col, val, dia, vt, hcode);
+      if (dia_ok) e = dia_encode_host(n, npad, col_lo, ncols, rp, col, val, dia, vt, hcode);
     }
     if (e == 2) {
       release();
@@ -600,6 +603,11 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
       return finish_upload(t0);
     }
     memset(&dia, 0, sizeof dia);
+  }
+  if (col_lo < 0) {  // the in-place numbering exists for the DIA step only
+    release();
+    set_error("set_matrix: in-place ghost columns need the DIA-VI layout");
+    return CGX_EINVAL;
   }
   if (!gen && nnz > 0) {
     std::vector<int> bad((size_t)host_threads(nnz), 0);
@@ -806,9 +814,9 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
 }
 
 template int DevMatrix::upload<double>(int, int, int, const int *, const int *, const double *,
-                                       int, bool, const LapSpec *);
+                                       int, bool, const LapSpec *, int);
 template int DevMatrix::upload<float>(int, int, int, const int *, const int *, const float *,
-                                      int, bool, const LapSpec *);
+                                      int, bool, const LapSpec *, int);
 
 // The item order, the non-temporal choice and the setup times, once the
 // layout's arrays are on the device.
@@ -1036,6 +1044,7 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
   a.kdiag = kdiag;
   for (int k = 0; k < kDiaMax; ++k) a.doff[k] = dia.doff[k];
   a.ncols = ncols;
+  a.xlo = col_lo - 1;
   a.near = 0;
   a.hl = a.hr = 0;
   int nf = 0;

@@ -29,6 +29,9 @@ struct DevMatrix {
   int dtype = CGX_F64;
   int n = 0, nnz = 0;
   int ncols = 0;             // columns of x (n, or n_loc + ghosts when partitioned)
+  // lowest column (0; a partition's in-place numbering: -(ghost rows below),
+  // columns = global - row_begin, DIA only)
+  int col_lo = 0;
   int layout = L_CSR;
   bool nt = false;           // matrix stream + y store non-temporal
   size_t dev_bytes = 0;
@@ -67,9 +70,11 @@ struct DevMatrix {
   // apply falls back along DIA -> DC -> CSR).  ncols: columns of x (>= n for
   // the partitioned solver's ghost tail).  gen: col/val generated on the
   // device (rp is the host closed form).  allow_panels: single-GPU only.
+  // col_lo < 0: columns in [col_lo, ncols) (a partition's in-place ghost
+  // rows); DIA-VI only -- CGX_EINVAL when it does not apply.
   template <typename T>
   int upload(int n, int ncols, int nnz, const int *rp, const int *col, const T *val, int want,
-             bool allow_panels, const LapSpec *gen = nullptr);
+             bool allow_panels, const LapSpec *gen = nullptr, int col_lo = 0);
   int finish_upload(double t0);
   int set_stencil(const LapSpec &g);
   // The matrix as CSR on the host (fp64; DIA decodes its codes).

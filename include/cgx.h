@@ -390,6 +390,14 @@ typedef struct {
                                             once the ranks are connected) */
   int fuse_status;                       /* CGX_FUSE_STATUS_* (cgx_info)  */
   int breakdown;                         /* as cgx_info.breakdown         */
+  int march;                             /* > 0: CGX_ALG_SR runs as ONE
+                                            k_sr1_dia_m step per iteration
+                                            (interior + boundary launches),
+                                            this many interior steps per
+                                            workgroup; 0: it does not     */
+  int inplace;                           /* 1: this rank's rows have the
+                                            in-place ghost numbering the
+                                            one-launch SR step needs      */
 } cgx_dist_stats;
 
 /* Rank 0 creates the id and distributes it (e.g. torch.distributed). */
@@ -428,6 +436,17 @@ int  cgx_dist_set_alg(cgx_dist *d, int alg);
  * history are bit-identical to the unfused path.  Call on every rank (on a
  * local group, part 0 sets the group). */
 int  cgx_dist_set_fused(cgx_dist *d, int mode);
+/* CGX_ALG_SR as ONE launch pair per iteration (the single-GPU k_sr1_dia_m
+ * step: the r update of the previous iteration, p, x and s = A p in one plane
+ * march) where every rank's ghost columns are the rows next to its own
+ * (a banded matrix cut into row slabs, e.g. C4's planes): the ranks number
+ * their rows in place (columns = global - row_begin, the neighbours' planes
+ * below 0 and from n_loc), march the interior steps while the halo of
+ * p_k = (r - alpha s) + beta p is in flight and the boundary steps after it.
+ * steps: -1 auto (default), 0 off (the two-launch fused SR step), > 0
+ * interior steps per workgroup.  cgx_dist_stats.march reports it.  Call on
+ * every rank (on a local group, part 0 sets the group). */
+int  cgx_dist_set_march(cgx_dist *d, int steps);
 /* hipGraph replay of the iteration batches (RCCL calls included); on by
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
 int  cgx_dist_set_graph(cgx_dist *d, int on);

@@ -445,13 +445,15 @@ def test_fused_cg1_rccl_one_rank_graph_parity():
         assert H.same_bits_or_both_nan(x0, x1)
 
 
-def _sr_group(rp, col, val, b, P, runs, alg=cgx.CGX_ALG_SR, fused="auto", layout="auto"):
+def _sr_group(rp, col, val, b, P, runs, alg=cgx.CGX_ALG_SR, fused="auto", layout="auto",
+              march=-1):
     n = len(rp) - 1
     parts = cgx.DistSolver.local_group(0, P)
     out = []
     try:
         parts[0].set_alg(alg)
         parts[0].set_fused(fused)
+        parts[0].set_march(march)
         for g, d in enumerate(parts):
             d.set_layout(layout)
             rb, re_ = cgx.partition_rows(n, P, g)
@@ -495,6 +497,92 @@ def test_sr_partitions(shape, P):
     m = min(len(hist), len(hist_sr)) - 2
     assert np.allclose(hist[:m], hist_sr[:m], rtol=1e-6, atol=0)
     assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
+
+
+SR1_CASES = [((32, 48, 20), 1), ((32, 48, 20), 2), ((32, 48, 20), 3), ((32, 48, 20), 8),
+             ((64, 64, 12), 2), ((64, 64, 12), 5), ((64, 64, 12), 8), ((64, 64, 12), 16),
+             ((300, 7, 20), 4)]
+
+
+@pytest.mark.parametrize("shape,P", SR1_CASES)
+def test_sr_one_launch_partitions(shape, P):
+    """CGX_ALG_SR on partitioned ranks as ONE k_sr1_dia_m step
+    per iteration -- the ranks' rows in the in-place numbering (ghost planes
+    below 0 and from n_loc), the interior steps launched while the halo of p_k
+    is in flight, the boundary steps after it -- on plane-aligned and
+    plane-cutting slabs and slabs thinner than the plane reach (P = 8 at
+    32 x 48 x 20: 2.5 planes per part; P = 16 at 64 x 64 x 12: 0.75 of a
+    plane, ghost rows from two owners on each side).  Against the two-launch fused SR
+    group (set_march(0)) within 1e-10 at fixed max_iter (the same recurrence,
+    the dot products grouped otherwise), against oracle_solve_sr within 1e-9
+    with the stop iteration within 1 (and of the HS oracle), true residual
+    below the tolerance; interior segment lengths 1, 3 and auto within
+    1e-12 of each other."""
+    rp, col, val = cgx.laplacian3d(*shape)
+    b = np.random.default_rng(27).standard_normal(len(rp) - 1)
+    runs = [(0, 0.0), (1, 0.0), (2, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]
+    one, st1 = _sr_group(rp, col, val, b, P, runs)
+    two, st2 = _sr_group(rp, col, val, b, P, runs, march=0)
+    assert all(s["march"] > 0 and s["inplace"] == 1 and s["fused"] == 1 for s in st1), st1
+    assert all(s["march"] == 0 for s in st2)
+    for (i0, x0, _), (i1, x1, _) in zip(one[:-1], two[:-1]):
+        assert i0 == i1
+        assert np.linalg.norm(x0 - x1) <= 1e-10 * np.linalg.norm(x1), i0
+    its, x, hist = one[-1]
+    x_sr, its_sr, hist_sr = H.o_solve(3000, 1e-10, rp, col, val, b, sr=True)
+    x_hs, its_hs, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+    assert abs(its - its_sr) <= 1 and abs(its - its_hs) <= 1 and its < 3000
+    assert abs(its - two[-1][0]) <= 1
+    assert np.linalg.norm(x - x_sr) <= 1e-9 * np.linalg.norm(x_sr)
+    m = min(len(hist), len(hist_sr))
+    assert np.allclose(hist[:m], hist_sr[:m], rtol=1e-6, atol=0)
+    assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
+    for march in (1, 3):
+        seg, _ = _sr_group(rp, col, val, b, P, runs[:-1], march=march)
+        for (i0, x0, _), (i1, x1, _) in zip(seg, one[:-1]):
+            assert i0 == i1
+            assert np.linalg.norm(x0 - x1) <= 1e-12 * np.linalg.norm(x1), (march, i0)
+
+
+def test_sr_one_launch_rccl_one_rank_graph_parity():
+    """The one-launch SR step through a 1-rank RCCL communicator (FIN_SUM3,
+    the all-reduce of three doubles, FIN_SR1 in the replayed graphs), eager,
+    and without a communicator (FIN_SR1 on the partials, as the single-GPU
+    solver): bit-identical x, iteration counts and histories; and the
+    single-GPU solver's SR within 1e-12 (its partials are grouped otherwise)."""
+    rp, col, val = cgx.laplacian3d(32, 48, 20)
+    b = np.random.default_rng(25).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    res = {}
+    for key in (("rccl", True), ("rccl", False), ("solo", True)):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id() if key[0] == "rccl" else None)
+        try:
+            d.set_alg(cgx.CGX_ALG_SR)
+            d.set_graph(key[1])
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            out = []
+            for maxit in (17, 33, 40):
+                its = d.run(maxit, 0.0)
+                out.append((its, d.x(), d.history(its)))
+            its = d.run(3000, 1e-10)
+            out.append((its, d.x(), d.history(its)))
+            i = d.info()
+            assert i["fused"] == 1 and i["march"] > 0 and i["alg"] == cgx.CGX_ALG_SR
+        finally:
+            d.close()
+        res[key] = out
+    for key in (("rccl", False), ("solo", True)):
+        for (i0, x0, h0), (i1, x1, h1) in zip(res[("rccl", True)], res[key]):
+            assert i0 == i1
+            assert H.same_bits_or_both_nan(x0, x1), key
+            assert H.same_bits_or_both_nan(h0, h1), key
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        for (its, x, _), maxit in zip(res[("solo", True)], (17, 33, 40)):
+            assert s.run(maxit) == its
+            assert np.linalg.norm(s.x() - x) <= 1e-12 * np.linalg.norm(x)
 
 
 def test_sr_rccl_one_rank_graph_parity():

@@ -157,7 +157,7 @@ def test_c4_sr_one_gpu_vs_oracle():
     assert rel(x, x_hs) <= 1e-9
 
 
-def c4_group(alg, fused, maxit, P=8):
+def c4_group(alg, fused, maxit, P=8, march=-1):
     """C4 row-partitioned into P slabs (cgx_partition_rows: 400^3 / 8 = 50
     planes each) as an in-process group on GPU 0; x of all rows."""
     nx = 400
@@ -166,6 +166,7 @@ def c4_group(alg, fused, maxit, P=8):
     try:
         parts[0].set_alg(alg)
         parts[0].set_fused(fused)
+        parts[0].set_march(march)
         for g, d in enumerate(parts):
             rb, re_ = cgx.partition_rows(n, P, g)
             rp, col, val = cgx.laplacian3d(nx, nx, nx, rb, re_)
@@ -220,6 +221,14 @@ def test_c4_partitioned_8_slabs_in_process():
     assert all(s["fused"] == 1 and s["alg"] == cgx.CGX_ALG_SR for s in st_s)
     assert its_s == 11
     assert rel(x_s, x1) <= 1e-10
+    # the ranks run the one-launch step (k_sr1_dia_m on the
+    # in-place numbering, 400^2-row ghost planes); the two-launch SR group
+    # (set_march(0)) within 1e-10
+    assert all(s["march"] > 0 and s["inplace"] == 1 for s in st_s), st_s
+    its_2, x_2, _, st_2 = c4_group(cgx.CGX_ALG_SR, "auto", 10, march=0)
+    assert all(s["march"] == 0 for s in st_2)
+    assert its_2 == 11
+    assert rel(x_s, x_2) <= 1e-10
 
 
 @pytest.fixture(scope="module")

@@ -1,31 +1,56 @@
 """Per-rank iteration time of the partitioned solver on ONE GPU: a 1-rank
 RCCL communicator (the multi-GPU phase code: pack, halo loop with no peers,
 ncclAllReduce) on a slab of C4 (400 x 400 x nz planes, 8M rows at nz = 50 =
-C4's slab at N = 8), HS, SR (HS with one all-reduce) and CG1, fused and
-unfused, graph-replayed (HS fused and SR twice, alternating)."""
-import sys, time
+C4's slab at N = 8), graph-replayed.
+
+  python tools/dist_probe.py [nz] [local3] [--cases=a,b,...]
+
+cases: hs_fused, hs, cg1, sr (auto: the one-launch k_sr1_dia_m step where it
+applies), sr2 (the two-launch fused SR step, set_march(0)), srN (one-launch
+with N interior steps per workgroup).  Default: hs_fused, sr, sr2, hs, cg1,
+then hs_fused, sr, sr2 again (alternating)."""
+import sys
 sys.path.insert(0, "conjugate-gradient_amd")
 import numpy as np, cgx
 
-nz = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+opts = dict(a[2:].split("=", 1) for a in sys.argv[1:] if a.startswith("--") and "=" in a)
+nz = int(args[0]) if args else 50
+cases = (opts.get("cases") or "hs_fused,sr,sr2,hs,cg1,hs_fused,sr,sr2").split(",")
 rp, col, val = cgx.laplacian3d(400, 400, nz)
 n = len(rp) - 1
 b = np.ones(n)
-for name, alg, fused in (("hs_fused", cgx.CGX_ALG_HS, True), ("sr", cgx.CGX_ALG_SR, "auto"),
-                         ("hs", cgx.CGX_ALG_HS, False), ("cg1", cgx.CGX_ALG_CG1, False),
-                         ("hs_fused", cgx.CGX_ALG_HS, True), ("sr", cgx.CGX_ALG_SR, "auto")):
+
+
+def case(name):
+    if name == "hs_fused":
+        return cgx.CGX_ALG_HS, True, -1
+    if name == "hs":
+        return cgx.CGX_ALG_HS, False, -1
+    if name == "cg1":
+        return cgx.CGX_ALG_CG1, False, -1
+    if name == "sr":
+        return cgx.CGX_ALG_SR, "auto", -1
+    if name == "sr2":
+        return cgx.CGX_ALG_SR, "auto", 0
+    return cgx.CGX_ALG_SR, "auto", int(name[2:])
+
+
+for name in cases:
+    alg, fused, march = case(name)
     d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
     try:
         d.set_alg(alg)
         d.set_fused(fused)
+        d.set_march(march)
         d.set_matrix(n, rp, col, val)
         d.set_rhs(b)
         d.bench_prepare(5)
         ms, _ = d.bench_run(100)
         _, sp = d.bench_run(30, graph=False, spmv_events=True)
         i = d.info()
-        print("%-9s n %d  %.1f us/iter  spmv(launches) %.1f us  fused %d layout %s" %
-              (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["layout"]), flush=True)
+        print("%-9s n %d  %.1f us/iter  spmv(launches) %.1f us  fused %d march %d layout %s" %
+              (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["march"], i["layout"]), flush=True)
     finally:
         d.close()
 
