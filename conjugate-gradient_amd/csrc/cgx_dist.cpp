@@ -376,7 +376,11 @@ int split_items(cgx_dist *d, const int *rp, const std::vector<int> &col_local) {
 int build_inplace(cgx_dist *d, int n_loc, int nnz, const int *rp, const int *col_global,
                   const double *val) {
   d->ai_ok = false;
-  if (d->A.layout != L_DIA || n_loc == 0) return 0;
+  // (the standard numbering's layout may be DC where thin slabs give it
+  // ghost offsets beyond DIA's 16 diagonals; the in-place one has the
+  // matrix's own offsets)
+  if ((d->want_layout != CGX_LAYOUT_AUTO && d->want_layout != CGX_LAYOUT_DIA) || n_loc == 0)
+    return 0;
   std::vector<int> gh((size_t)d->n_ghost);
   cgx_part_ghosts(d->part, gh.data());
   const long long rb = d->row_begin, re = rb + n_loc;
@@ -1564,8 +1568,10 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
                                                                      : CGX_FUSE_STATUS_RUNS;
   }
   s->breakdown = d->h_st ? d->h_st->brk : 0;
-  s->layout = d->have_matrix ? cgx::public_layout(d->A) : CGX_LAYOUT_AUTO;
-  s->n_dict = d->A.layout == cgx::L_DC ? d->A.ndict : d->A.layout == cgx::L_DIA ? d->A.dia.ndiag : 0;
+  // the layout the SpMV runs on (the one-launch SR step: the in-place one)
+  const DevMatrix &M = d->have_matrix && sr1(d) ? d->Ai : d->A;
+  s->layout = d->have_matrix ? cgx::public_layout(M) : CGX_LAYOUT_AUTO;
+  s->n_dict = M.layout == cgx::L_DC ? M.ndict : M.layout == cgx::L_DIA ? M.dia.ndiag : 0;
   s->graph = d->graph_state;
   s->alg = d->alg;
   return 0;
