@@ -737,14 +737,16 @@ def gather_x(x_local, n_global, world, rank):
 
 
 def parity_gate(world, rank, local_rank, uid, tol=1e-10):
-    """A small 3-D Laplacian (48 x 48 x 16 N rows) solved across the N ranks
-    to tol with both recurrences (HS unfused and fused) over RCCL; rank 0 checks the gathered x
-    against a single-GPU solve of the same system (cgx.Solver, HS), the
-    iteration count (within 1) and the true residual (scipy, on the host)."""
+    """A small 3-D Laplacian (64 x 64 x 16 N rows: planes 8 slices apart, so
+    SR runs the one-launch march step on the ranks, as at C4) solved across
+    the N ranks to tol with every recurrence the trial may pick (HS unfused
+    and fused, SR one-launch and two-launch, CG1) over RCCL; rank 0 checks the
+    gathered x against a single-GPU solve of the same system (cgx.Solver, HS),
+    the iteration count (within 1) and the true residual (scipy, on the host)."""
     import numpy as np
     import scipy.sparse as sp
     import cgx
-    nx, ny, nz = 48, 48, 16 * world
+    nx, ny, nz = 64, 64, 16 * world
     n = nx * ny * nz
     rb, re_ = cgx.partition_rows(n, world, rank)
     rp, col, val = cgx.laplacian3d(nx, ny, nz, rb, re_)
@@ -756,16 +758,20 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
         d.set_rhs(b_full[rb:re_])
         # the fused HS step forced on: the timed C4 run takes it (auto), this
         # small system would not; SR is always the fused step
-        for name, alg, fused, want in (("hs", cgx.CGX_ALG_HS, False, 0),
-                                       ("hs_fused", cgx.CGX_ALG_HS, True, 1),
-                                       ("sr", cgx.CGX_ALG_SR, "auto", 1),
-                                       ("cg1", cgx.CGX_ALG_CG1, False, 0)):
+        for name, alg, fused, march, want in (("hs", cgx.CGX_ALG_HS, False, -1, 0),
+                                              ("hs_fused", cgx.CGX_ALG_HS, True, -1, 1),
+                                              ("sr", cgx.CGX_ALG_SR, "auto", -1, 1),
+                                              ("sr_two_launch", cgx.CGX_ALG_SR, "auto", 0, 1),
+                                              ("cg1", cgx.CGX_ALG_CG1, False, -1, 0)):
             d.set_alg(alg)
             d.set_fused(fused)
+            d.set_march(march)
             its = d.run(5000, tol)
             i = d.info()
-            res[name] = (its, gather_x(d.x(), n, world, rank), i["graph"], i["fused"] == want)
+            ok_shape = i["fused"] == want and (name != "sr" or i["march"] > 0)
+            res[name] = (its, gather_x(d.x(), n, world, rank), i["graph"], ok_shape)
         d.set_fused("auto")
+        d.set_march(-1)
     finally:
         d.close()
     if rank != 0:
@@ -833,10 +839,15 @@ def run_dist(args, wl_name, world, rank, local_rank):
     # CG1 one (CG1 with 8-13 B/row more traffic); a timed trial (max over
     # ranks) picks
     trial = {}
-    algs = {"hs": cgx.CGX_ALG_HS, "sr": cgx.CGX_ALG_SR, "cg1": cgx.CGX_ALG_CG1}
+    # name -> (recurrence, march): "sr" is SR's one-launch step on the ranks
+    # where their rows take it (the C4 slabs), "sr_two_launch" its fused
+    # two-launch form
+    algs = {"hs": (cgx.CGX_ALG_HS, -1), "sr": (cgx.CGX_ALG_SR, -1),
+            "sr_two_launch": (cgx.CGX_ALG_SR, 0), "cg1": (cgx.CGX_ALG_CG1, -1)}
     refused = {}
-    for name in ([args.alg] if args.alg else ["hs", "sr", "cg1"]):
-        s.set_alg(algs[name])
+    for name in ([args.alg] if args.alg else ["hs", "sr", "sr_two_launch", "cg1"]):
+        s.set_alg(algs[name][0])
+        s.set_march(algs[name][1])
         try:
             s.bench_prepare(3)  # collective: every rank refuses SR alike (no fused step)
         except cgx.CgxError as e:
@@ -845,7 +856,8 @@ def run_dist(args, wl_name, world, rank, local_rank):
         dist.barrier()
         trial[name] = round(allmax(s.bench_run(20)[0] / 20), 4)
     alg = min(trial, key=trial.get)
-    s.set_alg(algs[alg])
+    s.set_alg(algs[alg][0])
+    s.set_march(algs[alg][1])
     info = s.info()
 
     value = None
@@ -887,7 +899,8 @@ def run_dist(args, wl_name, world, rank, local_rank):
             higher_is_better=True, scaling="strong", vs_baseline=None, dtype=wl["dtype"],
             data="synthetic",
             config=dict(workload=wl["desc"], n=sysm["n_global"], rows_per_rank=info["n_loc"],
-                        nnz_rank0=info["nnz"], alg=alg, alg_trial_ms_per_iter=trial,
+                        nnz_rank0=info["nnz"], alg=alg, march=info["march"],
+                        alg_trial_ms_per_iter=trial,
                         alg_refused=refused or None, fuse_status=info["fuse_status"],
                         graph=info["graph"], fused=info["fused"],
                         parallelism=f"row-partition x{world} (RCCL)",
