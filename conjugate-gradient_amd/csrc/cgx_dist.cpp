@@ -222,6 +222,12 @@ bool part_marchable(const cgx_dist *d) {
   return d->ai_ok && d->march != 0 && d->fuse != CGX_FUSE_OFF;
 }
 
+// the all-reduced sums the one-launch SR step's kernels apply themselves
+// (FIN_SR1 folded into the next iteration's launches, FIN_SUM3_SR1 applies
+// them to the state); nullptr without a transport (FIN_SR1 on the partials)
+// or with the fold switched off (CGX_EXP & 1, the A/B variant)
+const double *sr1_g(const cgx_dist *d);
+
 // The one-launch SR step's launch shapes: boundary steps [0, blo) and
 // [ms - bhi, ms) of every chain -- the steps one of whose three windows
 // reaches a ghost row -- and the interior steps' segment length.
@@ -716,7 +722,7 @@ int phase_pack(cgx_dist *d) {
   CGX_HIP(hipStreamWaitEvent(d->st_comm, d->ev_fork, 0));
   if (sr1(d))
     CGX_HIP(launch_pack_sr<double>(d->n_send, d->d_send_idx, r_old(d), p_old(d), s_old(d),
-                                   d->d_sendbuf, d->d_st, d->st_comm));
+                                   d->d_sendbuf, d->d_st, d->st_comm, sr1_g(d)));
   else if (fz(d))
     CGX_HIP(launch_pack_pnext<double>(d->n_send, d->d_send_idx, d->d_r, p_old(d), d->d_sendbuf,
                                       d->d_st, rr_new_src(d), d->st_comm));
@@ -784,6 +790,7 @@ int phase_sr1(cgx_dist *d) {
       d->Ai.args<double>(nullptr, s_new(d), nullptr, &d->d_st->done, d->Ai.all_items());
   Sr1Args<double> f{d->d_x, p_old(d), p_new(d), r_old(d), r_new(d), s_old(d), d->d_st,
                     d->d_pq, d->d_pc, pl.len};
+  f.g = sr1_g(d);
   f.blo = pl.blo;
   f.bhi = pl.bhi;
   f.seg = 1;
@@ -810,21 +817,35 @@ int phase_sr1(cgx_dist *d) {
   if (d->local)  // as phase_spmv: every part's last group sum has read d_sums
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
-  CGX_HIP(launch_finalize(FIN_SUM3, d->d_pq, gi + gb, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
-                          d->st, d->d_pc, gi + gb));
+  if (sr1_g(d))  // the previous all-reduce applied to the state, then the local sums
+    CGX_HIP(launch_finalize(FIN_SUM3_SR1, d->d_pq, gi + gb, d->d_gsums, 3, d->d_st, d->d_hist,
+                            d->d_sums, d->st, d->d_pc, gi + gb));
+  else
+    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pq, gi + gb, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
+                            d->st, d->d_pc, gi + gb));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
 
-// the iteration's one all-reduce of (p.s, s.s, r.r), then FIN_SR1 on it
-// (the stop test of the previous iteration, alpha, the estimate, beta);
-// the r, p, s buffers swap roles
+const double *sr1_g(const cgx_dist *d) {
+#if defined(CGX_EXP) && (CGX_EXP & 1)
+  return nullptr;
+#else
+  return solo(d) ? nullptr : d->d_gsums;
+#endif
+}
+
+// the iteration's one all-reduce of (p.s, s.s, r.r); without the fold, then
+// FIN_SR1 on it (the stop test of the previous iteration, alpha, the
+// estimate, beta) -- with it the next iteration's kernels apply it; the r,
+// p, s buffers swap roles
 int sr1_reduce(cgx_dist *d) {
   if (!solo(d)) {
     int rc = allreduce(d, 0, 3);
     if (rc) return rc;
-    CGX_HIP(launch_finalize(FIN_SR1, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist, nullptr,
-                            d->st, d->d_gsums + 2, 1));
+    if (!sr1_g(d))
+      CGX_HIP(launch_finalize(FIN_SR1, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist, nullptr,
+                              d->st, d->d_gsums + 2, 1));
   }
   d->pbuf ^= 1;
   return 0;
@@ -1207,8 +1228,9 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
   // complete at done = 2 (an even stop iteration's x update still pending
   // at 1)
   const bool sr0 = sr(g->parts[0]);
-  const long long total =
-      (long long)maxit + 1 + (fz(g->parts[0]) || sr1(g->parts[0]) ? 1 : 0) + (sr0 ? 1 : 0);
+  // (the folded FIN_SR1 marks the stop one iteration later: one more)
+  const long long total = (long long)maxit + 1 + (fz(g->parts[0]) || sr1(g->parts[0]) ? 1 : 0) +
+                          (sr0 ? 1 : 0) + (sr1(g->parts[0]) && sr1_g(g->parts[0]) ? 1 : 0);
   const int fin_done = sr0 ? 2 : 1;
   if (tol <= 0.0) {
     if ((rc = run_phases(g, false, total))) return rc;

@@ -81,8 +81,13 @@ struct CgState {
   // fused step: alpha of an even iteration whose x update is deferred to the
   // next (odd) one -- written by the launch that defers it
   double alpha_def;
+  // partitioned one-launch SR: 1 when the all-reduced (p.s, s.s, r.r) of the
+  // last launch pair are not yet applied to this state (every kernel of the
+  // next iteration applies them to its own copy, FIN_SUM3_SR1 to the state)
+  int sr_pend;
+  int pad_;
 };
-static_assert(sizeof(CgState) == 128, "CgState layout");
+static_assert(sizeof(CgState) == 136, "CgState layout");
 
 // Finalize ops (single-workgroup scalar steps of the recurrence).
 enum FinOp {
@@ -96,6 +101,9 @@ enum FinOp {
   FIN_SUM3 = 7,      // out[0..2] = sums of a's (x, y) pairs and of c (SR local sums)
   FIN_SR1 = 8,       // single-GPU SR step: (p.s, s.s) pairs + r.r -> alpha, estimate,
                      // stop test, beta (k_sr1_dia_m's partials)
+  FIN_SUM3_SR1 = 9,  // partitioned one-launch SR: FIN_SR1 of the previous all-reduce
+                     // (pb: the all-reduced sums, when st->sr_pend) applied to the
+                     // state, then FIN_SUM3's local sums (sr_pend = 1)
 };
 
 constexpr int kVecBS = 256;
@@ -310,6 +318,11 @@ struct Sr1Args {
   double *pq, *pc;
   int march;  // steps per segment
   int seg = 0, blo = 0, bhi = 0;
+  // partitioned: the all-reduced (p.s, s.s, r.r) of the last iteration,
+  // applied (FIN_SR1's step) to a private copy of *st when st->sr_pend --
+  // no scalar launch between the all-reduce and this one; nullptr: *st is
+  // current (single GPU, transport-free)
+  const double *g = nullptr;
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
@@ -357,7 +370,8 @@ int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
 // iteration) -- the roundings k_sr1_dia_m uses for its window rows
 template <typename T>
 hipError_t launch_pack_sr(int n_send, const int *idx, const T *rold, const T *pold,
-                          const T *sold, T *out, const CgState *stt, hipStream_t st);
+                          const T *sold, T *out, const CgState *stt, hipStream_t st,
+                          const double *g = nullptr);
 template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev = LaunchEv{});

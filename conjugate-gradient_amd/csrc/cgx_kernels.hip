@@ -191,6 +191,7 @@ __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *his
       st->k_x = 0;
       st->k_u = -1;  // fused step: no previous iteration yet
       st->done = 0;
+      st->sr_pend = 0;
       break;
     case FIN_HS_ALPHA:
       st->ps = sa;
@@ -260,7 +261,7 @@ __device__ void fin_sr1(double ps, double ss, double rr, CgState *st, double *hi
   const int j = st->k_u + 1;
   if (j >= 1) {
     const int k = j - 1;
-    if (k < st->hist_cap) hist[k] = rr;
+    if (hist && k < st->hist_cap) hist[k] = rr;
     st->rr = rr;
     st->k = k;
     if (k >= st->max_iter || (st->use_tol && rr <= st->tol2bb)) {
@@ -277,6 +278,31 @@ __device__ void fin_sr1(double ps, double ss, double rr, CgState *st, double *hi
   st->alpha = alpha;
   st->k_u = j;
   st->beta = est / rr;
+}
+
+// The scalars a partitioned one-launch SR kernel runs with: *st, with the
+// all-reduced sums g of the last launch pair applied (fin_sr1 on a private
+// copy) while FIN_SUM3_SR1 has not applied them to *st yet (sr_pend) -- so
+// no kernel writes a state field another kernel of the iteration reads.
+struct Sr1Now {
+  int k_u, done;
+  double alpha, beta;
+};
+
+__device__ __forceinline__ Sr1Now sr1_now(const CgState *st, const double *g) {
+  if (!g || !st->sr_pend) return Sr1Now{st->k_u, st->done, st->alpha, st->beta};
+  CgState c;
+  c.done = st->done;
+  c.k_u = st->k_u;
+  c.max_iter = st->max_iter;
+  c.use_tol = st->use_tol;
+  c.tol2bb = st->tol2bb;
+  c.hist_cap = 0;
+  c.brk = 1;  // (not written back)
+  c.alpha = st->alpha;
+  c.beta = st->beta;
+  fin_sr1(g[0], g[1], g[2], &c, nullptr);
+  return Sr1Now{c.k_u, c.done, c.alpha, c.beta};
 }
 
 // XCD-contiguous workgroup order (speed only, never correctness): the
@@ -1290,14 +1316,15 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       m1 = m < msteps ? m + 1 : m;
     }
   }
-  if (f.st->done > 1) return;  // uniform
-  const int k = f.st->k_u;  // the last finalized iteration (-1: none)
-  const bool first = k < 0, stop = f.st->done == 1;
+  const Sr1Now sn = sr1_now(f.st, f.g);
+  if (sn.done > 1) return;  // uniform
+  const int k = sn.k_u;  // the last finalized iteration (-1: none)
+  const bool first = k < 0, stop = sn.done == 1;
   const bool odd = (k & 1) != 0;
   const bool xup = !first && odd;
-  const T alpha = (T)f.st->alpha, beta = (T)f.st->beta, alpha_d = (T)f.st->alpha_def;
+  const T alpha = (T)sn.alpha, beta = (T)sn.beta, alpha_d = (T)f.st->alpha_def;
   if (!first && !odd && !stop && blockIdx.x == 0 && t == 0)
-    const_cast<CgState *>(f.st)->alpha_def = f.st->alpha;
+    const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
   const int QR = a.mq * kDiaSliceRows;
   const int padn = a.mslices * kDiaSliceRows;
   const bool nt = a.nt != 0;
@@ -1696,10 +1723,11 @@ __global__ __launch_bounds__(256) void k_pack_sr(int n_send, const int *__restri
                                                  const T *__restrict__ rold,
                                                  const T *__restrict__ pold,
                                                  const T *__restrict__ sold, T *__restrict__ out,
-                                                 const CgState *st) {
-  if (st->done > 1) return;
-  const bool first = st->k_u < 0;
-  const T alpha = (T)st->alpha, beta = (T)st->beta;
+                                                 const CgState *st, const double *g) {
+  const Sr1Now sn = sr1_now(st, g);
+  if (sn.done > 1) return;
+  const bool first = sn.k_u < 0;
+  const T alpha = (T)sn.alpha, beta = (T)sn.beta;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n_send; i += gridDim.x * 256) {
     const int j = idx[i];
     if (first) {
@@ -2417,11 +2445,19 @@ __global__ __launch_bounds__(BS) void k_finalize(int op, const double *pa, int n
                                                  int nc) {
   __shared__ double red[BS / kWave];
   double sa, sb = 0.0, sc = 0.0;
-  if (op == FIN_SUM3 || op == FIN_SR1)
+  if (op == FIN_SUM3 || op == FIN_SR1 || op == FIN_SUM3_SR1)
     sum_parts_sr<BS>(pa, na, pc, nc, red, sa, sb, sc);  // pa: (p.s, s.s) pairs
   else if (pb) sum_parts2<BS>(pa, na, pb, nb, red, sa, sb);
   else sa = sum_parts<BS>(pa, na, red);
   if (threadIdx.x != 0) return;
+  if (op == FIN_SUM3_SR1) {  // pb: the previous all-reduce's (p.s, s.s, r.r)
+    if (st->sr_pend) fin_sr1(pb[0], pb[1], pb[2], st, hist);
+    st->sr_pend = 1;
+    out[0] = sa;
+    out[1] = sb;
+    out[2] = sc;
+    return;
+  }
   if (op == FIN_SUM3) out[2] = sc;
   if (op == FIN_SR1) {
     fin_sr1(sa, sb, sc, st, hist);
@@ -3001,11 +3037,12 @@ hipError_t launch_pack_pnext(int n_send, const int *idx, const T *r, const T *po
 
 template <typename T>
 hipError_t launch_pack_sr(int n_send, const int *idx, const T *rold, const T *pold,
-                          const T *sold, T *out, const CgState *stt, hipStream_t st) {
+                          const T *sold, T *out, const CgState *stt, hipStream_t st,
+                          const double *g) {
   if (n_send <= 0) return hipSuccess;
   const int grid = std::min((n_send + 255) / 256, 1024);
   hipLaunchKernelGGL((k_pack_sr<T>), dim3(grid), dim3(256), 0, st, n_send, idx, rold, pold, sold,
-                     out, stt);
+                     out, stt, g);
   return hipGetLastError();
 }
 
@@ -3123,7 +3160,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
   template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
   template hipError_t launch_pack_sr<T>(int, const int *, const T *, const T *, const T *, T *,  \
-                                        const CgState *, hipStream_t);                            \
+                                        const CgState *, hipStream_t, const double *);            \
   template hipError_t launch_sr1_march<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,  \
                                           const LaunchEv &);                                     \
   template hipError_t launch_spmv_fused<T>(const SpmvArgs<T> &, const FuseArgs<T> &, hipStream_t, \
