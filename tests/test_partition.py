@@ -121,3 +121,27 @@ def test_partition_rejects_wrong_range():
     rp, col, _ = MATS["lap2d_40x30"]
     with pytest.raises(cgx.CgxError):
         cgx.Partition(len(rp) - 1, 4, 1, rp[:11] - rp[0], col[:rp[10]])
+
+
+@pytest.mark.parametrize("shape,G", [((32, 48, 20), 2), ((32, 48, 20), 3), ((32, 48, 20), 8),
+                                     ((64, 64, 12), 5), ((64, 64, 12), 16), ((400, 400, 8), 8)])
+def test_slab_ghosts_are_neighbouring_planes(shape, G):
+    """The precondition of the one-launch SR step's in-place numbering
+    (cgx_dist.cpp build_inplace): on a 3-D Laplacian cut into
+    row slabs at least one plane (F = nx ny rows) thick, each partition's
+    ghost columns are EXACTLY the rows [row_begin - F, row_begin) and
+    [row_end, row_end + F) inside [0, n) -- plane-aligned or not -- so the
+    columns global - row_begin put them in place below 0 and after n_loc;
+    thinner slabs leave holes (and keep the two-launch step)."""
+    nx, ny, nz = shape
+    F, n = nx * ny, nx * ny * nz
+    for g in range(G):
+        rb, re_ = cgx.partition_rows(n, G, g)
+        rp, col, _ = cgx.laplacian3d(nx, ny, nz, rb, re_)
+        p = cgx.Partition(n, G, g, rp, col)
+        ghosts = list(p.ghosts())
+        want = list(range(max(0, rb - F), rb)) + list(range(re_, min(n, re_ + F)))
+        if re_ - rb >= F:
+            assert ghosts == want, g
+        else:
+            assert set(ghosts) < set(want) and ghosts != want, g
