@@ -237,10 +237,8 @@ struct Sr1Plan {
 
 Sr1Plan sr1_plan(const cgx_dist *d) {
   const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
-  const long long QR = (long long)a.mq * kDiaSliceRows, SR = (long long)a.msb * kDiaSliceRows;
   Sr1Plan p;
-  p.blo = 1 + (int)((a.hl + QR - 1) / QR);
-  p.bhi = 1 + (int)((SR + a.hr - 1 + QR - 1) / QR);
+  sr1_boundary_counts(a, p.blo, p.bhi);  // per chain: the steps whose windows reach a ghost row
   const int steps = (a.mslices + a.mq - 1) / a.mq;
   const int inner = std::max(1, steps - p.blo - p.bhi);
   if (d->march > 0) {

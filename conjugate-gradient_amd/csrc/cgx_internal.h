@@ -300,12 +300,12 @@ struct FuseArgs {
 // k_finalize(FIN_SR1).  r, s, p are double-buffered (read _o, write _n; s_n
 // = SpmvArgs::y).
 // Partitioned (in-place ghost rows, DevMatrix::col_lo): the steps of each
-// chain split into two launches -- seg 1, the interior steps [blo, ms - bhi)
-// (no window reaches a ghost row) in segments of `march`, run while the halo
-// is in flight; seg 2, the boundary steps [0, blo) and [ms - bhi, ms), one
-// workgroup per step, after it (GH: window rows outside [0, n) take p from
-// the p_new buffer's ghost rows, where the halo put the neighbours' p).
-// seg 0: every step (single GPU).
+// chain split into two launches -- seg 1, the chain's interior steps (no
+// window reaches a ghost row: sr1_chain_bounds) in segments of `march`, run
+// while the halo is in flight; seg 2, its boundary steps below and above,
+// one workgroup per step (blo / bhi: the most of any chain), after it (GH:
+// window rows outside [0, n) take p from the p_new buffer's ghost rows,
+// where the halo put the neighbours' p).  seg 0: every step (single GPU).
 template <typename T>
 struct Sr1Args {
   T *x;
@@ -365,6 +365,9 @@ int march_grid(const SpmvArgs<T> &a, int len);
 // the same for one launch of the partitioned split (Sr1Args::seg 1 / 2)
 template <typename T>
 int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
+// the most boundary steps below / above of any chain (Sr1Args::blo / bhi)
+template <typename T>
+void sr1_boundary_counts(const SpmvArgs<T> &a, int &blo, int &bhi);
 // out[i] = p_k[idx[i]] = (r - alpha s) + beta p of the last iteration's
 // buffers (the one-launch SR step's halo send rows; r itself on the first
 // iteration) -- the roundings k_sr1_dia_m uses for its window rows

@@ -1264,6 +1264,23 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
   }
 }
 
+// The interior steps [lo_end, hi0) of the chain starting at slice j0 on a
+// partition's in-place numbering: those whose three windows (m - 1, m, m + 1;
+// rows [base - hl, base + SR + hr)) hold no row outside [0, n) -- the ghost
+// rows the halo fills.  Window w starts at row (j0 + w mq) 512.
+template <typename T>
+__host__ __device__ inline void sr1_chain_bounds(const SpmvArgs<T> &a, int j0, int msteps,
+                                                 int &lo_end, int &hi0) {
+  const long long QR = (long long)a.mq * kDiaSliceRows, jb = (long long)j0 * kDiaSliceRows;
+  const long long SRr = (long long)a.msb * kDiaSliceRows;
+  lo_end = jb >= a.hl ? 1 : 1 + (int)((a.hl - jb + QR - 1) / QR);  // window lo_end - 1 clear
+  const long long top = (long long)a.n - SRr - a.hr - jb;         // window w clear: w QR <= top
+  const int wmax = top < 0 ? -1 : (int)(top / QR);
+  lo_end = lo_end < msteps ? lo_end : msteps;
+  const int h = wmax < msteps ? wmax : msteps;  // step m interior needs window m + 1 <= wmax
+  hi0 = h > lo_end ? h : lo_end;
+}
+
 // ------------------------------ single-GPU SR iteration, plane march (DIA-VI)
 // CGX_ALG_SR on one GPU in ONE launch per iteration (+ k_finalize FIN_SR1):
 // the partitioned solver's SR recurrence (oracle_solve_sr: alpha = r.r / p.s
@@ -1306,7 +1323,8 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     m0 = seg * f.march;
     m1 = min(m0 + f.march, msteps);
   } else {
-    const int lo_end = min(f.blo, msteps), hi0 = max(lo_end, msteps - f.bhi);
+    int lo_end, hi0;
+    sr1_chain_bounds(a, j0, msteps, lo_end, hi0);
     if (f.seg == 1) {  // interior steps [lo_end, hi0) in segments of f.march
       m0 = lo_end + seg * f.march;
       m1 = min(m0 + f.march, hi0);
@@ -2849,16 +2867,33 @@ template <typename T>
 int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f) {
   if (f.seg == 0) return march_grid(a, f.march);
   if (f.seg == 2) return a.mchains * (f.blo + f.bhi);
-  const int steps = (a.mslices + a.mq - 1) / a.mq;  // chain 0's, the longest
-  const int inner = std::max(0, steps - std::min(f.blo, steps) - f.bhi);
+  int inner = 0;  // the most interior steps of any chain
+  for (int c = 0; c < a.mchains; ++c) {
+    const int j0 = c * a.msb, ms = (a.mslices - j0 + a.mq - 1) / a.mq;
+    int lo, hi;
+    sr1_chain_bounds(a, j0, ms, lo, hi);
+    inner = std::max(inner, hi - lo);
+  }
   return a.mchains * ((inner + f.march - 1) / f.march);
+}
+
+template <typename T>
+void sr1_boundary_counts(const SpmvArgs<T> &a, int &blo, int &bhi) {
+  blo = bhi = 0;  // the most boundary steps of any chain, below and above
+  for (int c = 0; c < a.mchains; ++c) {
+    const int j0 = c * a.msb, ms = (a.mslices - j0 + a.mq - 1) / a.mq;
+    int lo, hi;
+    sr1_chain_bounds(a, j0, ms, lo, hi);
+    blo = std::max(blo, lo);
+    bhi = std::max(bhi, ms - hi);
+  }
 }
 
 template <typename T>
 hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev) {
   if (a.mq <= 0 || f.march <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
-      f.seg < 0 || f.seg > 2 || (f.seg != 0 && (f.blo < 1 || f.bhi < 1)))
+      f.seg < 0 || f.seg > 2 || (f.seg != 0 && (f.blo < 1 || f.bhi < 0)))
     return hipErrorInvalidValue;
   const int sb = a.msb;
   const int wn = sb * kDiaSliceRows + a.hl + a.hr;
@@ -3159,6 +3194,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int fused_grid<T>(const SpmvArgs<T> &);                                               \
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
   template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
+  template void sr1_boundary_counts<T>(const SpmvArgs<T> &, int &, int &);                      \
   template hipError_t launch_pack_sr<T>(int, const int *, const T *, const T *, const T *, T *,  \
                                         const CgState *, hipStream_t, const double *);            \
   template hipError_t launch_sr1_march<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,  \
