@@ -228,27 +228,36 @@ bool part_marchable(const cgx_dist *d) {
 // or with the fold switched off (CGX_EXP & 1, the A/B variant)
 const double *sr1_g(const cgx_dist *d);
 
-// The one-launch SR step's launch shapes: boundary steps [0, blo) and
-// [ms - bhi, ms) of every chain -- the steps one of whose three windows
-// reaches a ghost row -- and the interior steps' segment length.
+bool has_peers(const cgx_dist *d);
+
+// The one-launch SR step's launch shapes: segments (set_march's length, or
+// the balanced count sr1_pick_nseg finds for the device) and, on a rank with
+// neighbours, the edge rows k_sr1_edge recomputes after the halo -- [0, elo)
+// below when there are ghost rows below (the rows that reach column < 0:
+// -(lowest diagonal offset)), [ehi, n) above (n - the highest offset), both
+// bounds even (row pairs); a slab too thin to have interior rows is all edge.
 struct Sr1Plan {
-  int blo, bhi, len;
+  int nseg, len, elo, ehi;
 };
 
 Sr1Plan sr1_plan(const cgx_dist *d) {
   const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
   Sr1Plan p;
-  sr1_boundary_counts(a, p.blo, p.bhi);  // per chain: the steps whose windows reach a ghost row
-  const int steps = (a.mslices + a.mq - 1) / a.mq;
-  const int inner = std::max(1, steps - p.blo - p.bhi);
-  if (d->march > 0) {
-    p.len = d->march;
-  } else {
-    // about two resident workgroups per CU (the ring's LDS) in one wave
-    const int nseg = std::max(1, (2 * d->cus + a.mchains / 2) / std::max(1, a.mchains));
-    p.len = (inner + nseg - 1) / nseg;
+  p.nseg = d->march > 0 ? 0 : sr1_pick_nseg(a, d->cus);
+  p.len = d->march > 0 ? d->march : 0;
+  p.elo = 0;
+  p.ehi = 0x7fffffff;
+  if (has_peers(d) && a.ndiag > 0) {
+    const int n = a.n;
+    if (d->g_lo > 0) p.elo = std::min(n, std::max(0, -a.doff[0]));
+    if (d->g_hi > 0) p.ehi = std::max(0, n - std::max(0, a.doff[a.ndiag - 1]));
+    p.elo = (p.elo + 1) & ~1;
+    if (p.ehi < n) p.ehi &= ~1;
+    if (p.elo >= p.ehi) {  // every row an edge row
+      p.elo = (n + 1) & ~1;
+      p.ehi = 0x7fffffff;
+    }
   }
-  p.len = std::max(1, p.len);
   return p;
 }
 
@@ -475,16 +484,10 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
   }
   if (d->ai_ok) {
     // the one-launch SR step's partials: one (p.s, s.s) pair and one r.r per
-    // workgroup of its two launches (the widest segmentation: length 1)
-    Sr1Plan pl = sr1_plan(d);
-    pl.len = 1;
+    // workgroup of its launches (at most: every step its own workgroup, and
+    // one edge workgroup per 512 rows)
     const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
-    Sr1Args<double> f{};
-    f.march = 1;
-    f.blo = pl.blo;
-    f.bhi = pl.bhi;
-    f.seg = 1;
-    const int cap = sr1_grid(a, f) + a.mchains * (pl.blo + pl.bhi) + 8;
+    const int cap = a.mchains * ((a.mslices + a.mq - 1) / a.mq) + (d->n_loc + 511) / 512 + 8;
     if ((rc = dev_alloc(&d->d_pq, (size_t)cap * 16, cb)) || (rc = dev_alloc(&d->d_pc, (size_t)cap * 8, cb))) {
       free_system(d);
       return rc;
@@ -776,10 +779,11 @@ int phase_halo(cgx_dist *d) {
 // it may retire: 70 us on an 8 M-row slab, against ~5 us for the launch.)
 int allreduce(cgx_dist *d, int i, int count);
 
-// The one-launch SR step (k_sr1_dia_m on the in-place numbering): interior
-// steps while the halo is in flight, then the boundary steps; the local
-// (p.s, s.s, r.r) (FIN_SUM3), or with no transport the scalar step itself
-// (FIN_SR1, as the single-GPU solver).
+// The one-launch SR step (k_sr1_dia_m on the in-place numbering): every step
+// while the halo of p_k is in flight, then (a rank with neighbours) the edge
+// rows' s and (p.s, s.s) after it (k_sr1_edge); then the local (p.s, s.s,
+// r.r) (FIN_SUM3 / FIN_SUM3_SR1), or with no transport the scalar step
+// itself (FIN_SR1, as the single-GPU solver).
 int phase_sr1(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
   const bool rec = d->rec_spmv && d->ev_i + 4 <= d->spmv_ev.size();
@@ -789,38 +793,44 @@ int phase_sr1(cgx_dist *d) {
   Sr1Args<double> f{d->d_x, p_old(d), p_new(d), r_old(d), r_new(d), s_old(d), d->d_st,
                     d->d_pq, d->d_pc, pl.len};
   f.g = sr1_g(d);
-  f.blo = pl.blo;
-  f.bhi = pl.bhi;
-  f.seg = 1;
+  f.nseg = pl.nseg;
+  f.elo = pl.elo;
+  f.ehi = pl.ehi;
   const int gi = sr1_grid(a, f);
-  Sr1Args<double> fb = f;
-  fb.seg = 2;
-  fb.pq = d->d_pq + 2 * (size_t)gi;
-  fb.pc = d->d_pc + gi;
-  const int gb = sr1_grid(a, fb);
+  Sr1Args<double> fe = f;
+  fe.pq = d->d_pq + 2 * (size_t)gi;
+  fe.pc = d->d_pc + gi;
+  const bool edge = has_peers(d);
+  const int ge = edge ? sr1_edge_grid(a.n, fe) : 0;
   d->gi1 = gi;
-  d->gb1 = gb;
+  d->gb1 = ge;
   auto ev = [&](int e) {
     return rec ? LaunchEv{d->spmv_ev[d->ev_i + e], d->spmv_ev[d->ev_i + e + 1]} : LaunchEv{};
   };
   CGX_HIP(launch_sr1_march<double>(a, f, d->st, ev(0)));
-  if (has_peers(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
-  CGX_HIP(launch_sr1_march<double>(a, fb, d->st, ev(2)));
+  if (edge) {
+    CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
+    CGX_HIP(launch_sr1_edge<double>(a, fe, d->st, ev(2)));
+  } else if (rec) {  // the second event pair brackets nothing
+    CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 2], d->st));
+    CGX_HIP(hipEventRecord(d->spmv_ev[d->ev_i + 3], d->st));
+  }
   if (rec) d->ev_i += 4;
+  const int np = gi + ge;
   if (solo(d)) {
-    CGX_HIP(launch_finalize(FIN_SR1, d->d_pq, gi + gb, nullptr, 0, d->d_st, d->d_hist, nullptr,
-                            d->st, d->d_pc, gi + gb));
+    CGX_HIP(launch_finalize(FIN_SR1, d->d_pq, np, nullptr, 0, d->d_st, d->d_hist, nullptr, d->st,
+                            d->d_pc, np));
     return 0;
   }
   if (d->local)  // as phase_spmv: every part's last group sum has read d_sums
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
   if (sr1_g(d))  // the previous all-reduce applied to the state, then the local sums
-    CGX_HIP(launch_finalize(FIN_SUM3_SR1, d->d_pq, gi + gb, d->d_gsums, 3, d->d_st, d->d_hist,
-                            d->d_sums, d->st, d->d_pc, gi + gb));
+    CGX_HIP(launch_finalize(FIN_SUM3_SR1, d->d_pq, np, d->d_gsums, 3, d->d_st, d->d_hist,
+                            d->d_sums, d->st, d->d_pc, np));
   else
-    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pq, gi + gb, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
-                            d->st, d->d_pc, gi + gb));
+    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pq, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
+                            d->st, d->d_pc, np));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
@@ -1573,7 +1583,15 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   // fused CG1: + r, w, s, p, x read and p, s, r, w, x written (cgx_info)
   if (d->have_matrix && fz1(d)) s->spmv_iter_bytes += 8.0 * d->n_loc * 8.0;
   s->fused = fz(d) || fz1(d) || sr1(d) ? 1 : 0;
-  s->march = d->have_matrix && sr1(d) ? sr1_plan(d).len : 0;
+  if (d->have_matrix && sr1(d)) {  // steps per segment (the longest)
+    const Sr1Plan pl = sr1_plan(d);
+    const SpmvArgs<double> a =
+        d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
+    const int L = (a.mslices + a.mq - 1) / a.mq;
+    s->march = std::max(1, pl.len > 0 ? pl.len : (L + pl.nseg - 1) / std::max(1, pl.nseg));
+  } else {
+    s->march = 0;
+  }
   s->inplace = d->ai_ok ? 1 : 0;
   {
     const int own = d->fuse == CGX_FUSE_OFF ? CGX_FUSE_STATUS_OFF

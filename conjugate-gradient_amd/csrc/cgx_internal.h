@@ -299,13 +299,13 @@ struct FuseArgs {
 // (p.s, s.s) pairs (pq[2 b], pq[2 b + 1]) and r.r (pc[b]) per workgroup b for
 // k_finalize(FIN_SR1).  r, s, p are double-buffered (read _o, write _n; s_n
 // = SpmvArgs::y).
-// Partitioned (in-place ghost rows, DevMatrix::col_lo): the steps of each
-// chain split into two launches -- seg 1, the chain's interior steps (no
-// window reaches a ghost row: sr1_chain_bounds) in segments of `march`, run
-// while the halo is in flight; seg 2, its boundary steps below and above,
-// one workgroup per step (blo / bhi: the most of any chain), after it (GH:
-// window rows outside [0, n) take p from the p_new buffer's ghost rows,
-// where the halo put the neighbours' p).  seg 0: every step (single GPU).
+// Partitioned (in-place ghost rows, DevMatrix::col_lo): the same launch over
+// every step while the halo is in flight (a window's ghost rows hold no p_k
+// yet), then k_sr1_edge after it: s of the edge rows [0, elo) and [ehi, n)
+// (even bounds; rows whose row reaches a ghost column) from the p_new buffer
+// (own rows as stored, ghost rows from the halo), and their (p.s, s.s) --
+// k_sr1_dia_m leaves those rows out of its pairs.  A chain's steps are cut
+// into nseg balanced segments, or (nseg 0) segments of `march` steps.
 template <typename T>
 struct Sr1Args {
   T *x;
@@ -316,8 +316,9 @@ struct Sr1Args {
   const T *sold;
   const CgState *st;
   double *pq, *pc;
-  int march;  // steps per segment
-  int seg = 0, blo = 0, bhi = 0;
+  int march;  // steps per segment (nseg == 0)
+  int nseg = 0;
+  int elo = 0, ehi = 0x7fffffff;
   // partitioned: the all-reduced (p.s, s.s, r.r) of the last iteration,
   // applied (FIN_SR1's step) to a private copy of *st when st->sr_pend --
   // no scalar launch between the all-reduce and this one; nullptr: *st is
@@ -362,12 +363,24 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream
 // workgroups (= partial pairs) of the plane march at `len` steps per segment
 template <typename T>
 int march_grid(const SpmvArgs<T> &a, int len);
-// the same for one launch of the partitioned split (Sr1Args::seg 1 / 2)
+// workgroups (= partial pairs) of one k_sr1_dia_m launch
 template <typename T>
 int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
-// the most boundary steps below / above of any chain (Sr1Args::blo / bhi)
+// Segments per chain on `cus` CUs: the nseg whose launch takes the fewest
+// step-times in the resident-workgroup model (ceil(chains nseg / slots)
+// rounds of ceil(L / nseg) + 2 windows, L the longest chain; slots from the
+// kernel's occupancy).  An explicit march length (> 0) is used as given
+// instead (nseg 0).
 template <typename T>
-void sr1_boundary_counts(const SpmvArgs<T> &a, int &blo, int &bhi);
+int sr1_pick_nseg(const SpmvArgs<T> &a, int cus);
+// workgroups (= partial pairs) of k_sr1_edge over f's edge rows of n rows
+template <typename T>
+int sr1_edge_grid(int n, const Sr1Args<T> &f);
+// k_sr1_edge: s of the edge rows after the halo, their (p.s, s.s) pairs
+// (a.y = s; f.pnew = p_k with ghost rows; f.pq / f.pc: this launch's slots)
+template <typename T>
+hipError_t launch_sr1_edge(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
+                           const LaunchEv &ev);
 // out[i] = p_k[idx[i]] = (r - alpha s) + beta p of the last iteration's
 // buffers (the one-launch SR step's halo send rows; r itself on the first
 // iteration) -- the roundings k_sr1_dia_m uses for its window rows

@@ -1264,23 +1264,6 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
   }
 }
 
-// The interior steps [lo_end, hi0) of the chain starting at slice j0 on a
-// partition's in-place numbering: those whose three windows (m - 1, m, m + 1;
-// rows [base - hl, base + SR + hr)) hold no row outside [0, n) -- the ghost
-// rows the halo fills.  Window w starts at row (j0 + w mq) 512.
-template <typename T>
-__host__ __device__ inline void sr1_chain_bounds(const SpmvArgs<T> &a, int j0, int msteps,
-                                                 int &lo_end, int &hi0) {
-  const long long QR = (long long)a.mq * kDiaSliceRows, jb = (long long)j0 * kDiaSliceRows;
-  const long long SRr = (long long)a.msb * kDiaSliceRows;
-  lo_end = jb >= a.hl ? 1 : 1 + (int)((a.hl - jb + QR - 1) / QR);  // window lo_end - 1 clear
-  const long long top = (long long)a.n - SRr - a.hr - jb;         // window w clear: w QR <= top
-  const int wmax = top < 0 ? -1 : (int)(top / QR);
-  lo_end = lo_end < msteps ? lo_end : msteps;
-  const int h = wmax < msteps ? wmax : msteps;  // step m interior needs window m + 1 <= wmax
-  hi0 = h > lo_end ? h : lo_end;
-}
-
 // ------------------------------ single-GPU SR iteration, plane march (DIA-VI)
 // CGX_ALG_SR on one GPU in ONE launch per iteration (+ k_finalize FIN_SR1):
 // the partitioned solver's SR recurrence (oracle_solve_sr: alpha = r.r / p.s
@@ -1299,12 +1282,11 @@ __host__ __device__ inline void sr1_chain_bounds(const SpmvArgs<T> &a, int j0, i
 // tree and the waves in order -- deterministic.
 // Partitioned ranks (in-place ghost rows: columns = global - row_begin, the
 // rows of the neighbours' boundary planes at [col_lo, 0) and [n, ncols)):
-// the same step, split by Sr1Args::seg into the interior steps (no window
-// reaches a ghost row; launched while the halo is in flight) and the boundary
-// steps (GH: p_k of a window row outside [0, n) is the neighbour's, received
-// into the p_new buffer's ghost rows by the halo exchange; k_pack_sr computed
-// it there with these roundings).
-template <typename T, int SB, int NF, int CB, bool GH>
+// the same launch over every step while the halo is in flight; the windows'
+// ghost rows hold no p_k yet, so s of the edge rows (Sr1Args::elo / ehi:
+// those whose row reaches a ghost column) is provisional and stays out of
+// the (p.s, s.s) sums -- k_sr1_edge recomputes it after the halo.
+template <typename T, int SB, int NF, int CB>
 __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
@@ -1319,20 +1301,12 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   const int j0 = chain * SB;
   const int msteps = (a.mslices - j0 + a.mq - 1) / a.mq;
   int m0, m1;
-  if (f.seg == 0) {  // every step, in segments of f.march
+  if (f.nseg > 0) {  // the chain's steps in nseg balanced segments
+    m0 = (int)((long long)seg * msteps / f.nseg);
+    m1 = (int)((long long)(seg + 1) * msteps / f.nseg);
+  } else {  // segments of f.march steps
     m0 = seg * f.march;
     m1 = min(m0 + f.march, msteps);
-  } else {
-    int lo_end, hi0;
-    sr1_chain_bounds(a, j0, msteps, lo_end, hi0);
-    if (f.seg == 1) {  // interior steps [lo_end, hi0) in segments of f.march
-      m0 = lo_end + seg * f.march;
-      m1 = min(m0 + f.march, hi0);
-    } else {  // boundary steps, one per workgroup: [0, lo_end), then [hi0, msteps)
-      const int m = seg < f.blo ? (seg < lo_end ? seg : msteps) : hi0 + (seg - f.blo);
-      m0 = m;
-      m1 = m < msteps ? m + 1 : m;
-    }
   }
   const Sr1Now sn = sr1_now(f.st, f.g);
   if (sn.done > 1) return;  // uniform
@@ -1407,9 +1381,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     publish();
     return;
   }
-  constexpr int NG = GH ? NF : 1;
-  P wr[NF], wp[NF], wsv[NF], wg[NG];
-  int wj[NG];
+  P wr[NF], wp[NF], wsv[NF];
   auto load_win = [&](int m) {
     const int w0 = base_of(m) - a.hl;
 #pragma unroll
@@ -1418,10 +1390,6 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       wr[q] = ld_pair(f.rold, j);
       wp[q] = ld_pair(f.pold, j);
       wsv[q] = ld_pair(f.sold, j);
-      if constexpr (GH) {
-        wj[q] = j;
-        wg[q] = ld_pair((const T *)f.pnew, j);
-      }
     }
   };
   auto store_win = [&](int m) {
@@ -1435,11 +1403,6 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
         rk.x = wr[q].x - as0;
         rk.y = wr[q].y - as1;
         pk = p_next<T>(rk, wp[q], beta);
-      }
-      if constexpr (GH) {  // a ghost row: the neighbour's p_k from the halo
-        const int j = wj[q];
-        if (j < 0 || j >= a.n) pk.x = wg[q].x;
-        if (j + 1 < 0 || j + 1 >= a.n) pk.y = wg[q].y;
       }
       if (i + 1 < wn) lds_st2(win, i, pk.x, pk.y);  // wn even (march plan)
       else if (i < wn) win[i] = pk.x;
@@ -1502,12 +1465,17 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       st_pair(f.pnew, r, rend, pn0, pn1, false);
       st_pair(f.rnew, r, rend, rk0, rk1, false);
       if (xup) x_update(cx, r, rend);
-      sps = sps + (double)pn0 * (double)a0;
-      sss = sss + (double)a0 * (double)a0;
+      const bool own = r >= f.elo && r < f.ehi;  // edge pairs: k_sr1_edge's (p.s, s.s)
+      if (own) {
+        sps = sps + (double)pn0 * (double)a0;
+        sss = sss + (double)a0 * (double)a0;
+      }
       srr = srr + (double)rk0 * (double)rk0;
       if (r + 1 < rend) {
-        sps = sps + (double)pn1 * (double)a1;
-        sss = sss + (double)a1 * (double)a1;
+        if (own) {
+          sps = sps + (double)pn1 * (double)a1;
+          sss = sss + (double)a1 * (double)a1;
+        }
         srr = srr + (double)rk1 * (double)rk1;
       }
     }
@@ -1518,6 +1486,81 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     if (m + 1 < m1) step(m + 1, cwn, xn, cw, xc);
   }
   publish();
+}
+
+// The edge rows of a partitioned rank's one-launch SR step, after the halo:
+// rows [0, elo) and [ehi, n) (row pairs; Sr1Args), whose rows reach a ghost
+// column.  s = A p_k with p_k from the p_new buffer -- the own rows as
+// k_sr1_dia_m stored them, the ghost rows as the halo put them -- in the
+// row's diagonal order with k_sr1_dia_m's roundings (so s is what one launch
+// with every p_k in place computes), then the (p.s, s.s) pair per workgroup
+// (r.r: k_sr1_dia_m has all own rows; 0 here).
+template <typename T>
+__global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
+  __shared__ T lv[kDiaMax * 16];
+  __shared__ double red[2][4];
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const Sr1Now sn = sr1_now(f.st, f.g);
+  if (sn.done) return;  // uniform (a stop: k_sr1_dia_m's x update only)
+  // pair i of the edge rows: na below, nb above (no ehi arithmetic unless
+  // there are rows above: ehi is INT_MAX then)
+  const int na = f.elo / 2, nb = f.ehi < a.n ? (a.n - f.ehi + 1) / 2 : 0;
+  const int i = blockIdx.x * 256 + t;
+  const bool live = i < na + nb;
+  const int r = i < na ? 2 * i : live ? f.ehi + 2 * (i - na) : 0;
+  if (t < a.ndiag * 16) lv[t] = a.vtab[t];
+  const T *p = f.pnew;
+  const int rl = live ? r : 0;
+  const bool two = live && r + 1 < a.n;
+  unsigned c0, c1;
+  ld_codes(a.dcode, a.cb, rl, c0, c1);
+  // every load out before the first use, unconditionally (a missing entry
+  // reloads p[r]): a conditional load makes the compiler wait on it
+  T v0[kDiaMax], v1[kDiaMax];
+#pragma unroll
+  for (int kk = 0; kk < kDiaMax; ++kk) {
+    if (kk < a.ndiag) {
+      const int d = a.doff[kk];
+      v0[kk] = p[fld(a, c0, kk) != a.cmask[kk] ? rl + d : rl];
+      v1[kk] = p[two && fld(a, c1, kk) != a.cmask[kk] ? rl + 1 + d : rl];
+    }
+  }
+  const T p0 = p[rl], p1 = p[two ? rl + 1 : rl];
+  __syncthreads();  // lv
+  T a0 = T(0), a1 = T(0);
+#pragma unroll
+  for (int kk = 0; kk < kDiaMax; ++kk) {
+    if (kk < a.ndiag) {
+      const unsigned n0 = fld(a, c0, kk), n1 = fld(a, c1, kk);
+      const T q0 = lv[kk * 16 + n0] * v0[kk], q1 = lv[kk * 16 + n1] * v1[kk];
+      a0 = n0 != a.cmask[kk] ? a0 + q0 : a0;
+      a1 = n1 != a.cmask[kk] ? a1 + q1 : a1;
+    }
+  }
+  double ps = 0.0, ss = 0.0;
+  if (live) {
+    a.y[r] = a0;
+    ps = (double)p0 * (double)a0;
+    ss = (double)a0 * (double)a0;
+    if (two) {
+      a.y[r + 1] = a1;
+      ps = ps + (double)p1 * (double)a1;
+      ss = ss + (double)a1 * (double)a1;
+    }
+  }
+  ps = wave_sum(ps);
+  ss = wave_sum(ss);
+  if (lane == 0) {
+    red[0][wid] = ps;
+    red[1][wid] = ss;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const double p0 = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    const double p1 = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    reinterpret_cast<double2 *>(f.pq)[blockIdx.x] = make_double2(p0, p1);
+    f.pc[blockIdx.x] = 0.0;
+  }
 }
 
 // ---------------------------------------- fused CG1 step (DIA-VI)
@@ -2851,80 +2894,109 @@ static hipError_t launch_march(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipSt
   return hipGetLastError();
 }
 
-template <typename T, int SB, int NF, bool GH>
-static const void *sr1_kernel_g(int cb) {
-  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, GH>))
-         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2, GH>))
-                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4, GH>));
-}
-
 template <typename T, int SB, int NF>
-static const void *sr1_kernel(int cb, bool gh) {
-  return gh ? sr1_kernel_g<T, SB, NF, true>(cb) : sr1_kernel_g<T, SB, NF, false>(cb);
+static const void *sr1_kernel(int cb) {
+  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1>))
+         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2>))
+                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4>));
 }
 
 template <typename T>
 int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f) {
-  if (f.seg == 0) return march_grid(a, f.march);
-  if (f.seg == 2) return a.mchains * (f.blo + f.bhi);
-  int inner = 0;  // the most interior steps of any chain
-  for (int c = 0; c < a.mchains; ++c) {
-    const int j0 = c * a.msb, ms = (a.mslices - j0 + a.mq - 1) / a.mq;
-    int lo, hi;
-    sr1_chain_bounds(a, j0, ms, lo, hi);
-    inner = std::max(inner, hi - lo);
-  }
-  return a.mchains * ((inner + f.march - 1) / f.march);
+  const int steps = (a.mslices + a.mq - 1) / a.mq;  // chain 0's, the longest
+  if (f.nseg > 0) return a.mchains * std::min(f.nseg, steps);
+  if (f.march <= 0) return 0;
+  return a.mchains * ((steps + f.march - 1) / f.march);
 }
 
 template <typename T>
-void sr1_boundary_counts(const SpmvArgs<T> &a, int &blo, int &bhi) {
-  blo = bhi = 0;  // the most boundary steps of any chain, below and above
-  for (int c = 0; c < a.mchains; ++c) {
-    const int j0 = c * a.msb, ms = (a.mslices - j0 + a.mq - 1) / a.mq;
-    int lo, hi;
-    sr1_chain_bounds(a, j0, ms, lo, hi);
-    blo = std::max(blo, lo);
-    bhi = std::max(bhi, ms - hi);
+int sr1_edge_grid(int n, const Sr1Args<T> &f) {
+  const long long pairs = f.elo / 2 + (f.ehi < n ? (n - f.ehi + 1) / 2 : 0);
+  return (int)((pairs + 255) / 256);
+}
+
+// the kernel instance for the matrix's march plan (nullptr: none) and its LDS
+template <typename T>
+static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
+  const int sb = a.msb;
+  const int wn = sb * kDiaSliceRows + a.hl + a.hr;
+  const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
+  if (a.mws < wn + 2 || (sb != 1 && sb != 2) || nf > (sb == 1 ? 5 : 3)) return nullptr;
+  const int nfc = nf <= 2 ? 2 : nf <= 3 ? 3 : 5;
+  const int cb = a.cb;
+  if (cb != 1 && cb != 2 && cb != 4) return nullptr;
+  // the three-window ring and two slots of own-row r
+  lds = ((size_t)3 * a.mws + 2 * sb * kDiaSliceRows) * sizeof(T) + 16;
+  switch (sb * 10 + nfc) {
+    case 12: return sr1_kernel<T, 1, 2>(cb);
+    case 13: return sr1_kernel<T, 1, 3>(cb);
+    case 15: return sr1_kernel<T, 1, 5>(cb);
+    case 22: return sr1_kernel<T, 2, 2>(cb);
+    case 23: return sr1_kernel<T, 2, 3>(cb);
+    default: return nullptr;
   }
+}
+
+template <typename T>
+int sr1_pick_nseg(const SpmvArgs<T> &a, int cus) {
+  size_t lds = 0;
+  const void *k = sr1_pick(a, lds);
+  if (!k || a.mchains <= 0) return 1;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * a.msb, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const long long slots = (long long)per_cu * std::max(1, cus);
+  const int L = std::max(1, (a.mslices + a.mq - 1) / a.mq);
+  int best = 1;
+  long long best_cost = -1;
+  for (int ns = 1; ns <= L; ++ns) {
+    const long long rounds = ((long long)a.mchains * ns + slots - 1) / slots;
+    const long long cost = rounds * ((L + ns - 1) / ns + 2);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = ns;
+    }
+  }
+  return best;
 }
 
 template <typename T>
 hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev) {
-  if (a.mq <= 0 || f.march <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
-      f.seg < 0 || f.seg > 2 || (f.seg != 0 && (f.blo < 1 || f.bhi < 0)))
+  if (a.mq <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
+      (f.march <= 0 && f.nseg <= 0) || f.nseg < 0 || (f.elo & 1) || (f.ehi < a.n && (f.ehi & 1)))
     return hipErrorInvalidValue;
-  const int sb = a.msb;
-  const int wn = sb * kDiaSliceRows + a.hl + a.hr;
-  const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
-  if (a.mws < wn + 2 || (sb != 1 && sb != 2) || nf > (sb == 1 ? 5 : 3)) return hipErrorInvalidValue;
-  const int nfc = nf <= 2 ? 2 : nf <= 3 ? 3 : 5;
-  const int cb = a.cb;
-  if (cb != 1 && cb != 2 && cb != 4) return hipErrorInvalidValue;
-  const void *k = nullptr;
-  const bool gh = f.seg == 2;
-  switch (sb * 10 + nfc) {
-    case 12: k = sr1_kernel<T, 1, 2>(cb, gh); break;
-    case 13: k = sr1_kernel<T, 1, 3>(cb, gh); break;
-    case 15: k = sr1_kernel<T, 1, 5>(cb, gh); break;
-    case 22: k = sr1_kernel<T, 2, 2>(cb, gh); break;
-    case 23: k = sr1_kernel<T, 2, 3>(cb, gh); break;
-    default: return hipErrorInvalidValue;
-  }
+  size_t lds = 0;
+  const void *k = sr1_pick(a, lds);
+  if (!k) return hipErrorInvalidValue;
   const int g = sr1_grid(a, f);
-  if (g <= 0) {  // nothing to run: the launch's events still bracket it
+  void *args[] = {(void *)&a, (void *)&f};
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256 * a.msb), args, lds, st, ev.start, ev.stop, 0);
+  else
+    (void)hipLaunchKernel(k, dim3(g), dim3(256 * a.msb), args, lds, st);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_sr1_edge(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
+                           const LaunchEv &ev) {
+  if (a.layout != L_DIA || (f.elo & 1) || f.elo < 0 || f.elo > a.n + 1 || f.ehi < f.elo ||
+      (f.ehi < a.n && (f.ehi & 1)) || a.ndiag > kDiaMax)
+    return hipErrorInvalidValue;
+  const int g = sr1_edge_grid(a.n, f);
+  if (g <= 0) {  // no edge rows: the launch's events still bracket it
     if (ev.start) (void)hipEventRecord(ev.start, st);
     if (ev.stop) (void)hipEventRecord(ev.stop, st);
     return hipGetLastError();
   }
   void *args[] = {(void *)&a, (void *)&f};
-  // the three-window ring and two slots of own-row r
-  const size_t lds = ((size_t)3 * a.mws + 2 * sb * kDiaSliceRows) * sizeof(T) + 16;
+  const void *k = CGX_K(k_sr1_edge<T>);
   if (ev.start || ev.stop)
-    (void)hipExtLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st, ev.start, ev.stop, 0);
+    (void)hipExtLaunchKernel(k, dim3(g), dim3(256), args, 0, st, ev.start, ev.stop, 0);
   else
-    (void)hipLaunchKernel(k, dim3(g), dim3(256 * sb), args, lds, st);
+    (void)hipLaunchKernel(k, dim3(g), dim3(256), args, 0, st);
   return hipGetLastError();
 }
 
@@ -3194,7 +3266,10 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int fused_grid<T>(const SpmvArgs<T> &);                                               \
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
   template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
-  template void sr1_boundary_counts<T>(const SpmvArgs<T> &, int &, int &);                      \
+  template int sr1_pick_nseg<T>(const SpmvArgs<T> &, int);                                      \
+  template int sr1_edge_grid<T>(int, const Sr1Args<T> &);                                       \
+  template hipError_t launch_sr1_edge<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,   \
+                                         const LaunchEv &);                                      \
   template hipError_t launch_pack_sr<T>(int, const int *, const T *, const T *, const T *, T *,  \
                                         const CgState *, hipStream_t, const double *);            \
   template hipError_t launch_sr1_march<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,  \

@@ -342,8 +342,10 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     T *ro = (T *)(q ? s->d_r2 : s->d_r), *rn = (T *)(q ? s->d_r : s->d_r2);
     T *so = (T *)(q ? s->d_s2 : s->d_s), *sn = (T *)(q ? s->d_s : s->d_s2);
     const SpmvArgs<T> a = s->A.args<T>(nullptr, sn, nullptr, &s->d_st->done, s->A.all_items());
-    const Sr1Args<T> f{x, po, pn, ro, rn, so, s->d_st, s->d_pa, s->d_pb, march_len(s)};
-    const int g = march_grid(a, f.march);
+    Sr1Args<T> f{x, po, pn, ro, rn, so, s->d_st, s->d_pa, s->d_pb, march_len(s)};
+    // set_march's length as given; auto: the balanced segment count
+    if (s->march <= 0) f.nseg = sr1_pick_nseg(a, s->cus);
+    const int g = sr1_grid(a, f);
     if (2 * g > s->part_cap) return CGX_EINVAL;
     CGX_HIP(launch_sr1_march<T>(a, f, st, LaunchEv{ev0, ev1}));
     CGX_HIP(launch_finalize(FIN_SR1, s->d_pa, g, nullptr, 0, s->d_st, s->d_hist, nullptr, st,

@@ -7,7 +7,8 @@ C4's slab at N = 8), graph-replayed.
 
 cases: hs_fused, hs, cg1, sr (auto: the one-launch k_sr1_dia_m step where it
 applies), sr2 (the two-launch fused SR step, set_march(0)), srN (one-launch
-with N interior steps per workgroup).  Default: hs_fused, sr, sr2, hs, cg1,
+with N steps per workgroup), one / oneN (the single-GPU solver's SR
+step on the same slab: auto or N steps per workgroup -- the rank step's base).  Default: hs_fused, sr, sr2, hs, cg1,
 then hs_fused, sr, sr2 again (alternating)."""
 import sys
 sys.path.insert(0, "conjugate-gradient_amd")
@@ -36,7 +37,23 @@ def case(name):
     return cgx.CGX_ALG_SR, "auto", int(name[2:])
 
 
+def one(name):
+    with cgx.Solver(alg=cgx.CGX_ALG_SR) as s:
+        s.gen_laplacian(3, 400, 400, nz)
+        s.set_march(int(name[3:]) if len(name) > 3 else -1)
+        s.set_rhs(b)
+        s.bench_prepare(5)
+        ms, _ = s.bench_run(100)
+        _, sp = s.bench_run(30, graph=False, spmv_events=True)
+        i = s.info()
+        print("%-9s n %d  %.1f us/iter  spmv(launches) %.1f us  fused %d layout %s" %
+              (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["layout_name"]), flush=True)
+
+
 for name in cases:
+    if name.startswith("one"):
+        one(name)
+        continue
     alg, fused, march = case(name)
     d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
     try:
@@ -53,6 +70,29 @@ for name in cases:
               (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["march"], i["layout"]), flush=True)
     finally:
         d.close()
+
+# partitions with ghost faces: an in-process group of 2 slabs of nz planes
+# (SR: each part's k_sr1_dia_m over its own steps, then k_sr1_edge of its
+# ghost-facing plane after the D2D halo; part 0's launches timed)
+if len(sys.argv) > 2 and sys.argv[2] == "local2sr":
+    rp, col, val = cgx.laplacian3d(400, 400, 2 * nz)
+    n = len(rp) - 1
+    for march in (-1, 0):
+        parts = cgx.DistSolver.local_group(0, 2)
+        try:
+            parts[0].set_alg(cgx.CGX_ALG_SR)
+            parts[0].set_march(march)
+            for g, d in enumerate(parts):
+                rb, re_ = cgx.partition_rows(n, 2, g)
+                d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+                d.set_rhs(np.ones(re_ - rb))
+            parts[0].bench_prepare(3)
+            ms, sp = parts[0].bench_run(20, spmv_events=True)
+            i = parts[0].info()
+            print("local2sr march %d: part-0 SR launches %.1f us, group iteration %.1f us (march %d inplace %d)" %
+                  (march, 1e3 * sp, 1e3 * ms / 20, i["march"], i["inplace"]), flush=True)
+        finally:
+            parts[0].close()
 
 # partitions with ghost faces: an in-process group of 3 slabs of nz planes
 # each (part 0's SpMV launches timed: its far slots are -nx*ny, +nx*ny and
