@@ -1500,8 +1500,6 @@ __global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
   __shared__ T lv[kDiaMax * 16];
   __shared__ double red[2][4];
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const Sr1Now sn = sr1_now(f.st, f.g);
-  if (sn.done) return;  // uniform (a stop: k_sr1_dia_m's x update only)
   // pair i of the edge rows: na below, nb above (no ehi arithmetic unless
   // there are rows above: ehi is INT_MAX then)
   const int na = f.elo / 2, nb = f.ehi < a.n ? (a.n - f.ehi + 1) / 2 : 0;
@@ -1526,6 +1524,9 @@ __global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
     }
   }
   const T p0 = p[rl], p1 = p[two ? rl + 1 : rl];
+  // the state after the loads are out (its loads would otherwise go first)
+  const Sr1Now sn = sr1_now(f.st, f.g);
+  if (sn.done) return;  // uniform (a stop: k_sr1_dia_m's x update only)
   __syncthreads();  // lv
   T a0 = T(0), a1 = T(0);
 #pragma unroll
