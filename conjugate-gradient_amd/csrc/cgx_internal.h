@@ -432,13 +432,18 @@ template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
                             const FinArgs *fin = nullptr, const double *sr = nullptr,
-                            double *hist = nullptr);
+                            double *hist = nullptr, bool nt = false);
 // p -> pn (pn == p: in place, x every iteration; pn != p: x every other
-// iteration, k_xpay_xf)
+// iteration, k_xpay_xf).  nt (update_rf's r, xpay_xf's x and p): non-temporal
+// stores, for an unfused iteration whose working set exceeds the Infinity
+// Cache (DevMatrix::nt): the lines go to HBM inside the vector kernel instead
+// of lingering dirty until the next SpMV's matrix stream evicts them (C3 CSR:
+// 192.9 -> 184.8 us per in-iteration SpMV, 3,355 -> 3,467 it/s; C4 1,252 ->
+// 1,217 us)
 template <typename T>
 hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *stt,
                           const double *rr_part, int nrr, double *hist, int grid,
-                          hipStream_t st);
+                          hipStream_t st, bool nt = false);
 template <typename T>
 hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w,
                              const CgState *stt, double *part, int grid, hipStream_t st);

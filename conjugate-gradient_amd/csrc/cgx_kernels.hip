@@ -2148,7 +2148,7 @@ __device__ __forceinline__ void sum_parts_sr(const double *pq, int na, const dou
 // The first grid-stride element's loads are issued before the partial sum,
 // so the HBM round trip overlaps the L2 round trip of the partials (same
 // elements, same order: bit-identical).
-template <typename T>
+template <typename T, bool NT>
 __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
                                                        const T *__restrict__ s,
                                                        CgState *__restrict__ st,
@@ -2220,7 +2220,8 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
       rv[j] = rv[j] - as;
       acc = acc + (double)rv[j] * (double)rv[j];
     }
-    reinterpret_cast<V *>(r)[i] = rv;
+    if constexpr (NT) __builtin_nontemporal_store(rv, reinterpret_cast<V *>(r) + i);
+    else reinterpret_cast<V *>(r)[i] = rv;
   };
   int i = gid;
   if (i < nv) {
@@ -2276,7 +2277,7 @@ __global__ __launch_bounds__(kFoldBS) void k_update_rf(int n, T *__restrict__ r,
 // roundings in order; a stop applies what is pending.  8 B per row less on
 // average, and the SpMV after an even iteration finds half the dirty lines.
 // pn == p: x every iteration, p in place.
-template <typename T>
+template <typename T, bool NT>
 __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, const T *p, T *pn,
                                                      const T *__restrict__ r,
                                                      CgState *__restrict__ st,
@@ -2342,7 +2343,8 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, c
         const T ap = alpha * pv[j];
         xv[j] = xv[j] + ap;
       }
-      reinterpret_cast<V *>(x)[i] = xv;
+      if constexpr (NT) __builtin_nontemporal_store(xv, reinterpret_cast<V *>(x) + i);
+      else reinterpret_cast<V *>(x)[i] = xv;
     }
     if (!stop) {
 #pragma unroll
@@ -2350,7 +2352,8 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, c
         const T bp = beta * pv[j];
         pv[j] = rv[j] + bp;
       }
-      reinterpret_cast<V *>(pn)[i] = pv;
+      if constexpr (NT) __builtin_nontemporal_store(pv, reinterpret_cast<V *>(pn) + i);
+      else reinterpret_cast<V *>(pn)[i] = pv;
     }
   };
   int i = gid;
@@ -3157,18 +3160,27 @@ hipError_t launch_pack_sr(int n_send, const int *idx, const T *rold, const T *po
 template <typename T>
 hipError_t launch_update_rf(int n, T *r, const T *s, CgState *stt, const double *ps_part,
                             int nps, double *rr_part, int grid, hipStream_t st,
-                            const FinArgs *fin, const double *sr, double *hist) {
+                            const FinArgs *fin, const double *sr, double *hist, bool nt) {
   const FinArgs f = fin ? *fin : FinArgs{};
-  hipLaunchKernelGGL((k_update_rf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt, ps_part,
-                     nps, rr_part, f, sr, hist);
+  if (nt)
+    hipLaunchKernelGGL((k_update_rf<T, true>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt,
+                       ps_part, nps, rr_part, f, sr, hist);
+  else
+    hipLaunchKernelGGL((k_update_rf<T, false>), dim3(grid), dim3(kFoldBS), 0, st, n, r, s, stt,
+                       ps_part, nps, rr_part, f, sr, hist);
   return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *stt,
-                          const double *rr_part, int nrr, double *hist, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((k_xpay_xf<T>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, pn, r, stt,
-                     rr_part, nrr, hist);
+                          const double *rr_part, int nrr, double *hist, int grid, hipStream_t st,
+                          bool nt) {
+  if (nt)
+    hipLaunchKernelGGL((k_xpay_xf<T, true>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, pn, r,
+                       stt, rr_part, nrr, hist);
+  else
+    hipLaunchKernelGGL((k_xpay_xf<T, false>), dim3(grid), dim3(kFoldBS), 0, st, n, x, p, pn, r,
+                       stt, rr_part, nrr, hist);
   return hipGetLastError();
 }
 
@@ -3292,9 +3304,9 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                                            T *, const CgState *, hipStream_t);                   \
   template hipError_t launch_update_rf<T>(int, T *, const T *, CgState *, const double *, int,   \
                                           double *, int, hipStream_t, const FinArgs *,           \
-                                          const double *, double *);                             \
+                                          const double *, double *, bool);                       \
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \
-                                        const double *, int, double *, int, hipStream_t);        \
+                                        const double *, int, double *, int, hipStream_t, bool);  \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *, const T *, const CgState *,  \
                                            double *, int, hipStream_t);                          \
   template hipError_t launch_dot_seq<T>(int, const T *, const T *, double *, const int *,        \

@@ -405,8 +405,10 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
       CGX_HIP(launch_xpay<T>(n, p, r, s->d_st, s->vec_grid, st));             // cg.c:131-132
     } else {
       const int gf = s->vec_grid / 4;  // 1024-thread workgroups, 4 partials each
-      CGX_HIP(launch_update_rf<T>(n, r, sv, s->d_st, s->d_pa, np, s->d_pb, gf, st));
-      CGX_HIP(launch_xpay_xf<T>(n, x, p, pn, r, s->d_st, s->d_pb, 4 * gf, s->d_hist, gf, st));
+      CGX_HIP(launch_update_rf<T>(n, r, sv, s->d_st, s->d_pa, np, s->d_pb, gf, st, nullptr,
+                                  nullptr, nullptr, s->A.nt));
+      CGX_HIP(launch_xpay_xf<T>(n, x, p, pn, r, s->d_st, s->d_pb, 4 * gf, s->d_hist, gf, st,
+                                s->A.nt));
       s->pbuf ^= 1;
     }
   } else {
