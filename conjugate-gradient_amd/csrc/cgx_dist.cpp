@@ -119,7 +119,8 @@ struct cgx_dist {
          *d_w = nullptr;
   double *d_p2 = nullptr;  // fused step: the second p buffer (with ghost tail)
   // fused CG1 step: the second r, s, w buffers (with ghost tails)
-  double *d_r2 = nullptr, *d_s2 = nullptr, *d_w2 = nullptr;
+  double *d_r2 = nullptr, *d_s2 = nullptr, *d_w2 = nullptr;  // lazily: ensure_rsw2
+  size_t ng_alloc = 0;  // entries of a ghosted vector from element 0 (upload_local)
   int pbuf = 0;            // fused step: which buffer holds p_old (0: d_p) / r, s, w_old
   bool in_init = false;    // the CG1 prologue's phases (unfused SpMV w = A r)
   int fuse = CGX_FUSE_AUTO;  // cgx_dist_set_fused
@@ -470,12 +471,13 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
     *p = r ? nullptr : (double *)raw + d->vfront;
     return r;
   };
-  // r, p, s, w and their second buffers carry the ghost rows (s, w: the fused
-  // CG1 step's window / far-slot loads reach them; only zeros are read there)
+  // r, p, s, w carry the ghost rows (s, w: the fused CG1 step's window /
+  // far-slot loads reach them; only zeros are read there); the second r, s, w
+  // buffers only the recurrences that alternate them allocate (ensure_rsw2)
+  d->ng_alloc = ng;
   if ((rc = dev_alloc(&d->d_b, nv * 8, cb)) || (rc = dev_alloc(&d->d_x, nv * 8, cb)) ||
       (rc = ghosted(&d->d_r)) || (rc = ghosted(&d->d_p)) || (rc = ghosted(&d->d_s)) ||
-      (rc = ghosted(&d->d_w)) || (rc = ghosted(&d->d_p2)) || (rc = ghosted(&d->d_r2)) ||
-      (rc = ghosted(&d->d_s2)) || (rc = ghosted(&d->d_w2)) ||
+      (rc = ghosted(&d->d_w)) || (rc = ghosted(&d->d_p2)) ||
       (rc = dev_alloc(&d->d_pa, npa * 8, cb)) ||
       (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb)) ||
       (rc = dev_alloc(&d->d_pss, ((size_t)d->g_int + d->g_bnd + 8) * 16, cb))) {
@@ -493,7 +495,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
       return rc;
     }
   }
-  for (double *v : {d->d_r, d->d_p, d->d_p2, d->d_s, d->d_w, d->d_r2, d->d_s2, d->d_w2})
+  for (double *v : {d->d_r, d->d_p, d->d_p2, d->d_s, d->d_w})
     CGX_HIP(hipMemsetAsync(v - d->vfront, 0, (d->vfront + ng) * 8, d->st));
   CGX_HIP(hipMemsetAsync(d->d_x, 0, nv * 8, d->st));
   CGX_HIP(hipStreamSynchronize(d->st));
@@ -649,8 +651,31 @@ int ensure_fused_known(Group *g) {
 }
 
 int ensure_connected_fz(Group *g);
+bool sr1(const cgx_dist *d);
+bool fz1(const cgx_dist *d);
 
-// connected, the fused step decided, and the recurrence runnable on it
+// The second r, s, w buffers (ghosted, zeroed), allocated the first time a
+// recurrence that alternates them runs -- the one-launch SR step, the fused
+// CG1 step -- not for HS (3 n_loc doubles, 1.5 GB at C4 on one rank: ADVICE
+// r03).  Before any graph capture (their pointers are captured).
+int ensure_rsw2(Group *g) {
+  for (cgx_dist *d : g->parts) {
+    if (d->d_r2 || !(sr1(d) || fz1(d))) continue;
+    CGX_HIP(hipSetDevice(d->device));
+    for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2}) {
+      void *raw = nullptr;
+      int rc = dev_alloc(&raw, (d->vfront + d->ng_alloc) * 8, &d->vec_bytes);
+      if (rc) return rc;
+      *p = (double *)raw + d->vfront;
+      CGX_HIP(hipMemsetAsync(raw, 0, (d->vfront + d->ng_alloc) * 8, d->st));
+    }
+    CGX_HIP(hipStreamSynchronize(d->st));
+  }
+  return 0;
+}
+
+// connected, the fused step decided, the recurrence runnable on it and its
+// buffers allocated
 int ensure_connected(Group *g) {
   int rc = ensure_connected_fz(g);
   if (rc) return rc;
@@ -658,7 +683,7 @@ int ensure_connected(Group *g) {
     set_error("dist: CGX_ALG_SR needs the fused DIA step on every partition (fuse_status)");
     return CGX_EINVAL;
   }
-  return 0;
+  return ensure_rsw2(g);
 }
 
 int ensure_connected_fz(Group *g) {
