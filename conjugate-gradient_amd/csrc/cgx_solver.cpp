@@ -956,6 +956,14 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
                                                                    : CGX_FUSE_STATUS_RUNS;
   info->breakdown = s->h_st ? s->h_st->brk : 0;
   info->fuse_march = s->have_matrix ? march_len(s) : 0;
+  if (info->fuse_march > 0 && s->alg == CGX_ALG_SR && s->march <= 0) {
+    // the balanced segments k_sr1_dia_m runs (enqueue_iter): the longest
+    const SpmvArgs<double> a =
+        s->A.args<double>(nullptr, nullptr, nullptr, nullptr, s->A.all_items());
+    const int steps = (a.mslices + a.mq - 1) / a.mq;
+    const int ns = sr1_pick_nseg(a, s->cus);
+    info->fuse_march = (steps + ns - 1) / std::max(1, ns);
+  }
   return 0;
 }
 

@@ -180,9 +180,9 @@ typedef struct {
                            NaN (cg.c:113, 129) -- or 0.  Diagnostic only: the
                            iteration itself keeps the reference's IEEE
                            semantics (failure detection)        */
-  int fuse_march;       /* > 0: the fused HS step runs as a plane march
-                           (cgx_solver_set_march), this many steps per
-                           workgroup; 0: it does not                         */
+  int fuse_march;       /* > 0: the fused HS / SR step runs as a plane
+                           march (cgx_solver_set_march), this many steps per
+                           workgroup (the longest segment); 0: it does not  */
 } cgx_info;
 
 /* cgx_info.fuse_status / cgx_dist_stats.fuse_status */
@@ -228,9 +228,11 @@ int  cgx_solver_set_fused(cgx_solver *s, int mode);
  * F apart, keeping p of three consecutive slices (and their halos) in LDS, so
  * the +-F neighbours are read from LDS instead of recomputed from r / p
  * gathers.  Same values, same order: x and the r.r history are bit-identical
- * to the unfused path.  steps: -1 auto (default; about 2,048 workgroups per
- * launch), 0 off (the per-slice fused kernel), > 0 slices of a chain per
- * workgroup.  cgx_info.fuse_march reports what runs. */
+ * to the unfused path.  steps: -1 auto (default; HS: about 2,048 workgroups
+ * per launch; CGX_ALG_SR's k_sr1_dia_m: each chain cut into the balanced
+ * segment count that fills the device's resident workgroup slots), 0 off
+ * (the per-slice fused kernel), > 0 slices of a chain per workgroup.
+ * cgx_info.fuse_march reports what runs. */
 int  cgx_solver_set_march(cgx_solver *s, int steps);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);
@@ -392,9 +394,10 @@ typedef struct {
   int breakdown;                         /* as cgx_info.breakdown         */
   int march;                             /* > 0: CGX_ALG_SR runs as ONE
                                             k_sr1_dia_m step per iteration
-                                            (interior + boundary launches),
-                                            this many interior steps per
-                                            workgroup; 0: it does not     */
+                                            (+ k_sr1_edge after the halo),
+                                            this many steps per workgroup
+                                            (the longest segment); 0: it
+                                            does not                      */
   int inplace;                           /* 1: this rank's rows have the
                                             in-place ghost numbering the
                                             one-launch SR step needs      */
@@ -441,11 +444,12 @@ int  cgx_dist_set_fused(cgx_dist *d, int mode);
  * march) where every rank's ghost columns are the rows next to its own
  * (a banded matrix cut into row slabs, e.g. C4's planes): the ranks number
  * their rows in place (columns = global - row_begin, the neighbours' planes
- * below 0 and from n_loc), march the interior steps while the halo of
- * p_k = (r - alpha s) + beta p is in flight and the boundary steps after it.
- * steps: -1 auto (default), 0 off (the two-launch fused SR step), > 0
- * interior steps per workgroup.  cgx_dist_stats.march reports it.  Call on
- * every rank (on a local group, part 0 sets the group). */
+ * below 0 and from n_loc), march every step while the halo of
+ * p_k = (r - alpha s) + beta p is in flight, and recompute s of the edge rows
+ * (those reaching a ghost column) after it.  steps: -1 auto (default: the
+ * balanced segment count for the device), 0 off (the two-launch fused SR
+ * step), > 0 steps per workgroup segment.  cgx_dist_stats.march reports it.
+ * Call on every rank (on a local group, part 0 sets the group). */
 int  cgx_dist_set_march(cgx_dist *d, int steps);
 /* hipGraph replay of the iteration batches (RCCL calls included); on by
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
@@ -455,7 +459,8 @@ int  cgx_dist_get_x(cgx_dist *d, double *x_local);
 int  cgx_dist_get_history(cgx_dist *d, double *rr, int cap);
 int  cgx_dist_bench_prepare(cgx_dist *d, int warmup);
 /* flags: CGX_BENCH_SPMV_EVENTS brackets the interior and boundary SpMV
- * launches of partition 0 with events; *spmv_ms = their average sum. */
+ * launches of partition 0 (one-launch SR: the march and the edge launch)
+ * with events; *spmv_ms = their average sum. */
 int  cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms,
                         double *spmv_ms);
 int  cgx_dist_info(cgx_dist *d, cgx_dist_stats *s);
