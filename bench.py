@@ -766,7 +766,11 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
             d.set_alg(alg)
             d.set_fused(fused)
             d.set_march(march)
-            its = d.run(5000, tol)
+            try:  # a refusal is collective (every rank alike): that recurrence fails the gate
+                its = d.run(5000, tol)
+            except cgx.CgxError as e:
+                res[name] = (None, str(e), None, False)
+                continue
             i = d.info()
             ok_shape = i["fused"] == want and (name != "sr" or i["march"] > 0)
             res[name] = (its, gather_x(d.x(), n, world, rank), i["graph"], ok_shape)
@@ -788,6 +792,10 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
                single_gpu_iters=its1)
     ok = True
     for name, (its, x, graph, fused_ok) in res.items():
+        if its is None:
+            ok = False
+            out[name] = dict(error=x, ok=False)
+            continue
         rel = float(np.linalg.norm(x - x1) / np.linalg.norm(x1))
         tr = float(np.linalg.norm(b_full - A @ x) / np.linalg.norm(b_full))
         good = rel <= 1e-9 and abs(its - its1) <= 1 and tr <= 10 * tol and fused_ok
@@ -822,10 +830,18 @@ def run_dist(args, wl_name, world, rank, local_rank):
     dist.broadcast_object_list(uids, src=0)
     uid_parity, uid = uids[0]
 
-    # ---- parity gate (RCCL path, both recurrences) before anything is timed
+    # ---- parity gate (RCCL path, every recurrence) before anything is timed;
+    # a recurrence that fails it is not timed, the others still are
     parity = parity_gate(world, rank, local_rank, uid_parity)
-    ok = [parity["ok"] if rank == 0 else None]
-    dist.broadcast_object_list(ok, src=0)
+    gate = [{k: v["ok"] for k, v in parity.items() if isinstance(v, dict)} if rank == 0 else None]
+    dist.broadcast_object_list(gate, src=0)
+    gate = gate[0]
+    # trial name -> the gate entries it needs ("hs": unfused and fused, AUTO
+    # takes either)
+    needs = {"hs": ("hs", "hs_fused"), "sr": ("sr",), "sr_two_launch": ("sr_two_launch",),
+             "cg1": ("cg1",)}
+    passed = [a for a in needs if all(gate.get(g, False) for g in needs[a])]
+    ok = [bool(passed)]
 
     sysm = make_system(wl, rank, world)
     t_up = time.perf_counter()
@@ -846,6 +862,9 @@ def run_dist(args, wl_name, world, rank, local_rank):
             "sr_two_launch": (cgx.CGX_ALG_SR, 0), "cg1": (cgx.CGX_ALG_CG1, -1)}
     refused = {}
     for name in ([args.alg] if args.alg else ["hs", "sr", "sr_two_launch", "cg1"]):
+        if name not in passed:
+            refused[name] = "failed the parity gate"
+            continue
         s.set_alg(algs[name][0])
         s.set_march(algs[name][1])
         try:
@@ -855,7 +874,9 @@ def run_dist(args, wl_name, world, rank, local_rank):
             continue
         dist.barrier()
         trial[name] = round(allmax(s.bench_run(20)[0] / 20), 4)
-    alg = min(trial, key=trial.get)
+    if not trial:
+        ok = [False]
+    alg = min(trial, key=trial.get) if trial else (args.alg or "hs")
     s.set_alg(algs[alg][0])
     s.set_march(algs[alg][1])
     info = s.info()
