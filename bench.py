@@ -805,6 +805,15 @@ def parity_gate(world, rank, local_rank, uid, tol=1e-10):
     return out
 
 
+def gate_passed(gate):
+    """The trial's recurrences whose parity-gate entries all passed (gate:
+    entry name -> ok; "hs" needs the unfused and the fused HS runs, AUTO
+    takes either at the timed size)."""
+    needs = {"hs": ("hs", "hs_fused"), "sr": ("sr",), "sr_two_launch": ("sr_two_launch",),
+             "cg1": ("cg1",)}
+    return [a for a in needs if all(gate.get(g, False) for g in needs[a])]
+
+
 def run_dist(args, wl_name, world, rank, local_rank):
     import numpy as np
     import torch
@@ -835,12 +844,7 @@ def run_dist(args, wl_name, world, rank, local_rank):
     parity = parity_gate(world, rank, local_rank, uid_parity)
     gate = [{k: v["ok"] for k, v in parity.items() if isinstance(v, dict)} if rank == 0 else None]
     dist.broadcast_object_list(gate, src=0)
-    gate = gate[0]
-    # trial name -> the gate entries it needs ("hs": unfused and fused, AUTO
-    # takes either)
-    needs = {"hs": ("hs", "hs_fused"), "sr": ("sr",), "sr_two_launch": ("sr_two_launch",),
-             "cg1": ("cg1",)}
-    passed = [a for a in needs if all(gate.get(g, False) for g in needs[a])]
+    passed = gate_passed(gate[0])
     ok = [bool(passed)]
 
     sysm = make_system(wl, rank, world)

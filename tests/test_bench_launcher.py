@@ -105,3 +105,14 @@ def test_committed_pmc_summaries_name_their_kernel():
         key = f.stem.split("_", 2)[2]
         if key in bench.KERNEL_PREFIX:
             assert json.loads(f.read_text())["kernel"].startswith(bench.KERNEL_PREFIX[key]), f.name
+
+
+def test_gate_decides_per_recurrence():
+    """bench.py N > 1: a recurrence that fails the parity gate (or is refused
+    there) is left out of the timed trial; the others still run."""
+    import bench
+    every = dict(hs=True, hs_fused=True, sr=True, sr_two_launch=True, cg1=True)
+    assert bench.gate_passed(every) == ["hs", "sr", "sr_two_launch", "cg1"]
+    assert bench.gate_passed(dict(every, sr=False)) == ["hs", "sr_two_launch", "cg1"]
+    assert bench.gate_passed(dict(every, hs_fused=False)) == ["sr", "sr_two_launch", "cg1"]
+    assert bench.gate_passed({}) == []
