@@ -225,8 +225,9 @@ bool part_marchable(const cgx_dist *d) {
 
 // the all-reduced sums the one-launch SR step's kernels apply themselves
 // (FIN_SR1 folded into the next iteration's launches, FIN_SUM3_SR1 applies
-// them to the state); nullptr without a transport (FIN_SR1 on the partials)
-// or with the fold switched off (CGX_EXP & 1, the A/B variant)
+// them to the state: no scalar launch between the all-reduce and the next
+// SpMV, 3-4 us per iteration on the C4/8 slab); nullptr without a transport
+// (FIN_SR1 on the partials)
 const double *sr1_g(const cgx_dist *d);
 
 bool has_peers(const cgx_dist *d);
@@ -807,7 +808,7 @@ int allreduce(cgx_dist *d, int i, int count);
 // The one-launch SR step (k_sr1_dia_m on the in-place numbering): every step
 // while the halo of p_k is in flight, then (a rank with neighbours) the edge
 // rows' s and (p.s, s.s) after it (k_sr1_edge); then the local (p.s, s.s,
-// r.r) (FIN_SUM3 / FIN_SUM3_SR1), or with no transport the scalar step
+// r.r) (FIN_SUM3_SR1), or with no transport the scalar step
 // itself (FIN_SR1, as the single-GPU solver).
 int phase_sr1(cgx_dist *d) {
   CGX_HIP(hipSetDevice(d->device));
@@ -850,35 +851,22 @@ int phase_sr1(cgx_dist *d) {
   if (d->local)  // as phase_spmv: every part's last group sum has read d_sums
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
-  if (sr1_g(d))  // the previous all-reduce applied to the state, then the local sums
-    CGX_HIP(launch_finalize(FIN_SUM3_SR1, d->d_pq, np, d->d_gsums, 3, d->d_st, d->d_hist,
-                            d->d_sums, d->st, d->d_pc, np));
-  else
-    CGX_HIP(launch_finalize(FIN_SUM3, d->d_pq, np, nullptr, 0, d->d_st, d->d_hist, d->d_sums,
-                            d->st, d->d_pc, np));
+  // the previous all-reduce applied to the state, then the local sums
+  CGX_HIP(launch_finalize(FIN_SUM3_SR1, d->d_pq, np, d->d_gsums, 3, d->d_st, d->d_hist,
+                          d->d_sums, d->st, d->d_pc, np));
   CGX_HIP(hipEventRecord(d->ev_sums, d->st));
   return 0;
 }
 
-const double *sr1_g(const cgx_dist *d) {
-#if defined(CGX_EXP) && (CGX_EXP & 1)
-  return nullptr;
-#else
-  return solo(d) ? nullptr : d->d_gsums;
-#endif
-}
+const double *sr1_g(const cgx_dist *d) { return solo(d) ? nullptr : d->d_gsums; }
 
-// the iteration's one all-reduce of (p.s, s.s, r.r); without the fold, then
-// FIN_SR1 on it (the stop test of the previous iteration, alpha, the
-// estimate, beta) -- with it the next iteration's kernels apply it; the r,
-// p, s buffers swap roles
+// the iteration's one all-reduce of (p.s, s.s, r.r) -- the next iteration's
+// kernels apply it (the stop test of the previous iteration, alpha, the
+// estimate, beta: sr1_g); the r, p, s buffers swap roles
 int sr1_reduce(cgx_dist *d) {
   if (!solo(d)) {
     int rc = allreduce(d, 0, 3);
     if (rc) return rc;
-    if (!sr1_g(d))
-      CGX_HIP(launch_finalize(FIN_SR1, d->d_gsums, 1, nullptr, 0, d->d_st, d->d_hist, nullptr,
-                              d->st, d->d_gsums + 2, 1));
   }
   d->pbuf ^= 1;
   return 0;
