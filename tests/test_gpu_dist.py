@@ -508,8 +508,9 @@ SR1_CASES = [((32, 48, 20), 1), ((32, 48, 20), 2), ((32, 48, 20), 3), ((32, 48, 
 def test_sr_one_launch_partitions(shape, P):
     """CGX_ALG_SR on partitioned ranks as ONE k_sr1_dia_m step
     per iteration -- the ranks' rows in the in-place numbering (ghost planes
-    below 0 and from n_loc), the interior steps launched while the halo of p_k
-    is in flight, the boundary steps after it -- on plane-aligned and
+    below 0 and from n_loc), every step marched while the halo of p_k is in
+    flight, s of the edge rows recomputed after it (k_sr1_edge) -- on
+    plane-aligned and
     plane-cutting slabs and thin slabs (P = 8 at 32 x 48 x 20: 2.5 planes per
     part; P = 16 at 64 x 64 x 12: 0.75 of a plane, whose ghost rows are not
     contiguous, so it runs the two-launch step -- to the same oracle bars).
@@ -518,7 +519,7 @@ def test_sr_one_launch_partitions(shape, P):
     where the slabs allow that step (plane-aligned); against oracle_solve_sr
     within 1e-10 at fixed max_iter and within 1e-9 with the stop iteration
     within 1 (and of the HS oracle) at a tolerance, true residual below it;
-    interior segment lengths 1, 3 and auto within 1e-12 of each other."""
+    segment lengths 1, 3 and auto (balanced) within 1e-12 of each other."""
     rp, col, val = cgx.laplacian3d(*shape)
     b = np.random.default_rng(27).standard_normal(len(rp) - 1)
     runs = [(0, 0.0), (1, 0.0), (2, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]
