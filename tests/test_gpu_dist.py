@@ -501,7 +501,7 @@ def test_sr_partitions(shape, P):
 
 SR1_CASES = [((32, 48, 20), 1), ((32, 48, 20), 2), ((32, 48, 20), 3), ((32, 48, 20), 8),
              ((64, 64, 12), 2), ((64, 64, 12), 5), ((64, 64, 12), 8), ((64, 64, 12), 16),
-             ((300, 7, 20), 4)]
+             ((300, 7, 20), 4), ((41, 25, 20), 3), ((41, 25, 20), 4)]
 
 
 @pytest.mark.parametrize("shape,P", SR1_CASES)
@@ -511,7 +511,9 @@ def test_sr_one_launch_partitions(shape, P):
     below 0 and from n_loc), every step marched while the halo of p_k is in
     flight, s of the edge rows recomputed after it (k_sr1_edge) -- on
     plane-aligned and
-    plane-cutting slabs and thin slabs (P = 8 at 32 x 48 x 20: 2.5 planes per
+    plane-cutting slabs, odd planes and odd slabs (41 x 25: F = 1,025, 5,125
+    rows per part at P = 4, both edge bounds rounded to row pairs), and thin
+    slabs (P = 8 at 32 x 48 x 20: 2.5 planes per
     part; P = 16 at 64 x 64 x 12: 0.75 of a plane, whose ghost rows are not
     contiguous, so it runs the two-launch step -- to the same oracle bars).
     Against the two-launch fused SR group (set_march(0)) within 1e-10 at
