@@ -1512,15 +1512,16 @@ __global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
   const bool two = live && r + 1 < a.n;
   unsigned c0, c1;
   ld_codes(a.dcode, a.cb, rl, c0, c1);
-  // every load out before the first use, unconditionally (a missing entry
-  // reloads p[r]): a conditional load makes the compiler wait on it
+  // every load out before the first use, unconditionally and independent of
+  // the codes (clamped into the ghosted vector; a missing entry's value is
+  // never used): one memory round trip, not a code load then the gathers
   T v0[kDiaMax], v1[kDiaMax];
 #pragma unroll
   for (int kk = 0; kk < kDiaMax; ++kk) {
     if (kk < a.ndiag) {
       const int d = a.doff[kk];
-      v0[kk] = p[fld(a, c0, kk) != a.cmask[kk] ? rl + d : rl];
-      v1[kk] = p[two && fld(a, c1, kk) != a.cmask[kk] ? rl + 1 + d : rl];
+      v0[kk] = p[min(max(rl + d, a.xlo), a.ncols - 1)];
+      v1[kk] = p[min(max(rl + 1 + d, a.xlo), a.ncols - 1)];
     }
   }
   const T p0 = p[rl], p1 = p[two ? rl + 1 : rl];
