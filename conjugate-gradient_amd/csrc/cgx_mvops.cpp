@@ -108,8 +108,8 @@ int upload_matrix(cgx_solver *s, const struct __mv_sparse *A, unsigned long long
 // host threads beside it (the check costs the caller only what it does not
 // overlap: ~0 for a C3 solve, whose hash takes ~5-8 ms); a hash that differs
 // (A edited in place since the upload) re-uploads A and runs op() again, so
-// the result is always that of the A passed in.  Otherwise A is hashed and
-// uploaded first.
+// the result is always that of the A passed in.  Otherwise A is uploaded and
+// op() runs while A is hashed beside it.
 struct MatTiming {
   double hash_ms = 0, upload_ms = 0, op_ms = 0;  // hash: time spent waiting for it
   bool uploaded = false;
@@ -136,11 +136,16 @@ int with_matrix(cgx_solver *s, const struct __mv_sparse *A, F &&op, MatTiming *t
   };
   int rc = 0;
   if (!same_key) {
-    const double th = now_ms();
-    const unsigned long long h = matrix_hash(A);
-    t.hash_ms = now_ms() - th;
-    rc = upload(h);
+    // the hash only keys the next call: it runs on host threads beside the
+    // device work (A cannot change while this call holds the caller)
+    rc = upload(0);
+    unsigned long long h = 0;
+    std::thread th([&] { h = matrix_hash(A); });
     if (rc == 0) rc = run();
+    const double tw = now_ms();
+    th.join();
+    t.hash_ms = now_ms() - tw;
+    if (rc == 0 && g_res.valid) g_res.hash = h;
   } else {
     unsigned long long h = 0;
     std::thread th([&] { h = matrix_hash(A); });
