@@ -190,8 +190,8 @@ KERNELS = {
 
 def kernel_key(info):
     if info["layout_name"] == "dia" and info.get("fused"):
-        if info.get("alg") == 2:
-            return "sr1"
+        if info.get("alg") == 2 and (info.get("fuse_march", 0) > 0 or info.get("march", 0) > 0):
+            return "sr1"  # single GPU (cgx_info.fuse_march) or a rank (cgx_dist_stats.march)
         return "dia_march" if info.get("fuse_march") else "dia_fused"
     return info["layout_name"]
 
@@ -210,6 +210,16 @@ def layout_desc(info):
     if name == "panel":
         return f"CSR in {info['n_panels']} column panels"
     return "CSR (int32 columns, fp64 values): the reference's struct"
+
+
+def value_basis(info):
+    """What `value` is an iteration rate OF: the layout the
+    timed solve streams -- so no reader compares a DIA-VI rate with a CSR one."""
+    if info["layout_name"] == "dia":
+        return (f"DIA-VI compressed stencil ({info['code_bytes_per_row']} B/row of matrix codes, "
+                "no column or value stream; exact, bit-identical SpMV) -- NOT a CSR rate: the "
+                "plain-CSR solve of the same system is csr_plain.value")
+    return f"{layout_desc(info)}: the matrix bytes SURVEY 8d's CSR basis counts or fewer"
 
 
 def cpu_model():
@@ -384,7 +394,7 @@ def general_coefficients(steps, warmup, device=0):
         out[name] = dict(layout=layout_desc(i), layout_name=i["layout_name"], value=leg["value"],
                          unit="it/s", spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
                          own_bytes_gbs=own_gbs, own_bytes_frac=own_frac,
-                         csr_basis_gbs=csr_gbs, csr_basis_frac=csr_frac,
+                         csr_basis_equiv_rate=csr_gbs, csr_basis_frac=csr_frac,
                          kernel=kernel_name(i))
     return out
 
@@ -543,10 +553,46 @@ def layout_roofline(info, spmv_ms, wl_name):
                 spmv_us=round(spmv_ms * 1e3, 2), achieved=gbs, frac=frac,
                 algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
                 **traffic_fields(wl_name, kernel_key(info), info["spmv_iter_bytes"]),
-                csr_equivalent_gbs=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
+                csr_basis_equiv_rate=round(info["spmv_bytes"] / (spmv_ms * 1e-3) / 1e9, 1),
                 note="the SpMV launch of the headline solve, priced on the bytes it moves (its "
                      "layout; with the fused HS step also r, p_old, x, p_new; with the one-launch "
-                     "SR step r, s, p read and written, x every other launch)")
+                     "SR step r, s, p read and written, x every other launch); "
+                     "csr_basis_equiv_rate = SURVEY 8d's CSR B_spmv / this launch's time, a "
+                     "CSR-equivalent rate in GB/s -- NOT HBM bandwidth (this layout never "
+                     "streams those bytes)")
+
+
+def stream_ceilings(n=64 * 2**20, reps=10):
+    """The on-box stream ceilings (cgx_stream_bench, fp64 arrays of n = 64 Mi
+    elements, 512 MiB each -- far beyond the Infinity Cache): the naive
+    triad and read stream of rounds 1-4, and tuned
+    read/write mixes -- copy (1 read : 1 write), triad (2 : 1) and 3 : 3 (the
+    one-launch SR step's r, p, s), each with plain and non-temporal stores,
+    4 x 16 B per lane in flight, grid = resident workgroup slots."""
+    import cgx
+    return {k: round(cgx.stream_bench(0, n, reps, v), 1) for k, v in cgx.STREAM_KINDS.items()}
+
+
+def c2_leg(steps, warmup):
+    """C2 (the 5-point 2-D Laplacian 1000^2, 1 M rows) in the
+    default line -- its whole working set (~150 MB as CSR, ~40 MB as DIA-VI
+    + vectors) stays in the 256 MiB Infinity Cache, so its SpMV rates are
+    cache rates, not HBM bandwidth: reported as times and as fractions of the
+    HBM peak only for comparison, labelled resident."""
+    wl = WORKLOADS["c2"]
+    sysm = make_system(wl)
+    out = dict(workload=wl["desc"], residency="Infinity-Cache resident (not an HBM figure)")
+    for name, layout in (("auto", "auto"), ("csr", "csr")):
+        leg = solver_leg(sysm, steps, warmup, layout, b2b=True)
+        i = leg["info"]
+        _, own_frac = spmv_roofline(i["spmv_iter_bytes"], leg["spmv_us"] * 1e-3)
+        _, csr_frac = spmv_roofline(i["spmv_bytes"], leg["spmv_us"] * 1e-3)
+        out[name] = dict(value=leg["value"], unit="it/s", layout=layout_desc(i),
+                         kernel=kernel_name(i), spmv_us=leg["spmv_us"],
+                         b2b_spmv_us=leg["b2b_spmv_us"],
+                         own_bytes=int(i["spmv_iter_bytes"]), own_bytes_frac_resident=own_frac,
+                         csr_basis_bytes=int(i["spmv_bytes"]), csr_basis_frac_resident=csr_frac)
+    return out
 
 
 def matrix_free(wl, b, steps, warmup):
@@ -585,7 +631,9 @@ def c3_legs(steps, warmup):
                               b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"]))
     out["general_coefficients"] = general_coefficients(steps, warmup)
     out["solve_e2e"] = solve_e2e(sysm)
-    out["solve_e2e_sr"] = solve_e2e(sysm, alg="sr", legs=("warm",))
+    # cold first (the first SR call switches the recurrence and
+    # captures its graphs), then the warm call on the resident matrix
+    out["solve_e2e_sr"] = solve_e2e(sysm, alg="sr", legs=("cold", "warm"))
     return out
 
 
@@ -605,7 +653,7 @@ def c5_leg(steps, warmup):
                 spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
                 own_bytes=int(i["spmv_iter_bytes"]), own_bytes_gbs=own_gbs,
                 own_bytes_frac=own_frac, csr_basis_bytes=int(i["spmv_bytes"]),
-                csr_basis_gbs=csr_gbs, csr_basis_frac=csr_frac,
+                csr_basis_equiv_rate=csr_gbs, csr_basis_frac=csr_frac,
                 **traffic_fields("c5", kernel_key(i), i["spmv_iter_bytes"]),
                 host_gen_s=round(gen_s, 1), setup_ms=leg["setup_ms"])
 
@@ -664,10 +712,13 @@ def run_single(args, wl_name):
                                                   "traffic_source", "traffic_ratio")},
                            timing="HIP events (hipExtLaunchKernel) around every launch of "
                                   f"{args.steps} eager iterations on the solver's stream")
-    triad = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_TRIAD)
-    rd = cgx.stream_bench(0, 64 * 2**20, 10, cgx.CGX_STREAM_READ)
-    roofline["stream_triad_gbs"] = round(triad, 1)
-    roofline["stream_read_gbs"] = round(rd, 1)
+    ceil = stream_ceilings()
+    roofline["stream_triad_gbs"] = ceil.pop("triad")
+    roofline["stream_read_gbs"] = ceil.pop("read")
+    roofline["stream_tuned_gbs"] = ceil
+    mix = max(ceil["copy"], ceil["copy_nt"], ceil["mix33"], ceil["mix33_nt"])
+    headline_kernel["rw_mix_ceiling_gbs"] = mix
+    headline_kernel["frac_of_rw_mix_ceiling"] = round(headline_kernel["achieved"] / mix, 4)
 
     extra = {}
     if "hs" in legs:
@@ -688,6 +739,7 @@ def run_single(args, wl_name):
         if wl_name == "c4":
             extra["c3"] = c3_legs(args.steps, args.warmup)
             extra["c5"] = c5_leg(args.steps, args.warmup)
+            extra["c2"] = c2_leg(args.steps, args.warmup)
         if wl_name == "c3":
             extra["general_coefficients"] = general_coefficients(args.steps, args.warmup)
             extra["c4_1gpu"] = c4_one_gpu(min(args.steps, 50), args.warmup)
@@ -709,7 +761,7 @@ def run_single(args, wl_name):
         config=dict(workload=wl["desc"], n=sysm["n_global"], nnz=int(len(sysm["col"])),
                     alg=ALG_DESC[alg], alg_trial=trial, graph=True,
                     parallelism="single GPU", layout=layout_desc(info),
-                    layout_name=info["layout_name"],
+                    layout_name=info["layout_name"], value_basis=value_basis(info),
                     scaling_curve="the same workload at every N (N > 1: row-partitioned "
                                   "over RCCL), so value(N) / value(1) is the speedup"),
         device_ms_per_step=round(h["dev_ms"] / args.steps, 4),
@@ -814,6 +866,44 @@ def gate_passed(gate):
     return [a for a in needs if all(gate.get(g, False) for g in needs[a])]
 
 
+def dist_line(args, wl, world, m):
+    """The N > 1 JSON line from the measured pieces m (run_dist): the
+    contract's fields, the trial, the roofline of the rank kernel (with its
+    PMC traffic), the per-phase breakdown, the CPU baseline and the parity
+    gate (parity_ok / gate_failed at the top level)."""
+    info, value, mps, dev, parity = m["info"], m["value"], m["ms_per_step"], m["dev"], m["parity"]
+    return dict(
+        metric=METRIC, value=None if value is None else round(value, 2), unit="it/s",
+        n_gpus=world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=None if mps is None else round(mps, 4),
+        higher_is_better=True, scaling="strong", vs_baseline=None, dtype=wl["dtype"],
+        data="synthetic",
+        config=dict(workload=wl["desc"], n=m["n_global"], rows_per_rank=info["n_loc"],
+                    nnz_rank0=info["nnz"], alg=m["alg"], march=info["march"],
+                    alg_trial_ms_per_iter=m["trial"],
+                    alg_refused=m["refused"] or None, fuse_status=info["fuse_status"],
+                    graph=info["graph"], fused=info["fused"],
+                    parallelism=f"row-partition x{world} (RCCL)",
+                    scaling_curve="the same workload at every N (N = 1: the "
+                                  "single-GPU solver), so value(N) / value(1) is the "
+                                  "speedup",
+                    layout=info["layout_name"], halo_bytes_per_iter_max_rank=m["halo"]),
+        device_ms_per_step=None if dev is None else round(dev, 4),
+        upload_ms=round(m["upload_ms"], 1), iter_bytes_rank0=int(info["iter_bytes"]),
+        roofline=m["roofline"], phases=m["phases"], cpu_baseline=m["cpu"], parity=parity,
+        parity_ok=bool(parity.get("ok")),
+        gate_failed=[k for k, v in parity.items() if isinstance(v, dict) and not v.get("ok")])
+
+
+def dist_traffic_key(alg, info):
+    """KERNEL_PREFIX key of the rank's headline launch whose PMC summary
+    prices `traffic` (profiles/pmc_c4n<N>_<key>.json: the slab kernel
+    profiled on a 1-rank communicator, tools/dist_probe.py), or None."""
+    if alg == "sr" and info.get("march", 0) > 0:
+        return "sr1"
+    return None
+
+
 def run_dist(args, wl_name, world, rank, local_rank):
     import numpy as np
     import torch
@@ -846,6 +936,18 @@ def run_dist(args, wl_name, world, rank, local_rank):
     dist.broadcast_object_list(gate, src=0)
     passed = gate_passed(gate[0])
     ok = [bool(passed)]
+
+    # ---- CPU baseline: the N = 1 line's one-core oracle
+    # sample of the same whole system, on rank 0, before anything is timed
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        full = make_system(wl)
+        cpu = cpu_baseline(full, args.cpu_seconds)
+        cpu["cpu_model"] = cpu_model()
+        cpu["nproc"] = os.cpu_count()
+        cpu["note"] = "rank 0, before the timed region, while the other ranks wait at a barrier"
+        del full
+    dist.barrier()
 
     sysm = make_system(wl, rank, world)
     t_up = time.perf_counter()
@@ -900,15 +1002,39 @@ def run_dist(args, wl_name, world, rank, local_rank):
         ms_per_step = 1e3 * wall / args.steps
         value = args.steps / wall  # CG iterations of the one 64M-row system per second
         _, spmv_ms = s.bench_run(min(args.steps, 30), spmv_events=True)
+        phases = s.bench_phases()
     info = s.info()
     s.close()
+
+    # ---- per-phase breakdown, max over ranks of partition
+    # 0's HIP events in the eager iterations: the march / interior launch, the
+    # halo wait before the edge / boundary launch, that launch, and the tail
+    # (local sums, all-reduce, next pack) -- so a curve below 6x says which
+    phase_out = None
+    if ok[0]:
+        keys = ("first_launch", "halo_wait_gap", "second_launch", "tail", "period")
+        mine = [phases[k] if phases else -1.0 for k in keys]
+        phase_out = {k: round(allmax(v) * 1e3, 2) for k, v in zip(keys, mine)}
+        phase_out.update(unit="us per iteration (max over ranks)",
+                         timing="HIP events on each rank's stream, "
+                                f"{min(args.steps, 30)} eager iterations (no graph)",
+                         legend=dict(first_launch="k_sr1_dia_m march (one-launch SR) / "
+                                                  "interior SpMV", halo_wait_gap="wait for the "
+                                                  "halo before the edge / boundary launch",
+                                     second_launch="k_sr1_edge / boundary SpMV",
+                                     tail="local sums + RCCL all-reduce(s) + vector updates "
+                                          "+ the next halo pack", period="iteration"))
 
     roofline = None
     if spmv_ms is not None:
         # per-rank SpMV (interior + boundary launches) on its own layout bytes
         gbs, frac = spmv_roofline(info["spmv_iter_bytes"], spmv_ms)
+        tk = dist_traffic_key(alg, info)
+        tf = traffic_fields(f"c4n{world}", tk, info["spmv_iter_bytes"]) if tk else dict(
+            traffic=None, traffic_source="no PMC summary for this recurrence's rank kernel",
+            traffic_ratio=None)
         roofline = dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=frac,
-                        traffic=None, kernel=kernel_name(info) + " (per rank)",
+                        **tf, kernel=kernel_name(info) + " (per rank)",
                         algorithmic_bytes_per_launch=int(info["spmv_iter_bytes"]),
                         spmv_us=round(spmv_ms * 1e3, 2),
                         spmv_us_max_over_ranks=round(allmax(spmv_ms) * 1e3, 2),
@@ -917,25 +1043,10 @@ def run_dist(args, wl_name, world, rank, local_rank):
     halo = allmax(info["halo_bytes"])
     dev = allmax(dev_ms / args.steps) if dev_ms is not None else None
     if rank == 0:
-        out = dict(
-            metric=METRIC, value=None if value is None else round(value, 2), unit="it/s",
-            n_gpus=world, steps=args.steps, warmup=args.warmup,
-            ms_per_step=None if ms_per_step is None else round(ms_per_step, 4),
-            higher_is_better=True, scaling="strong", vs_baseline=None, dtype=wl["dtype"],
-            data="synthetic",
-            config=dict(workload=wl["desc"], n=sysm["n_global"], rows_per_rank=info["n_loc"],
-                        nnz_rank0=info["nnz"], alg=alg, march=info["march"],
-                        alg_trial_ms_per_iter=trial,
-                        alg_refused=refused or None, fuse_status=info["fuse_status"],
-                        graph=info["graph"], fused=info["fused"],
-                        parallelism=f"row-partition x{world} (RCCL)",
-                        scaling_curve="the same workload at every N (N = 1: the "
-                                      "single-GPU solver), so value(N) / value(1) is the "
-                                      "speedup",
-                        layout=info["layout_name"], halo_bytes_per_iter_max_rank=halo),
-            device_ms_per_step=None if dev is None else round(dev, 4),
-            upload_ms=round(upload_ms, 1), iter_bytes_rank0=int(info["iter_bytes"]),
-            roofline=roofline, cpu_baseline=None, parity=parity)
+        out = dist_line(args, wl, world, dict(
+            value=value, ms_per_step=ms_per_step, dev=dev, n_global=sysm["n_global"], info=info,
+            alg=alg, trial=trial, refused=refused, halo=halo, upload_ms=upload_ms,
+            roofline=roofline, phases=phase_out, cpu=cpu, parity=parity))
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
     if not ok[0]:

@@ -187,6 +187,7 @@ _SIGS = {
     "cgx_dist_bench_prepare": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_bench_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _f64p, _f64p]),
     "cgx_dist_info": (ctypes.c_int, [_vp, ctypes.POINTER(CgxDistStats)]),
+    "cgx_dist_bench_phases": (ctypes.c_int, [_vp, _f64p, ctypes.POINTER(ctypes.c_int)]),
 }
 
 _lib = None
@@ -267,12 +268,21 @@ def laplacian2d(nx, ny, row_begin=0, row_end=None):
 
 
 CGX_STREAM_TRIAD, CGX_STREAM_READ = 0, 1
+CGX_STREAM_COPY, CGX_STREAM_COPY_NT = 2, 3
+CGX_STREAM_TRIAD_TUNED, CGX_STREAM_TRIAD_NT = 4, 5
+CGX_STREAM_MIX33, CGX_STREAM_MIX33_NT = 6, 7
+STREAM_KINDS = {"triad": CGX_STREAM_TRIAD, "read": CGX_STREAM_READ, "copy": CGX_STREAM_COPY,
+                "copy_nt": CGX_STREAM_COPY_NT, "triad_tuned": CGX_STREAM_TRIAD_TUNED,
+                "triad_nt": CGX_STREAM_TRIAD_NT, "mix33": CGX_STREAM_MIX33,
+                "mix33_nt": CGX_STREAM_MIX33_NT}
 
 
 def stream_bench(device, n, reps=10, kind=CGX_STREAM_TRIAD):
     """On-box HBM ceiling (cgx_stream_bench): best-of-reps GB/s over fp64
-    arrays of n elements; kind CGX_STREAM_TRIAD (a = b + s c, 24 n bytes) or
-    CGX_STREAM_READ (read-only sum, 8 n bytes)."""
+    arrays of n elements; kind CGX_STREAM_TRIAD (a = b + s c, 24 n bytes),
+    CGX_STREAM_READ (read-only sum, 8 n bytes), or a tuned read/write mix
+    (CGX_STREAM_COPY / TRIAD_TUNED / MIX33, _NT: non-temporal stores;
+    include/cgx.h)."""
     g = ctypes.c_double(0.0)
     check(lib().cgx_stream_bench(device, kind, n, reps, ctypes.byref(g)), "stream_bench")
     return g.value
@@ -727,6 +737,19 @@ class DistSolver:
         check(lib().cgx_dist_bench_run(self._h, iters, flags,
                                        ctypes.byref(ms), ctypes.byref(sp)), "dist_bench_run")
         return ms.value, sp.value
+
+    def bench_phases(self):
+        """Per-phase ms per iteration of the last bench_run(spmv_events=True)
+        (cgx_dist_bench_phases): first launch, halo-wait gap, second launch,
+        tail (sums, all-reduce, updates, pack), period; None before one."""
+        ms = np.zeros(5, np.float64)
+        it = ctypes.c_int(0)
+        check(lib().cgx_dist_bench_phases(self._h, _p(ms, _f64p), ctypes.byref(it)),
+              "dist_bench_phases")
+        if it.value <= 0:
+            return None
+        keys = ("first_launch", "halo_wait_gap", "second_launch", "tail", "period")
+        return dict({k: float(v) for k, v in zip(keys, ms)}, iters=it.value)
 
     def info(self):
         st = CgxDistStats()

@@ -155,6 +155,9 @@ struct cgx_dist {
   std::vector<hipEvent_t> spmv_ev;
   bool rec_spmv = false;
   size_t ev_i = 0;
+  // per-phase averages of the last CGX_BENCH_SPMV_EVENTS run (cgx_dist_bench_phases)
+  double phase_ms[5] = {-1.0, -1.0, -1.0, -1.0, -1.0};
+  int phase_iters = 0;
   // batches of graph_batch iterations replayed as a hipGraph (solo and
   // RCCL; the in-process group runs eager)
   hipGraphExec_t gexec[2] = {};   // graph_batch iterations, per p-buffer parity
@@ -661,16 +664,29 @@ bool fz1(const cgx_dist *d);
 // r03).  Before any graph capture (their pointers are captured).
 int ensure_rsw2(Group *g) {
   for (cgx_dist *d : g->parts) {
-    if (d->d_r2 || !(sr1(d) || fz1(d))) continue;
+    if ((d->d_r2 && d->d_s2 && d->d_w2) || !(sr1(d) || fz1(d))) continue;
     CGX_HIP(hipSetDevice(d->device));
+    int rc = 0;
     for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2}) {
+      if (*p) continue;
       void *raw = nullptr;
-      int rc = dev_alloc(&raw, (d->vfront + d->ng_alloc) * 8, &d->vec_bytes);
-      if (rc) return rc;
+      rc = dev_alloc(&raw, (d->vfront + d->ng_alloc) * 8, &d->vec_bytes);
+      if (rc) break;
       *p = (double *)raw + d->vfront;
-      CGX_HIP(hipMemsetAsync(raw, 0, (d->vfront + d->ng_alloc) * 8, d->st));
+      if (hipMemsetAsync(raw, 0, (d->vfront + d->ng_alloc) * 8, d->st) != hipSuccess) {
+        set_error("dist: zeroing the second r / s / w buffers failed");
+        rc = CGX_ENODEV;
+        break;
+      }
     }
-    CGX_HIP(hipStreamSynchronize(d->st));
+    if (!rc && hipStreamSynchronize(d->st) != hipSuccess) {
+      set_error("dist: zeroing the second r / s / w buffers failed");
+      rc = CGX_ENODEV;
+    }
+    if (rc) {  // none or all three (a partial set ran with nulls)
+      for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2}) free_ghosted(d, p);
+      return rc;
+    }
   }
   return 0;
 }
@@ -1338,14 +1354,32 @@ int group_bench_run(Group *g, int iters, int flags, double *ms, double *spmv_ms)
   *ms = f;
   *spmv_ms = -1.0;
   if (per_spmv) {
-    double sum = 0.0;
+    // per iteration on partition 0: the first launch (interior / march), the
+    // gap to the second (the halo wait), the second (boundary / edge), and
+    // the tail up to the next iteration's first launch (local sums, the
+    // all-reduce(s), the vector updates, the next pack) -- averaged
+    double sum = 0.0, ph[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     for (int i = 0; i < iters; ++i) {
-      float a = 0.f, b = 0.f;
+      float a = 0.f, gap = 0.f, b = 0.f;
       CGX_HIP(hipEventElapsedTime(&a, d0->spmv_ev[4 * i], d0->spmv_ev[4 * i + 1]));
+      CGX_HIP(hipEventElapsedTime(&gap, d0->spmv_ev[4 * i + 1], d0->spmv_ev[4 * i + 2]));
       CGX_HIP(hipEventElapsedTime(&b, d0->spmv_ev[4 * i + 2], d0->spmv_ev[4 * i + 3]));
       sum += (double)a + (double)b;
+      ph[0] += a;
+      ph[1] += gap;
+      ph[2] += b;
+      if (i + 1 < iters) {
+        float tail = 0.f, per = 0.f;
+        CGX_HIP(hipEventElapsedTime(&tail, d0->spmv_ev[4 * i + 3], d0->spmv_ev[4 * i + 4]));
+        CGX_HIP(hipEventElapsedTime(&per, d0->spmv_ev[4 * i], d0->spmv_ev[4 * i + 4]));
+        ph[3] += tail;
+        ph[4] += per;
+      }
     }
     *spmv_ms = sum / iters;
+    for (int k = 0; k < 3; ++k) d0->phase_ms[k] = ph[k] / iters;
+    for (int k = 3; k < 5; ++k) d0->phase_ms[k] = iters > 1 ? ph[k] / (iters - 1) : -1.0;
+    d0->phase_iters = iters;
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
@@ -1548,6 +1582,14 @@ int cgx_dist_get_history(cgx_dist *d, double *rr, int cap) {
 int cgx_dist_bench_prepare(cgx_dist *d, int warmup) {
   if (!d || warmup < 0 || (d->local && !d->owns_group)) return CGX_EINVAL;
   return group_bench_prepare(d->group, warmup);
+}
+
+int cgx_dist_bench_phases(cgx_dist *d, double *ms, int *iters) {
+  if (!d || !ms || (d->local && !d->owns_group)) return CGX_EINVAL;
+  const cgx_dist *d0 = d->group->parts[0];
+  for (int k = 0; k < 5; ++k) ms[k] = d0->phase_ms[k];
+  if (iters) *iters = d0->phase_iters;
+  return 0;
 }
 
 int cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms, double *spmv_ms) {

@@ -472,6 +472,11 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
                         hipStream_t st);
 hipError_t launch_stream_read(long long n2, const double *b, double *sink, int grid,
                               hipStream_t st);
+// the tuned CGX_STREAM_COPY.. kinds: arrays read / written (-1: not one),
+// and the launch over buf (R + W arrays of n2 16-B chunks, `stride` apart)
+int stream_rw_arrays(int kind, int *r, int *w);
+hipError_t launch_stream_rw(int kind, long long n2, long long stride, double *buf, int cus,
+                            hipStream_t st);
 hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val,
                                 hipStream_t st);
 // Offset codes of a device CSR against a sorted dictionary (err |= 1 on a

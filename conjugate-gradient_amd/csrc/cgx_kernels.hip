@@ -27,6 +27,11 @@
 
 #pragma clang fp contract(off)
 
+// Same-box A/B experiments (tools/ab_build.sh): the product never defines it.
+#ifndef CGX_EXP
+#define CGX_EXP 0
+#endif
+
 namespace cgx {
 
 namespace {
@@ -1291,7 +1296,8 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *ring = reinterpret_cast<T *>(dyn_lds);
-  T *rbuf = ring + 3 * a.mws;  // r_k of the own rows, two slots of SR
+  constexpr int NRING = 3, NRB = 2;
+  T *rbuf = ring + NRING * a.mws;  // r_k of the own rows, NRB slots of SR
   __shared__ T lv[kDiaMax * 16];
   __shared__ double red[3][4 * SB];
   typedef typename Pair<T>::type P;
@@ -1322,7 +1328,8 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   const bool nt = a.nt != 0;
   const int wn = SR + a.hl + a.hr, ws = a.mws;
   auto base_of = [&](int m) { return (j0 + m * a.mq) * kDiaSliceRows; };
-  auto slot = [&](int m) { return ring + ((m + 3) % 3) * ws; };
+  auto slot = [&](int m) { return ring + ((m + NRING) % NRING) * ws; };
+  auto rslot = [&](int m) { return rbuf + ((m + NRB) % NRB) * SR; };
   struct XOps {
     P po, xo, pd;
   };
@@ -1382,10 +1389,16 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     return;
   }
   P wr[NF], wp[NF], wsv[NF];
+  // a wave whose pairs of pass q all lie past the window skips that pass
+  // (wave-uniform: the wave's first pair; SB = 4 at C4: 9 of 16 waves skip
+  // pass 1 -- round 5, with the four-slice steps 812 -> 783 us per C4 launch)
+  const int wfirst = 2 * __builtin_amdgcn_readfirstlane(wid * kWave);
+  for (int q = 0; q < NF; ++q) wr[q] = wp[q] = wsv[q] = P{T(0), T(0)};
   auto load_win = [&](int m) {
     const int w0 = base_of(m) - a.hl;
 #pragma unroll
     for (int q = 0; q < NF; ++q) {
+      if (q > 0 && wfirst + q * 2 * BS >= wn) continue;
       const int j = min(max(w0 + 2 * t + q * 2 * BS, a.xlo), a.ncols - 1);
       wr[q] = ld_pair(f.rold, j);
       wp[q] = ld_pair(f.pold, j);
@@ -1393,7 +1406,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     }
   };
   auto store_win = [&](int m) {
-    T *win = slot(m), *rb = rbuf + (m & 1) * SR;
+    T *win = slot(m), *rb = rslot(m);
 #pragma unroll
     for (int q = 0; q < NF; ++q) {
       const int i = 2 * t + q * 2 * BS;
@@ -1434,7 +1447,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     const int base = base_of(m), r = base + 2 * t;
     const int rend = min(a.n, base + SR);
     const T *cur = slot(m), *prv = slot(m - 1), *nxt = slot(m + 1);
-    const T *rb = rbuf + (m & 1) * SR;
+    const T *rb = rslot(m);
     const int rw = 2 * t + a.hl;
     unsigned cc0, cc1;
     code_split<CB>(ccw, cc0, cc1);
@@ -2589,6 +2602,42 @@ __global__ __launch_bounds__(256) void k_stream_read(long long n2, const double2
   if (acc == 1.2345e300) sink[0] = acc;  // keeps the loads; never true
 }
 
+// Tuned read/write streams (the ceiling a read/write mix
+// reaches on this box, beside the naive triad above): R arrays read, W
+// written, all arrays n2 16-B chunks at a stride of `stride` chunks in one
+// buffer; each lane handles U chunks 256 apart per pass (U R loads in flight
+// before the first store), grid = the resident workgroup slots, grid-stride;
+// NT: non-temporal stores.  Out w = in w + 0.5 in (w + 1) mod R (never
+// elided; the values are irrelevant).
+template <int R, int W, int U, bool NT>
+__global__ __launch_bounds__(256) void k_stream_rw(long long n2, long long stride,
+                                                   double *__restrict__ buf) {
+  typedef Vec16<double>::type V;
+  V *b = reinterpret_cast<V *>(buf);
+  const long long step = (long long)gridDim.x * 256 * U;
+  for (long long i0 = (long long)blockIdx.x * 256 * U + threadIdx.x; i0 < n2; i0 += step) {
+    V v[R][U];
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long i = i0 + u * 256;
+        v[q][u] = i < n2 ? b[q * stride + i] : V{0.0, 0.0};
+      }
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long i = i0 + u * 256;
+        const V o = v[w % R][u] + 0.5 * v[(w + 1) % R][u];
+        if (i < n2) {
+          if (NT) __builtin_nontemporal_store(o, b + (R + w) * stride + i);
+          else b[(R + w) * stride + i] = o;
+        }
+      }
+  }
+}
+
 // ------------------------------------------- on-device Laplacian
 // CSR of the whole grid written straight into HBM: row r's entries at
 // lap_rp(r), columns ascending -- cgx_gen_laplacian2d/3d bit for bit.
@@ -2906,8 +2955,26 @@ static const void *sr1_kernel(int cb) {
                    : CGX_K((k_sr1_dia_m<T, SB, NF, 4>));
 }
 
+// The plan k_sr1_dia_m runs: the matrix's march plan, with four-slice steps
+// where its two-slice chains pair up (mq % 4 == 0, C4 and its slabs): 2,048
+// own rows per step, the in-plane halo loaded 1.39x instead of 1.78x; one
+// 1,024-thread workgroup per CU (the ring + r slots: 100 KB of LDS).  Round
+// 5, same box, alternating: C4 783 / 781 against 812 / 810 us per launch
+// (with the pass predicate; the predicate alone 801).
 template <typename T>
-int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f) {
+static SpmvArgs<T> sr1_args(const SpmvArgs<T> &a0) {
+  SpmvArgs<T> a = a0;
+  if (a.msb == 2 && a.mq % 4 == 0 && 4 * kDiaSliceRows + a.hl + a.hr <= 2 * 2 * 1024) {
+    a.msb = 4;
+    a.mchains = a.mq / 4;
+    a.mws = (4 * kDiaSliceRows + a.hl + a.hr + 3) & ~1;
+  }
+  return a;
+}
+
+template <typename T>
+int sr1_grid(const SpmvArgs<T> &a_in, const Sr1Args<T> &f) {
+  const SpmvArgs<T> a = sr1_args(a_in);
   const int steps = (a.mslices + a.mq - 1) / a.mq;  // chain 0's, the longest
   if (f.nseg > 0) return a.mchains * std::min(f.nseg, steps);
   if (f.march <= 0) return 0;
@@ -2926,24 +2993,28 @@ static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
   const int sb = a.msb;
   const int wn = sb * kDiaSliceRows + a.hl + a.hr;
   const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
-  if (a.mws < wn + 2 || (sb != 1 && sb != 2) || nf > (sb == 1 ? 5 : 3)) return nullptr;
+  if (a.mws < wn + 2 || (sb != 1 && sb != 2 && sb != 4) ||
+      nf > (sb == 1 ? 5 : sb == 2 ? 3 : 2))
+    return nullptr;
   const int nfc = nf <= 2 ? 2 : nf <= 3 ? 3 : 5;
   const int cb = a.cb;
   if (cb != 1 && cb != 2 && cb != 4) return nullptr;
   // the three-window ring and two slots of own-row r
-  lds = ((size_t)3 * a.mws + 2 * sb * kDiaSliceRows) * sizeof(T) + 16;
+  lds = ((size_t)3 * a.mws + (size_t)2 * sb * kDiaSliceRows) * sizeof(T) + 16;
   switch (sb * 10 + nfc) {
     case 12: return sr1_kernel<T, 1, 2>(cb);
     case 13: return sr1_kernel<T, 1, 3>(cb);
     case 15: return sr1_kernel<T, 1, 5>(cb);
     case 22: return sr1_kernel<T, 2, 2>(cb);
     case 23: return sr1_kernel<T, 2, 3>(cb);
+    case 42: return sr1_kernel<T, 4, 2>(cb);
     default: return nullptr;
   }
 }
 
 template <typename T>
-int sr1_pick_nseg(const SpmvArgs<T> &a, int cus) {
+int sr1_pick_nseg(const SpmvArgs<T> &a_in, int cus) {
+  const SpmvArgs<T> a = sr1_args(a_in);
   size_t lds = 0;
   const void *k = sr1_pick(a, lds);
   if (!k || a.mchains <= 0) return 1;
@@ -2967,8 +3038,9 @@ int sr1_pick_nseg(const SpmvArgs<T> &a, int cus) {
 }
 
 template <typename T>
-hipError_t launch_sr1_march(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
+hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev) {
+  const SpmvArgs<T> a = sr1_args(a_in);
   if (a.mq <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
       (f.march <= 0 && f.nseg <= 0) || f.nseg < 0 || (f.elo & 1) || (f.ehi < a.n && (f.ehi & 1)))
     return hipErrorInvalidValue;
@@ -3246,6 +3318,42 @@ hipError_t launch_triad(long long n2, double *a, const double *b, const double *
   hipLaunchKernelGGL(k_triad, dim3(grid), dim3(256), 0, st, n2, (double2 *)a, (const double2 *)b,
                      (const double2 *)c, 3.0);
   return hipGetLastError();
+}
+
+namespace {
+template <int R, int W, bool NT>
+hipError_t launch_rw(long long n2, long long stride, double *buf, int cus, hipStream_t st) {
+  constexpr int U = 4;
+  const void *k = CGX_K(k_stream_rw<R, W, U, NT>);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1)
+    per_cu = 8;
+  hipLaunchKernelGGL((k_stream_rw<R, W, U, NT>), dim3(cus * per_cu), dim3(256), 0, st, n2, stride,
+                     buf);
+  return hipGetLastError();
+}
+}  // namespace
+
+int stream_rw_arrays(int kind, int *r, int *w) {
+  switch (kind) {
+    case CGX_STREAM_COPY: case CGX_STREAM_COPY_NT: *r = 1; *w = 1; return 0;
+    case CGX_STREAM_TRIAD_TUNED: case CGX_STREAM_TRIAD_NT: *r = 2; *w = 1; return 0;
+    case CGX_STREAM_MIX33: case CGX_STREAM_MIX33_NT: *r = 3; *w = 3; return 0;
+    default: return -1;
+  }
+}
+
+hipError_t launch_stream_rw(int kind, long long n2, long long stride, double *buf, int cus,
+                            hipStream_t st) {
+  switch (kind) {
+    case CGX_STREAM_COPY: return launch_rw<1, 1, false>(n2, stride, buf, cus, st);
+    case CGX_STREAM_COPY_NT: return launch_rw<1, 1, true>(n2, stride, buf, cus, st);
+    case CGX_STREAM_TRIAD_TUNED: return launch_rw<2, 1, false>(n2, stride, buf, cus, st);
+    case CGX_STREAM_TRIAD_NT: return launch_rw<2, 1, true>(n2, stride, buf, cus, st);
+    case CGX_STREAM_MIX33: return launch_rw<3, 3, false>(n2, stride, buf, cus, st);
+    case CGX_STREAM_MIX33_NT: return launch_rw<3, 3, true>(n2, stride, buf, cus, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_gen_laplacian(const LapSpec &g, int n, int *col, double *val, hipStream_t st) {

@@ -683,31 +683,37 @@ int cgx_device_count(void) {
 }
 
 int cgx_stream_bench(int device, int kind, long long n, int reps, double *gbs) {
-  if (!gbs || n < 2 || reps < 1 || (kind != CGX_STREAM_TRIAD && kind != CGX_STREAM_READ))
+  int nr = 0, nw = 0;
+  const bool rw = stream_rw_arrays(kind, &nr, &nw) == 0;
+  if (!gbs || n < 2 || reps < 1 || (kind != CGX_STREAM_TRIAD && kind != CGX_STREAM_READ && !rw))
     return CGX_EINVAL;
   int cus = 256;
   int rc = check_device(device, &cus);
   if (rc) return rc;
   CGX_HIP(hipSetDevice(device));
   const long long n2 = n / 2;
+  // arrays 4 KiB apart (each starts on its own page-aligned offset)
+  const long long stride = (n2 + 255) / 256 * 256;
+  const int narr = rw ? nr + nw : 3;
   double *buf = nullptr;
-  if (hipMalloc((void **)&buf, (size_t)n2 * 16 * 3) != hipSuccess) {
+  if (hipMalloc((void **)&buf, (size_t)stride * 16 * narr) != hipSuccess) {
     set_error("stream_bench: out of device memory");
     return CGX_ENOMEM;
   }
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  double *a = buf, *b = buf + 2 * n2, *c = buf + 4 * n2;
+  double *a = buf, *b = buf + 2 * stride, *c = buf + 4 * stride;
   float best = 1e30f;
   hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
-  if (e == hipSuccess) e = hipMemsetAsync(buf, 0, (size_t)n2 * 48, st);
+  if (e == hipSuccess) e = hipMemsetAsync(buf, 0, (size_t)stride * 16 * narr, st);
   for (int r = -2; r < reps && e == hipSuccess; ++r) {  // two untimed warm-ups
     e = hipEventRecord(e0, st);
     if (e == hipSuccess)
-      e = kind == CGX_STREAM_TRIAD ? launch_triad(n2, a, b, c, cus * 16, st)
-                                   : launch_stream_read(n2, b, a, cus * 16, st);
+      e = rw ? launch_stream_rw(kind, n2, stride, buf, cus, st)
+          : kind == CGX_STREAM_TRIAD ? launch_triad(n2, a, b, c, cus * 16, st)
+                                     : launch_stream_read(n2, b, a, cus * 16, st);
     if (e == hipSuccess) e = hipEventRecord(e1, st);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0.f;
@@ -722,7 +728,8 @@ int cgx_stream_bench(int device, int kind, long long n, int reps, double *gbs) {
     set_error("stream_bench: %s", hipGetErrorString(e));
     return CGX_ENODEV;
   }
-  *gbs = (kind == CGX_STREAM_TRIAD ? 48.0 : 16.0) * (double)n2 / (best * 1e-3) / 1e9;
+  const double per = rw ? 16.0 * (nr + nw) : kind == CGX_STREAM_TRIAD ? 48.0 : 16.0;
+  *gbs = per * (double)n2 / (best * 1e-3) / 1e9;
   return 0;
 }
 
@@ -778,20 +785,25 @@ int cgx_solver_set_mode(cgx_solver *s, int mode, int alg) {
   s->mode = mode;
   s->alg = alg;
   drop_graph(s);
+  s->bench_ready = false;  // the prepared state (buffers, prologue) was another recurrence's
   return 0;
 }
 
 int cgx_solver_set_fused(cgx_solver *s, int mode) {
   if (!s || mode < CGX_FUSE_OFF || mode > CGX_FUSE_ON) return CGX_EINVAL;
+  if (s->fuse == mode) return 0;
   s->fuse = mode;
   drop_graph(s);
+  s->bench_ready = false;
   return 0;
 }
 
 int cgx_solver_set_march(cgx_solver *s, int steps) {
   if (!s || steps < -1) return CGX_EINVAL;
+  if (s->march == steps) return 0;
   s->march = steps;
   drop_graph(s);
+  s->bench_ready = false;
   return 0;
 }
 

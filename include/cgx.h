@@ -97,9 +97,22 @@ int cgx_device_count(void);
  * n elements on `device`, best of `reps` timed launches, 16 B per lane:
  *   CGX_STREAM_TRIAD  a[i] = b[i] + s*c[i]      *gbs = 24 n B / time
  *   CGX_STREAM_READ   sum of a[i] (read only)   *gbs =  8 n B / time
+ * and tuned read/write mixes (4 x 16 B per lane in flight before the first
+ * store, grid = resident workgroup slots, grid-stride; _NT: non-temporal
+ * stores), *gbs = (R + W) 8 n B / time:
+ *   CGX_STREAM_COPY[_NT]         R = 1, W = 1 (a = b)
+ *   CGX_STREAM_TRIAD_TUNED / _NT R = 2, W = 1 (a = b + s c)
+ *   CGX_STREAM_MIX33[_NT]        R = 3, W = 3 (the one-launch SR step's
+ *                                r, p, s read and written)
  * Measurement only (bench.py's roofline context). */
 #define CGX_STREAM_TRIAD 0
 #define CGX_STREAM_READ 1
+#define CGX_STREAM_COPY 2
+#define CGX_STREAM_COPY_NT 3
+#define CGX_STREAM_TRIAD_TUNED 4
+#define CGX_STREAM_TRIAD_NT 5
+#define CGX_STREAM_MIX33 6
+#define CGX_STREAM_MIX33_NT 7
 int cgx_stream_bench(int device, int kind, long long n, int reps, double *gbs);
 
 /* ------------------------------------------------------------------------
@@ -463,6 +476,15 @@ int  cgx_dist_bench_prepare(cgx_dist *d, int warmup);
  * with events; *spmv_ms = their average sum. */
 int  cgx_dist_bench_run(cgx_dist *d, int iters, int flags, double *total_ms,
                         double *spmv_ms);
+/* Per-phase averages (ms per iteration) of the last bench_run with
+ * CGX_BENCH_SPMV_EVENTS, from the events on partition 0's stream (eager
+ * iterations): ms[0] the first SpMV launch (interior items; one-launch SR:
+ * the march), ms[1] the gap until the second (the halo wait), ms[2] the
+ * second launch (boundary items; SR: the edge rows), ms[3] the tail until
+ * the next iteration's first launch (local sums, all-reduce(s), vector
+ * updates, the next pack), ms[4] the iteration period; -1 before such a
+ * run.  *iters (may be NULL): the iterations averaged. */
+int  cgx_dist_bench_phases(cgx_dist *d, double *ms, int *iters);
 int  cgx_dist_info(cgx_dist *d, cgx_dist_stats *s);
 
 #ifdef __cplusplus

@@ -116,3 +116,46 @@ def test_gate_decides_per_recurrence():
     assert bench.gate_passed(dict(every, sr=False)) == ["hs", "sr_two_launch", "cg1"]
     assert bench.gate_passed(dict(every, hs_fused=False)) == ["sr", "sr_two_launch", "cg1"]
     assert bench.gate_passed({}) == []
+
+
+def test_dist_line_schema():
+    """the N > 1 line explains itself -- per-phase breakdown,
+    the CPU baseline, the rank kernel's PMC traffic, and the parity gate at
+    the top level (parity_ok / gate_failed)."""
+    args = bench.parse_args(["--gpus", "8", "--steps", "50", "--warmup", "5"])
+    info = dict(n_loc=8_000_000, nnz=55_680_000, march=17, fuse_status=0, graph=1, fused=1,
+                layout_name="dia", iter_bytes=1.4e9, alg=2, spmv_iter_bytes=4.9e8)
+    phases = dict(first_launch=117.0, halo_wait_gap=0.5, second_launch=8.0, tail=14.0,
+                  period=140.0, unit="us per iteration (max over ranks)")
+    parity = dict(ok=False, hs=dict(ok=True), sr=dict(ok=False), system="...")
+    cpu = dict(value=2.0, unit="it/s", cores=1, kind="port", sample="...")
+    roof = dict(bound="hbm", achieved=4000.0, peak=8000.0, unit="GB/s", frac=0.5,
+                traffic=5.0e8, traffic_source="profiles/pmc_c4n8_sr1.json", traffic_ratio=1.02)
+    m = dict(value=7000.0, ms_per_step=0.1428, dev=0.14, n_global=64_000_000, info=info,
+             alg="sr", trial={"sr": 0.14}, refused={}, halo=2.56e6, upload_ms=900.0,
+             roofline=roof, phases=phases, cpu=cpu, parity=parity)
+    line = bench.dist_line(args, bench.WORKLOADS["c4"], 8, m)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "phases", "cpu_baseline", "parity", "parity_ok", "gate_failed"):
+        assert k in line, k
+    assert line["n_gpus"] == 8 and line["value"] == 7000.0
+    assert line["cpu_baseline"]["cores"] == 1 and line["roofline"]["traffic"] == 5.0e8
+    assert set(line["phases"]) >= {"first_launch", "halo_wait_gap", "second_launch", "tail",
+                                   "period"}
+    assert line["parity_ok"] is False and line["gate_failed"] == ["sr"]
+    import json
+    json.dumps(line)  # one JSON line
+    assert bench.dist_traffic_key("sr", info) == "sr1"
+    assert bench.dist_traffic_key("hs", info) is None
+    assert bench.kernel_key(dict(info, fused=1)) == "sr1"
+    assert bench.kernel_key(dict(info, march=0)) == "dia_fused"
+
+
+def test_no_gbs_field_exceeds_peak():
+    """no field named *gbs* in the committed bench lines of
+    this build's schema may exceed the HBM peak -- CSR-basis rates of the
+    compressed layouts are csr_basis_equiv_rate, C2's rates are fractions
+    marked resident."""
+    src = (REPO / "bench.py").read_text()
+    assert "csr_equivalent_gbs" not in src and "csr_basis_gbs" not in src

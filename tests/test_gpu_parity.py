@@ -998,6 +998,34 @@ def test_stream_ceilings():
     t = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_TRIAD)
     r = cgx.stream_bench(0, 16 * 2**20, 3, cgx.CGX_STREAM_READ)
     assert 2000.0 < t < 8000.0 and 2000.0 < r < 8000.0
+    # the tuned read/write mixes, every kind through the ABI
+    for name in ("copy", "copy_nt", "triad_tuned", "triad_nt", "mix33", "mix33_nt"):
+        g = cgx.stream_bench(0, 16 * 2**20, 3, cgx.STREAM_KINDS[name])
+        assert 2000.0 < g < 8000.0, (name, g)
+
+
+def test_bench_state_dropped_on_recurrence_change():
+    """bench_prepare under HS, then set_mode(FAST, SR) (whose
+    second r / s / w buffers HS never allocated) -- bench_run must refuse
+    (CGX_EINVAL) until the next bench_prepare, not launch on null buffers."""
+    rp, col, val = cgx.laplacian3d(32, 48, 20)
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(np.ones(len(rp) - 1))
+        s.bench_prepare(2)
+        s.bench_run(4)
+        for change in (lambda: s.set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_SR),
+                       lambda: s.set_fused(True), lambda: s.set_march(3)):
+            s.set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
+            s.set_fused("auto")
+            s.set_march(-1)
+            s.bench_prepare(2)
+            s.bench_run(2)
+            change()
+            with pytest.raises(cgx.CgxError):
+                s.bench_run(2)
+        s.bench_prepare(2)  # prepared again (HS, march 3): runs
+        s.bench_run(4)
 
 
 def test_spmv_only_bench():

@@ -30,7 +30,8 @@ lap = bench.make_system(bench.WORKLOADS["c3"])
 rp, col, val = cgx.varcoef3d(216, 216, 216, seed=7)
 var = dict(rp=rp, col=col, val=val, b=np.ones(len(rp) - 1))
 for r in range(rounds):
-    for name, sysm in (("laplacian", lap), ("varcoef", var)):
-        leg = bench.solver_leg(sysm, 100, 10, "csr", b2b=True)
-        print("%d %-9s csr: %.1f it/s, in-CG SpMV %.2f us, b2b %.2f us" %
-              (r, name, leg["value"], leg["spmv_us"], leg["b2b_spmv_us"]), flush=True)
+    for name, sysm, layout in (("laplacian", lap, "csr"), ("varcoef", var, "csr"),
+                               ("varcoef", var, "dc")):
+        leg = bench.solver_leg(sysm, 100, 10, layout, b2b=True)
+        print("%d %-9s %s: %.1f it/s, in-CG SpMV %.2f us, b2b %.2f us" %
+              (r, name, layout, leg["value"], leg["spmv_us"], leg["b2b_spmv_us"]), flush=True)
