@@ -314,13 +314,14 @@ def spmv_roofline(bytes_, ms, peak=HBM_PEAK_GBS):
     return round(gbs, 1), round(gbs / peak, 4)
 
 
-def solver_leg(sysm, steps, warmup, layout, device=0, b2b=False):
+def solver_leg(sysm, steps, warmup, layout, device=0, b2b=False, alg="hs"):
     """One solver on the system in `layout`: CG it/s (graph replay), the
     average in-iteration SpMV time (HIP events around every SpMV launch on
     the solver's stream) and, with b2b, back-to-back SpMVs y = A p (the
-    standard SpMV benchmark, the kernel without the p.s epilogue)."""
+    standard SpMV benchmark, the kernel without the p.s epilogue).  alg:
+    the recurrence (ALGS)."""
     import cgx
-    with cgx.Solver(device, layout=layout) as s:
+    with cgx.Solver(device, layout=layout, alg=ALGS[alg]) as s:
         t0 = time.perf_counter()
         s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
         s.set_rhs(sysm["b"])
@@ -386,16 +387,44 @@ def general_coefficients(steps, warmup, device=0):
     sysm = dict(rp=rp, col=col, val=val, b=np.ones(len(rp) - 1))
     out = dict(matrix="7-point pattern of C3 (216^3), a_ij = a_ji = -(0.5 + U(0,1]) per edge, "
                       "diagonal = sum |a_ij| + 0.01 (cgx_gen_varcoef3d, seed 7), b = 1")
-    for name, layout in (("auto", "auto"), ("csr", "csr")):
-        leg = solver_leg(sysm, steps, warmup, layout, device, b2b=True)
+    gate = sr_gate(sysm, ("auto", "csr"))
+    out["sr_gate"] = gate
+    for name, layout, alg in (("auto", "auto", "hs"), ("auto_sr", "auto", "sr"),
+                              ("csr", "csr", "hs"), ("csr_sr", "csr", "sr")):
+        if alg == "sr" and not gate[layout]["ok"]:
+            out[name] = dict(refused=f"SR failed its parity gate: {gate[layout]}")
+            continue
+        leg = solver_leg(sysm, steps, warmup, layout, device, b2b=True, alg=alg)
         i = leg["info"]
         own_gbs, own_frac = spmv_roofline(i["spmv_iter_bytes"], leg["spmv_us"] * 1e-3)
         csr_gbs, csr_frac = spmv_roofline(i["spmv_bytes"], leg["spmv_us"] * 1e-3)
         out[name] = dict(layout=layout_desc(i), layout_name=i["layout_name"], value=leg["value"],
-                         unit="it/s", spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
+                         unit="it/s", alg=ALG_DESC[alg] if alg == "hs" else ALG_DESC["sr_unfused"],
+                         spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
                          own_bytes_gbs=own_gbs, own_bytes_frac=own_frac,
                          csr_basis_equiv_rate=csr_gbs, csr_basis_frac=csr_frac,
                          kernel=kernel_name(i))
+    ok = [k for k in ("auto", "auto_sr") if "value" in out.get(k, {})]
+    out["best_auto"] = max(ok, key=lambda k: out[k]["value"])
+    return out
+
+
+def sr_gate(sysm, layouts, maxit=20):
+    """The SR parity gate of a leg (as alg_trial's): SR x of `maxit`
+    iterations within 1e-10 of HS x in each layout."""
+    import numpy as np
+    import cgx
+    out = {}
+    for layout in layouts:
+        xs = {}
+        for alg in ("hs", "sr"):
+            with cgx.Solver(0, layout=layout, alg=ALGS[alg]) as s:
+                s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
+                s.set_rhs(sysm["b"])
+                s.run(maxit)
+                xs[alg] = s.x()
+        rel = float(np.linalg.norm(xs["sr"] - xs["hs"]) / np.linalg.norm(xs["hs"]))
+        out[layout] = dict(sr_vs_hs_rel=rel, maxit=maxit, ok=rel <= 1e-10)
     return out
 
 
@@ -428,7 +457,10 @@ ALG_DESC = {"hs": "hs (the reference recurrence, cg.c:88-141)",
                   "iteration, beta from r_new.r_new = alpha (alpha s.s) - r.r; on one GPU the "
                   "r update of iteration k runs inside the SpMV launch of k + 1: one launch per "
                   "iteration, k_sr1_dia_m; oracle_solve_sr)",
-            "cg1": "cg1 (Chronopoulos-Gear)"}
+            "cg1": "cg1 (Chronopoulos-Gear)",
+            "sr_unfused": "sr, unfused (any layout): the SpMV stores (p.s, s.s) per workgroup, "
+                          "one reduction, then r, p and x in one pass (k_update_sr): two "
+                          "launches per iteration; oracle_solve_sr"}
 
 
 _ORACLE_GATE = {}
@@ -582,12 +614,18 @@ def c2_leg(steps, warmup):
     wl = WORKLOADS["c2"]
     sysm = make_system(wl)
     out = dict(workload=wl["desc"], residency="Infinity-Cache resident (not an HBM figure)")
-    for name, layout in (("auto", "auto"), ("csr", "csr")):
-        leg = solver_leg(sysm, steps, warmup, layout, b2b=True)
+    gate = sr_gate(sysm, ("auto",))
+    out["sr_gate"] = gate
+    for name, layout, alg in (("auto", "auto", "hs"), ("auto_sr", "auto", "sr"),
+                              ("csr", "csr", "hs")):
+        if alg == "sr" and not gate[layout]["ok"]:
+            out[name] = dict(refused=f"SR failed its parity gate: {gate[layout]}")
+            continue
+        leg = solver_leg(sysm, steps, warmup, layout, b2b=True, alg=alg)
         i = leg["info"]
         _, own_frac = spmv_roofline(i["spmv_iter_bytes"], leg["spmv_us"] * 1e-3)
         _, csr_frac = spmv_roofline(i["spmv_bytes"], leg["spmv_us"] * 1e-3)
-        out[name] = dict(value=leg["value"], unit="it/s", layout=layout_desc(i),
+        out[name] = dict(value=leg["value"], unit="it/s", layout=layout_desc(i), alg=alg,
                          kernel=kernel_name(i), spmv_us=leg["spmv_us"],
                          b2b_spmv_us=leg["b2b_spmv_us"],
                          own_bytes=int(i["spmv_iter_bytes"]), own_bytes_frac_resident=own_frac,

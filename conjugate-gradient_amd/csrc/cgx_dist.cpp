@@ -204,6 +204,11 @@ bool sr(const cgx_dist *d) { return d->alg == CGX_ALG_SR; }
 // SR as ONE k_sr1_dia_m launch pair per iteration on the in-place numbering
 bool sr1(const cgx_dist *d) { return sr(d) && d->mi_all; }
 bool fz(const cgx_dist *d) { return d->fz_all && hs_like(d) && !sr1(d); }
+// SR without a fused step (round 5, VERDICT r04 #5: CSR, DC, wide-word DIA
+// ranks): the SpMV stores (p.s, s.s) pairs, ONE all-reduce of (p.s, s.s,
+// r.r), then k_update_sr does r, p (in place, its ghost tail refreshed by
+// the next halo) and x in one pass with the sums applied privately
+bool sru(const cgx_dist *d) { return sr(d) && !d->fz_all && !d->mi_all; }
 // The fused CG1 step (k_cg1_dia_h): only when forced on (CGX_FUSE_ON) --
 // on a rank's slab it loses to the unfused CG1 kernels (C4/8's 400 x 400 x
 // 50 slab: 164 vs 144 us per iteration, tools/dist_probe.py: the unfused
@@ -483,7 +488,7 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
       (rc = ghosted(&d->d_r)) || (rc = ghosted(&d->d_p)) || (rc = ghosted(&d->d_s)) ||
       (rc = ghosted(&d->d_w)) || (rc = ghosted(&d->d_p2)) ||
       (rc = dev_alloc(&d->d_pa, npa * 8, cb)) ||
-      (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 8, cb)) ||
+      (rc = dev_alloc(&d->d_pb, ((size_t)d->g_int + d->g_bnd + 8) * 16, cb)) ||  // SR pairs
       (rc = dev_alloc(&d->d_pss, ((size_t)d->g_int + d->g_bnd + 8) * 16, cb))) {
     free_system(d);
     return rc;
@@ -696,10 +701,6 @@ int ensure_rsw2(Group *g) {
 int ensure_connected(Group *g) {
   int rc = ensure_connected_fz(g);
   if (rc) return rc;
-  if (sr(g->parts[0]) && !g->parts[0]->fz_all && !g->parts[0]->mi_all) {
-    set_error("dist: CGX_ALG_SR needs the fused DIA step on every partition (fuse_status)");
-    return CGX_EINVAL;
-  }
   return ensure_rsw2(g);
 }
 
@@ -897,7 +898,9 @@ int phase_spmv(cgx_dist *d) {
   auto fgrid = [&](const Items &it) {
     return it.count ? fused_grid(d->A.args<double>(nullptr, nullptr, nullptr, nullptr, it)) : 0;
   };
-  const int gi = sr(d) ? fgrid(d->it_int) : 0, gb = sr(d) ? fgrid(d->it_bnd) : 0;
+  const bool pairs = sru(d);  // unfused SR: (p.s, s.s) pairs, 2 doubles per partial
+  const int gi = sr(d) && !pairs ? fgrid(d->it_int) : 0;
+  const int gb = sr(d) && !pairs ? fgrid(d->it_bnd) : 0;
   // rec: kernel timing events (hipExtLaunchKernel) of the two launches; an
   // empty launch records both of its events on the stream instead
   auto launch = [&](const Items &it, double *part, int e) -> hipError_t {
@@ -927,12 +930,18 @@ int phase_spmv(cgx_dist *d) {
                                sr(d) ? d->d_pss + (e == 2 ? 2 * gi : 0) : nullptr};
       return launch_spmv_fused<double>(a, f, d->st, ev);
     }
+    a.pair = pairs ? 1 : 0;
     return launch_spmv<double>(a, d->st, ev);
   };
   CGX_HIP(launch(d->it_int, d->d_pb, 0));
   if (has_peers(d)) CGX_HIP(hipStreamWaitEvent(d->st, d->ev_halo, 0));
-  CGX_HIP(launch(d->it_bnd, d->d_pb + d->g_int, 2));
+  CGX_HIP(launch(d->it_bnd, d->d_pb + (pairs ? 2 : 1) * d->g_int, 2));
   if (rec) d->ev_i += 4;
+  if (pairs && solo(d)) {  // the scalar step itself (the single-GPU solver's FIN_SR1)
+    CGX_HIP(launch_finalize(FIN_SR1, d->d_pb, np, nullptr, 0, d->d_st, d->d_hist, nullptr, d->st,
+                            d->d_pa, d->vec_grid));
+    return 0;
+  }
   if (solo(d) && !sr(d)) return 0;
   // local transport: every part's group sum of the last reduction must have
   // read this part's local sums before they are overwritten.  The halo orders
@@ -943,7 +952,10 @@ int phase_spmv(cgx_dist *d) {
   if (d->local)
     for (cgx_dist *o : d->group->parts)
       if (o != d) CGX_HIP(hipStreamWaitEvent(d->st, o->ev_red, 0));
-  if (sr(d))  // p.s, s.s, and r.r of the last r update (the prologue's b.b at first)
+  if (pairs)  // the previous all-reduce applied to the state, then the local sums
+    CGX_HIP(launch_finalize(FIN_SUM3_SR1, d->d_pb, np, d->d_gsums, 3, d->d_st, d->d_hist,
+                            d->d_sums, d->st, d->d_pa, d->vec_grid));
+  else if (sr(d))  // p.s, s.s, and r.r of the last r update (the prologue's b.b at first)
     CGX_HIP(launch_finalize(FIN_SUM3, d->d_pss, gi + gb, nullptr, 0, d->d_st, d->d_hist,
                             d->d_sums, d->st, d->d_pa, d->vec_grid));
   else if (d->alg == CGX_ALG_HS)
@@ -1046,6 +1058,20 @@ int hs_beta(cgx_dist *d) {
   return 0;
 }
 
+// unfused SR: the iteration's one all-reduce, then r, p (in place) and x
+// in one pass, the all-reduced sums applied privately (sr1_now)
+int sru_update(cgx_dist *d) {
+  CGX_HIP(hipSetDevice(d->device));
+  if (!solo(d)) {
+    int rc = allreduce(d, 0, 3);
+    if (rc) return rc;
+  }
+  CGX_HIP(launch_update_sr<double>(d->n_loc, d->d_x, d->d_r, d->d_s, d->d_p, d->d_p, d->d_st,
+                                   solo(d) ? nullptr : d->d_gsums, d->d_pa, d->vec_grid / 4,
+                                   d->st, false));
+  return 0;
+}
+
 // ---- CG1
 // (fused CG1: the vector recurrences run inside the SpMV launch; only the
 // halo rows of r_new are packed here)
@@ -1104,6 +1130,15 @@ int run_phases_eager(Group *g, bool init, long long iters) {
         for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
         for (cgx_dist *d : P) if ((rc = phase_sr1(d))) return rc;
         for (cgx_dist *d : P) if ((rc = sr1_reduce(d))) return rc;
+      }
+      return 0;
+    }
+    if (sru(P[0])) {
+      for (long long it = 0; it < iters; ++it) {
+        for (cgx_dist *d : P) if ((rc = phase_pack(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = phase_halo(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = phase_spmv(d))) return rc;
+        for (cgx_dist *d : P) if ((rc = sru_update(d))) return rc;
       }
       return 0;
     }
@@ -1266,8 +1301,11 @@ int group_run(Group *g, int maxit, double tol, int *iters) {
   // at 1)
   const bool sr0 = sr(g->parts[0]);
   // (the folded FIN_SR1 marks the stop one iteration later: one more)
+  // (unfused SR: the stop of iteration maxit is known to update_sr(maxit + 1)
+  // and reaches the state with the next FIN_SUM3_SR1: two more)
   const long long total = (long long)maxit + 1 + (fz(g->parts[0]) || sr1(g->parts[0]) ? 1 : 0) +
-                          (sr0 ? 1 : 0) + (sr1(g->parts[0]) && sr1_g(g->parts[0]) ? 1 : 0);
+                          (sr0 ? 1 : 0) + (sr1(g->parts[0]) && sr1_g(g->parts[0]) ? 1 : 0) +
+                          (sru(g->parts[0]) ? 2 : 0);
   const int fin_done = sr0 ? 2 : 1;
   if (tol <= 0.0) {
     if ((rc = run_phases(g, false, total))) return rc;

@@ -269,6 +269,9 @@ struct SpmvArgs {
   // stencil
   LapSpec lap;
   double inv_nx, inv_pl;  // 1 / nx, 1 / (nx ny): exact floor divisions (fdiv)
+  // CGX_ALG_SR without the fused step: the epilogue stores the (p.s, s.s)
+  // pair per workgroup (part[2 b], part[2 b + 1]) instead of p.s
+  int pair = 0;
 };
 
 // The fused HS step (single GPU, DIA layout): one launch does the previous
@@ -444,6 +447,14 @@ template <typename T>
 hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *stt,
                           const double *rr_part, int nrr, double *hist, int grid,
                           hipStream_t st, bool nt = false);
+// CGX_ALG_SR without the fused step (k_update_sr): the rest of iteration j
+// after its SpMV's (p.s, s.s) reduction -- r -= alpha s, p_new = r + beta p
+// (pn: the other p buffer), x += alpha p every other iteration, the exact
+// r.r partials (4 per workgroup of grid).  g: the all-reduced sums applied
+// privately (sr1_now; a partition's ranks), nullptr: *stt is current.
+template <typename T>
+hipError_t launch_update_sr(int n, T *x, T *r, const T *sv, const T *p, T *pn, CgState *stt,
+                            const double *g, double *rr_part, int grid, hipStream_t st, bool nt);
 template <typename T>
 hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w,
                              const CgState *stt, double *part, int grid, hipStream_t st);

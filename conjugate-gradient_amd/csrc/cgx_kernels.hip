@@ -171,6 +171,35 @@ __device__ __forceinline__ void epi_store(double dot, double *part) {
   }
 }
 
+// The epilogue of a CGX_ALG_SR SpMV (SpmvArgs::pair): the (p.s, s.s) pair
+// per workgroup, each reduced as epi_store, stored together at part[2 b]
+// (k_finalize FIN_SR1's layout); otherwise epi_store of p.s.
+template <int WPB>
+__device__ __forceinline__ void epi_store_p(double dot, double dot2, double *part, int pair) {
+  if (!pair) {
+    epi_store<WPB>(dot, part);
+    return;
+  }
+  __shared__ double red2[2][WPB];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  dot = wave_sum(dot);
+  dot2 = wave_sum(dot2);
+  if (lane == 0) {
+    red2[0][wid] = dot;
+    red2[1][wid] = dot2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = red2[0][0], s2 = red2[1][0];
+#pragma unroll
+    for (int w = 1; w < WPB; ++w) {
+      s = s + red2[0][w];
+      s2 = s2 + red2[1][w];
+    }
+    reinterpret_cast<double2 *>(part)[blockIdx.x] = make_double2(s, s2);
+  }
+}
+
 // The scalar lines of the recurrence (cg.c:113, 125-129; CG1 analogues) on
 // the reduced sums sa, sb -- run by ONE thread (k_finalize).
 __device__ void apply_fin(int op, double sa, double sb, CgState *st, double *hist,
@@ -441,7 +470,7 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
   T *lval = lval_all + wid * CAPW;
   int *lcol = lcol_all + wid * CAPW;
   const int wi = __builtin_amdgcn_readfirstlane(xcd_block() * WPB + wid);
-  double dot = 0.0;
+  double dot = 0.0, dot2 = 0.0;
   if (wi < a.items.count) {
     Blk B;
     if (!load_block(a, wi, B, LIST)) return;
@@ -518,10 +547,11 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
       if (EPI) {
         if (!have_x) xrow = a.x[r0 + lane];
         dot = (double)xrow * (double)acc;
+        dot2 = (double)acc * (double)acc;
       }
     }
   }
-  if (EPI) epi_store<WPB>(dot, a.part);
+  if (EPI) epi_store_p<WPB>(dot, dot2, a.part, a.pair);
 }
 
 // ------------------------------------------------------------- k_spmv_dc
@@ -548,7 +578,7 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
   unsigned char *lcode = lcode_all + wid * CAPC;
   int *ldict = ldict_all + wid * ND;
   const int wi = __builtin_amdgcn_readfirstlane(xcd_block() * WPB + wid);
-  double dot = 0.0;
+  double dot = 0.0, dot2 = 0.0;
   if (wi < a.items.count) {
     Blk B;
     if (!load_block(a, wi, B, LIST)) return;
@@ -632,10 +662,11 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
       if (EPI) {
         if (!have_x) xrow = a.x[row];
         dot = (double)xrow * (double)acc;
+        dot2 = (double)acc * (double)acc;
       }
     }
   }
-  if (EPI) epi_store<WPB>(dot, a.part);
+  if (EPI) epi_store_p<WPB>(dot, dot2, a.part, a.pair);
 }
 
 // ------------------------------------------------------------ k_spmv_dia
@@ -780,12 +811,18 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
     }
   }
   st_pair(a.y, r, a.n, a0, a1, NT);
-  double dot = 0.0;
+  double dot = 0.0, dot2 = 0.0;
   if (EPI) {
-    if (r < a.n) dot = (double)xr.x * (double)a0;
-    if (r + 1 < a.n) dot = dot + (double)xr.y * (double)a1;
+    if (r < a.n) {
+      dot = (double)xr.x * (double)a0;
+      dot2 = (double)a0 * (double)a0;
+    }
+    if (r + 1 < a.n) {
+      dot = dot + (double)xr.y * (double)a1;
+      dot2 = dot2 + (double)a1 * (double)a1;
+    }
   }
-  if (EPI) epi_store<4>(dot, a.part);
+  if (EPI) epi_store_p<4>(dot, dot2, a.part, a.pair);
 }
 
 // ------------------------------------------------- fused HS step (DIA-VI)
@@ -1891,15 +1928,19 @@ __global__ __launch_bounds__(256) void k_stencil(SpmvArgs<T> a) {
   a1 = f1.pi ? a1 + m1 * right : a1;
   a1 = f1.pj ? a1 + m1 * yp.y : a1;
   a1 = f1.pL ? a1 + m1 * zp.y : a1;
-  double dot = 0.0;
+  double dot = 0.0, dot2 = 0.0;
   if (r < n) {
     st_pair(a.y, r, n, a0, a1, NT);
     if (EPI) {
       dot = (double)c.x * (double)a0;
-      if (v1) dot = dot + (double)c.y * (double)a1;
+      dot2 = (double)a0 * (double)a0;
+      if (v1) {
+        dot = dot + (double)c.y * (double)a1;
+        dot2 = dot2 + (double)a1 * (double)a1;
+      }
     }
   }
-  if (EPI) epi_store<4>(dot, a.part);
+  if (EPI) epi_store_p<4>(dot, dot2, a.part, a.pair);
 }
 
 // ------------------------------------------------------- vector kernels
@@ -2395,6 +2436,139 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, c
         pn[k] = r[k] + bp;
       }
     }
+}
+
+// CGX_ALG_SR without the fused step (any layout -- CSR, DC, column panels,
+// cache-resident DIA, a partition's ranks): the SpMV stores
+// (p.s, s.s) pairs (SpmvArgs::pair), k_finalize FIN_SR1 -- or, on the ranks,
+// the all-reduce applied privately (sr1_now; FIN_SUM3_SR1 applies it to the
+// state one iteration later) -- gives alpha_j = r_j.r_j / p_j.s_j
+// (cg.c:113), beta_j from the estimate alpha (alpha s.s) - r.r (cg.c:129)
+// and the stop test of iteration j - 1 on the exact r_j.r_j (cg.c:125's
+// rule, one launch late); this launch does the rest of iteration j in ONE
+// pass, with oracle_solve_sr's roundings: r_{j+1} = r_j - alpha s_j,
+// p_{j+1} = r_{j+1} + beta p_j (into the other p buffer), x += alpha p_j
+// deferred pairwise as k_xpay_xf (an odd j adds alpha_{j-1} p_{j-1}, read
+// from pn before p_{j+1} overwrites it, then alpha_j p_j), and the exact
+// r_{j+1}.r_{j+1} partials (4 per workgroup, k_update_rf's layout) for the
+// next reduction.  Reads r, s, p (+ x, p_{j-1} every other launch), writes
+// r, p_{j+1} (+ x): 40 B/row + 12 on average, against the HS pair of
+// vector launches' 48 + 12.  done == 1 (a stop at an even iteration, its x
+// update deferred): x += alpha_def p_{j-1} only -- the next finalize marks
+// done = 2.  pn == p (a partition's ranks: p in place, its ghost tail
+// refreshed by the halo): x += alpha p every iteration, nothing deferred.
+template <typename T, bool NT>
+__global__ __launch_bounds__(kFoldBS) void k_update_sr(int n, T *__restrict__ x,
+                                                       T *__restrict__ r,
+                                                       const T *__restrict__ s, const T *p,
+                                                       T *pn, CgState *__restrict__ st,
+                                                       const double *g,
+                                                       double *__restrict__ rr_part) {
+  __shared__ double red[kFoldBS / kWave];
+  const Sr1Now sn = sr1_now(st, g);
+  if (sn.done > 1) return;  // uniform
+  typedef typename Vec16<T>::type V;
+  constexpr int W = Vec16<T>::W;
+  const int nv = n / W;
+  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+  const T alpha_d = (T)st->alpha_def;
+  const bool defer = pn != p;
+  if (sn.done == 1) {  // the stop iteration's deferred x update, nothing else
+    if (!defer) return;  // x is complete
+    for (int i = gid; i < nv; i += stride) {
+      V xv = reinterpret_cast<const V *>(x)[i];
+      const V pd = reinterpret_cast<const V *>(pn)[i];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T ad = alpha_d * pd[j];
+        xv[j] = xv[j] + ad;
+      }
+      reinterpret_cast<V *>(x)[i] = xv;
+    }
+    if (gid == 0)
+      for (int k = nv * W; k < n; ++k) {
+        const T ad = alpha_d * pn[k];
+        x[k] = x[k] + ad;
+      }
+    return;
+  }
+  const int k = sn.k_u;  // this iteration (fin_sr1 made it k_u)
+  const bool odd = defer && (k & 1) != 0;       // x += alpha_{k-1} p_{k-1} + alpha_k p_k
+  const bool xup = !defer || odd, xone = !defer;  // xone: x += alpha_k p_k alone
+  const T alpha = (T)sn.alpha, beta = (T)sn.beta;
+  if (defer && !odd && blockIdx.x == 0 && threadIdx.x == 0)
+    st->alpha_def = sn.alpha;  // read at k + 1
+  double acc = 0.0;
+  for (int i = gid; i < nv; i += stride) {
+    V rv = reinterpret_cast<const V *>(r)[i];
+    const V sv = reinterpret_cast<const V *>(s)[i];
+    V pv = reinterpret_cast<const V *>(p)[i];
+    V xv = V(), pd = V();
+    if (xup) xv = reinterpret_cast<const V *>(x)[i];
+    if (odd) pd = reinterpret_cast<const V *>(pn)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T as = alpha * sv[j];
+      rv[j] = rv[j] - as;
+      acc = acc + (double)rv[j] * (double)rv[j];
+    }
+    if (xup) {
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (!xone) {
+          const T ad = alpha_d * pd[j];
+          xv[j] = xv[j] + ad;
+        }
+        const T ap = alpha * pv[j];
+        xv[j] = xv[j] + ap;
+      }
+      if constexpr (NT) __builtin_nontemporal_store(xv, reinterpret_cast<V *>(x) + i);
+      else reinterpret_cast<V *>(x)[i] = xv;
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const T bp = beta * pv[j];
+      pv[j] = rv[j] + bp;
+    }
+    if constexpr (NT) {
+      __builtin_nontemporal_store(rv, reinterpret_cast<V *>(r) + i);
+      __builtin_nontemporal_store(pv, reinterpret_cast<V *>(pn) + i);
+    } else {
+      reinterpret_cast<V *>(r)[i] = rv;
+      reinterpret_cast<V *>(pn)[i] = pv;
+    }
+  }
+  if (gid == 0)
+    for (int e = nv * W; e < n; ++e) {
+      const T as = alpha * s[e];
+      const T re = r[e] - as;
+      acc = acc + (double)re * (double)re;
+      const T pe = p[e];
+      if (xup) {
+        T xe = x[e];
+        if (!xone) {
+          const T ad = alpha_d * pn[e];
+          xe = xe + ad;
+        }
+        const T ap = alpha * pe;
+        x[e] = xe + ap;
+      }
+      const T bp = beta * pe;
+      r[e] = re;
+      pn[e] = re + bp;
+    }
+  // one partial per 256-thread quarter (k_update_rf's layout and order)
+  acc = wave_sum(acc);
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) red[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x < kFoldBS / 256) {
+    constexpr int WQ = 256 / kWave;
+    double q = red[threadIdx.x * WQ];
+#pragma unroll
+    for (int w = 1; w < WQ; ++w) q = q + red[threadIdx.x * WQ + w];
+    rr_part[blockIdx.x * (kFoldBS / 256) + threadIdx.x] = q;
+  }
 }
 
 // Chronopoulos-Gear update: p = r + beta p; s = w + beta s; x += alpha p;
@@ -3258,6 +3432,18 @@ hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *s
 }
 
 template <typename T>
+hipError_t launch_update_sr(int n, T *x, T *r, const T *sv, const T *p, T *pn, CgState *stt,
+                            const double *g, double *rr_part, int grid, hipStream_t st, bool nt) {
+  if (nt)
+    hipLaunchKernelGGL((k_update_sr<T, true>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r, sv, p,
+                       pn, stt, g, rr_part);
+  else
+    hipLaunchKernelGGL((k_update_sr<T, false>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r, sv, p,
+                       pn, stt, g, rr_part);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w, const CgState *stt,
                              double *part, int grid, hipStream_t st) {
   hipLaunchKernelGGL((k_cg1_update<T, kVecBS>), dim3(grid), dim3(kVecBS), 0, st, n, x, p, r, s,
@@ -3416,6 +3602,8 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
                                           const double *, double *, bool);                       \
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \
                                         const double *, int, double *, int, hipStream_t, bool);  \
+  template hipError_t launch_update_sr<T>(int, T *, T *, const T *, const T *, T *, CgState *,    \
+                                          const double *, double *, int, hipStream_t, bool);      \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *, const T *, const CgState *,  \
                                            double *, int, hipStream_t);                          \
   template hipError_t launch_dot_seq<T>(int, const T *, const T *, double *, const int *,        \

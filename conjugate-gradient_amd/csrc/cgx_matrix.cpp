@@ -1087,13 +1087,18 @@ int DevMatrix::partials(Items it) const {
 
 template <typename T>
 hipError_t DevMatrix::spmv(const T *x, T *y, double *part, const int *done, Items it,
-                           hipStream_t s, int *nparts, LaunchEv ev) const {
+                           hipStream_t s, int *nparts, LaunchEv ev, bool pair) const {
   if (nparts) *nparts = partials(it);
   if (layout == L_STENCIL) it = Items{nullptr, 0, (n + kDiaSliceRows - 1) / kDiaSliceRows};
-  if (npanel <= 1) return launch_spmv<T>(args<T>(x, y, part, done, it), s, ev);
+  if (npanel <= 1) {
+    SpmvArgs<T> a = args<T>(x, y, part, done, it);
+    a.pair = pair ? 1 : 0;
+    return launch_spmv<T>(a, s, ev);
+  }
   for (int q = 0; q < npanel; ++q) {
     SpmvArgs<T> a = args<T>(x, y, q + 1 == npanel ? part : nullptr, done,
                             Items{nullptr, panel_first[q], panel_count[q]});
+    a.pair = pair && q + 1 == npanel ? 1 : 0;
     a.rp = d_rp + (size_t)q * ((size_t)n + 1);
     a.yacc = q ? y : nullptr;
     a.capw = capw;
@@ -1111,8 +1116,8 @@ template SpmvArgs<double> DevMatrix::args<double>(const double *, double *, doub
 template SpmvArgs<float> DevMatrix::args<float>(const float *, float *, double *, const int *,
                                                 Items) const;
 template hipError_t DevMatrix::spmv<double>(const double *, double *, double *, const int *,
-                                            Items, hipStream_t, int *, LaunchEv) const;
+                                            Items, hipStream_t, int *, LaunchEv, bool) const;
 template hipError_t DevMatrix::spmv<float>(const float *, float *, double *, const int *, Items,
-                                           hipStream_t, int *, LaunchEv) const;
+                                           hipStream_t, int *, LaunchEv, bool) const;
 
 }  // namespace cgx

@@ -113,10 +113,11 @@ struct DevMatrix {
   // One SpMV (panels: one launch per panel, rows continuing their sums;
   // the epilogue partials on the last panel).  Returns the partial count.
   // ev: timing events around the whole SpMV (start on its first launch,
-  // stop on its last).
+  // stop on its last).  pair: (p.s, s.s) pairs instead of p.s partials
+  // (SpmvArgs::pair; 2 doubles per partial).
   template <typename T>
   hipError_t spmv(const T *x, T *y, double *part, const int *done, Items it, hipStream_t s,
-                  int *nparts = nullptr, LaunchEv ev = LaunchEv{}) const;
+                  int *nparts = nullptr, LaunchEv ev = LaunchEv{}, bool pair = false) const;
   // The number of partials spmv() writes for the given items.
   int partials(Items it) const;
 };

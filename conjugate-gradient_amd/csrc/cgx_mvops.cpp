@@ -276,16 +276,11 @@ int run_solve(const struct __mv_sparse *A, const struct __mv_sparse *b, struct _
   int iters = maxit + 1, ran = g_alg;
   MatTiming mt;
   rc = with_matrix(s, A, [&] {
-    // CGX_ALG_SR only where the matrix takes its one-launch step (the plane-
-    // marched DIA layout); otherwise the reference's HS -- reported in
-    // cgx_ops_last_timing().alg
+    // CGX_ALG_SR runs on every matrix (round 5): the one-launch plane march
+    // where the matrix plans one, the unfused two-launch SR step otherwise;
+    // cgx_ops_last_timing().alg reports the recurrence that ran
     ran = g_alg;
     int r = cgx_solver_set_mode(s, g_mode, ran);
-    if (r == 0 && ran == CGX_ALG_SR) {
-      cgx_info inf;
-      r = cgx_solver_info(s, &inf);
-      if (r == 0 && !inf.fused) r = cgx_solver_set_mode(s, g_mode, ran = CGX_ALG_HS);
-    }
     if (r == 0) r = cgx_solver_set_rhs(s, b->values);
     if (r == 0 && A->size > 0) r = cgx_solver_run(s, maxit, tol, &iters);
     return r;

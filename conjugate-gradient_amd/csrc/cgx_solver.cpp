@@ -220,6 +220,8 @@ int alloc_vectors(cgx_solver *s) {
   // CGX_ALG_SR: one (p.s, s.s) pair per march workgroup, at most one
   // workgroup per slice and chain (segments of one step)
   if (s->A.mq > 0) s->part_cap = std::max(s->part_cap, 2 * (s->A.items() + s->A.mchains) + 2);
+  // unfused CGX_ALG_SR: the SpMV's (p.s, s.s) pair per workgroup
+  s->part_cap = std::max(s->part_cap, 2 * s->A.partials(s->A.all_items()) + 2);
   int rc;
   if ((rc = dev_alloc(&s->d_b, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_x, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_r, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_p, nv, &s->vec_bytes)) ||
@@ -262,11 +264,13 @@ int ensure_rsw2(cgx_solver *s) {
   return 0;
 }
 
-// A recurrence the loaded matrix cannot run (SR without the plane-marched
-// DIA step) is refused before anything is enqueued.
+// A recurrence the loaded matrix cannot run is refused before anything is
+// enqueued.  (CGX_ALG_SR runs on every layout since round 5: the one-launch
+// plane march where the matrix plans one, else the unfused two-launch step
+// -- SpMV with (p.s, s.s) pairs, then k_update_sr.)
 int check_runnable(const cgx_solver *s) {
-  if (s->alg == CGX_ALG_SR && !fused(s)) {
-    set_error("CGX_ALG_SR on one GPU needs the plane-marched DIA step (cgx_info.fuse_march)");
+  if (s->alg == CGX_ALG_SR && s->mode != CGX_MODE_FAST) {
+    set_error("CGX_ALG_SR is defined in fast mode only");
     return CGX_EINVAL;
   }
   return 0;
@@ -333,6 +337,25 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   const int n = s->A.n;
   T *x = (T *)s->d_x, *r = (T *)s->d_r, *p = (T *)s->d_p, *sv = (T *)s->d_s, *w = (T *)s->d_w;
   int np = 0;
+  if (s->alg == CGX_ALG_SR && !fused(s)) {
+    // unfused SR (any layout): s = A p with the (p.s, s.s) pair per
+    // workgroup (cg.c:111), k_finalize FIN_SR1 (alpha cg.c:113, the
+    // estimate's beta cg.c:129, the stop test of the previous iteration on
+    // the exact r.r), k_update_sr: r, p, x of the iteration in one pass
+    // (cg.c:115-132) + the exact r.r partials -- two launches and one
+    // reduction per iteration (oracle_solve_sr)
+    const int q = s->pbuf;
+    T *pc = (T *)(q ? s->d_p2 : s->d_p), *pn = (T *)(q ? s->d_p : s->d_p2);
+    CGX_HIP(s->A.spmv<T>(pc, sv, s->d_pb, &s->d_st->done, s->A.all_items(), st, &np,
+                         LaunchEv{ev0, ev1}, true));
+    if (2 * np > s->part_cap) return CGX_EINVAL;
+    CGX_HIP(launch_finalize(FIN_SR1, s->d_pb, np, nullptr, 0, s->d_st, s->d_hist, nullptr, st,
+                            s->d_pa, s->vec_grid));
+    CGX_HIP(launch_update_sr<T>(n, x, r, sv, pc, pn, s->d_st, nullptr, s->d_pa, s->vec_grid / 4,
+                                st, s->A.nt));
+    s->pbuf ^= 1;
+    return 0;
+  }
   if (s->alg == CGX_ALG_SR) {
     // k_sr1_dia_m: r = r - alpha s, p = r + beta p (window rows), x update,
     // s = A p, (p.s, s.s) pairs + r.r per workgroup; k_finalize FIN_SR1: the

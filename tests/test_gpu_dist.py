@@ -635,14 +635,61 @@ def test_sr_rccl_one_rank_graph_parity():
             assert H.same_bits_or_both_nan(h0, h1), key
 
 
-def test_sr_refused_without_fused_step():
-    """SR has no unfused form: a CSR layout (or CGX_FUSE_OFF) makes run()
-    fail with CGX_EINVAL and a message, not run another recurrence."""
-    rp, col, val = cgx.laplacian3d(12, 10, 8)
-    b = np.ones(len(rp) - 1)
-    for layout, fused in (("csr", "auto"), ("auto", "off")):
-        with pytest.raises(cgx.CgxError, match="CGX_ALG_SR"):
-            _sr_group(rp, col, val, b, 2, [(5, 0.0)], layout=layout, fused=fused)
+@pytest.mark.parametrize("layout,fused,P", [("csr", "auto", 1), ("csr", "auto", 2),
+                                            ("dc", "auto", 3), ("auto", "off", 2),
+                                            ("csr", "auto", 8)])
+def test_sr_unfused_partitions(layout, fused, P):
+    """CGX_ALG_SR on ranks whose layout takes no fused step
+    (CSR, DC, CGX_FUSE_OFF) runs the unfused SR step -- the SpMV's (p.s, s.s)
+    pairs, ONE all-reduce of (p.s, s.s, r.r) per iteration, k_update_sr with
+    p in place and x every iteration -- within 1e-10 of oracle_solve_sr at
+    fixed max_iter, and at a 1e-10 stop the iteration count within 1 of it
+    and of the HS oracle, x within 1e-9, true residual below the tolerance."""
+    rp, col, val = cgx.laplacian3d(24, 20, 30)
+    b = np.random.default_rng(31).standard_normal(len(rp) - 1)
+    runs = [(0, 0.0), (1, 0.0), (2, 0.0), (17, 0.0), (3000, 1e-10)]
+    out, st = _sr_group(rp, col, val, b, P, runs, layout=layout, fused=fused)
+    assert all(s["alg"] == cgx.CGX_ALG_SR and s["fused"] == 0 and s["march"] == 0 for s in st)
+    for (maxit, _), (its, x, hist) in zip(runs[:-1], out[:-1]):
+        x_sr, its_sr, h_sr = H.o_solve(maxit, 0.0, rp, col, val, b, sr=True)
+        assert its == its_sr == maxit + 1
+        assert np.linalg.norm(x - x_sr) <= 1e-10 * np.linalg.norm(x_sr), maxit
+        assert np.allclose(hist, h_sr[:its], rtol=1e-8, atol=0)
+    its, x, _ = out[-1]
+    x_sr, its_sr, _ = H.o_solve(3000, 1e-10, rp, col, val, b, sr=True)
+    x_hs, its_hs, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+    assert abs(its - its_sr) <= 1 and abs(its - its_hs) <= 1 and its < 3000
+    assert np.linalg.norm(x - x_sr) <= 1e-9 * np.linalg.norm(x_sr)
+    assert np.linalg.norm(x - x_hs) <= 1e-9 * np.linalg.norm(x_hs)
+    assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
+
+
+def test_sr_unfused_rccl_one_rank_graph_parity():
+    """The unfused SR step over a 1-rank RCCL communicator (every transport
+    phase: pack, all-reduce of the three sums, the privately applied scalar
+    step) graph-replayed and eager, bit-identical, within 1e-10 of
+    oracle_solve_sr."""
+    rp, col, val = cgx.varcoef3d(30, 20, 16, seed=5)
+    n = len(rp) - 1
+    b = np.random.default_rng(3).standard_normal(n)
+    res = {}
+    for graph in (True, False):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+        try:
+            d.set_alg(cgx.CGX_ALG_SR)
+            d.set_layout("csr")
+            d.set_graph(graph)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            its = d.run(25)
+            assert d.info()["fused"] == 0
+            res[graph] = (its, d.x())
+        finally:
+            d.close()
+    assert res[True][0] == res[False][0] == 26
+    assert H.same_bits_or_both_nan(res[True][1], res[False][1])
+    x_sr, _, _ = H.o_solve(25, 0.0, rp, col, val, b, sr=True)
+    assert np.linalg.norm(res[True][1] - x_sr) <= 1e-10 * np.linalg.norm(x_sr)
 
 
 def test_fuse_refusal_reported_for_plane_cutting_partitions():

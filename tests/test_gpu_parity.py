@@ -573,23 +573,28 @@ def test_fuse_status_reports_why():
             assert i["fused"] == (1 if want == cgx.CGX_FUSE_STATUS_RUNS else 0)
 
 
-def test_dropin_sr_falls_back_to_hs():
-    """cgx_ops_set_mode(FAST, SR) through the drop-in
-    solve() (cg.c:72's caller): a matrix without the plane-marched DIA step
-    (the random-pattern CSR fixture) runs the reference's HS recurrence and
-    cgx_ops_last_timing() says so, against oracle_solve; a 3-D Laplacian
-    whose planes are 8 slices apart runs the one-launch SR step, against
-    oracle_solve_sr and the HS oracle (the bars of test_sr_single_launch_vs_oracle)."""
+def test_dropin_sr_every_matrix():
+    """cgx_ops_set_mode(FAST, SR) through the
+    drop-in solve() (cg.c:72's caller): a matrix without the plane-marched
+    DIA step (the random-pattern CSR fixture) runs the unfused two-launch SR
+    step (SpMV with (p.s, s.s) pairs, k_update_sr) -- within 1e-9 of the HS
+    goldens at the tolerance stop (the stop iteration within 1) and within
+    1e-10 of oracle_solve_sr; a 3-D Laplacian whose planes are 8 slices
+    apart runs the one-launch SR step, against oracle_solve_sr and the HS
+    oracle (the bars of test_sr_single_launch_vs_oracle).
+    cgx_ops_last_timing() reports SR for both."""
     cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_SR)
     try:
         g = H.load_golden("rand_spd_2000")
         A = cgx.Mv(g["val"], g["col"], g["row_ptr"])
         b = cgx.Mv(g["b"])
         x, its = cgx.solve(A, b, 1e-10, 1000)
-        assert cgx.ops_last_timing()["alg"] == cgx.CGX_ALG_HS
+        assert cgx.ops_last_timing()["alg"] == cgx.CGX_ALG_SR
         x_o, its_o, _ = H.o_solve(1000, 1e-10, g["row_ptr"], g["col"], g["val"], g["b"])
-        assert its == its_o
-        assert rel(x, x_o) <= FAST_RTOL
+        x_sr, its_sr, _ = H.o_solve(1000, 1e-10, g["row_ptr"], g["col"], g["val"], g["b"],
+                                    sr=True)
+        assert abs(its - its_o) <= 1 and its == its_sr, (its, its_o, its_sr)
+        assert rel(x, x_o) <= 1e-9 and rel(x, x_sr) <= 1e-10
         rp, col, val = H.laplacian3d(64, 64, 40)
         bv = np.random.default_rng(23).standard_normal(len(rp) - 1)
         A, b = cgx.Mv(val, col, rp), cgx.Mv(bv)
@@ -602,6 +607,73 @@ def test_dropin_sr_falls_back_to_hs():
             assert rel(x, x_sr) <= 1e-10 and rel(x, x_hs) <= 1e-9, tol
     finally:
         cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
+
+
+def sr_unfused_cases():
+    # (name, system): every layout the unfused SR step runs on
+    for name in ("rand_spd_2000", "lap2d_32", "lap3d_12", "dense128"):
+        g = H.load_golden(name)
+        yield name, g["row_ptr"], g["col"], g["val"], g["b"], "auto"
+    rp, col, val = H.laplacian3d(40, 30, 24)
+    b = np.random.default_rng(5).standard_normal(len(rp) - 1)
+    for layout in ("csr", "dc", "dia"):
+        yield f"lap3d_40x30x24_{layout}", rp, col, val, b, layout
+
+
+@pytest.mark.parametrize("case", list(sr_unfused_cases()), ids=lambda c: c[0] + "_" + c[5])
+def test_sr_unfused_vs_oracle(case):
+    """CGX_ALG_SR without the plane march -- two launches
+    and ONE reduction per iteration on any layout (CSR, DC, DIA without a
+    march, column panels): at fixed max_iter within 1e-10 of
+    oracle_solve_sr (the recurrence it restates; only the grouping of the
+    dot products differs) with its r.r history within 1e-8; at a 1e-10
+    tolerance stop the iteration count of oracle_solve_sr, within 1 of the
+    HS oracle's, x within 1e-9 of HS."""
+    name, rp, col, val, b, layout = case
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR, layout=layout) as s:
+        s.set_matrix(rp, col, val)
+        s.set_march(0)  # the unfused step even where a march plan exists
+        i = s.info()
+        assert i["fused"] == 0 and i["alg"] == cgx.CGX_ALG_SR
+        for maxit in (0, 1, 2, 7, 20):
+            s.set_rhs(b)
+            its = s.run(maxit)
+            x_sr, its_sr, h_sr = H.o_solve(maxit, 0.0, rp, col, val, b, sr=True)
+            assert its == its_sr == maxit + 1
+            assert rel(s.x(), x_sr) <= 1e-10, (maxit, rel(s.x(), x_sr))
+            assert np.allclose(s.history(its), h_sr[:its], rtol=1e-8, atol=0)
+        s.set_rhs(b)
+        its = s.run(5000, 1e-10)
+        x = s.x()
+    x_sr, its_sr, _ = H.o_solve(5000, 1e-10, rp, col, val, b, sr=True)
+    x_hs, its_hs, _ = H.o_solve(5000, 1e-10, rp, col, val, b)
+    assert its == its_sr and abs(its - its_hs) <= 1, (its, its_sr, its_hs)
+    assert rel(x, x_sr) <= 1e-9 and rel(x, x_hs) <= 1e-9
+
+
+def test_sr_unfused_graph_and_bench():
+    """The unfused SR step graph-replayed and eager bit-identical, and its
+    bench loop (the bench's general-coefficient leg) runs."""
+    rp, col, val = cgx.varcoef3d(40, 30, 24, seed=3)
+    b = np.random.default_rng(9).standard_normal(len(rp) - 1)
+    xs = []
+    for graph in (True, False):
+        with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+            s.set_matrix(rp, col, val)
+            assert s.info()["fused"] == 0
+            s.set_rhs(b)
+            s.bench_prepare(0)
+            s.bench_run(33, graph=graph)
+            xs.append(s.x())
+    assert H.same_bits_or_both_nan(xs[0], xs[1])
+    assert np.all(np.isfinite(xs[0]))
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        s.bench_prepare(3)
+        ms, sp = s.bench_run(20, graph=False, spmv_events=True)
+        assert ms > 0 and 0 < sp <= ms / 20 * 1.01
+        assert s.bench_run(20)[0] > 0
 
 
 def test_sr_fuse_status():
@@ -617,8 +689,7 @@ def test_sr_fuse_status():
         i = s.info()
         assert i["fused"] == 0 and i["fuse_status"] == cgx.CGX_FUSE_STATUS_NO_MARCH
         s.set_rhs(np.ones(len(rp) - 1))
-        with pytest.raises(cgx.CgxError, match="plane-marched"):
-            s.run(5)
+        assert s.run(5) == 6  # round 5: the unfused SR step runs instead
     rp, col, val = H.laplacian2d(300, 200)
     with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
         s.set_matrix(rp, col, val)
