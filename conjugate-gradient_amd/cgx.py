@@ -107,6 +107,7 @@ _SIGS = {
     "cgx_solver_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_march": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_solver_set_sr_chain": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_matrix": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                              _i32p, _i32p, _f64p]),
     "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
@@ -179,6 +180,7 @@ _SIGS = {
     "cgx_dist_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_graph": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_march": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_set_sr_chain": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_run": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
                                     ctypes.POINTER(ctypes.c_int)]),
@@ -370,6 +372,11 @@ class Solver:
         """Plane march of the fused HS step (cgx_solver_set_march): -1 auto,
         0 off (the per-slice fused kernel), > 0 slices of a chain per workgroup."""
         check(lib().cgx_solver_set_march(self._h, int(steps)), "set_march")
+
+    def set_sr_chain(self, rows=0):
+        """Chain width (rows) of CGX_ALG_SR's one-launch plane march
+        (cgx_solver_set_sr_chain): 0 auto, > 0 that width."""
+        check(lib().cgx_solver_set_sr_chain(self._h, int(rows)), "set_sr_chain")
 
     def set_layout(self, layout):
         """CGX_LAYOUT_* (or its name) for the next set_matrix / gen_laplacian."""
@@ -706,6 +713,11 @@ class DistSolver:
         numbering (cgx_dist_set_march): -1 auto, 0 off (two-launch fused SR),
         > 0 interior steps per workgroup."""
         check(lib().cgx_dist_set_march(self._h, int(steps)), "dist_set_march")
+
+    def set_sr_chain(self, rows=0):
+        """Chain width (rows) of the ranks' one-launch SR march
+        (cgx_dist_set_sr_chain): 0 auto, > 0 that width."""
+        check(lib().cgx_dist_set_sr_chain(self._h, int(rows)), "dist_set_sr_chain")
 
     def set_fused(self, mode):
         """The fused HS step on all ranks or none: "auto", True, False."""

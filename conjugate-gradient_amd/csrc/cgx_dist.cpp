@@ -138,6 +138,7 @@ struct cgx_dist {
   std::vector<int> recv_pos; // in-place position of each owner's first ghost row
   size_t vfront = 0;         // entries before element 0 of the ghosted vectors
   int march = -1;            // cgx_dist_set_march: -1 auto, 0 off, > 0 interior steps/segment
+  int sr_chain = 0;          // cgx_dist_set_sr_chain: 0 auto, > 0 chain width (rows)
   bool mi_all = false;       // every partition runs the one-launch SR step (agreed)
   double *d_pq = nullptr, *d_pc = nullptr;  // its (p.s, s.s) pairs and r.r partials
   int gi1 = 0, gb1 = 0;      // workgroups of its interior / boundary launch
@@ -241,20 +242,22 @@ const double *sr1_g(const cgx_dist *d);
 bool has_peers(const cgx_dist *d);
 
 // The one-launch SR step's launch shapes: segments (set_march's length, or
-// the balanced count sr1_pick_nseg finds for the device) and, on a rank with
+// the segment count and chain width sr1_pick_shape finds for the device) and, on a rank with
 // neighbours, the edge rows k_sr1_edge recomputes after the halo -- [0, elo)
 // below when there are ghost rows below (the rows that reach column < 0:
 // -(lowest diagonal offset)), [ehi, n) above (n - the highest offset), both
 // bounds even (row pairs); a slab too thin to have interior rows is all edge.
 struct Sr1Plan {
-  int nseg, len, elo, ehi;
+  int nseg, len, elo, ehi, cw;
 };
 
 Sr1Plan sr1_plan(const cgx_dist *d) {
   const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
   Sr1Plan p;
-  p.nseg = d->march > 0 ? 0 : sr1_pick_nseg(a, d->cus);
+  const Sr1Shape sh = sr1_pick_shape(a, d->cus, d->sr_chain);
+  p.nseg = d->march > 0 ? 0 : sh.nseg;
   p.len = d->march > 0 ? d->march : 0;
+  p.cw = d->march > 0 && d->sr_chain == 0 ? 0 : sh.cw;
   p.elo = 0;
   p.ehi = 0x7fffffff;
   if (has_peers(d) && a.ndiag > 0) {
@@ -495,10 +498,10 @@ int upload_local(cgx_dist *d, long long n_global, int n_loc, int nnz, const int 
   }
   if (d->ai_ok) {
     // the one-launch SR step's partials: one (p.s, s.s) pair and one r.r per
-    // workgroup of its launches (at most: every step its own workgroup, and
+    // workgroup of its launches (at most: sr1_max_grid for the march, and
     // one edge workgroup per 512 rows)
     const SpmvArgs<double> a = d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
-    const int cap = a.mchains * ((a.mslices + a.mq - 1) / a.mq) + (d->n_loc + 511) / 512 + 8;
+    const int cap = sr1_max_grid(a.mslices) + (d->n_loc + 511) / 512 + 8;
     if ((rc = dev_alloc(&d->d_pq, (size_t)cap * 16, cb)) || (rc = dev_alloc(&d->d_pc, (size_t)cap * 8, cb))) {
       free_system(d);
       return rc;
@@ -837,6 +840,7 @@ int phase_sr1(cgx_dist *d) {
                     d->d_pq, d->d_pc, pl.len};
   f.g = sr1_g(d);
   f.nseg = pl.nseg;
+  f.cw = pl.cw;
   f.elo = pl.elo;
   f.ehi = pl.ehi;
   const int gi = sr1_grid(a, f);
@@ -1571,6 +1575,19 @@ int cgx_dist_set_march(cgx_dist *d, int steps) {
   return 0;
 }
 
+int cgx_dist_set_sr_chain(cgx_dist *d, int rows) {
+  if (!d || (d->local && !d->owns_group) || rows < 0) return CGX_EINVAL;
+  for (cgx_dist *o : d->group->parts) {
+    if (o->gexec[0]) {
+      (void)hipStreamSynchronize(o->st);
+      drop_graph(o);
+    }
+    o->sr_chain = rows;
+    o->bench_ready = false;
+  }
+  return 0;
+}
+
 int cgx_dist_set_graph(cgx_dist *d, int on) {
   if (!d) return CGX_EINVAL;
   d->use_graph = on != 0;
@@ -1680,7 +1697,8 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
     const Sr1Plan pl = sr1_plan(d);
     const SpmvArgs<double> a =
         d->Ai.args<double>(nullptr, nullptr, nullptr, nullptr, d->Ai.all_items());
-    const int L = (a.mslices + a.mq - 1) / a.mq;
+    const long long QR = (long long)a.mq * kDiaSliceRows;
+    const int L = (int)((a.n + QR - 1) / QR);
     s->march = std::max(1, pl.len > 0 ? pl.len : (L + pl.nseg - 1) / std::max(1, pl.nseg));
   } else {
     s->march = 0;

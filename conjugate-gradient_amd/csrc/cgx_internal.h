@@ -321,6 +321,7 @@ struct Sr1Args {
   double *pq, *pc;
   int march;  // steps per segment (nseg == 0)
   int nseg = 0;
+  int cw = 0;  // chain width in rows (even, <= msb slices; 0: msb slices)
   int elo = 0, ehi = 0x7fffffff;
   // partitioned: the all-reduced (p.s, s.s, r.r) of the last iteration,
   // applied (FIN_SR1's step) to a private copy of *st when st->sr_pend --
@@ -369,13 +370,21 @@ int march_grid(const SpmvArgs<T> &a, int len);
 // workgroups (= partial pairs) of one k_sr1_dia_m launch
 template <typename T>
 int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
-// Segments per chain on `cus` CUs: the nseg whose launch takes the fewest
-// step-times in the resident-workgroup model (ceil(chains nseg / slots)
-// rounds of ceil(L / nseg) + 2 windows, L the longest chain; slots from the
-// kernel's occupancy).  An explicit march length (> 0) is used as given
-// instead (nseg 0).
+// Launch shape of k_sr1_dia_m on `cus` CUs: segments per chain and chain
+// width (rows), the pair whose launch takes the fewest window-times in the
+// resident-workgroup model (ceil(chains nseg / slots) rounds of ceil(L /
+// nseg) + 2 windows, L the longest chain; slots from the kernel's
+// occupancy).  cw_force > 0: that chain width, only nseg picked.  An
+// explicit march length (> 0) is used as given instead (nseg 0).
+struct Sr1Shape {
+  int nseg, cw;
+};
+// the most workgroups one k_sr1_dia_m launch may have (its partial pairs)
+// for a matrix of `slices` 512-row slices: sr1_pick_shape and
+// launch_sr1_march keep to it
+inline int sr1_max_grid(int slices) { return 4 * slices + 64; }
 template <typename T>
-int sr1_pick_nseg(const SpmvArgs<T> &a, int cus);
+Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a, int cus, int cw_force = 0);
 // workgroups (= partial pairs) of k_sr1_edge over f's edge rows of n rows
 template <typename T>
 int sr1_edge_grid(int n, const Sr1Args<T> &f);

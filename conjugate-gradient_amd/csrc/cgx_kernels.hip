@@ -1340,9 +1340,14 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   typedef typename Pair<T>::type P;
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int w = xcd_block();
-  const int chain = w % a.mchains, seg = w / a.mchains;
-  const int j0 = chain * SB;
-  const int msteps = (a.mslices - j0 + a.mq - 1) / a.mq;
+  // chains of cw rows (f.cw, even, <= SR; 0: SR = SB slices) side by side in
+  // each step of QR rows; chain c's step m holds rows [c0 + m QR, + wc)
+  const int QR = a.mq * kDiaSliceRows;
+  const int CW = f.cw > 0 ? f.cw : SR;
+  const int nch = (QR + CW - 1) / CW;
+  const int chain = w % nch, seg = w / nch;
+  const int c0 = chain * CW, wc = min(CW, QR - c0);
+  const int msteps = c0 < a.n ? (a.n - c0 + QR - 1) / QR : 0;
   int m0, m1;
   if (f.nseg > 0) {  // the chain's steps in nseg balanced segments
     m0 = (int)((long long)seg * msteps / f.nseg);
@@ -1360,11 +1365,10 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   const T alpha = (T)sn.alpha, beta = (T)sn.beta, alpha_d = (T)f.st->alpha_def;
   if (!first && !odd && !stop && blockIdx.x == 0 && t == 0)
     const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
-  const int QR = a.mq * kDiaSliceRows;
   const int padn = a.mslices * kDiaSliceRows;
   const bool nt = a.nt != 0;
-  const int wn = SR + a.hl + a.hr, ws = a.mws;
-  auto base_of = [&](int m) { return (j0 + m * a.mq) * kDiaSliceRows; };
+  const int wn = wc + a.hl + a.hr, ws = a.mws;
+  auto base_of = [&](int m) { return c0 + m * QR; };
   auto slot = [&](int m) { return ring + ((m + NRING) % NRING) * ws; };
   auto rslot = [&](int m) { return rbuf + ((m + NRB) % NRB) * SR; };
   struct XOps {
@@ -1414,7 +1418,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     // fin_sr1 stopped at an even iteration k (k_u): its deferred x +=
     // alpha_k p_k only, p_k in the p_new buffer of this launch
     for (int m = m0; m < m1; ++m) {
-      const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + SR), rs = r < a.n ? r : 0;
+      const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + wc), rs = r < a.n ? r : 0;
       const P pd = ld_pair((const T *)f.pnew, rs), xo = ld_pair(f.x, rs);
       const T d0 = alpha_d * pd.x, d1 = alpha_d * pd.y;
       if (r < rend) st_pair(f.x, r, rend, xo.x + d0, xo.y + d1, false);
@@ -1482,7 +1486,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     if (xup && m + 1 < m1) load_x(m + 1, nx);
     __syncthreads();
     const int base = base_of(m), r = base + 2 * t;
-    const int rend = min(a.n, base + SR);
+    const int rend = min(a.n, base + wc);
     const T *cur = slot(m), *prv = slot(m - 1), *nxt = slot(m + 1);
     const T *rb = rslot(m);
     const int rw = 2 * t + a.hl;
@@ -3146,13 +3150,29 @@ static SpmvArgs<T> sr1_args(const SpmvArgs<T> &a0) {
   return a;
 }
 
+// chains per step (k_sr1_dia_m: QR = mq slices of rows in chains of cw rows)
+// and chain 0's step count (the longest chain)
+template <typename T>
+static int sr1_chains(const SpmvArgs<T> &a, int cw) {
+  const int QR = a.mq * kDiaSliceRows;
+  const int w = cw > 0 ? cw : a.msb * kDiaSliceRows;
+  return (QR + w - 1) / w;
+}
+
+template <typename T>
+static int sr1_steps(const SpmvArgs<T> &a) {
+  const long long QR = (long long)a.mq * kDiaSliceRows;
+  return a.n > 0 ? (int)((a.n + QR - 1) / QR) : 0;
+}
+
 template <typename T>
 int sr1_grid(const SpmvArgs<T> &a_in, const Sr1Args<T> &f) {
   const SpmvArgs<T> a = sr1_args(a_in);
-  const int steps = (a.mslices + a.mq - 1) / a.mq;  // chain 0's, the longest
-  if (f.nseg > 0) return a.mchains * std::min(f.nseg, steps);
+  const int steps = std::max(1, sr1_steps(a));
+  const int nch = sr1_chains(a, f.cw);
+  if (f.nseg > 0) return nch * std::min(f.nseg, steps);
   if (f.march <= 0) return 0;
-  return a.mchains * ((steps + f.march - 1) / f.march);
+  return nch * ((steps + f.march - 1) / f.march);
 }
 
 template <typename T>
@@ -3186,27 +3206,57 @@ static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
   }
 }
 
+// The launch shape of k_sr1_dia_m on `cus` CUs: chain width and segments per
+// chain, from a resident-workgroup model -- ceil(chains nseg / slots) rounds
+// of (ceil(L / nseg) + 2) windows (L the longest chain, slots from the
+// kernel's occupancy), a window costing its own rows plus a fifth of its
+// in-plane halo (those rows come from L2: the neighbouring chains load them
+// at the same time).  Chain widths: SR (SB slices) and, for a chain count c
+// up to 48 above SR's, ceil(QR / c) rounded up to 32 rows -- the width that
+// lets chains x segments fill the slots exactly instead of leaving CUs idle
+// in the last round (round 5: C4's 78 chains x 3 segments ran on 234 of 256
+// CUs).  cw_force > 0: that width (even, SR / 4 ... SR), only nseg picked.
+// With an explicit segment length (set_march > 0) callers use cw_force's
+// width or SR: the auto width assumes the auto segment count.
 template <typename T>
-int sr1_pick_nseg(const SpmvArgs<T> &a_in, int cus) {
+Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force) {
   const SpmvArgs<T> a = sr1_args(a_in);
+  Sr1Shape best{1, 0};
   size_t lds = 0;
   const void *k = sr1_pick(a, lds);
-  if (!k || a.mchains <= 0) return 1;
+  if (!k || a.mq <= 0) return best;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * a.msb, lds) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
   const long long slots = (long long)per_cu * std::max(1, cus);
-  const int L = std::max(1, (a.mslices + a.mq - 1) / a.mq);
-  int best = 1;
-  long long best_cost = -1;
-  for (int ns = 1; ns <= L; ++ns) {
-    const long long rounds = ((long long)a.mchains * ns + slots - 1) / slots;
-    const long long cost = rounds * ((L + ns - 1) / ns + 2);
-    if (best_cost < 0 || cost < best_cost) {
-      best_cost = cost;
-      best = ns;
+  const int SR = a.msb * kDiaSliceRows, QR = a.mq * kDiaSliceRows;
+  const int L = std::max(1, sr1_steps(a));
+  const double halo = 0.2 * (a.hl + a.hr);
+  double best_cost = -1.0;
+  auto consider = [&](int cw) {
+    const long long nch = sr1_chains(a, cw);
+    const int w = cw > 0 ? cw : SR;
+    for (int ns = 1; ns <= L; ++ns) {
+      if (nch * ns > sr1_max_grid(a.mslices)) break;
+      const long long rounds = (nch * ns + slots - 1) / slots;
+      const double cost = (double)rounds * ((L + ns - 1) / ns + 2) * (w + halo);
+      if (best_cost < 0 || cost < best_cost * (1.0 - 1e-9)) {
+        best_cost = cost;
+        best = Sr1Shape{ns, cw};
+      }
     }
+  };
+  if (cw_force > 0) {
+    consider(std::max(SR / 4, std::min(SR, cw_force)) & ~1);
+    return best;
+  }
+  consider(0);
+  const int c_min = (QR + SR - 1) / SR;
+  for (int c = c_min + 1; c <= c_min + 48; ++c) {
+    const int cw = std::min(SR, ((QR + c - 1) / c + 31) & ~31);
+    if (cw < SR / 4 || sr1_chains(a, cw) != c) continue;
+    consider(cw);
   }
   return best;
 }
@@ -3216,7 +3266,9 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStr
                             const LaunchEv &ev) {
   const SpmvArgs<T> a = sr1_args(a_in);
   if (a.mq <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
-      (f.march <= 0 && f.nseg <= 0) || f.nseg < 0 || (f.elo & 1) || (f.ehi < a.n && (f.ehi & 1)))
+      (f.march <= 0 && f.nseg <= 0) || f.nseg < 0 || (f.elo & 1) || (f.ehi < a.n && (f.ehi & 1)) ||
+      f.cw < 0 || (f.cw & 1) || f.cw > a.msb * kDiaSliceRows ||
+      sr1_grid(a, f) > sr1_max_grid(a.mslices))
     return hipErrorInvalidValue;
   size_t lds = 0;
   const void *k = sr1_pick(a, lds);
@@ -3574,7 +3626,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int fused_grid<T>(const SpmvArgs<T> &);                                               \
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
   template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
-  template int sr1_pick_nseg<T>(const SpmvArgs<T> &, int);                                      \
+  template Sr1Shape sr1_pick_shape<T>(const SpmvArgs<T> &, int, int);                           \
   template int sr1_edge_grid<T>(int, const Sr1Args<T> &);                                       \
   template hipError_t launch_sr1_edge<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,   \
                                          const LaunchEv &);                                      \

@@ -129,6 +129,7 @@ struct cgx_solver {
   int pbuf = 0;          // fused step: which buffer holds p_old (0: d_p) / r, s, w_old
   int fuse = CGX_FUSE_AUTO;  // cgx_solver_set_fused
   int march = -1;            // cgx_solver_set_march: -1 auto, 0 off, > 0 steps per segment
+  int sr_chain = 0;          // cgx_solver_set_sr_chain: 0 auto, > 0 chain width (rows)
   unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
   int part_cap = 0;
@@ -217,9 +218,9 @@ int alloc_vectors(cgx_solver *s) {
   s->vec_grid = vec_grid_for(n, s->cus);
   s->vec_grid = (std::max(s->vec_grid, 1) + 3) / 4 * 4;  // folded kernels: 4 x 256 threads
   s->part_cap = std::max(s->A.partials(s->A.all_items()), s->vec_grid) + 1;
-  // CGX_ALG_SR: one (p.s, s.s) pair per march workgroup, at most one
-  // workgroup per slice and chain (segments of one step)
-  if (s->A.mq > 0) s->part_cap = std::max(s->part_cap, 2 * (s->A.items() + s->A.mchains) + 2);
+  // CGX_ALG_SR: one (p.s, s.s) pair per march workgroup, at most
+  // kSr1MaxGrid(items) (sr1_pick_shape keeps chains x segments within it)
+  if (s->A.mq > 0) s->part_cap = std::max(s->part_cap, 2 * sr1_max_grid(s->A.items()) + 2);
   // unfused CGX_ALG_SR: the SpMV's (p.s, s.s) pair per workgroup
   s->part_cap = std::max(s->part_cap, 2 * s->A.partials(s->A.all_items()) + 2);
   int rc;
@@ -366,8 +367,11 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     T *so = (T *)(q ? s->d_s2 : s->d_s), *sn = (T *)(q ? s->d_s : s->d_s2);
     const SpmvArgs<T> a = s->A.args<T>(nullptr, sn, nullptr, &s->d_st->done, s->A.all_items());
     Sr1Args<T> f{x, po, pn, ro, rn, so, s->d_st, s->d_pa, s->d_pb, march_len(s)};
-    // set_march's length as given; auto: the balanced segment count
-    if (s->march <= 0) f.nseg = sr1_pick_nseg(a, s->cus);
+    // set_march's length as given; auto: the balanced segment count; the
+    // chain width set_sr_chain gives, or the picked one
+    const Sr1Shape sh = sr1_pick_shape(a, s->cus, s->sr_chain);
+    if (s->march <= 0) f.nseg = sh.nseg;
+    f.cw = s->march > 0 && s->sr_chain == 0 ? 0 : sh.cw;
     const int g = sr1_grid(a, f);
     if (2 * g > s->part_cap) return CGX_EINVAL;
     CGX_HIP(launch_sr1_march<T>(a, f, st, LaunchEv{ev0, ev1}));
@@ -830,6 +834,15 @@ int cgx_solver_set_march(cgx_solver *s, int steps) {
   return 0;
 }
 
+int cgx_solver_set_sr_chain(cgx_solver *s, int rows) {
+  if (!s || rows < 0) return CGX_EINVAL;
+  if (s->sr_chain == rows) return 0;
+  s->sr_chain = rows;
+  drop_graph(s);
+  s->bench_ready = false;
+  return 0;
+}
+
 int cgx_solver_set_layout(cgx_solver *s, int layout) {
   if (!s || layout < CGX_LAYOUT_AUTO || layout > CGX_LAYOUT_PANEL) {
     cgx::set_error("set_layout: bad arguments");
@@ -995,8 +1008,9 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
     // the balanced segments k_sr1_dia_m runs (enqueue_iter): the longest
     const SpmvArgs<double> a =
         s->A.args<double>(nullptr, nullptr, nullptr, nullptr, s->A.all_items());
-    const int steps = (a.mslices + a.mq - 1) / a.mq;
-    const int ns = sr1_pick_nseg(a, s->cus);
+    const long long QR = (long long)a.mq * kDiaSliceRows;
+    const int steps = (int)((a.n + QR - 1) / QR);
+    const int ns = sr1_pick_shape(a, s->cus, s->sr_chain).nseg;
     info->fuse_march = (steps + ns - 1) / std::max(1, ns);
   }
   return 0;

@@ -247,6 +247,14 @@ int  cgx_solver_set_fused(cgx_solver *s, int mode);
  * (the per-slice fused kernel), > 0 slices of a chain per workgroup.
  * cgx_info.fuse_march reports what runs. */
 int  cgx_solver_set_march(cgx_solver *s, int steps);
+/* CGX_ALG_SR's one-launch plane march (k_sr1_dia_m): the width, in rows, of
+ * the chains a step of the march is cut into.  0 auto (default): the width
+ * and segment count whose chains x segments fill the device's resident
+ * workgroup slots best; > 0 that width (even, at most one step's 2,048 /
+ * 1,024 / 512 rows; larger values are clamped), the segment count still
+ * picked.  Results do not depend on it beyond the grouping of the partial
+ * sums (tolerance, as every SR launch shape). */
+int  cgx_solver_set_sr_chain(cgx_solver *s, int rows);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);
 /* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.
@@ -464,6 +472,9 @@ int  cgx_dist_set_fused(cgx_dist *d, int mode);
  * step), > 0 steps per workgroup segment.  cgx_dist_stats.march reports it.
  * Call on every rank (on a local group, part 0 sets the group). */
 int  cgx_dist_set_march(cgx_dist *d, int steps);
+/* As cgx_solver_set_sr_chain, for the ranks' one-launch SR step.  Call on
+ * every rank (on a local group, part 0 sets the group). */
+int  cgx_dist_set_sr_chain(cgx_dist *d, int rows);
 /* hipGraph replay of the iteration batches (RCCL calls included); on by
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
 int  cgx_dist_set_graph(cgx_dist *d, int on);

@@ -446,7 +446,7 @@ def test_fused_cg1_rccl_one_rank_graph_parity():
 
 
 def _sr_group(rp, col, val, b, P, runs, alg=cgx.CGX_ALG_SR, fused="auto", layout="auto",
-              march=-1):
+              march=-1, chain=0):
     n = len(rp) - 1
     parts = cgx.DistSolver.local_group(0, P)
     out = []
@@ -454,6 +454,7 @@ def _sr_group(rp, col, val, b, P, runs, alg=cgx.CGX_ALG_SR, fused="auto", layout
         parts[0].set_alg(alg)
         parts[0].set_fused(fused)
         parts[0].set_march(march)
+        parts[0].set_sr_chain(chain)
         for g, d in enumerate(parts):
             d.set_layout(layout)
             rb, re_ = cgx.partition_rows(n, P, g)
@@ -521,7 +522,8 @@ def test_sr_one_launch_partitions(shape, P):
     where the slabs allow that step (plane-aligned); against oracle_solve_sr
     within 1e-10 at fixed max_iter and within 1e-9 with the stop iteration
     within 1 (and of the HS oracle) at a tolerance, true residual below it;
-    segment lengths 1, 3 and auto (balanced) within 1e-12 of each other."""
+    segment lengths 1, 3 and auto (balanced) and chain widths (a quarter step,
+    458 rows) within 1e-12 of each other."""
     rp, col, val = cgx.laplacian3d(*shape)
     b = np.random.default_rng(27).standard_normal(len(rp) - 1)
     runs = [(0, 0.0), (1, 0.0), (2, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]
@@ -553,11 +555,13 @@ def test_sr_one_launch_partitions(shape, P):
     m = min(len(hist), len(hist_sr))
     assert np.allclose(hist[:m], hist_sr[:m], rtol=1e-6, atol=0)
     assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
-    for march in (1, 3):
-        seg, _ = _sr_group(rp, col, val, b, P, runs[:-1], march=march)
+    # segment lengths, and chain widths (round 5: the narrowest, a quarter
+    # step, with a ragged last chain; a width not a multiple of 64 rows)
+    for march, chain in ((1, 0), (3, 0), (1, 1), (-1, 458)):
+        seg, _ = _sr_group(rp, col, val, b, P, runs[:-1], march=march, chain=chain)
         for (i0, x0, _), (i1, x1, _) in zip(seg, one[:-1]):
             assert i0 == i1
-            assert np.linalg.norm(x0 - x1) <= 1e-12 * np.linalg.norm(x1), (march, i0)
+            assert np.linalg.norm(x0 - x1) <= 1e-12 * np.linalg.norm(x1), (march, chain, i0)
 
 
 def test_sr_one_launch_rccl_one_rank_graph_parity():

@@ -928,9 +928,13 @@ def test_sr_single_launch_vs_oracle(case):
     n = len(rp) - 1
     if b is None:
         b = np.random.default_rng(13).standard_normal(n)
-    for march in (-1, 1, 100000):
+    # (march, chain width): auto; one step per segment with the narrowest
+    # chains (a quarter step, the ragged last chain); whole chains at a width
+    # that is not a multiple of 64 rows
+    for march, chain in ((-1, 0), (1, 1), (100000, 0), (-1, 458)):
         with cgx.Solver(0, alg=cgx.CGX_ALG_SR, layout="dia") as s:
             s.set_march(march)
+            s.set_sr_chain(chain)
             s.set_matrix(rp, col, val)
             info = s.info()
             assert info["fused"] == 1 and info["fuse_march"] > 0
@@ -939,9 +943,9 @@ def test_sr_single_launch_vs_oracle(case):
                 its = s.run(maxit)
                 x, h = s.x(), s.history(its)
                 x_ref, its_ref, h_ref = H.o_solve(maxit, 0.0, rp, col, val, b, sr=True)
-                assert its == its_ref == maxit + 1, (march, maxit)
-                assert rel(x, x_ref) <= 1e-10, (march, maxit)
-                assert np.allclose(h, h_ref, rtol=1e-6, atol=0), (march, maxit)
+                assert its == its_ref == maxit + 1, (march, chain, maxit)
+                assert rel(x, x_ref) <= 1e-10, (march, chain, maxit)
+                assert np.allclose(h, h_ref, rtol=1e-6, atol=0), (march, chain, maxit)
             s.set_rhs(b)
             its = s.run(3000, 1e-10)
             x = s.x()

@@ -7,7 +7,7 @@ C4's slab at N = 8), graph-replayed.
 
 cases: hs_fused, hs, cg1, sr (auto: the one-launch k_sr1_dia_m step where it
 applies), sr2 (the two-launch fused SR step, set_march(0)), srN (one-launch
-with N steps per workgroup), one / oneN (the single-GPU solver's SR
+with N steps per workgroup), srcW (one-launch, chain width W rows), one / oneN (the single-GPU solver's SR
 step on the same slab: auto or N steps per workgroup -- the rank step's base).  Default: hs_fused, sr, sr2, hs, cg1,
 then hs_fused, sr, sr2 again (alternating)."""
 import sys
@@ -34,6 +34,8 @@ def case(name):
         return cgx.CGX_ALG_SR, "auto", -1
     if name == "sr2":
         return cgx.CGX_ALG_SR, "auto", 0
+    if name.startswith("src"):  # srcW: auto segments, chain width W rows
+        return cgx.CGX_ALG_SR, "auto", -1
     return cgx.CGX_ALG_SR, "auto", int(name[2:])
 
 
@@ -60,6 +62,8 @@ for name in cases:
         d.set_alg(alg)
         d.set_fused(fused)
         d.set_march(march)
+        if name.startswith("src"):
+            d.set_sr_chain(int(name[3:]))
         d.set_matrix(n, rp, col, val)
         d.set_rhs(b)
         d.bench_prepare(5)
