@@ -248,7 +248,7 @@ bool has_peers(const cgx_dist *d);
 // -(lowest diagonal offset)), [ehi, n) above (n - the highest offset), both
 // bounds even (row pairs); a slab too thin to have interior rows is all edge.
 struct Sr1Plan {
-  int nseg, len, elo, ehi, cw;
+  int nseg, len, elo, ehi, cw, sb;
 };
 
 Sr1Plan sr1_plan(const cgx_dist *d) {
@@ -257,7 +257,9 @@ Sr1Plan sr1_plan(const cgx_dist *d) {
   const Sr1Shape sh = sr1_pick_shape(a, d->cus, d->sr_chain);
   p.nseg = d->march > 0 ? 0 : sh.nseg;
   p.len = d->march > 0 ? d->march : 0;
-  p.cw = d->march > 0 && d->sr_chain == 0 ? 0 : sh.cw;
+  const bool shaped = d->march <= 0 || d->sr_chain > 0;
+  p.cw = shaped ? sh.cw : 0;
+  p.sb = shaped ? sh.sb : 0;
   p.elo = 0;
   p.ehi = 0x7fffffff;
   if (has_peers(d) && a.ndiag > 0) {
@@ -841,6 +843,7 @@ int phase_sr1(cgx_dist *d) {
   f.g = sr1_g(d);
   f.nseg = pl.nseg;
   f.cw = pl.cw;
+  f.sb = pl.sb;
   f.elo = pl.elo;
   f.ehi = pl.ehi;
   const int gi = sr1_grid(a, f);

@@ -321,7 +321,8 @@ struct Sr1Args {
   double *pq, *pc;
   int march;  // steps per segment (nseg == 0)
   int nseg = 0;
-  int cw = 0;  // chain width in rows (even, <= msb slices; 0: msb slices)
+  int cw = 0;  // chain width in rows (even, <= sb slices; 0: sb slices)
+  int sb = 0;  // rows per step in slices (1, 2, 4; 0: the matrix's plan)
   int elo = 0, ehi = 0x7fffffff;
   // partitioned: the all-reduced (p.s, s.s, r.r) of the last iteration,
   // applied (FIN_SR1's step) to a private copy of *st when st->sr_pend --
@@ -377,7 +378,7 @@ int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
 // occupancy).  cw_force > 0: that chain width, only nseg picked.  An
 // explicit march length (> 0) is used as given instead (nseg 0).
 struct Sr1Shape {
-  int nseg, cw;
+  int nseg, cw, sb;
 };
 // the most workgroups one k_sr1_dia_m launch may have (its partial pairs)
 // for a matrix of `slices` 512-row slices: sr1_pick_shape and

@@ -447,6 +447,23 @@ __device__ __forceinline__ bool load_block(const SpmvArgs<T> &a, int wi, Blk &B,
   return stop == 0;
 }
 
+template <typename T> struct Pair;
+template <> struct Pair<double> {
+  typedef double type __attribute__((ext_vector_type(2), aligned(8)));
+};
+template <> struct Pair<float> {
+  typedef float type __attribute__((ext_vector_type(2), aligned(4)));
+};
+
+// (x[b], x[b+1]) as one load, for -1 <= b <= ncols - 1: a pair reaches
+// past x only where one of its two rows holds no entry there, and the
+// product of that half is selected away.  x[-1] is the allocation's front
+// guard (dev_alloc), x[ncols] the first padding entry (vectors carry kPad).
+template <typename T>
+__device__ __forceinline__ typename Pair<T>::type ld_pair(const T *x, int b) {
+  return *reinterpret_cast<const typename Pair<T>::type *>(x + b);
+}
+
 // ------------------------------------------------------------ k_spmv_csr
 // Plain CSR (the reference's struct, mv_ops.h:17-23).  One 64-row block per
 // wave (<= CAPW nonzeros, planned on the host): the block's val/col window
@@ -455,7 +472,8 @@ __device__ __forceinline__ bool load_block(const SpmvArgs<T> &a, int wi, Blk &B,
 // sums row t from LDS sequentially in column order from 0.0 -- the
 // reference's per-row order (mv_ops.c:190-194), so y is bit-identical to it
 // on chained matrices.  8 x-gathers in flight per row chunk (a 7-point row
-// is one round trip); padding terms are selected away (never multiplied by
+// is one round trip; two consecutive columns in every row of the wave -- a
+// stencil's -1, 0 -- are one 16-byte pair load); padding terms are selected away (never multiplied by
 // 0: an inf/NaN x must not leak into a row that does not reference it).
 // A row longer than the window gets a block of its own and is streamed in
 // window-sized chunks by lane 0.  NT: the once-per-iteration matrix stream
@@ -512,23 +530,66 @@ __global__ __launch_bounds__(256) void k_spmv_csr(SpmvArgs<T> a) {
         for (int j = j0 - kb; j < j1 - kb; j += U) {
           const int cnt = min(U, j1 - kb - j);
           int cc[U];
-          T vv[U], xx[U];
+          T vv[U];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int idx = u < cnt ? j + u : j;  // clamped: every LDS read is valid
             cc[u] = u < cnt ? lcol[idx] : 0;
             vv[u] = lval[idx];
           }
+          // the chunk's gathers with entries (Q, Q + 1) as ONE pair load of
+          // (x[c], x[c + 1]) (Q < 0: none), then the row's products in its
+          // order -- the same values as single loads
+          auto chunk = [&](auto qc) {
+            constexpr int Q = decltype(qc)::value;
+            T xx[U];
+            typename Pair<T>::type xp{};
 #pragma unroll
-          for (int u = 0; u < U; ++u) xx[u] = a.x[cc[u]];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const T pr = vv[u] * xx[u];
-            acc = u < cnt ? acc + pr : acc;
-            if (EPI && u < cnt && cc[u] == row) {
-              xrow = xx[u];
-              have_x = true;
+            for (int u = 0; u < U; ++u) {
+              if (u == Q) xp = ld_pair(a.x, cc[u]);
+              else if (Q < 0 || u != Q + 1) xx[u] = a.x[cc[u]];
             }
+            if constexpr (Q >= 0) {
+              xx[Q] = xp.x;
+              xx[Q + 1] = xp.y;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const T pr = vv[u] * xx[u];
+              acc = u < cnt ? acc + pr : acc;
+              if (EPI && u < cnt && cc[u] == row) {
+                xrow = xx[u];
+                have_x = true;
+              }
+            }
+          };
+          if constexpr (U == 7 && sizeof(T) == 8) {
+            // a run of consecutive columns (a stencil's -1, 0, +1): the lowest
+            // q whose entries q, q + 1 are consecutive in every active lane's
+            // row that holds entry q + 1 -- wave-uniform (ballot over the
+            // active lanes), so the chunk issues one gather instruction less
+            // and no lane diverges.  A pair reaches x[c + 1] <= x[ncols], the
+            // vectors' padding; a lane past its row's end loads a pair it
+            // never uses.  Round 5, same box, alternating
+            // (profiles/r05_ab_csr_pairs_c*.log): C3 in the iteration 185.8 ->
+            // 184.8 us, C4 1,215.6 -> 1,212.4 (back to back 1,236 -> 1,225).
+            int q = -1;
+#pragma unroll
+            for (int u = U - 2; u >= 0; --u) {
+              const bool ok = u + 1 >= cnt || cc[u + 1] == cc[u] + 1;
+              if (__ballot(!ok) == 0) q = u;
+            }
+            switch (q) {
+              case 0: chunk(std::integral_constant<int, 0>{}); break;
+              case 1: chunk(std::integral_constant<int, 1>{}); break;
+              case 2: chunk(std::integral_constant<int, 2>{}); break;
+              case 3: chunk(std::integral_constant<int, 3>{}); break;
+              case 4: chunk(std::integral_constant<int, 4>{}); break;
+              case 5: chunk(std::integral_constant<int, 5>{}); break;
+              default: chunk(std::integral_constant<int, -1>{}); break;
+            }
+          } else {
+            chunk(std::integral_constant<int, -1>{});
           }
         }
       }
@@ -686,23 +747,6 @@ __global__ __launch_bounds__(256) void k_spmv_dc(SpmvArgs<T> a) {
 // the vector-memory instructions of a row-per-thread gather, the lesson of
 // the lab (tools/mb/spmv_lab.hip: 82 -> 38 us at C3).  The codes of the two
 // rows are one load; the only dependent round trip is codes -> x.
-template <typename T> struct Pair;
-template <> struct Pair<double> {
-  typedef double type __attribute__((ext_vector_type(2), aligned(8)));
-};
-template <> struct Pair<float> {
-  typedef float type __attribute__((ext_vector_type(2), aligned(4)));
-};
-
-// (x[b], x[b+1]) as one load, for -1 <= b <= ncols - 1: a pair reaches
-// past x only where one of its two rows holds no entry there, and the
-// product of that half is selected away.  x[-1] is the allocation's front
-// guard (dev_alloc), x[ncols] the first padding entry (vectors carry kPad).
-template <typename T>
-__device__ __forceinline__ typename Pair<T>::type ld_pair(const T *x, int b) {
-  return *reinterpret_cast<const typename Pair<T>::type *>(x + b);
-}
-
 template <typename T>
 __device__ __forceinline__ void st_pair(T *y, int r, int n, T a0, T a1, bool nt) {
   typedef typename Pair<T>::type P;
@@ -3133,19 +3177,22 @@ static const void *sr1_kernel(int cb) {
                    : CGX_K((k_sr1_dia_m<T, SB, NF, 4>));
 }
 
-// The plan k_sr1_dia_m runs: the matrix's march plan, with four-slice steps
-// where its two-slice chains pair up (mq % 4 == 0, C4 and its slabs): 2,048
-// own rows per step, the in-plane halo loaded 1.39x instead of 1.78x; one
-// 1,024-thread workgroup per CU (the ring + r slots: 100 KB of LDS).  Round
-// 5, same box, alternating: C4 783 / 781 against 812 / 810 us per launch
-// (with the pass predicate; the predicate alone 801).
+// The plan k_sr1_dia_m runs on the matrix's march plan (mq slices between
+// the steps of a chain): steps of sb slices of rows (sb = 1, 2, 4: a
+// workgroup of 256 sb threads, two rows each), its LDS ring slots sized for
+// them.  sb 0: the matrix's own (msb), four where its two-slice chains pair
+// up (mq % 4 == 0, C4 and its slabs; round 5, same box: C4 783 against 812
+// us per launch).  With chains of any width (Sr1Args::cw) sb no longer has
+// to divide mq: sr1_pick_shape picks it (C3: 91 slices per plane).
 template <typename T>
-static SpmvArgs<T> sr1_args(const SpmvArgs<T> &a0) {
+static SpmvArgs<T> sr1_args(const SpmvArgs<T> &a0, int sb = 0) {
   SpmvArgs<T> a = a0;
-  if (a.msb == 2 && a.mq % 4 == 0 && 4 * kDiaSliceRows + a.hl + a.hr <= 2 * 2 * 1024) {
-    a.msb = 4;
-    a.mchains = a.mq / 4;
-    a.mws = (4 * kDiaSliceRows + a.hl + a.hr + 3) & ~1;
+  if (sb <= 0 && a.msb == 2 && a.mq % 4 == 0 && 4 * kDiaSliceRows + a.hl + a.hr <= 2 * 2 * 1024)
+    sb = 4;
+  if (sb > 0) {
+    a.msb = sb;
+    a.mchains = (a.mq + sb - 1) / sb;
+    a.mws = (sb * kDiaSliceRows + a.hl + a.hr + 3) & ~1;
   }
   return a;
 }
@@ -3167,7 +3214,7 @@ static int sr1_steps(const SpmvArgs<T> &a) {
 
 template <typename T>
 int sr1_grid(const SpmvArgs<T> &a_in, const Sr1Args<T> &f) {
-  const SpmvArgs<T> a = sr1_args(a_in);
+  const SpmvArgs<T> a = sr1_args(a_in, f.sb);
   const int steps = std::max(1, sr1_steps(a));
   const int nch = sr1_chains(a, f.cw);
   if (f.nseg > 0) return nch * std::min(f.nseg, steps);
@@ -3206,65 +3253,99 @@ static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
   }
 }
 
-// The launch shape of k_sr1_dia_m on `cus` CUs: chain width and segments per
-// chain, from a resident-workgroup model -- ceil(chains nseg / slots) rounds
-// of (ceil(L / nseg) + 2) windows (L the longest chain, slots from the
-// kernel's occupancy), a window costing its own rows plus a fifth of its
+// The launch shape of k_sr1_dia_m on `cus` CUs: step width sb, chain width
+// and segments per chain, from a per-CU work model fitted to round 5's
+// same-box sweeps (profiles/r05_sr_width_probe.log) -- a CU runs
+// ceil(workgroups / cus) workgroups of (ceil(L / nseg) + 2) windows each (L
+// the longest chain), a window costing a quarter step of fixed work (the
+// workgroup's idle lanes still issue), its own rows, and a fifth of its
 // in-plane halo (those rows come from L2: the neighbouring chains load them
-// at the same time).  Chain widths: SR (SB slices) and, for a chain count c
-// up to 48 above SR's, ceil(QR / c) rounded up to 32 rows -- the width that
-// lets chains x segments fill the slots exactly instead of leaving CUs idle
-// in the last round (round 5: C4's 78 chains x 3 segments ran on 234 of 256
-// CUs).  cw_force > 0: that width (even, SR / 4 ... SR), only nseg picked.
-// With an explicit segment length (set_march > 0) callers use cw_force's
-// width or SR: the auto width assumes the auto segment count.
+// at the same time); 5 % more per extra round of resident workgroups (a
+// later round's neighbours are not in step: its halos miss L2), 10 % less
+// with two or more workgroups per CU (one's barriers overlap the other's
+// loads), and a CU with fewer than 12 waves pays for the latency it cannot
+// hide.  A step narrower than four slices must hold at least twice its halo
+// (C4's sb 2: 826 against 744 us).  Chain widths: sb slices and, for a
+// chain count c up to 48 above that one's, ceil(QR / c) rounded up to 32
+// rows (> sb / 2 slices) -- the width that lets chains x segments fill the
+// CUs instead of leaving some idle (C4's 78 chains x 3 segments ran on 234
+// of 256 CUs; 85 chains of 1,888 rows: 744 -> 730 us; C3 picks sb 2, 1,024
+// rows: 139 -> 133 us).  cw_force > 0: that width (even) on the narrowest
+// sb that holds it, only nseg picked.  With an explicit segment length
+// (set_march > 0) callers use cw_force's width or the matrix's sb and its
+// width: the auto shape assumes the auto segment count.
 template <typename T>
 Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force) {
-  const SpmvArgs<T> a = sr1_args(a_in);
-  Sr1Shape best{1, 0};
-  size_t lds = 0;
-  const void *k = sr1_pick(a, lds);
-  if (!k || a.mq <= 0) return best;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * a.msb, lds) != hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
-  const long long slots = (long long)per_cu * std::max(1, cus);
-  const int SR = a.msb * kDiaSliceRows, QR = a.mq * kDiaSliceRows;
-  const int L = std::max(1, sr1_steps(a));
-  const double halo = 0.2 * (a.hl + a.hr);
+  Sr1Shape best{1, 0, 0};
+  if (a_in.mq <= 0) return best;
+  const int QR = a_in.mq * kDiaSliceRows;
+  const double halo = 0.2 * (a_in.hl + a_in.hr);
+  const int ncu = std::max(1, cus);
   double best_cost = -1.0;
-  auto consider = [&](int cw) {
-    const long long nch = sr1_chains(a, cw);
-    const int w = cw > 0 ? cw : SR;
-    for (int ns = 1; ns <= L; ++ns) {
-      if (nch * ns > sr1_max_grid(a.mslices)) break;
-      const long long rounds = (nch * ns + slots - 1) / slots;
-      const double cost = (double)rounds * ((L + ns - 1) / ns + 2) * (w + halo);
-      if (best_cost < 0 || cost < best_cost * (1.0 - 1e-9)) {
-        best_cost = cost;
-        best = Sr1Shape{ns, cw};
+  auto consider_sb = [&](int sb, int cw_only) {
+    const SpmvArgs<T> a = sr1_args(a_in, sb);
+    size_t lds = 0;
+    const void *k = sr1_pick(a, lds);
+    if (!k) return;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * sb, lds) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    const long long slots = (long long)per_cu * ncu;
+    const int SR = sb * kDiaSliceRows;
+    const int L = std::max(1, sr1_steps(a));
+    auto consider = [&](int cw) {
+      const long long nch = sr1_chains(a, cw);
+      const int w = cw > 0 ? cw : SR;
+      for (int ns = 1; ns <= L; ++ns) {
+        const long long g = nch * ns;
+        if (g > sr1_max_grid(a.mslices)) break;
+        const long long rounds = (g + slots - 1) / slots;
+        const long long per = (g + ncu - 1) / ncu;  // workgroups per CU
+        const long long conc = std::min<long long>(per, per_cu);
+        const double waves = 4.0 * sb * (double)conc;
+        double cost = (double)per * ((L + ns - 1) / ns + 2) * (0.25 * SR + w + halo);
+        cost *= 1.0 + 0.05 * (double)(rounds - 1);
+        if (conc >= 2) cost *= 0.9;
+        if (waves < 12.0) cost *= 12.0 / waves;
+        if (best_cost < 0 || cost < best_cost * (1.0 - 1e-9)) {
+          best_cost = cost;
+          best = Sr1Shape{ns, cw, sb};
+        }
       }
+    };
+    if (cw_only > 0) {
+      consider(cw_only);
+      return;
+    }
+    consider(0);
+    const int c_min = (QR + SR - 1) / SR;
+    for (int c = c_min + 1; c <= c_min + 48; ++c) {
+      const int cw = std::min(SR, ((QR + c - 1) / c + 31) & ~31);
+      if (cw <= SR / 2 || sr1_chains(a, cw) != c) continue;
+      consider(cw);
     }
   };
   if (cw_force > 0) {
-    consider(std::max(SR / 4, std::min(SR, cw_force)) & ~1);
+    const int cw = std::max(kDiaSliceRows / 4, std::min(4 * kDiaSliceRows, cw_force)) & ~1;
+    for (int sb : {1, 2, 4})
+      if (cw <= sb * kDiaSliceRows) {
+        consider_sb(sb, cw);
+        if (best_cost >= 0) break;
+      }
     return best;
   }
-  consider(0);
-  const int c_min = (QR + SR - 1) / SR;
-  for (int c = c_min + 1; c <= c_min + 48; ++c) {
-    const int cw = std::min(SR, ((QR + c - 1) / c + 31) & ~31);
-    if (cw < SR / 4 || sr1_chains(a, cw) != c) continue;
-    consider(cw);
-  }
+  for (int sb : {1, 2, 4})
+    if (sb == 4 || 2 * (a_in.hl + a_in.hr) <= sb * kDiaSliceRows) consider_sb(sb, 0);
+  if (best_cost < 0)  // no step of four slices (a wide halo): any that runs
+    for (int sb : {1, 2}) consider_sb(sb, 0);
   return best;
 }
 
 template <typename T>
 hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev) {
-  const SpmvArgs<T> a = sr1_args(a_in);
+  const SpmvArgs<T> a = sr1_args(a_in, f.sb);
   if (a.mq <= 0 || a.items.count != a.mslices || a.layout != L_DIA ||
       (f.march <= 0 && f.nseg <= 0) || f.nseg < 0 || (f.elo & 1) || (f.ehi < a.n && (f.ehi & 1)) ||
       f.cw < 0 || (f.cw & 1) || f.cw > a.msb * kDiaSliceRows ||

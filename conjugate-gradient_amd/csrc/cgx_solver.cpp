@@ -371,7 +371,10 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     // chain width set_sr_chain gives, or the picked one
     const Sr1Shape sh = sr1_pick_shape(a, s->cus, s->sr_chain);
     if (s->march <= 0) f.nseg = sh.nseg;
-    f.cw = s->march > 0 && s->sr_chain == 0 ? 0 : sh.cw;
+    if (s->march <= 0 || s->sr_chain > 0) {
+      f.cw = sh.cw;
+      f.sb = sh.sb;
+    }
     const int g = sr1_grid(a, f);
     if (2 * g > s->part_cap) return CGX_EINVAL;
     CGX_HIP(launch_sr1_march<T>(a, f, st, LaunchEv{ev0, ev1}));
