@@ -139,7 +139,7 @@ def make_system(wl, rank=0, world=1):
 
 
 # kernel key -> the name prefix its rocprofv3 PMC summary must carry
-KERNEL_PREFIX = {"sr1": "k_sr1_dia_m<", "sr1r": "k_sr1r_dia_m<", "dia_march": "k_spmv_dia_m<", "dia_fused": "k_spmv_dia_h<",
+KERNEL_PREFIX = {"sr1": "k_sr1_dia_m<", "dia_march": "k_spmv_dia_m<", "dia_fused": "k_spmv_dia_h<",
                  "dia": "k_spmv_dia<", "dc": "k_spmv_dc<", "csr": "k_spmv_csr<",
                  "panel": "k_spmv_csr<", "stencil": "k_stencil<"}
 
@@ -181,10 +181,6 @@ KERNELS = {
     "sr1": "k_sr1_dia_m (one-launch SR iteration on DIA-VI as a plane march: r = r - alpha s "
            "and p = r + beta p of the previous iteration for each window row, x update, "
            "s = A p from an LDS ring of three windows, (p.s, s.s, r.r) per workgroup)",
-    "sr1r": "k_sr1r_dia_m (one-launch SR iteration on DIA-VI as a plane march WITHOUT an s "
-            "vector: s_k = A p_k recomputed for each window row from an LDS ring of wide p_k "
-            "windows, r = r - alpha s_k and p = r + beta p into a second ring, x update, "
-            "s = A p of the own rows for (p.s, s.s) only, r.r per workgroup; 45 B/row)",
     "dc": "k_spmv_dc (LDS-DMA code window + value window per 64-row block, dictionary-coded columns)",
     "csr": "k_spmv_csr (LDS-DMA val/col window per 64-row block, lane-per-row sums from LDS)",
     "panel": "k_spmv_csr over column panels",
@@ -195,9 +191,7 @@ KERNELS = {
 def kernel_key(info):
     if info["layout_name"] == "dia" and info.get("fused"):
         if info.get("alg") == 2 and (info.get("fuse_march", 0) > 0 or info.get("march", 0) > 0):
-            # single GPU (cgx_info.fuse_march; without an s vector: sr_no_s) or
-            # a rank (cgx_dist_stats.march)
-            return "sr1r" if info.get("sr_no_s") else "sr1"
+            return "sr1"  # single GPU (cgx_info.fuse_march) or a rank (cgx_dist_stats.march)
         return "dia_march" if info.get("fuse_march") else "dia_fused"
     return info["layout_name"]
 

@@ -56,8 +56,7 @@ class CgxInfo(ctypes.Structure):
                 ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double),
                 ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int),
                 ("fused", ctypes.c_int), ("fuse_status", ctypes.c_int),
-                ("breakdown", ctypes.c_int), ("fuse_march", ctypes.c_int),
-                ("sr_no_s", ctypes.c_int)]
+                ("breakdown", ctypes.c_int), ("fuse_march", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):
@@ -109,7 +108,6 @@ _SIGS = {
     "cgx_solver_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_march": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_sr_chain": (ctypes.c_int, [_vp, ctypes.c_int]),
-    "cgx_solver_set_sr_recompute": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_solver_set_matrix": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                              _i32p, _i32p, _f64p]),
     "cgx_solver_set_matrix_f32": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
@@ -379,11 +377,6 @@ class Solver:
         """Chain width (rows) of CGX_ALG_SR's one-launch plane march
         (cgx_solver_set_sr_chain): 0 auto, > 0 that width."""
         check(lib().cgx_solver_set_sr_chain(self._h, int(rows)), "set_sr_chain")
-
-    def set_sr_recompute(self, on=True):
-        """CGX_ALG_SR without an s vector (cgx_solver_set_sr_recompute):
-        True (default) where it applies, False the step that stores s."""
-        check(lib().cgx_solver_set_sr_recompute(self._h, 1 if on else 0), "set_sr_recompute")
 
     def set_layout(self, layout):
         """CGX_LAYOUT_* (or its name) for the next set_matrix / gen_laplacian."""

@@ -323,7 +323,6 @@ struct Sr1Args {
   int nseg = 0;
   int cw = 0;  // chain width in rows (even, <= sb slices; 0: sb slices)
   int sb = 0;  // rows per step in slices (1, 2, 4; 0: the matrix's plan)
-  int sfree = 0;  // 1: k_sr1r_dia_m (s recomputed, never stored) where it applies
   int elo = 0, ehi = 0x7fffffff;
   // partitioned: the all-reduced (p.s, s.s, r.r) of the last iteration,
   // applied (FIN_SR1's step) to a private copy of *st when st->sr_pend --
@@ -387,10 +386,6 @@ struct Sr1Shape {
 inline int sr1_max_grid(int slices) { return 4 * slices + 64; }
 template <typename T>
 Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a, int cus, int cw_force = 0);
-// launch_sr1_march runs k_sr1r_dia_m (no s vector: f.sfree, single GPU,
-// four-slice steps, both LDS rings fit) for these arguments
-template <typename T>
-bool sr1r_runs(const SpmvArgs<T> &a, const Sr1Args<T> &f);
 // workgroups (= partial pairs) of k_sr1_edge over f's edge rows of n rows
 template <typename T>
 int sr1_edge_grid(int n, const Sr1Args<T> &f);

@@ -1550,7 +1550,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
           v1 = src[i + 1];
         }
         const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
-        const T p0 = lv[kk * 16 + (CGX_EXP & 4 ? 0 : n0)] * v0, p1 = lv[kk * 16 + (CGX_EXP & 4 ? 0 : n1)] * v1;
+        const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
         a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
         a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
       }
@@ -1661,323 +1661,6 @@ __global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
     reinterpret_cast<double2 *>(f.pq)[blockIdx.x] = make_double2(p0, p1);
     f.pc[blockIdx.x] = 0.0;
   }
-}
-
-// ------------------------ single-GPU SR iteration without an s vector
-// k_sr1_dia_m's iteration with s_k never stored (the same s_k, bit for bit;
-// the r.r partials grouped by window pairs instead of own-row pairs, so x
-// agrees to 1e-12): the launch of iteration k + 1 RECOMPUTES s_k = A p_k for the rows
-// of each window from an LDS ring of wider p_k windows (rows [B - 2 hl,
-// B + wc + 2 hr): a window row's in-plane neighbours, the +-F ones from the
-// ring's neighbour slots), in the row's diagonal order with the same
-// roundings as the launch that summed it -- then r_{k+1} = r_k - alpha s_k,
-// p_{k+1} = r_{k+1} + beta p_k into the p_{k+1} ring, and s_{k+1} = A p_{k+1}
-// of the own rows for the (p.s, s.s) sums only.  Bytes per row: code + r, p
-// read, r, p written + x / p_{k-1} every other launch = 45 against k_sr1's
-// 61 (s written and read back: 16).  Round 3 measured this form slower
-// (k_sr2_dia_m, 967 against 813 us at C4 with 13 segments of 31 steps per
-// chain); round 5 runs it on the chain widths / segments of
-// sr1_pick_shape (three segments of 134 steps) with the window loads of step
-// m + 1 and the p_k window of step m + 3 in flight during step m.  Per step
-// m (phase A, barrier, phase B, barrier): A builds p_{k+1} window m + 1 from
-// p_k windows m, m + 1, m + 2 and stores the own rows' r_{k+1}; B stores p_k
-// window m + 3 into the ring slot A(m) freed and computes s_{k+1} of step m's
-// own rows from p_{k+1} windows m - 1, m, m + 1.  A segment starts two steps
-// early (A only) so its first B has three p_{k+1} windows.  Single GPU only
-// (no ghost rows, no edge launch): launch_sr1r_march checks.
-template <typename T, int SB, int NF, int NFE, int CB>
-__global__ __launch_bounds__(256 * SB) void k_sr1r_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
-  constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
-  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
-  constexpr int NRING = 3;
-  const int wse = (SR + 2 * a.hl + 2 * a.hr + 3) & ~1;  // p_k ring slot stride
-  T *ringE = reinterpret_cast<T *>(dyn_lds);            // p_k windows (wide)
-  T *ringP = ringE + NRING * wse;                       // p_{k+1} windows
-  __shared__ T lv[kDiaMax * 16];
-  __shared__ double red[3][4 * SB];
-  typedef typename Pair<T>::type P;
-  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int w = xcd_block();
-  const int QR = a.mq * kDiaSliceRows;
-  const int CW = f.cw > 0 ? f.cw : SR;
-  const int nch = (QR + CW - 1) / CW;
-  const int chain = w % nch, seg = w / nch;
-  const int c0 = chain * CW, wc = min(CW, QR - c0);
-  const int msteps = c0 < a.n ? (a.n - c0 + QR - 1) / QR : 0;
-  int m0, m1;
-  if (f.nseg > 0) {
-    m0 = (int)((long long)seg * msteps / f.nseg);
-    m1 = (int)((long long)(seg + 1) * msteps / f.nseg);
-  } else {
-    m0 = seg * f.march;
-    m1 = min(m0 + f.march, msteps);
-  }
-  const Sr1Now sn = sr1_now(f.st, nullptr);
-  if (sn.done > 1) return;  // uniform
-  const int k = sn.k_u;
-  const bool first = k < 0, stop = sn.done == 1;
-  const bool odd = (k & 1) != 0;
-  const bool xup = !first && odd;
-  const T alpha = (T)sn.alpha, beta = (T)sn.beta, alpha_d = (T)f.st->alpha_def;
-  if (!first && !odd && !stop && blockIdx.x == 0 && t == 0)
-    const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
-  const int padn = a.mslices * kDiaSliceRows;
-  const int wn = wc + a.hl + a.hr, we = wc + 2 * (a.hl + a.hr), ws = a.mws;
-  auto base_of = [&](int m) { return c0 + m * QR; };
-  auto slotE = [&](int m) { return ringE + ((m + NRING) % NRING) * wse; };
-  auto slotP = [&](int m) { return ringP + ((m + NRING) % NRING) * ws; };
-  // the x update of step m's own rows (odd launches): x and p_{k-1} (the
-  // p_new buffer before this launch overwrites it) loaded during step m - 1,
-  // p_k from the wide ring (its slot m still holds window m during A(m))
-  struct XOps {
-    P xo, pd;
-  };
-  auto load_x = [&](int m, XOps &o) {
-    const int r = base_of(m) + 2 * t, rs = r < a.n ? r : 0;
-    o.xo = ld_pair(f.x, rs);
-    o.pd = ld_pair((const T *)f.pnew, rs);
-  };
-  auto x_update = [&](int m, const XOps &o) {
-    const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + wc);
-    T po0, po1;
-    lds_ld2(slotE(m), 2 * t + 2 * a.hl, po0, po1);
-    const T d0 = alpha_d * o.pd.x, d1 = alpha_d * o.pd.y;
-    const T x0 = o.xo.x + d0, x1 = o.xo.y + d1;
-    const T a0 = alpha * po0, a1 = alpha * po1;
-    if (r < rend) st_pair(f.x, r, rend, x0 + a0, x1 + a1, false);
-  };
-  double sps = 0.0, sss = 0.0, srr = 0.0;
-  auto publish = [&]() {
-    sps = wave_sum(sps);
-    sss = wave_sum(sss);
-    srr = wave_sum(srr);
-    if (lane == 0) {
-      red[0][wid] = sps;
-      red[1][wid] = sss;
-      red[2][wid] = srr;
-    }
-    __syncthreads();
-    if (t == 0) {
-      double p0 = red[0][0], p1 = red[1][0], p2 = red[2][0];
-#pragma unroll
-      for (int v = 1; v < 4 * SB; ++v) {
-        p0 = p0 + red[0][v];
-        p1 = p1 + red[1][v];
-        p2 = p2 + red[2][v];
-      }
-      reinterpret_cast<double2 *>(f.pq)[blockIdx.x] = make_double2(p0, p1);
-      f.pc[blockIdx.x] = p2;
-    }
-  };
-  if (stop) {  // as k_sr1_dia_m: the deferred x += alpha_k p_k only
-    for (int m = m0; m < m1; ++m) {
-      const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + wc), rs = r < a.n ? r : 0;
-      const P pd = ld_pair((const T *)f.pnew, rs), xo = ld_pair(f.x, rs);
-      const T d0 = alpha_d * pd.x, d1 = alpha_d * pd.y;
-      if (r < rend) st_pair(f.x, r, rend, xo.x + d0, xo.y + d1, false);
-    }
-    return;
-  }
-  if (m0 >= m1) {
-    publish();
-    return;
-  }
-  typedef typename CodeRaw<CB>::type CR;
-  const int wfirst = 2 * __builtin_amdgcn_readfirstlane(wid * kWave);
-  // p_k of the wide window m (not on the first launch: p_0 = r_0)
-  P pe[NFE];
-#pragma unroll
-  for (int q = 0; q < NFE; ++q) pe[q] = P{T(0), T(0)};
-  auto load_ext = [&](int m) {
-    if (first) return;
-    const int w0 = base_of(m) - 2 * a.hl;
-#pragma unroll
-    for (int q = 0; q < NFE; ++q) {
-      if (q > 0 && wfirst + q * 2 * BS >= we) continue;
-      const int j = min(max(w0 + 2 * t + q * 2 * BS, a.xlo), a.ncols - 1);
-      pe[q] = ld_pair(f.pold, j);
-    }
-  };
-  auto store_ext = [&](int m) {
-    if (first) return;
-    T *e = slotE(m);
-#pragma unroll
-    for (int q = 0; q < NFE; ++q) {
-      const int i = 2 * t + q * 2 * BS;
-      if (i + 1 < we) lds_st2(e, i, pe[q].x, pe[q].y);
-      else if (i < we) e[i] = pe[q].x;
-    }
-  };
-  // phase A's operands of window m: its codes (two register sets: loaded
-  // at A(m - 2)) and r_k (one set: loaded at B(m - 2), after A(m - 2) used
-  // it; r is needed last in A(m - 1))
-  struct WinCodes {
-    CR c[NF];
-  };
-  P wr[NF];
-#pragma unroll
-  for (int q = 0; q < NF; ++q) wr[q] = P{T(0), T(0)};
-  auto load_codes = [&](int m, WinCodes &o) {
-    const int w0 = base_of(m) - a.hl;
-#pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      if (q > 0 && wfirst + q * 2 * BS >= wn) continue;
-      const int row = w0 + 2 * t + q * 2 * BS;
-      o.c[q] = ld_code_raw<CB>(a.dcode, min(max(row, 0), padn - 2));
-    }
-  };
-  auto load_r = [&](int m) {
-    const int w0 = base_of(m) - a.hl;
-#pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      if (q > 0 && wfirst + q * 2 * BS >= wn) continue;
-      wr[q] = ld_pair(f.rold, min(max(w0 + 2 * t + q * 2 * BS, a.xlo), a.ncols - 1));
-    }
-  };
-  // phase A: p_{k+1} of window m + 1 into its ring slot, r_{k+1} of its own
-  // rows stored (and summed)
-  auto phase_a = [&](int m, const WinCodes &o) {
-    const int mm = m + 1;
-    const bool mine = mm >= m0 && mm < m1;  // uniform
-    T *dst = slotP(mm);
-    const T *ec = slotE(mm), *ep = slotE(mm - 1), *en = slotE(mm + 1);
-    const int ob = base_of(mm);
-#pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      if (q > 0 && wfirst + q * 2 * BS >= wn) continue;
-      const int i = 2 * t + q * 2 * BS;
-      P rk = wr[q], pk = wr[q];
-      if (!first) {
-        unsigned cc0, cc1;
-        code_split<CB>(o.c[q], cc0, cc1);
-        const int ie = (i < wn ? i : 0) + a.hl;  // the row's index in the wide windows
-        T s0 = T(0), s1 = T(0);
-#pragma unroll
-        for (int kk = 0; kk < kDiaMax; ++kk) {
-          if (kk < a.ndiag) {
-            const int d = a.doff[kk];
-            const T *src = (a.near >> kk) & 1u ? ec : d < 0 ? ep : en;
-            const int ix = (a.near >> kk) & 1u ? ie + d : d < 0 ? ie + d + QR : ie + d - QR;
-            T v0, v1;
-            if ((d & 1) == 0) lds_ld2(src, ix, v0, v1);
-            else {
-              v0 = src[ix];
-              v1 = src[ix + 1];
-            }
-            const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
-            const T p0 = lv[kk * 16 + (CGX_EXP & 4 ? 0 : n0)] * v0, p1 = lv[kk * 16 + (CGX_EXP & 4 ? 0 : n1)] * v1;
-            s0 = n0 != a.cmask[kk] ? s0 + p0 : s0;
-            s1 = n1 != a.cmask[kk] ? s1 + p1 : s1;
-          }
-        }
-        T pk0, pk1;
-        lds_ld2(ec, ie, pk0, pk1);
-        P pkk;
-        pkk.x = pk0;
-        pkk.y = pk1;
-        const T as0 = alpha * s0, as1 = alpha * s1;
-        rk.x = wr[q].x - as0;
-        rk.y = wr[q].y - as1;
-        pk = p_next<T>(rk, pkk, beta);
-      }
-      if (i + 1 < wn) lds_st2(dst, i, pk.x, pk.y);
-      else if (i < wn) dst[i] = pk.x;
-      // r_{k+1} of the own rows of the segment's steps only (windows m0 - 1
-      // and m1 are other segments' steps, or before row 0 / past row n - 1)
-      const int oi = i - a.hl;  // hl even: a pair is in the own rows or not
-      if (mine && oi >= 0 && oi < wc) {
-        const int r = ob + oi, rend = min(a.n, ob + wc);
-        if (r < rend) {
-          st_pair(f.rnew, r, rend, rk.x, rk.y, false);
-          srr = srr + (double)rk.x * (double)rk.x;
-          if (r + 1 < rend) srr = srr + (double)rk.y * (double)rk.y;
-        }
-      }
-    }
-  };
-  // phase B: s_{k+1} = A p_{k+1} of step m's own rows, p_{k+1} stored
-  auto phase_b = [&](int m, const CR &ccw) {
-    const int base = base_of(m), r = base + 2 * t;
-    const int rend = min(a.n, base + wc);
-    const T *cur = slotP(m), *prv = slotP(m - 1), *nxt = slotP(m + 1);
-    const int rw = 2 * t + a.hl;
-    unsigned cc0, cc1;
-    code_split<CB>(ccw, cc0, cc1);
-    T a0 = T(0), a1 = T(0);
-#pragma unroll
-    for (int kk = 0; kk < kDiaMax; ++kk) {
-      if (kk < a.ndiag) {
-        const int d = a.doff[kk];
-        const T *src = (a.near >> kk) & 1u ? cur : d < 0 ? prv : nxt;
-        const int i = (a.near >> kk) & 1u ? rw + d : d < 0 ? rw + d + QR : rw + d - QR;
-        T v0, v1;
-        if ((d & 1) == 0) lds_ld2(src, i, v0, v1);
-        else {
-          v0 = src[i];
-          v1 = src[i + 1];
-        }
-        const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
-        const T p0 = lv[kk * 16 + (CGX_EXP & 4 ? 0 : n0)] * v0, p1 = lv[kk * 16 + (CGX_EXP & 4 ? 0 : n1)] * v1;
-        a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
-        a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
-      }
-    }
-    T pn0, pn1;
-    lds_ld2(cur, rw, pn0, pn1);
-    if (r < rend) {
-      st_pair(f.pnew, r, rend, pn0, pn1, false);
-      sps = sps + (double)pn0 * (double)a0;
-      sss = sss + (double)a0 * (double)a0;
-      if (r + 1 < rend) {
-        sps = sps + (double)pn1 * (double)a1;
-        sss = sss + (double)a1 * (double)a1;
-      }
-    }
-  };
-  auto codes_at = [&](int m, CR &cw) {
-    const int r = base_of(m) + 2 * t;
-    cw = ld_code_raw<CB>(a.dcode, r < padn ? r : base_of(m));
-  };
-  // prologue: p_k windows m0 - 2 .. m0 in the ring, m0 + 1 in flight;
-  // window m0 - 1 (phase A of step m0 - 2) and the own-row operands of m0
-  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
-  WinCodes wa, wb;
-  CR ca{}, cb{};
-  XOps xc{};
-  load_codes(m0 - 1, wa);
-  load_r(m0 - 1);
-  load_ext(m0 - 2);
-  store_ext(m0 - 2);
-  load_ext(m0 - 1);
-  store_ext(m0 - 1);
-  load_ext(m0);
-  store_ext(m0);
-  load_ext(m0 + 1);
-  if (t < a.ndiag * 16) lv[t] = tv;
-  __syncthreads();
-  // one step m: A(m) with window m + 1's operands (cur), window m + 2's
-  // loads issued into nxt first, and step m's x update; then B(m) (steps
-  // before m0: the ring work only) with step m's codes (ccw), those of
-  // m + 1 and its x operands issued first
-  auto step = [&](int m, const WinCodes &cur, WinCodes &nxt, const CR &ccw, CR &ncw) {
-    load_codes(min(m + 2, m1), nxt);
-    if (xup && m >= m0) x_update(m, xc);
-    phase_a(m, cur);
-    __syncthreads();  // p_{k+1} window m + 1 complete; A(m)'s reads of p_k slot m done
-    store_ext(min(m + 3, m1 + 1));  // into slot m, free now
-    load_ext(min(m + 4, m1 + 1));
-    load_r(min(m + 2, m1));
-    const int mn = max(m0, min(m + 1, m1 - 1));
-    codes_at(mn, ncw);
-    if (xup && m + 1 < m1 && m + 1 >= m0) load_x(m + 1, xc);
-    if (m >= m0) phase_b(m, ccw);
-    __syncthreads();  // B(m)'s reads of p_{k+1} slot m - 1 done before A(m + 1) refills it
-  };
-  for (int m = m0 - 2; m < m1; m += 2) {
-    step(m, wa, wb, ca, cb);
-    if (m + 1 < m1) step(m + 1, wb, wa, cb, ca);
-  }
-  publish();
 }
 
 // ---------------------------------------- fused CG1 step (DIA-VI)
@@ -3659,33 +3342,6 @@ Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force) {
   return best;
 }
 
-// k_sr1r_dia_m (the SR step without an s vector): single GPU (no ghost
-// rows, no transport), four-slice steps, the window and the wide p_k window
-// in two pair passes, both rings in LDS
-template <typename T>
-static const void *sr1r_pick(const SpmvArgs<T> &a, const Sr1Args<T> &f, size_t &lds) {
-  const int SR = 4 * kDiaSliceRows;
-  if (!f.sfree || f.g || f.elo != 0 || f.ehi < a.n || a.msb != 4 || a.xlo != -1) return nullptr;
-  if (SR + a.hl + a.hr > 2 * 2 * 1024 || SR + 2 * (a.hl + a.hr) > 2 * 2 * 1024) return nullptr;
-  const int wse = (SR + 2 * a.hl + 2 * a.hr + 3) & ~1;
-  if (a.mws < SR + a.hl + a.hr + 2) return nullptr;
-  lds = (size_t)3 * (wse + a.mws) * sizeof(T) + 16;
-  const size_t stat = (size_t)kDiaMax * 16 * sizeof(T) + 3 * 4 * 4 * sizeof(double);
-  if (lds + stat > 160 * 1024) return nullptr;
-  switch (a.cb) {
-    case 1: return CGX_K((k_sr1r_dia_m<T, 4, 2, 2, 1>));
-    case 2: return CGX_K((k_sr1r_dia_m<T, 4, 2, 2, 2>));
-    case 4: return CGX_K((k_sr1r_dia_m<T, 4, 2, 2, 4>));
-    default: return nullptr;
-  }
-}
-
-template <typename T>
-bool sr1r_runs(const SpmvArgs<T> &a_in, const Sr1Args<T> &f) {
-  size_t lds = 0;
-  return sr1r_pick(sr1_args(a_in, f.sb), f, lds) != nullptr;
-}
-
 template <typename T>
 hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStream_t st,
                             const LaunchEv &ev) {
@@ -3696,8 +3352,7 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStr
       sr1_grid(a, f) > sr1_max_grid(a.mslices))
     return hipErrorInvalidValue;
   size_t lds = 0;
-  const void *k = sr1r_pick(a, f, lds);  // without an s vector where it applies
-  if (!k) k = sr1_pick(a, lds);
+  const void *k = sr1_pick(a, lds);
   if (!k) return hipErrorInvalidValue;
   const int g = sr1_grid(a, f);
   void *args[] = {(void *)&a, (void *)&f};
@@ -4053,7 +3708,6 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
   template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
   template Sr1Shape sr1_pick_shape<T>(const SpmvArgs<T> &, int, int);                           \
-  template bool sr1r_runs<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                          \
   template int sr1_edge_grid<T>(int, const Sr1Args<T> &);                                       \
   template hipError_t launch_sr1_edge<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,   \
                                          const LaunchEv &);                                      \

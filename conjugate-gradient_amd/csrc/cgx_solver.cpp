@@ -130,7 +130,6 @@ struct cgx_solver {
   int fuse = CGX_FUSE_AUTO;  // cgx_solver_set_fused
   int march = -1;            // cgx_solver_set_march: -1 auto, 0 off, > 0 steps per segment
   int sr_chain = 0;          // cgx_solver_set_sr_chain: 0 auto, > 0 chain width (rows)
-  int sr_recompute = 1;      // cgx_solver_set_sr_recompute: SR without an s vector
   unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
   int part_cap = 0;
@@ -334,8 +333,7 @@ int enqueue_init(cgx_solver *s) {
 
 // The one-launch SR step's shape: set_march's length as given, else the
 // balanced segment count; the chain width set_sr_chain gives, or the picked
-// one (with the step width it needs); s recomputed (k_sr1r_dia_m) unless
-// set_sr_recompute(0)
+// one (with the step width it needs)
 template <typename T>
 void sr1_shape(const cgx_solver *s, const SpmvArgs<T> &a, Sr1Args<T> &f) {
   const Sr1Shape sh = sr1_pick_shape(a, s->cus, s->sr_chain);
@@ -344,7 +342,6 @@ void sr1_shape(const cgx_solver *s, const SpmvArgs<T> &a, Sr1Args<T> &f) {
     f.cw = sh.cw;
     f.sb = sh.sb;
   }
-  f.sfree = s->sr_recompute;
 }
 
 // One CG iteration.  ev0/ev1 (optional): the SpMV kernel's start / end.
@@ -846,15 +843,6 @@ int cgx_solver_set_march(cgx_solver *s, int steps) {
   return 0;
 }
 
-int cgx_solver_set_sr_recompute(cgx_solver *s, int on) {
-  if (!s || on < 0 || on > 1) return CGX_EINVAL;
-  if (s->sr_recompute == on) return 0;
-  s->sr_recompute = on;
-  drop_graph(s);
-  s->bench_ready = false;
-  return 0;
-}
-
 int cgx_solver_set_sr_chain(cgx_solver *s, int rows) {
   if (!s || rows < 0) return CGX_EINVAL;
   if (s->sr_chain == rows) return 0;
@@ -1001,16 +989,6 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
     // SR (one launch): r, s, p read and written, x / p_{k-2} every other
     // launch: + 5.5 n vectors
     info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : s->alg == CGX_ALG_SR ? 5.5 : 3.5) * A.n * sv;
-  if (s->have_matrix && fused(s) && s->alg == CGX_ALG_SR && A.dtype == CGX_F64) {
-    // without an s vector (k_sr1r_dia_m): s neither written nor read back
-    const SpmvArgs<double> a = A.args<double>(nullptr, nullptr, nullptr, nullptr, A.all_items());
-    Sr1Args<double> f{};
-    f.march = march_len(s);
-    f.ehi = 0x7fffffff;
-    sr1_shape(s, a, f);
-    info->sr_no_s = sr1r_runs(a, f) ? 1 : 0;
-    if (info->sr_no_s) info->spmv_iter_bytes -= 2.0 * A.n * sv;
-  }
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;

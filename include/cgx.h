@@ -196,8 +196,6 @@ typedef struct {
   int fuse_march;       /* > 0: the fused HS / SR step runs as a plane
                            march (cgx_solver_set_march), this many steps per
                            workgroup (the longest segment); 0: it does not  */
-  int sr_no_s;          /* 1: CGX_ALG_SR runs without an s vector
-                           (k_sr1r_dia_m, cgx_solver_set_sr_recompute)      */
 } cgx_info;
 
 /* cgx_info.fuse_status / cgx_dist_stats.fuse_status */
@@ -257,13 +255,6 @@ int  cgx_solver_set_march(cgx_solver *s, int steps);
  * picked.  Results do not depend on it beyond the grouping of the partial
  * sums (tolerance, as every SR launch shape). */
 int  cgx_solver_set_sr_chain(cgx_solver *s, int rows);
-/* CGX_ALG_SR's one-launch step without an s vector (default 1): launch k + 1
- * recomputes s_k = A p_k for the rows whose r_{k+1} it forms, from an LDS ring
- * of wider p_k windows, instead of reading the s_k launch k stored (45 B per
- * row instead of 61; the same values bit for bit).  Applies on one GPU with
- * four-slice steps where both LDS rings fit (cgx_info.sr_no_s says); 0 runs
- * the step that stores s. */
-int  cgx_solver_set_sr_recompute(cgx_solver *s, int on);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */
 int  cgx_solver_set_layout(cgx_solver *s, int layout);
 /* Host CSR (int32 row_ptr[n+1], col[nnz]; values f64 or f32) -> device.

@@ -150,9 +150,6 @@ def test_dist_line_schema():
     assert bench.dist_traffic_key("hs", info) is None
     assert bench.kernel_key(dict(info, fused=1)) == "sr1"
     assert bench.kernel_key(dict(info, march=0)) == "dia_fused"
-    # round 5: the single-GPU step without an s vector prices its own kernel
-    assert bench.kernel_key(dict(info, fused=1, sr_no_s=1)) == "sr1r"
-    assert bench.KERNEL_PREFIX["sr1r"] == "k_sr1r_dia_m<"
 
 
 def test_no_gbs_field_exceeds_peak():

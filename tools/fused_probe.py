@@ -2,7 +2,7 @@
 device-generated Laplacian), same box, same build, back to back; HS, or the
 CG1 recurrence with --cg1.
   python tools/fused_probe.py [--cg1|--sr] [--modes=on,off,...] [--march=-1,0,...]
-                              [--chain=0,1888,...] [--recompute=1,0] [dim:nx[:ny:nz] ...]
+                              [--chain=0,1888,...] [dim:nx[:ny:nz] ...]
 default 3:216 3:400 (C3, C4); 2:1000 = C2.  --march: cgx_solver_set_march values tried
 for each mode (-1 auto, 0 off, > 0 steps per segment)."""
 import sys
@@ -18,10 +18,7 @@ for a in sys.argv[1:]:
         modes = a.split("=", 1)[1].split(",")
 marches = [-1]
 chains = [0]
-recs = [1]
 for a in sys.argv[1:]:
-    if a.startswith("--recompute="):  # SR: cgx_solver_set_sr_recompute values
-        recs = [int(t) for t in a.split("=", 1)[1].split(",")]
     if a.startswith("--march="):
         marches = [int(t) for t in a.split("=", 1)[1].split(",")]
     if a.startswith("--chain="):  # SR: cgx_solver_set_sr_chain widths (0 auto)
@@ -31,19 +28,17 @@ for spec in args or ["3:216", "3:400"]:
     dim, nx = v[0], v[1]
     ny, nz = (v[2], v[3]) if len(v) > 2 else (nx, nx if dim == 3 else 1)
     n = nx * ny * nz
-    for fused, march, chain, rec in [(f, m, c, r) for f in modes for m in marches for c in chains
-                                     for r in recs]:
+    for fused, march, chain in [(f, m, c) for f in modes for m in marches for c in chains]:
         with cgx.Solver(0, alg=alg, fused=fused) as s:
             s.set_march(march)
             s.set_sr_chain(chain)
-            s.set_sr_recompute(rec)
             s.gen_laplacian(dim, nx, ny, nz)
             s.set_rhs(np.ones(n))
             s.bench_prepare(5)
             ms = s.bench_run(200)[0]
             _, sp = s.bench_run(30, graph=False, spmv_events=True)
             i = s.info()
-            print("%s %dD nx %d mode %s march %d (runs %d) chain %d no_s %d fused %d: %.1f us/iter, "
+            print("%s %dD nx %d mode %s march %d (runs %d) chain %d fused %d: %.1f us/iter, "
                   "spmv launch %.1f us" %
                   (["hs", "cg1", "sr"][alg], dim, nx, fused, march, i["fuse_march"], chain,
-                   i["sr_no_s"], i["fused"], 1e3 * ms / 200, 1e3 * sp), flush=True)
+                   i["fused"], 1e3 * ms / 200, 1e3 * sp), flush=True)
