@@ -6,6 +6,7 @@
 # (the north-star figure) and C5's column-panel SpMV.  Summaries:
 #   python tools/pmc_summary.py r05c4sr r05 c4_sr1 3904000000 "k_sr1_dia_m<double, 4"
 #   python tools/pmc_summary.py r05c4n8 r05 c4n8_sr1 488000000 "k_sr1_dia_m<double, 4"
+#   (c4n4 / c4n2: 976000000 / 1952000000 bytes, the N = 4 / 2 slabs)
 #   python tools/pmc_units.py r05c4sr "k_sr1_dia_m<double, 4"
 #   python tools/pmc_summary.py r05c3csr r05 c3_csr 1044721156 "k_spmv_csr<double, 456, 7, true"
 #   python tools/pmc_summary.py r05c4csr r05 c4_csr 6644480004 "k_spmv_csr<double, 456, 7, true"
@@ -19,6 +20,8 @@ for what in $steps; do
   case $what in
     c4sr)  bash tools/profile.sh r05c4sr $B --alg sr || exit $? ;;
     c4n8)  bash tools/profile.sh r05c4n8 python3 tools/dist_probe.py 50 --cases=sr || exit $? ;;
+    c4n4)  bash tools/profile.sh r05c4n4 python3 tools/dist_probe.py 100 --cases=sr || exit $? ;;
+    c4n2)  bash tools/profile.sh r05c4n2 python3 tools/dist_probe.py 200 --cases=sr || exit $? ;;
     units) bash tools/pmc_passes.sh r05c4sr $B --alg sr || exit $? ;;
     c3csr) bash tools/profile.sh r05c3csr $B --workload c3 --layout csr --alg hs || exit $? ;;
     c4csr) bash tools/profile.sh r05c4csr $B --layout csr --alg hs || exit $? ;;
