@@ -462,9 +462,22 @@ hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *s
 // (pn: the other p buffer), x += alpha p every other iteration, the exact
 // r.r partials (4 per workgroup of grid).  g: the all-reduced sums applied
 // privately (sr1_now; a partition's ranks), nullptr: *stt is current.
+// fo (the single-GPU solver): no k_finalize before it -- every workgroup
+// sums the SpMV's (p.s, s.s) pairs and the previous r.r partials (fo->pc,
+// not rr_part) and runs FIN_SR1's step privately; the last arriver (fo->tick)
+// writes the state and the history.
+struct SrFold {
+  const double *pq;  // the SpMV's (p.s, s.s) pairs
+  int nq;
+  const double *pc;  // r.r partials of the previous update (or the init)
+  int nc;
+  unsigned *tick;
+  double *hist;
+};
 template <typename T>
 hipError_t launch_update_sr(int n, T *x, T *r, const T *sv, const T *p, T *pn, CgState *stt,
-                            const double *g, double *rr_part, int grid, hipStream_t st, bool nt);
+                            const double *g, double *rr_part, int grid, hipStream_t st, bool nt,
+                            const SrFold *fo = nullptr);
 template <typename T>
 hipError_t launch_cg1_update(int n, T *x, T *p, T *r, T *s, const T *w,
                              const CgState *stt, double *part, int grid, hipStream_t st);

@@ -2505,117 +2505,183 @@ __global__ __launch_bounds__(kFoldBS) void k_xpay_xf(int n, T *__restrict__ x, c
 // update deferred): x += alpha_def p_{j-1} only -- the next finalize marks
 // done = 2.  pn == p (a partition's ranks: p in place, its ghost tail
 // refreshed by the halo): x += alpha p every iteration, nothing deferred.
-template <typename T, bool NT>
+// FOLD (the single-GPU solver, round 5): no k_finalize between the SpMV and
+// this launch -- every workgroup sums the SpMV's (p.s, s.s) pairs and the
+// previous r.r partials itself (sum_parts_sr, k_finalize<1024>'s order at
+// 1,024 threads: the same alpha, beta and stop test) and runs fin_sr1 on a
+// private copy of the state; the last workgroup to finish (two-level ticket:
+// every workgroup has read the state by then) writes the new state and the
+// history entry.  The r.r partials go to a buffer other than the one read
+// (pc_out: the solver alternates two).
+template <typename T, bool NT, bool FOLD>
 __global__ __launch_bounds__(kFoldBS) void k_update_sr(int n, T *__restrict__ x,
                                                        T *__restrict__ r,
                                                        const T *__restrict__ s, const T *p,
                                                        T *pn, CgState *__restrict__ st,
                                                        const double *g,
-                                                       double *__restrict__ rr_part) {
+                                                       double *__restrict__ rr_part,
+                                                       SrFold fo) {
   __shared__ double red[kFoldBS / kWave];
-  const Sr1Now sn = sr1_now(st, g);
-  if (sn.done > 1) return;  // uniform
-  typedef typename Vec16<T>::type V;
-  constexpr int W = Vec16<T>::W;
-  const int nv = n / W;
-  const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+  Sr1Now sn;
+  CgState c;
+  double rr_in = 0.0;
+  if constexpr (FOLD) {
+    static_assert(kFoldBS == 1024, "k_finalize<1024>'s summation order");
+    double ps, ss;
+    sum_parts_sr<kFoldBS>(fo.pq, fo.nq, fo.pc, fo.nc, red, ps, ss, rr_in);
+    __shared__ double bc[3];  // the sums are valid in thread 0: broadcast
+    if (threadIdx.x == 0) {
+      bc[0] = ps;
+      bc[1] = ss;
+      bc[2] = rr_in;
+    }
+    __syncthreads();
+    ps = bc[0];
+    ss = bc[1];
+    rr_in = bc[2];
+    c.done = st->done;
+    c.k_u = st->k_u;
+    c.k = st->k;
+    c.max_iter = st->max_iter;
+    c.use_tol = st->use_tol;
+    c.tol2bb = st->tol2bb;
+    c.hist_cap = 0;
+    c.brk = st->brk;
+    c.alpha = st->alpha;
+    c.beta = st->beta;
+    c.rr = st->rr;
+    c.ps = st->ps;
+    fin_sr1(ps, ss, rr_in, &c, nullptr);  // uniform: every workgroup the same
+    sn = Sr1Now{c.k_u, c.done, c.alpha, c.beta};
+  } else {
+    sn = sr1_now(st, g);
+  }
   const T alpha_d = (T)st->alpha_def;
   const bool defer = pn != p;
-  if (sn.done == 1) {  // the stop iteration's deferred x update, nothing else
-    if (!defer) return;  // x is complete
-    for (int i = gid; i < nv; i += stride) {
-      V xv = reinterpret_cast<const V *>(x)[i];
-      const V pd = reinterpret_cast<const V *>(pn)[i];
+  // the iteration's vector work (returns early on a stop)
+  auto body = [&]() {
+    if (sn.done > 1) return;  // uniform
+    typedef typename Vec16<T>::type V;
+    constexpr int W = Vec16<T>::W;
+    const int nv = n / W;
+    const int gid = blockIdx.x * kFoldBS + threadIdx.x, stride = gridDim.x * kFoldBS;
+    if (sn.done == 1) {  // the stop iteration's deferred x update, nothing else
+      if (!defer) return;  // x is complete
+      for (int i = gid; i < nv; i += stride) {
+        V xv = reinterpret_cast<const V *>(x)[i];
+        const V pd = reinterpret_cast<const V *>(pn)[i];
 #pragma unroll
-      for (int j = 0; j < W; ++j) {
-        const T ad = alpha_d * pd[j];
-        xv[j] = xv[j] + ad;
-      }
-      reinterpret_cast<V *>(x)[i] = xv;
-    }
-    if (gid == 0)
-      for (int k = nv * W; k < n; ++k) {
-        const T ad = alpha_d * pn[k];
-        x[k] = x[k] + ad;
-      }
-    return;
-  }
-  const int k = sn.k_u;  // this iteration (fin_sr1 made it k_u)
-  const bool odd = defer && (k & 1) != 0;       // x += alpha_{k-1} p_{k-1} + alpha_k p_k
-  const bool xup = !defer || odd, xone = !defer;  // xone: x += alpha_k p_k alone
-  const T alpha = (T)sn.alpha, beta = (T)sn.beta;
-  if (defer && !odd && blockIdx.x == 0 && threadIdx.x == 0)
-    st->alpha_def = sn.alpha;  // read at k + 1
-  double acc = 0.0;
-  for (int i = gid; i < nv; i += stride) {
-    V rv = reinterpret_cast<const V *>(r)[i];
-    const V sv = reinterpret_cast<const V *>(s)[i];
-    V pv = reinterpret_cast<const V *>(p)[i];
-    V xv = V(), pd = V();
-    if (xup) xv = reinterpret_cast<const V *>(x)[i];
-    if (odd) pd = reinterpret_cast<const V *>(pn)[i];
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const T as = alpha * sv[j];
-      rv[j] = rv[j] - as;
-      acc = acc + (double)rv[j] * (double)rv[j];
-    }
-    if (xup) {
-#pragma unroll
-      for (int j = 0; j < W; ++j) {
-        if (!xone) {
+        for (int j = 0; j < W; ++j) {
           const T ad = alpha_d * pd[j];
           xv[j] = xv[j] + ad;
         }
-        const T ap = alpha * pv[j];
-        xv[j] = xv[j] + ap;
+        reinterpret_cast<V *>(x)[i] = xv;
       }
-      if constexpr (NT) __builtin_nontemporal_store(xv, reinterpret_cast<V *>(x) + i);
-      else reinterpret_cast<V *>(x)[i] = xv;
-    }
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const T bp = beta * pv[j];
-      pv[j] = rv[j] + bp;
-    }
-    if constexpr (NT) {
-      __builtin_nontemporal_store(rv, reinterpret_cast<V *>(r) + i);
-      __builtin_nontemporal_store(pv, reinterpret_cast<V *>(pn) + i);
-    } else {
-      reinterpret_cast<V *>(r)[i] = rv;
-      reinterpret_cast<V *>(pn)[i] = pv;
-    }
-  }
-  if (gid == 0)
-    for (int e = nv * W; e < n; ++e) {
-      const T as = alpha * s[e];
-      const T re = r[e] - as;
-      acc = acc + (double)re * (double)re;
-      const T pe = p[e];
-      if (xup) {
-        T xe = x[e];
-        if (!xone) {
-          const T ad = alpha_d * pn[e];
-          xe = xe + ad;
+      if (gid == 0)
+        for (int k = nv * W; k < n; ++k) {
+          const T ad = alpha_d * pn[k];
+          x[k] = x[k] + ad;
         }
-        const T ap = alpha * pe;
-        x[e] = xe + ap;
-      }
-      const T bp = beta * pe;
-      r[e] = re;
-      pn[e] = re + bp;
+      return;
     }
-  // one partial per 256-thread quarter (k_update_rf's layout and order)
-  acc = wave_sum(acc);
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  if (lane == 0) red[wid] = acc;
-  __syncthreads();
-  if (threadIdx.x < kFoldBS / 256) {
-    constexpr int WQ = 256 / kWave;
-    double q = red[threadIdx.x * WQ];
+    const int k = sn.k_u;  // this iteration (fin_sr1 made it k_u)
+    const bool odd = defer && (k & 1) != 0;       // x += alpha_{k-1} p_{k-1} + alpha_k p_k
+    const bool xup = !defer || odd, xone = !defer;  // xone: x += alpha_k p_k alone
+    const T alpha = (T)sn.alpha, beta = (T)sn.beta;
+    if (defer && !odd && blockIdx.x == 0 && threadIdx.x == 0)
+      st->alpha_def = sn.alpha;  // read at k + 1 (only odd launches use it)
+    double acc = 0.0;
+    for (int i = gid; i < nv; i += stride) {
+      V rv = reinterpret_cast<const V *>(r)[i];
+      const V sv = reinterpret_cast<const V *>(s)[i];
+      V pv = reinterpret_cast<const V *>(p)[i];
+      V xv = V(), pd = V();
+      if (xup) xv = reinterpret_cast<const V *>(x)[i];
+      if (odd) pd = reinterpret_cast<const V *>(pn)[i];
 #pragma unroll
-    for (int w = 1; w < WQ; ++w) q = q + red[threadIdx.x * WQ + w];
-    rr_part[blockIdx.x * (kFoldBS / 256) + threadIdx.x] = q;
+      for (int j = 0; j < W; ++j) {
+        const T as = alpha * sv[j];
+        rv[j] = rv[j] - as;
+        acc = acc + (double)rv[j] * (double)rv[j];
+      }
+      if (xup) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          if (!xone) {
+            const T ad = alpha_d * pd[j];
+            xv[j] = xv[j] + ad;
+          }
+          const T ap = alpha * pv[j];
+          xv[j] = xv[j] + ap;
+        }
+        if constexpr (NT) __builtin_nontemporal_store(xv, reinterpret_cast<V *>(x) + i);
+        else reinterpret_cast<V *>(x)[i] = xv;
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const T bp = beta * pv[j];
+        pv[j] = rv[j] + bp;
+      }
+      if constexpr (NT) {
+        __builtin_nontemporal_store(rv, reinterpret_cast<V *>(r) + i);
+        __builtin_nontemporal_store(pv, reinterpret_cast<V *>(pn) + i);
+      } else {
+        reinterpret_cast<V *>(r)[i] = rv;
+        reinterpret_cast<V *>(pn)[i] = pv;
+      }
+    }
+    if (gid == 0)
+      for (int e = nv * W; e < n; ++e) {
+        const T as = alpha * s[e];
+        const T re = r[e] - as;
+        acc = acc + (double)re * (double)re;
+        const T pe = p[e];
+        if (xup) {
+          T xe = x[e];
+          if (!xone) {
+            const T ad = alpha_d * pn[e];
+            xe = xe + ad;
+          }
+          const T ap = alpha * pe;
+          x[e] = xe + ap;
+        }
+        const T bp = beta * pe;
+        r[e] = re;
+        pn[e] = re + bp;
+      }
+    // one partial per 256-thread quarter (k_update_rf's layout and order)
+    acc = wave_sum(acc);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) red[wid] = acc;
+    __syncthreads();
+    if (threadIdx.x < kFoldBS / 256) {
+      constexpr int WQ = 256 / kWave;
+      double q = red[threadIdx.x * WQ];
+  #pragma unroll
+      for (int w = 1; w < WQ; ++w) q = q + red[threadIdx.x * WQ + w];
+      rr_part[blockIdx.x * (kFoldBS / 256) + threadIdx.x] = q;
+    }
+  };
+  body();
+  if constexpr (FOLD) {
+    // the state once every workgroup has read it: the last arriver writes
+    // what fin_sr1 changed, and the history entry of iteration j - 1
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) last = take_ticket(fo.tick, gridDim.x);
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+      const int j = st->k_u + 1;
+      if (!st->done && j >= 1 && j - 1 < st->hist_cap) fo.hist[j - 1] = rr_in;
+      st->done = c.done;
+      st->k_u = c.k_u;
+      st->k = c.k;
+      st->brk = c.brk;
+      st->alpha = c.alpha;
+      st->beta = c.beta;
+      st->rr = c.rr;
+      st->ps = c.ps;
+    }
   }
 }
 
@@ -3566,13 +3632,26 @@ hipError_t launch_xpay_xf(int n, T *x, const T *p, T *pn, const T *r, CgState *s
 
 template <typename T>
 hipError_t launch_update_sr(int n, T *x, T *r, const T *sv, const T *p, T *pn, CgState *stt,
-                            const double *g, double *rr_part, int grid, hipStream_t st, bool nt) {
-  if (nt)
-    hipLaunchKernelGGL((k_update_sr<T, true>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r, sv, p,
-                       pn, stt, g, rr_part);
-  else
-    hipLaunchKernelGGL((k_update_sr<T, false>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r, sv, p,
-                       pn, stt, g, rr_part);
+                            const double *g, double *rr_part, int grid, hipStream_t st, bool nt,
+                            const SrFold *fo) {
+  if (fo && (g || !fo->pq || !fo->pc || !fo->tick || fo->pc == rr_part ||
+             grid > (kTickRegion - 1) * kTicketGroup))
+    return hipErrorInvalidValue;
+  const SrFold f = fo ? *fo : SrFold{};
+  if (fo) {
+    if (nt)
+      hipLaunchKernelGGL((k_update_sr<T, true, true>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r,
+                         sv, p, pn, stt, g, rr_part, f);
+    else
+      hipLaunchKernelGGL((k_update_sr<T, false, true>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r,
+                         sv, p, pn, stt, g, rr_part, f);
+  } else if (nt) {
+    hipLaunchKernelGGL((k_update_sr<T, true, false>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r,
+                       sv, p, pn, stt, g, rr_part, f);
+  } else {
+    hipLaunchKernelGGL((k_update_sr<T, false, false>), dim3(grid), dim3(kFoldBS), 0, st, n, x, r,
+                       sv, p, pn, stt, g, rr_part, f);
+  }
   return hipGetLastError();
 }
 
@@ -3736,7 +3815,8 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template hipError_t launch_xpay_xf<T>(int, T *, const T *, T *, const T *, CgState *,         \
                                         const double *, int, double *, int, hipStream_t, bool);  \
   template hipError_t launch_update_sr<T>(int, T *, T *, const T *, const T *, T *, CgState *,    \
-                                          const double *, double *, int, hipStream_t, bool);      \
+                                          const double *, double *, int, hipStream_t, bool,       \
+                                          const SrFold *);                                        \
   template hipError_t launch_cg1_update<T>(int, T *, T *, T *, T *, const T *, const CgState *,  \
                                            double *, int, hipStream_t);                          \
   template hipError_t launch_dot_seq<T>(int, const T *, const T *, double *, const int *,        \

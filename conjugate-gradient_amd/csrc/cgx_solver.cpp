@@ -132,6 +132,7 @@ struct cgx_solver {
   int sr_chain = 0;          // cgx_solver_set_sr_chain: 0 auto, > 0 chain width (rows)
   unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
+  double *d_pr2 = nullptr;   // unfused SR: the second r.r partial buffer
   int part_cap = 0;
   CgState *d_st = nullptr, *h_st = nullptr;
   double *d_hist = nullptr;
@@ -205,6 +206,7 @@ void free_system(cgx_solver *s) {
   dev_free(&s->d_w2);
   dev_free(&s->d_pa);
   dev_free(&s->d_pb);
+  dev_free(&s->d_pr2);
   dev_free(&s->d_hist);
   s->hist_alloc = 0;
   s->vec_bytes = 0;
@@ -229,7 +231,8 @@ int alloc_vectors(cgx_solver *s) {
       (rc = dev_alloc(&s->d_s, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_w, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_p2, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_pa, (size_t)s->part_cap * 8, &s->vec_bytes)) ||
-      (rc = dev_alloc(&s->d_pb, (size_t)s->part_cap * 8, &s->vec_bytes))) {
+      (rc = dev_alloc(&s->d_pb, (size_t)s->part_cap * 8, &s->vec_bytes)) ||
+      (rc = dev_alloc(&s->d_pr2, (size_t)s->part_cap * 8, &s->vec_bytes))) {
     free_system(s);
     return rc;
   }
@@ -353,20 +356,23 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
   int np = 0;
   if (s->alg == CGX_ALG_SR && !fused(s)) {
     // unfused SR (any layout): s = A p with the (p.s, s.s) pair per
-    // workgroup (cg.c:111), k_finalize FIN_SR1 (alpha cg.c:113, the
-    // estimate's beta cg.c:129, the stop test of the previous iteration on
-    // the exact r.r), k_update_sr: r, p, x of the iteration in one pass
-    // (cg.c:115-132) + the exact r.r partials -- two launches and one
-    // reduction per iteration (oracle_solve_sr)
+    // workgroup (cg.c:111), then k_update_sr with FIN_SR1 folded in (alpha
+    // cg.c:113, the estimate's beta cg.c:129, the stop test of the previous
+    // iteration on the exact r.r; round 5: no k_finalize launch between):
+    // r, p, x of the iteration in one pass (cg.c:115-132) + the exact r.r
+    // partials -- two launches and one reduction per iteration
+    // (oracle_solve_sr)
     const int q = s->pbuf;
     T *pc = (T *)(q ? s->d_p2 : s->d_p), *pn = (T *)(q ? s->d_p : s->d_p2);
     CGX_HIP(s->A.spmv<T>(pc, sv, s->d_pb, &s->d_st->done, s->A.all_items(), st, &np,
                          LaunchEv{ev0, ev1}, true));
     if (2 * np > s->part_cap) return CGX_EINVAL;
-    CGX_HIP(launch_finalize(FIN_SR1, s->d_pb, np, nullptr, 0, s->d_st, s->d_hist, nullptr, st,
-                            s->d_pa, s->vec_grid));
-    CGX_HIP(launch_update_sr<T>(n, x, r, sv, pc, pn, s->d_st, nullptr, s->d_pa, s->vec_grid / 4,
-                                st, s->A.nt));
+    // FIN_SR1 folded into the update (round 5): its r.r partials alternate
+    // between d_pa (the init's) and d_pr2
+    double *rr_in = q ? s->d_pr2 : s->d_pa, *rr_out = q ? s->d_pa : s->d_pr2;
+    const SrFold fo{s->d_pb, np, rr_in, s->vec_grid, s->d_tick, s->d_hist};
+    CGX_HIP(launch_update_sr<T>(n, x, r, sv, pc, pn, s->d_st, nullptr, rr_out, s->vec_grid / 4,
+                                st, s->A.nt, &fo));
     s->pbuf ^= 1;
     return 0;
   }
