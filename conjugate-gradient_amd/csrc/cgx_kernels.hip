@@ -153,6 +153,107 @@ __device__ double canon_sum(const double *pa, int na, double *red16) {
   return s;
 }
 
+// Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order, then the
+// block tree.  All of a thread's loads (up to U) are issued before the first
+// add, so a 40K-entry partial array costs one memory round trip, not one per
+// 16 entries.  Starts from the first partial, so a single partial passes
+// through unchanged.
+template <int BS>
+__device__ __forceinline__ double sum_parts(const double *pa, int na, double *red) {
+  constexpr int U = 48;
+  double acc = 0.0;
+  bool first = true;
+  for (int i = threadIdx.x; i < na; i += U * BS) {
+    double v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (i + j * BS < na) {
+        acc = first ? v[j] : acc + v[j];
+        first = false;
+      }
+  }
+  const double s = block_sum<BS>(acc, red);
+  __syncthreads();
+  return s;
+}
+
+// Two partial arrays summed with all loads of both in flight at once; each
+// sum keeps sum_parts' order (thread t: index order, then the block tree).
+template <int BS>
+__device__ __forceinline__ void sum_parts2(const double *pa, int na, const double *pb, int nb,
+                                           double *red, double &sa, double &sb) {
+  constexpr int U = 24;
+  double acc_a = 0.0, acc_b = 0.0;
+  bool fa = true, fb = true;
+  const int nmax = na > nb ? na : nb;
+  for (int i = threadIdx.x; i < nmax; i += U * BS) {
+    double va[U], vb[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      va[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
+      vb[j] = i + j * BS < nb ? pb[i + j * BS] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (i + j * BS < na) {
+        acc_a = fa ? va[j] : acc_a + va[j];
+        fa = false;
+      }
+      if (i + j * BS < nb) {
+        acc_b = fb ? vb[j] : acc_b + vb[j];
+        fb = false;
+      }
+    }
+  }
+  sa = block_sum<BS>(acc_a, red);
+  __syncthreads();
+  sb = block_sum<BS>(acc_b, red);
+  __syncthreads();
+}
+
+// CGX_ALG_SR's local sums in one pass: (p.s, s.s) pairs pq[0, na) -- one
+// 16-byte load each -- and the r.r partials pc[0, nc), all loads of a pass in
+// flight together; each sum in sum_parts' order (thread t: index order, then
+// the block tree).
+template <int BS>
+__device__ __forceinline__ void sum_parts_sr(const double *pq, int na, const double *pc, int nc,
+                                             double *red, double &sa, double &sb, double &sc) {
+  constexpr int U = 16;
+  const double2 *q2 = reinterpret_cast<const double2 *>(pq);
+  double a = 0.0, b = 0.0, c = 0.0;
+  bool fa = true, fc = true;
+  const int nmax = na > nc ? na : nc;
+  for (int i = threadIdx.x; i < nmax; i += U * BS) {
+    double2 v[U];
+    double w[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      v[j] = i + j * BS < na ? q2[i + j * BS] : make_double2(0.0, 0.0);
+      w[j] = i + j * BS < nc ? pc[i + j * BS] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (i + j * BS < na) {
+        a = fa ? v[j].x : a + v[j].x;
+        b = fa ? v[j].y : b + v[j].y;
+        fa = false;
+      }
+      if (i + j * BS < nc) {
+        c = fc ? w[j] : c + w[j];
+        fc = false;
+      }
+    }
+  }
+  sa = block_sum<BS>(a, red);
+  __syncthreads();
+  sb = block_sum<BS>(b, red);
+  __syncthreads();
+  sc = block_sum<BS>(c, red);
+  __syncthreads();
+}
+
 // The SpMV epilogue: the workgroup's x[row]*y[row] terms, wave sums added in
 // wave order, one partial per workgroup.
 template <int WPB>
@@ -2133,107 +2234,6 @@ __global__ __launch_bounds__(BS) void k_xpay(int n, T *__restrict__ p, const T *
       const T bp = beta * p[i];
       p[i] = r[i] + bp;
     }
-}
-
-// Thread t adds pa[t], pa[t+BS], pa[t+2BS], ... in index order, then the
-// block tree.  All of a thread's loads (up to U) are issued before the first
-// add, so a 40K-entry partial array costs one memory round trip, not one per
-// 16 entries.  Starts from the first partial, so a single partial passes
-// through unchanged.
-template <int BS>
-__device__ __forceinline__ double sum_parts(const double *pa, int na, double *red) {
-  constexpr int U = 48;
-  double acc = 0.0;
-  bool first = true;
-  for (int i = threadIdx.x; i < na; i += U * BS) {
-    double v[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) v[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (i + j * BS < na) {
-        acc = first ? v[j] : acc + v[j];
-        first = false;
-      }
-  }
-  const double s = block_sum<BS>(acc, red);
-  __syncthreads();
-  return s;
-}
-
-// Two partial arrays summed with all loads of both in flight at once; each
-// sum keeps sum_parts' order (thread t: index order, then the block tree).
-template <int BS>
-__device__ __forceinline__ void sum_parts2(const double *pa, int na, const double *pb, int nb,
-                                           double *red, double &sa, double &sb) {
-  constexpr int U = 24;
-  double acc_a = 0.0, acc_b = 0.0;
-  bool fa = true, fb = true;
-  const int nmax = na > nb ? na : nb;
-  for (int i = threadIdx.x; i < nmax; i += U * BS) {
-    double va[U], vb[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      va[j] = i + j * BS < na ? pa[i + j * BS] : 0.0;
-      vb[j] = i + j * BS < nb ? pb[i + j * BS] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (i + j * BS < na) {
-        acc_a = fa ? va[j] : acc_a + va[j];
-        fa = false;
-      }
-      if (i + j * BS < nb) {
-        acc_b = fb ? vb[j] : acc_b + vb[j];
-        fb = false;
-      }
-    }
-  }
-  sa = block_sum<BS>(acc_a, red);
-  __syncthreads();
-  sb = block_sum<BS>(acc_b, red);
-  __syncthreads();
-}
-
-// CGX_ALG_SR's local sums in one pass: (p.s, s.s) pairs pq[0, na) -- one
-// 16-byte load each -- and the r.r partials pc[0, nc), all loads of a pass in
-// flight together; each sum in sum_parts' order (thread t: index order, then
-// the block tree).
-template <int BS>
-__device__ __forceinline__ void sum_parts_sr(const double *pq, int na, const double *pc, int nc,
-                                             double *red, double &sa, double &sb, double &sc) {
-  constexpr int U = 16;
-  const double2 *q2 = reinterpret_cast<const double2 *>(pq);
-  double a = 0.0, b = 0.0, c = 0.0;
-  bool fa = true, fc = true;
-  const int nmax = na > nc ? na : nc;
-  for (int i = threadIdx.x; i < nmax; i += U * BS) {
-    double2 v[U];
-    double w[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      v[j] = i + j * BS < na ? q2[i + j * BS] : make_double2(0.0, 0.0);
-      w[j] = i + j * BS < nc ? pc[i + j * BS] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (i + j * BS < na) {
-        a = fa ? v[j].x : a + v[j].x;
-        b = fa ? v[j].y : b + v[j].y;
-        fa = false;
-      }
-      if (i + j * BS < nc) {
-        c = fc ? w[j] : c + w[j];
-        fc = false;
-      }
-    }
-  }
-  sa = block_sum<BS>(a, red);
-  __syncthreads();
-  sb = block_sum<BS>(b, red);
-  __syncthreads();
-  sc = block_sum<BS>(c, red);
-  __syncthreads();
 }
 
 // Folded HS (the default fast path): no finalize kernels.  Every workgroup
