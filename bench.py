@@ -557,16 +557,43 @@ def headline_solve(sysm, steps, warmup, layout="auto", alg="hs"):
     return dict(info=info, upload_ms=upload_ms, wall=wall, dev_ms=dev_ms, spmv_ms=spmv_ms)
 
 
+def csr_legs(sysm, steps, warmup, alg):
+    """The plain-CSR solve of the system in the recurrence the line runs (HS,
+    or SR: since round 5 two launches and one reduction on any layout) with
+    back-to-back SpMVs, and -- when that is SR -- the HS iteration beside it."""
+    a = alg if alg in ("hs", "sr") else "hs"
+    gate = None
+    if a == "sr":  # SR's x against HS's on this layout first (sr_gate); HS if it fails
+        gate = sr_gate(sysm, ("csr",))["csr"]
+        if not gate["ok"]:
+            a = "hs"
+    csr = solver_leg(sysm, steps, warmup, "csr", b2b=True, alg=a)
+    csr["alg"] = a
+    csr["sr_gate"] = gate
+    if a != "hs":
+        csr["hs"] = solver_leg(sysm, steps, warmup, "csr", alg="hs")
+    return csr
+
+
 def csr_roofline(csr, wl_name):
     """SURVEY.md 8d's roofline figure: the plain-CSR SpMV on B_spmv = 12 nnz +
-    4 (n+1) + 16 n, in the CG iteration and back to back."""
+    4 (n+1) + 16 n, in the CG iteration of the line's recurrence (csr_legs),
+    in the HS iteration, and back to back."""
     ci = csr["info"]
     c_gbs, c_frac = spmv_roofline(ci["spmv_bytes"], csr["spmv_us"] * 1e-3)
     b_gbs, b_frac = spmv_roofline(ci["spmv_bytes"], csr["b2b_spmv_us"] * 1e-3)
+    hs = csr.get("hs")
+    hs_fields = {}
+    if hs is not None:
+        h_gbs, h_frac = spmv_roofline(ci["spmv_bytes"], hs["spmv_us"] * 1e-3)
+        hs_fields = dict(in_hs_iteration=dict(frac=h_frac, achieved=h_gbs,
+                                              spmv_us=hs["spmv_us"], cg_its=hs["value"]))
     return dict(
         bound="hbm", achieved=c_gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=c_frac,
         **traffic_fields(wl_name, "csr", ci["spmv_bytes"]),
-        kernel=KERNELS["csr"] + ", in the CG iteration",
+        kernel=KERNELS["csr"] + ", in the CG iteration (" +
+        ALG_DESC["sr_unfused" if csr.get("alg") == "sr" else "hs"] + ")",
+        recurrence=csr.get("alg", "hs"), sr_gate=csr.get("sr_gate"), **hs_fields,
         basis="SURVEY.md 8d B_spmv = 12 nnz + 4 (n+1) + 16 n (CSR int32 col + fp64 val, "
               "row_ptr, x read once, y written once)",
         algorithmic_bytes_per_launch=int(ci["spmv_bytes"]), spmv_us=csr["spmv_us"],
@@ -658,7 +685,7 @@ def c3_legs(steps, warmup):
     sysm = make_system(wl)
     alg, trial = alg_trial(sysm, warmup)
     h = headline_solve(sysm, steps, warmup, alg=alg)
-    csr = solver_leg(sysm, steps, warmup, "csr", b2b=True)
+    csr = csr_legs(sysm, steps, warmup, alg)
     out = dict(workload=wl["desc"], value=round(steps / h["wall"], 2), unit="it/s",
                alg=ALG_DESC[alg], alg_trial=trial,
                ms_per_step=round(1e3 * h["wall"] / steps, 4), layout=layout_desc(h["info"]),
@@ -666,7 +693,9 @@ def c3_legs(steps, warmup):
                default_layout=layout_roofline(h["info"], h["spmv_ms"], "c3"),
                csr_roofline=csr_roofline(csr, "c3"),
                csr_plain=dict(value=csr["value"], unit="it/s", spmv_us=csr["spmv_us"],
-                              b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"]))
+                              b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"],
+                              recurrence=csr["alg"],
+                              hs_value=csr["hs"]["value"] if "hs" in csr else csr["value"]))
     out["general_coefficients"] = general_coefficients(steps, warmup)
     out["solve_e2e"] = solve_e2e(sysm)
     # cold first (the first SR call switches the recurrence and
@@ -724,7 +753,7 @@ def run_single(args, wl_name):
                           default_layout=layout_roofline(hh["info"], hh["spmv_ms"], wl_name))
     if not args.no_legs:
         if info["layout_name"] != "csr":
-            legs["csr"] = solver_leg(sysm, args.steps, args.warmup, "csr", b2b=True)
+            legs["csr"] = csr_legs(sysm, args.steps, args.warmup, alg)
         if wl["kind"] in ("lap3d", "lap2d") and info["layout_name"] != "dc":
             legs["dc"] = solver_leg(sysm, args.steps, args.warmup, "dc")
     csr = legs.get("csr")
@@ -771,7 +800,11 @@ def run_single(args, wl_name):
         if csr is not None:
             extra["csr_plain"] = dict(value=csr["value"], unit="it/s", spmv_us=csr["spmv_us"],
                                       b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"],
-                                      note="the same solve on the reference's CSR (layout csr)")
+                                      recurrence=csr["alg"],
+                                      hs_value=csr["hs"]["value"] if "hs" in csr else csr["value"],
+                                      note="the same solve on the reference's CSR (layout csr), "
+                                           "in the line's recurrence (sr: unfused, two launches "
+                                           "and one reduction); hs_value: the HS iteration")
         if wl["kind"] in ("lap3d", "lap2d"):
             extra["matrix_free"] = matrix_free(wl, sysm["b"], args.steps, args.warmup)
         if wl_name == "c4":
