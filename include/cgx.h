@@ -55,10 +55,10 @@ void cgx_free_mv_deep(struct __mv_sparse *m);
  *   mode CGX_MODE_EXACT: the reference's sequential dot-product order, x
  *        bit-identical to cg.c on chained matrices (HS only)
  *   alg  CGX_ALG_HS (the reference recurrence, default), CGX_ALG_CG1, or
- *        CGX_ALG_SR (fast mode only: the one-launch single-reduction step
- *        where the matrix takes the plane-marched DIA step -- the bench's
- *        N = 1 recurrence; any other matrix runs HS instead, and
- *        cgx_ops_last_timing().alg reports which one ran)
+ *        CGX_ALG_SR (fast mode only: one reduction per iteration -- ONE
+ *        launch where the matrix takes the plane-marched DIA step, the
+ *        bench's N = 1 recurrence; two launches on any other matrix;
+ *        cgx_ops_last_timing().alg reports what ran)
  * The drop-in CLI maps CGX_MODE=exact / CGX_ALG=cg1|sr onto this call. */
 int cgx_ops_set_mode(int mode, int alg);
 /* GPU of those entry points (default 0); before their first call only. */
@@ -73,8 +73,7 @@ typedef struct {
   double total_ms, setup_ms, hash_ms, solve_ms, download_ms;
   int uploaded, iters;
   int breakdown;  /* as cgx_info.breakdown, for the last conj_grad / solve */
-  int alg;        /* CGX_ALG_* that ran: CGX_ALG_SR was requested but the
-                     matrix has no plane-marched DIA step -> CGX_ALG_HS */
+  int alg;        /* CGX_ALG_* that ran                                  */
 } cgx_ops_timing;
 int cgx_ops_last_timing(cgx_ops_timing *t);
 
@@ -125,9 +124,10 @@ enum { CGX_MODE_FAST = 0,    /* two-stage parallel reductions (default)      */
        CGX_MODE_EXACT = 1 }; /* sequential dots: reference bit order          */
 enum { CGX_ALG_HS = 0,       /* Hestenes-Stiefel, the reference recurrence    */
        CGX_ALG_CG1 = 1,      /* Chronopoulos-Gear, one fused reduction/iter   */
-       CGX_ALG_SR = 2 };     /* HS with one reduction/iter: cgx_dist, and one
-                                GPU where the plane-marched DIA step applies
-                                (one launch per iteration, cgx_solver_set_march) */
+       CGX_ALG_SR = 2 };     /* HS with one reduction/iter: one launch per
+                                iteration where the plane-marched DIA step
+                                applies (cgx_solver_set_march), else the SpMV
+                                + one vector launch; ranks alike           */
 enum { CGX_F64 = 0, CGX_F32 = 1 };
 
 /* Device layout of the matrix the SpMV streams (the C ABI always takes the
