@@ -85,9 +85,13 @@ struct CgState {
   // last launch pair are not yet applied to this state (every kernel of the
   // next iteration applies them to its own copy, FIN_SUM3_SR1 to the state)
   int sr_pend;
-  int pad_;
+  // the one-launch SR step's x deferral depth (2, or 4 on one GPU: x +=
+  // alpha p for four iterations in every fourth launch; 0 reads as 2) and
+  // alpha_i of the pending iterations (alpha_q[i % 4], depth 4)
+  int xdef;
+  double alpha_q[4];
 };
-static_assert(sizeof(CgState) == 136, "CgState layout");
+static_assert(sizeof(CgState) == 168, "CgState layout");
 
 // Finalize ops (single-workgroup scalar steps of the recurrence).
 enum FinOp {
@@ -322,6 +326,10 @@ struct Sr1Args {
   int march;  // steps per segment (nseg == 0)
   int nseg = 0;
   int cw = 0;  // chain width in rows (even, <= sb slices; 0: sb slices)
+  // x deferral depth 4 (st->xdef == 4; single GPU): the p buffers holding
+  // p_{k-2} (pa) and p_{k-1} (pb) -- pnew holds p_{k-3}, pold p_k; nullptr:
+  // depth 2
+  const T *pa = nullptr, *pb = nullptr;
   int sb = 0;  // rows per step in slices (1, 2, 4; 0: the matrix's plan)
   int elo = 0, ehi = 0x7fffffff;
   // partitioned: the all-reduced (p.s, s.s, r.r) of the last iteration,

@@ -400,7 +400,11 @@ __device__ void fin_sr1(double ps, double ss, double rr, CgState *st, double *hi
     st->rr = rr;
     st->k = k;
     if (k >= st->max_iter || (st->use_tol && rr <= st->tol2bb)) {
-      st->done = (k & 1) ? 2 : 1;
+      // x is complete after iteration k's launch when k closes a deferral
+      // group (depth 2: odd k; 4: k % 4 == 3), else the next launch adds
+      // the pending alpha_i p_i (done = 1)
+      const int xd = st->xdef >= 4 ? 4 : 2;
+      st->done = (k % xd == xd - 1) ? 2 : 1;
       return;
     }
   }
@@ -436,6 +440,7 @@ __device__ __forceinline__ Sr1Now sr1_now(const CgState *st, const double *g) {
   c.brk = 1;  // (not written back)
   c.alpha = st->alpha;
   c.beta = st->beta;
+  c.xdef = st->xdef;
   fin_sr1(g[0], g[1], g[2], &c, nullptr);
   return Sr1Now{c.k_u, c.done, c.alpha, c.beta};
 }
@@ -1505,11 +1510,21 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   if (sn.done > 1) return;  // uniform
   const int k = sn.k_u;  // the last finalized iteration (-1: none)
   const bool first = k < 0, stop = sn.done == 1;
-  const bool odd = (k & 1) != 0;
+  // x deferral: depth 2 (x += alpha p for two iterations in odd launches)
+  // or depth 4 (f.pa: four iterations in every launch with k % 4 == 3,
+  // p_{k-3} / p_{k-2} / p_{k-1} from pnew / pa / pb, their alphas from
+  // alpha_q) -- the same roundings in the same order as one update per
+  // iteration (cg.c:115-116)
+  const bool d4 = f.pa != nullptr;
+  const bool odd = d4 ? (k & 3) == 3 : (k & 1) != 0;  // this launch updates x
   const bool xup = !first && odd;
   const T alpha = (T)sn.alpha, beta = (T)sn.beta, alpha_d = (T)f.st->alpha_def;
-  if (!first && !odd && !stop && blockIdx.x == 0 && t == 0)
-    const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
+  if (!first && !odd && !stop && blockIdx.x == 0 && t == 0) {
+    if (d4) const_cast<CgState *>(f.st)->alpha_q[k & 3] = sn.alpha;
+    else const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
+  }
+  const T aq0 = d4 ? (T)f.st->alpha_q[0] : T(0), aq1 = d4 ? (T)f.st->alpha_q[1] : T(0),
+          aq2 = d4 ? (T)f.st->alpha_q[2] : T(0);
   const int padn = a.mslices * kDiaSliceRows;
   const bool nt = a.nt != 0;
   const int wn = wc + a.hl + a.hr, ws = a.mws;
@@ -1525,9 +1540,19 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     o.xo = ld_pair(f.x, rs);
     if (odd) o.pd = ld_pair((const T *)f.pnew, rs);
   };
-  auto x_update = [&](const XOps &o, int r, int rend) {
+  auto x_update = [&](const XOps &o, const P &qa, const P &qb, int r, int rend) {
     T x0 = o.xo.x, x1 = o.xo.y;
-    if (odd) {
+    if (d4) {  // k % 4 == 3: alpha_{k-3} p_{k-3}, alpha_{k-2} p_{k-2}, alpha_{k-1} p_{k-1}
+      const T d0 = aq0 * o.pd.x, d1 = aq0 * o.pd.y;
+      x0 = x0 + d0;
+      x1 = x1 + d1;
+      const T e0 = aq1 * qa.x, e1 = aq1 * qa.y;
+      x0 = x0 + e0;
+      x1 = x1 + e1;
+      const T g0 = aq2 * qb.x, g1 = aq2 * qb.y;
+      x0 = x0 + g0;
+      x1 = x1 + g1;
+    } else if (odd) {
       const T d0 = alpha_d * o.pd.x, d1 = alpha_d * o.pd.y;
       x0 = x0 + d0;
       x1 = x1 + d1;
@@ -1560,13 +1585,32 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     }
   };
   if (stop) {
-    // fin_sr1 stopped at an even iteration k (k_u): its deferred x +=
-    // alpha_k p_k only, p_k in the p_new buffer of this launch
+    // fin_sr1 stopped at iteration k (k_u) with x updates pending.  Depth 2
+    // (k even): alpha_k p_k, p_k in the p_new buffer of this launch.  Depth
+    // 4 (k % 4 = q < 3): alpha_i p_i for i = k - q .. k in order, p_{k-2} /
+    // p_{k-1} / p_k in this launch's pnew / pa / pb, alpha_i in alpha_q
+    const int q = k & 3;
+    const T b0 = d4 ? (T)f.st->alpha_q[(k - 2) & 3] : T(0),
+            b1 = d4 ? (T)f.st->alpha_q[(k - 1) & 3] : T(0),
+            b2 = d4 ? (T)f.st->alpha_q[k & 3] : alpha_d;
     for (int m = m0; m < m1; ++m) {
       const int r = base_of(m) + 2 * t, rend = min(a.n, base_of(m) + wc), rs = r < a.n ? r : 0;
-      const P pd = ld_pair((const T *)f.pnew, rs), xo = ld_pair(f.x, rs);
-      const T d0 = alpha_d * pd.x, d1 = alpha_d * pd.y;
-      if (r < rend) st_pair(f.x, r, rend, xo.x + d0, xo.y + d1, false);
+      P xo = ld_pair(f.x, rs);
+      if (d4 && q >= 2) {
+        const P v = ld_pair((const T *)f.pnew, rs);
+        const T e0 = b0 * v.x, e1 = b0 * v.y;
+        xo.x = xo.x + e0;
+        xo.y = xo.y + e1;
+      }
+      if (d4 && q >= 1) {
+        const P v = ld_pair(f.pa, rs);
+        const T e0 = b1 * v.x, e1 = b1 * v.y;
+        xo.x = xo.x + e0;
+        xo.y = xo.y + e1;
+      }
+      const P v = ld_pair(d4 ? f.pb : (const T *)f.pnew, rs);
+      const T e0 = b2 * v.x, e1 = b2 * v.y;
+      if (r < rend) st_pair(f.x, r, rend, xo.x + e0, xo.y + e1, false);
     }
     return;
   }
@@ -1626,6 +1670,14 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   if (t < a.ndiag * 16) lv[t] = tv;
   auto step = [&](int m, const CR &ccw, XOps &cx, CR &ncw, XOps &nx) {
     store_win(m + 1);
+    // depth 4's two more p operands of step m's rows: issued before this
+    // step's other loads, used after its compute (no wait on the prefetch)
+    P qa{}, qb{};
+    if (d4 && xup) {
+      const int r = base_of(m) + 2 * t, rs = r < a.n ? r : 0;
+      qa = ld_pair(f.pa, rs);
+      qb = ld_pair(f.pb, rs);
+    }
     codes_at(min(m + 1, m1 - 1), ncw);
     load_win(min(m + 2, m1));  // in flight during step m
     if (xup && m + 1 < m1) load_x(m + 1, nx);
@@ -1663,7 +1715,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       st_pair(a.y, r, rend, a0, a1, nt);
       st_pair(f.pnew, r, rend, pn0, pn1, false);
       st_pair(f.rnew, r, rend, rk0, rk1, false);
-      if (xup) x_update(cx, r, rend);
+      if (xup) x_update(cx, qa, qb, r, rend);
       const bool own = r >= f.elo && r < f.ehi;  // edge pairs: k_sr1_edge's (p.s, s.s)
       if (own) {
         sps = sps + (double)pn0 * (double)a0;
@@ -2551,6 +2603,7 @@ __global__ __launch_bounds__(kFoldBS) void k_update_sr(int n, T *__restrict__ x,
     c.beta = st->beta;
     c.rr = st->rr;
     c.ps = st->ps;
+    c.xdef = st->xdef;
     fin_sr1(ps, ss, rr_in, &c, nullptr);  // uniform: every workgroup the same
     sn = Sr1Now{c.k_u, c.done, c.alpha, c.beta};
   } else {

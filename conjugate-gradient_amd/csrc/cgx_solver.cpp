@@ -133,6 +133,7 @@ struct cgx_solver {
   unsigned *d_tick = nullptr;  // last-arriver counter of k_update_rf's r.r sum
   double *d_pa = nullptr, *d_pb = nullptr;
   double *d_pr2 = nullptr;   // unfused SR: the second r.r partial buffer
+  void *d_p3 = nullptr, *d_p4 = nullptr;  // the one-launch SR step's third / fourth p
   int part_cap = 0;
   CgState *d_st = nullptr, *h_st = nullptr;
   double *d_hist = nullptr;
@@ -140,8 +141,8 @@ struct cgx_solver {
   size_t vec_bytes = 0;
   bool have_matrix = false, have_rhs = false, bench_ready = false;
   int last_iters = 0;
-  hipGraphExec_t gexec[2] = {};   // graph_batch iterations, per p-buffer parity
-  hipGraphExec_t gexec1[2] = {};  // one iteration (remainders), per parity
+  hipGraphExec_t gexec[4] = {};   // graph_batch iterations, per p-buffer rotation
+  hipGraphExec_t gexec1[4] = {};  // one iteration (remainders), per rotation
   int gexec_key = -1;
   std::vector<hipEvent_t> events;
 };
@@ -153,7 +154,7 @@ using namespace cgx;
 size_t tsize(int dtype) { return dtype == CGX_F32 ? 4 : 8; }
 
 void drop_graph(cgx_solver *s) {
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < 4; ++q) {
     if (s->gexec[q]) (void)hipGraphExecDestroy(s->gexec[q]);
     if (s->gexec1[q]) (void)hipGraphExecDestroy(s->gexec1[q]);
     s->gexec[q] = s->gexec1[q] = nullptr;
@@ -191,6 +192,17 @@ bool alternating(const cgx_solver *s) {
   return (s->alg != CGX_ALG_CG1 && s->mode == CGX_MODE_FAST) || fused(s);
 }
 
+// The one-launch SR step defers x four iterations deep (round 5: x, p_{k-3},
+// p_{k-2}, p_{k-1} read and x written in every fourth launch -- 10 B per row
+// and iteration instead of 12; CgState::xdef): four p buffers rotate, p_i in
+// buffer (i + 1) % 4.  Other recurrences alternate two (or keep one).
+// Same box, alternating (profiles/r05_ab_sr_x4.log): C4 711.3-711.9 against
+// 739.0 us per iteration (launch 694 against 730), C3 134.4-135.9 against
+// 139.4-140.1.
+bool sr_x4(const cgx_solver *s) { return fused(s) && s->alg == CGX_ALG_SR; }
+
+int prot(const cgx_solver *s) { return sr_x4(s) ? 4 : alternating(s) ? 2 : 1; }
+
 void free_system(cgx_solver *s) {
   drop_graph(s);
   s->A.release();
@@ -207,6 +219,8 @@ void free_system(cgx_solver *s) {
   dev_free(&s->d_pa);
   dev_free(&s->d_pb);
   dev_free(&s->d_pr2);
+  dev_free(&s->d_p3);
+  dev_free(&s->d_p4);
   dev_free(&s->d_hist);
   s->hist_alloc = 0;
   s->vec_bytes = 0;
@@ -254,9 +268,17 @@ bool needs_rsw2(const cgx_solver *s) {
 }
 
 int ensure_rsw2(cgx_solver *s) {
-  if (!needs_rsw2(s) || s->d_r2) return 0;
   const size_t nv = ((size_t)s->A.n + kPad) * tsize(s->A.dtype);
   int rc;
+  if (sr_x4(s) && !s->d_p3) {  // the one-launch SR step's four p buffers
+    if ((rc = dev_alloc(&s->d_p3, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_p4, nv, &s->vec_bytes))) {
+      dev_free(&s->d_p3);
+      dev_free(&s->d_p4);
+      return rc;
+    }
+    for (void *v : {s->d_p3, s->d_p4}) CGX_HIP(hipMemsetAsync(v, 0, nv, s->stream));
+  }
+  if (!needs_rsw2(s) || s->d_r2) return 0;
   if ((rc = dev_alloc(&s->d_r2, nv, &s->vec_bytes)) || (rc = dev_alloc(&s->d_s2, nv, &s->vec_bytes)) ||
       (rc = dev_alloc(&s->d_w2, nv, &s->vec_bytes))) {
     dev_free(&s->d_r2);
@@ -380,19 +402,28 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     // k_sr1_dia_m: r = r - alpha s, p = r + beta p (window rows), x update,
     // s = A p, (p.s, s.s) pairs + r.r per workgroup; k_finalize FIN_SR1: the
     // scalar step (oracle_solve_sr's recurrence, one reduction)
-    const int q = s->pbuf;
-    T *po = (T *)(q ? s->d_p2 : s->d_p), *pn = (T *)(q ? s->d_p : s->d_p2);
-    T *ro = (T *)(q ? s->d_r2 : s->d_r), *rn = (T *)(q ? s->d_r : s->d_r2);
-    T *so = (T *)(q ? s->d_s2 : s->d_s), *sn = (T *)(q ? s->d_s : s->d_s2);
+    // p rotates over four buffers (sr_x4: p_{k-3}, p_{k-2}, p_{k-1} in pn,
+    // pa, pb) or alternates over two; r and s alternate
+    const int q = s->pbuf, rq = q & 1;
+    T *pb4[4] = {(T *)s->d_p, (T *)s->d_p2, (T *)s->d_p3, (T *)s->d_p4};
+    const int nr = sr_x4(s) ? 4 : 2;
+    T *po = pb4[q % nr], *pn = pb4[(q + 1) % nr];
+    T *ro = (T *)(rq ? s->d_r2 : s->d_r), *rn = (T *)(rq ? s->d_r : s->d_r2);
+    T *so = (T *)(rq ? s->d_s2 : s->d_s), *sn = (T *)(rq ? s->d_s : s->d_s2);
     const SpmvArgs<T> a = s->A.args<T>(nullptr, sn, nullptr, &s->d_st->done, s->A.all_items());
     Sr1Args<T> f{x, po, pn, ro, rn, so, s->d_st, s->d_pa, s->d_pb, march_len(s)};
+    if (nr == 4) {
+      if (!pb4[2] || !pb4[3]) return CGX_EINVAL;
+      f.pa = pb4[(q + 2) & 3];
+      f.pb = pb4[(q + 3) & 3];
+    }
     sr1_shape(s, a, f);
     const int g = sr1_grid(a, f);
     if (2 * g > s->part_cap) return CGX_EINVAL;
     CGX_HIP(launch_sr1_march<T>(a, f, st, LaunchEv{ev0, ev1}));
     CGX_HIP(launch_finalize(FIN_SR1, s->d_pa, g, nullptr, 0, s->d_st, s->d_hist, nullptr, st,
                             s->d_pb, g));
-    s->pbuf ^= 1;
+    s->pbuf = (q + 1) % nr;
     return 0;
   }
   if (fused(s) && s->alg == CGX_ALG_CG1) {
@@ -490,7 +521,7 @@ int capture_iters(cgx_solver *s, int count, int parity, hipGraphExec_t *out) {
 template <typename T>
 int ensure_graphs(cgx_solver *s) {
   const int key = s->alg * 4 + s->mode * 2 + (fused(s) ? 1 : 0);
-  const int nq = alternating(s) ? 2 : 1;
+  const int nq = prot(s);
   if (s->gexec_key == key) return 0;
   drop_graph(s);
   int rc = 0;
@@ -511,14 +542,16 @@ int enqueue_iters(cgx_solver *s, long long count) {
   if (s->use_graph && count > 0) {
     int rc = ensure_graphs<T>(s);
     if (rc) return rc;
-    const bool alt = alternating(s);  // an even batch keeps the p parity, one iteration flips it
+    // the graph captured at the current buffer rotation; a batch advances
+    // it by graph_batch, one iteration by one
+    const int nr = prot(s);
     for (; count >= s->graph_batch; count -= s->graph_batch) {
-      CGX_HIP(hipGraphLaunch(s->gexec[alt ? s->pbuf : 0], s->stream));
-      if (alt && (s->graph_batch & 1)) s->pbuf ^= 1;
+      CGX_HIP(hipGraphLaunch(s->gexec[s->pbuf % nr], s->stream));
+      s->pbuf = (s->pbuf + s->graph_batch) % nr;
     }
     for (; count > 0; --count) {
-      CGX_HIP(hipGraphLaunch(s->gexec1[alt ? s->pbuf : 0], s->stream));
-      if (alt) s->pbuf ^= 1;
+      CGX_HIP(hipGraphLaunch(s->gexec1[s->pbuf % nr], s->stream));
+      s->pbuf = (s->pbuf + 1) % nr;
     }
     return 0;
   }
@@ -564,6 +597,7 @@ int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
   s->h_st->use_tol = tol > 0.0 ? 1 : 0;
   s->h_st->max_iter = maxit;
   s->h_st->hist_cap = std::min(hist_cap, s->hist_alloc);
+  s->h_st->xdef = sr_x4(s) ? 4 : 2;
   CGX_HIP(hipMemcpyAsync(s->d_st, s->h_st, sizeof(CgState), hipMemcpyHostToDevice, s->stream));
   CGX_HIP(hipMemsetAsync(s->d_tick, 0, kTickRegion * sizeof(unsigned), s->stream));
   return 0;
@@ -994,7 +1028,11 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
     // read / y write included: + 8 n vectors
     // SR (one launch): r, s, p read and written, x / p_{k-2} every other
     // launch: + 5.5 n vectors
-    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0 : s->alg == CGX_ALG_SR ? 5.5 : 3.5) * A.n * sv;
+    // (SR with x four iterations deep, sr_x4: x, p_{k-3}, p_{k-2}, p_{k-1}
+    // read and x written every fourth launch: + 5.25 n vectors)
+    info->spmv_iter_bytes += (s->alg == CGX_ALG_CG1 ? 8.0
+                              : s->alg == CGX_ALG_SR ? (sr_x4(s) ? 5.25 : 5.5)
+                                                     : 3.5) * A.n * sv;
   info->device_bytes = A.dev_bytes + s->vec_bytes;
   info->n_panels = A.npanel;
   info->n_dict = A.layout == L_DC ? A.ndict : A.layout == L_DIA ? A.dia.ndiag : 0;
