@@ -118,6 +118,7 @@ struct cgx_dist {
   double *d_b = nullptr, *d_x = nullptr, *d_r = nullptr, *d_p = nullptr, *d_s = nullptr,
          *d_w = nullptr;
   double *d_p2 = nullptr;  // fused step: the second p buffer (with ghost tail)
+  double *d_p3 = nullptr, *d_p4 = nullptr;  // one-launch SR: the third / fourth p (x4)
   // fused CG1 step: the second r, s, w buffers (with ghost tails)
   double *d_r2 = nullptr, *d_s2 = nullptr, *d_w2 = nullptr;  // lazily: ensure_rsw2
   size_t ng_alloc = 0;  // entries of a ghosted vector from element 0 (upload_local)
@@ -161,8 +162,8 @@ struct cgx_dist {
   int phase_iters = 0;
   // batches of graph_batch iterations replayed as a hipGraph (solo and
   // RCCL; the in-process group runs eager)
-  hipGraphExec_t gexec[2] = {};   // graph_batch iterations, per p-buffer parity
-  hipGraphExec_t gexec1[2] = {};  // one iteration (remainders), per parity
+  hipGraphExec_t gexec[4] = {};   // graph_batch iterations, per p-buffer rotation
+  hipGraphExec_t gexec1[4] = {};  // one iteration (remainders), per rotation
   int gexec_alg = -1;
   int graph_batch = 16;
   bool use_graph = true;
@@ -188,7 +189,7 @@ bool solo(const cgx_dist *d) { return !d->local && d->comm == nullptr; }
   } while (0)
 
 void drop_graph(cgx_dist *d) {
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < 4; ++q) {
     if (d->gexec[q]) (void)hipGraphExecDestroy(d->gexec[q]);
     if (d->gexec1[q]) (void)hipGraphExecDestroy(d->gexec1[q]);
     d->gexec[q] = d->gexec1[q] = nullptr;
@@ -299,7 +300,8 @@ void free_system(cgx_dist *d) {
   dev_free(&d->d_pairs_bnd);
   dev_free(&d->d_b);
   dev_free(&d->d_x);
-  for (double **v : {&d->d_r, &d->d_p, &d->d_s, &d->d_w, &d->d_p2, &d->d_r2, &d->d_s2, &d->d_w2})
+  for (double **v : {&d->d_r, &d->d_p, &d->d_s, &d->d_w, &d->d_p2, &d->d_r2, &d->d_s2, &d->d_w2,
+                     &d->d_p3, &d->d_p4})
     free_ghosted(d, v);
   d->vfront = 0;
   dev_free(&d->d_send_idx);
@@ -674,10 +676,13 @@ bool fz1(const cgx_dist *d);
 // r03).  Before any graph capture (their pointers are captured).
 int ensure_rsw2(Group *g) {
   for (cgx_dist *d : g->parts) {
-    if ((d->d_r2 && d->d_s2 && d->d_w2) || !(sr1(d) || fz1(d))) continue;
+    const bool x4 = sr1(d);  // the one-launch SR step's four p buffers
+    if ((d->d_r2 && d->d_s2 && d->d_w2 && (!x4 || (d->d_p3 && d->d_p4))) || !(sr1(d) || fz1(d)))
+      continue;
     CGX_HIP(hipSetDevice(d->device));
     int rc = 0;
-    for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2}) {
+    for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2, &d->d_p3, &d->d_p4}) {
+      if (!x4 && (p == &d->d_p3 || p == &d->d_p4)) continue;
       if (*p) continue;
       void *raw = nullptr;
       rc = dev_alloc(&raw, (d->vfront + d->ng_alloc) * 8, &d->vec_bytes);
@@ -693,8 +698,8 @@ int ensure_rsw2(Group *g) {
       set_error("dist: zeroing the second r / s / w buffers failed");
       rc = CGX_ENODEV;
     }
-    if (rc) {  // none or all three (a partial set ran with nulls)
-      for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2}) free_ghosted(d, p);
+    if (rc) {  // none or all (a partial set ran with nulls)
+      for (double **p : {&d->d_r2, &d->d_s2, &d->d_w2, &d->d_p3, &d->d_p4}) free_ghosted(d, p);
       return rc;
     }
   }
@@ -728,15 +733,24 @@ int ensure_connected_fz(Group *g) {
 
 // the vector the SpMV gathers (its ghost tail is the halo) and its output;
 // fused: the p_new buffer
-double *p_old(cgx_dist *d) { return d->pbuf ? d->d_p2 : d->d_p; }
-double *p_new(cgx_dist *d) { return d->pbuf ? d->d_p : d->d_p2; }
+// the one-launch SR step rotates four p buffers (x deferred four iterations
+// deep: p_{k-3}, p_{k-2}, p_{k-1} in p_new, p_rot(2), p_rot(3); CgState::xdef,
+// as the single-GPU solver), every other recurrence alternates two; r, s, w
+// alternate with pbuf's parity
+int prot(const cgx_dist *d) { return sr1(d) ? 4 : 2; }
+double *p_rot(cgx_dist *d, int i) {
+  double *b[4] = {d->d_p, d->d_p2, d->d_p3, d->d_p4};
+  return b[(d->pbuf + i) % prot(d)];
+}
+double *p_old(cgx_dist *d) { return p_rot(d, 0); }
+double *p_new(cgx_dist *d) { return p_rot(d, 1); }
 // fused CG1: r, s, w of the last iteration (read) and of this one (written)
-double *r_old(cgx_dist *d) { return d->pbuf ? d->d_r2 : d->d_r; }
-double *r_new(cgx_dist *d) { return d->pbuf ? d->d_r : d->d_r2; }
-double *s_old(cgx_dist *d) { return d->pbuf ? d->d_s2 : d->d_s; }
-double *s_new(cgx_dist *d) { return d->pbuf ? d->d_s : d->d_s2; }
-double *w_old(cgx_dist *d) { return d->pbuf ? d->d_w2 : d->d_w; }
-double *w_new(cgx_dist *d) { return d->pbuf ? d->d_w : d->d_w2; }
+double *r_old(cgx_dist *d) { return (d->pbuf & 1) ? d->d_r2 : d->d_r; }
+double *r_new(cgx_dist *d) { return (d->pbuf & 1) ? d->d_r : d->d_r2; }
+double *s_old(cgx_dist *d) { return (d->pbuf & 1) ? d->d_s2 : d->d_s; }
+double *s_new(cgx_dist *d) { return (d->pbuf & 1) ? d->d_s : d->d_s2; }
+double *w_old(cgx_dist *d) { return (d->pbuf & 1) ? d->d_w2 : d->d_w; }
+double *w_new(cgx_dist *d) { return (d->pbuf & 1) ? d->d_w : d->d_w2; }
 double *spmv_x(cgx_dist *d) {
   if (!hs_like(d)) return fz1(d) ? r_new(d) : d->d_r;
   return fz(d) ? p_new(d) : d->d_p;
@@ -840,6 +854,12 @@ int phase_sr1(cgx_dist *d) {
       d->Ai.args<double>(nullptr, s_new(d), nullptr, &d->d_st->done, d->Ai.all_items());
   Sr1Args<double> f{d->d_x, p_old(d), p_new(d), r_old(d), r_new(d), s_old(d), d->d_st,
                     d->d_pq, d->d_pc, pl.len};
+  if (!d->d_p3 || !d->d_p4) {
+    set_error("dist: the one-launch SR step's p buffers are not allocated");
+    return CGX_EINVAL;
+  }
+  f.pa = p_rot(d, 2);  // p_{k-2}, p_{k-1}: x four iterations deep
+  f.pb = p_rot(d, 3);
   f.g = sr1_g(d);
   f.nseg = pl.nseg;
   f.cw = pl.cw;
@@ -892,7 +912,7 @@ int sr1_reduce(cgx_dist *d) {
     int rc = allreduce(d, 0, 3);
     if (rc) return rc;
   }
-  d->pbuf ^= 1;
+  d->pbuf = (d->pbuf + 1) % prot(d);
   return 0;
 }
 
@@ -1222,7 +1242,7 @@ int ensure_graphs(Group *g) {
   const int key = d->alg * 8 + (fz(d) || fz1(d) ? 1 : 0) + (sr1(d) ? 2 : 0);
   if (d->gexec[0] && d->gexec1[0] && d->gexec_alg == key) return 0;
   drop_graph(d);
-  const int nq = fz(d) || fz1(d) || sr1(d) ? 2 : 1;
+  const int nq = sr1(d) ? 4 : fz(d) || fz1(d) ? 2 : 1;
   for (int q = 0; q < nq; ++q)
     if (capture(d, g, d->graph_batch, q, &d->gexec[q]) || capture(d, g, 1, q, &d->gexec1[q])) {
       drop_graph(d);
@@ -1240,15 +1260,16 @@ int run_phases(Group *g, bool init, long long iters) {
     int rc = ensure_graphs(g);
     if (rc) return rc;
     if (d->gexec[0] && d->gexec1[0]) {
-      // an even batch keeps the parity, one iteration flips it
-      const bool alt = fz(d) || fz1(d) || sr1(d);
+      // the graph captured at the current buffer rotation; a batch
+      // advances it by graph_batch, one iteration by one
+      const int nr = sr1(d) ? 4 : fz(d) || fz1(d) ? 2 : 1;
       for (; iters >= d->graph_batch; iters -= d->graph_batch) {
-        CGX_HIP(hipGraphLaunch(d->gexec[alt ? d->pbuf : 0], d->st));
-        if (alt && (d->graph_batch & 1)) d->pbuf ^= 1;
+        CGX_HIP(hipGraphLaunch(d->gexec[d->pbuf % nr], d->st));
+        d->pbuf = (d->pbuf + d->graph_batch) % nr;
       }
       for (; iters > 0; --iters) {
-        CGX_HIP(hipGraphLaunch(d->gexec1[alt ? d->pbuf : 0], d->st));
-        if (alt) d->pbuf ^= 1;
+        CGX_HIP(hipGraphLaunch(d->gexec1[d->pbuf % nr], d->st));
+        d->pbuf = (d->pbuf + 1) % nr;
       }
       return 0;
     }
@@ -1275,6 +1296,7 @@ int prepare_states(Group *g, int maxit, double tol, int hist_cap) {
     d->h_st->use_tol = tol > 0.0 ? 1 : 0;
     d->h_st->max_iter = maxit;
     d->h_st->hist_cap = std::min(hist_cap, d->hist_alloc);
+    d->h_st->xdef = sr1(d) ? 4 : 2;
     CGX_HIP(hipMemcpyAsync(d->d_st, d->h_st, sizeof(CgState), hipMemcpyHostToDevice, d->st));
   }
   return 0;
@@ -1689,7 +1711,9 @@ int cgx_dist_info(cgx_dist *d, cgx_dist_stats *s) {
   s->spmv_iter_bytes = d->have_matrix ? d->A.layout_bytes() : 0.0;
   // the one-launch SR step: its layout, + r, s, p read and written, x /
   // p_{k-2} every other launch (cgx_info)
-  if (d->have_matrix && sr1(d)) s->spmv_iter_bytes = d->Ai.layout_bytes() + 5.5 * d->n_loc * 8.0;
+  // (x four iterations deep: x, p_{k-3}, p_{k-2}, p_{k-1} read and x
+  // written every fourth launch)
+  if (d->have_matrix && sr1(d)) s->spmv_iter_bytes = d->Ai.layout_bytes() + 5.25 * d->n_loc * 8.0;
   // fused: + r, p_old read and p_new written, x / p_{k-1} read and x
   // written every other launch (cgx_info)
   if (d->have_matrix && fz(d)) s->spmv_iter_bytes += 3.5 * d->n_loc * 8.0;
