@@ -197,11 +197,17 @@ def kernel_key(info):
 
 
 def kernel_name(info):
-    return KERNELS.get(kernel_key(info), info["layout_name"])
+    k = KERNELS.get(kernel_key(info), info["layout_name"])
+    if info.get("dia_value_stream"):
+        k += " -- its DIA-V instance: the values streamed per (row, diagonal), no value table"
+    return k
 
 
 def layout_desc(info):
     name = info["layout_name"]
+    if name == "dia" and info.get("dia_value_stream"):
+        return (f"DIA-V: {info['n_dict']} diagonals, 1 presence byte per row + the values "
+                "streamed diagonal-major (general coefficients), no column stream")
     if name == "dia":
         return (f"DIA-VI: {info['n_dict']} diagonals, {info['n_values']} values, "
                 f"{info['code_bytes_per_row']} code bytes per row, no column or value stream")
@@ -215,7 +221,7 @@ def layout_desc(info):
 def value_basis(info):
     """What `value` is an iteration rate OF: the layout the
     timed solve streams -- so no reader compares a DIA-VI rate with a CSR one."""
-    if info["layout_name"] == "dia":
+    if info["layout_name"] == "dia" and not info.get("dia_value_stream"):
         return (f"DIA-VI compressed stencil ({info['code_bytes_per_row']} B/row of matrix codes, "
                 "no column or value stream; exact, bit-identical SpMV) -- NOT a CSR rate: the "
                 "plain-CSR solve of the same system is csr_plain.value")

@@ -56,7 +56,8 @@ class CgxInfo(ctypes.Structure):
                 ("setup_host_ms", ctypes.c_double), ("setup_device_ms", ctypes.c_double),
                 ("n_values", ctypes.c_int), ("gathers_per_chunk", ctypes.c_int),
                 ("fused", ctypes.c_int), ("fuse_status", ctypes.c_int),
-                ("breakdown", ctypes.c_int), ("fuse_march", ctypes.c_int)]
+                ("breakdown", ctypes.c_int), ("fuse_march", ctypes.c_int),
+                ("dia_value_stream", ctypes.c_int)]
 
 
 class CgxDistStats(ctypes.Structure):
@@ -199,7 +200,7 @@ CGX_FUSE_OFF, CGX_FUSE_AUTO, CGX_FUSE_ON = 0, 1, 2
 # cgx_info.fuse_status / cgx_dist_stats.fuse_status (cgx.h)
 (CGX_FUSE_STATUS_RUNS, CGX_FUSE_STATUS_OFF, CGX_FUSE_STATUS_NOT_DIA, CGX_FUSE_STATUS_WIDE_CODES,
  CGX_FUSE_STATUS_FAR_DIAGS, CGX_FUSE_STATUS_CACHED, CGX_FUSE_STATUS_EXACT, CGX_FUSE_STATUS_PEER,
- CGX_FUSE_STATUS_CG1_AUTO, CGX_FUSE_STATUS_NO_MARCH) = range(10)
+ CGX_FUSE_STATUS_CG1_AUTO, CGX_FUSE_STATUS_NO_MARCH, CGX_FUSE_STATUS_VALUE_STREAM) = range(11)
 
 
 def fuse_mode(mode):

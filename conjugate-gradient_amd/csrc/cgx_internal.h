@@ -118,6 +118,7 @@ constexpr int kWindowPad = 1024;   // + one SpMV window (LDS-DMA reads 16-B piec
 constexpr int kDiaSliceRows = 512; // DIA-VI work item: one workgroup, 2 rows per thread
 constexpr int kDiaMax = 16;        // DIA-VI: diagonals (fields of a <= 64-bit row word)
 constexpr int kDiaVals = 15;       // DIA-VI: values per diagonal (all-ones field = no entry)
+constexpr int kDiaVMax = 8;        // DIA-V: diagonals (one-byte presence words)
 constexpr int kHaloMax = 1024;     // fused step: diagonals |d| <= this read p from the LDS window
 constexpr double kMallBytes = 256.0 * 1024 * 1024;  // Infinity Cache
 
@@ -162,6 +163,10 @@ std::vector<int> lap_offsets(const LapSpec &g);
 //              per diagonal (value index, all ones = no entry) in a 1-8
 //              byte word, no column or value stream; two rows per thread,
 //              pair loads of x (k_spmv_dia; fused step k_spmv_dia_h)
+//              DIA-V, its single-GPU variant for values no table indexes
+//              (general coefficients): <= 8 diagonals, a one-bit presence
+//              field per diagonal, the values streamed diagonal-major
+//              (SpmvArgs::dval; k_spmv_dia and the one-launch SR step)
 //   L_STENCIL  matrix-free 5/7-point Laplacian                (k_stencil)
 // Every kernel sums each row sequentially in column order from 0.0 with
 // separately rounded products: y is bit-identical across layouts and to the
@@ -250,6 +255,11 @@ struct SpmvArgs {
   int csh[kDiaMax];       // diagonal k's field: (word >> csh[k]) & cmask[k]
   unsigned cmask[kDiaMax];  // == cmask[k]: no entry on diagonal k
   const T *vtab;          // [16][16] values, vtab[16 k + v]
+  // DIA-V (value-streamed diagonals, <= kDiaVMax of them): diagonal k's
+  // value of row r at dval[k dvs + r] (0 where the row has none; the code
+  // field is then a one-bit presence flag); nullptr: DIA-VI
+  const T *dval;
+  int dvs;
   int ndiag;              // diagonals
   int kdiag;              // index of the main diagonal (offset 0), -1: none
   int doff[kDiaMax];      // diagonal offsets col - row, ascending

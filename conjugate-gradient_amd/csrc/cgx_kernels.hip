@@ -920,7 +920,9 @@ __device__ __forceinline__ unsigned fld(const SpmvArgs<T> &a, C c, int k) {
   return (unsigned)(c >> a.csh[k]) & a.cmask[k];
 }
 
-template <typename T, int KW, bool EPI, bool NT, bool LIST>
+// DV (DIA-V, KW 1): the values from the stream (SpmvArgs::dval), diagonal k
+// of rows r, r + 1 as one pair load, instead of the value table.
+template <typename T, int KW, bool EPI, bool NT, bool LIST, bool DV>
 __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
   constexpr int KM = 8 * KW;  // diagonals unrolled (<= 8: 32-bit words)
   typedef typename std::conditional<KW == 1, unsigned, unsigned long long>::type C;
@@ -948,6 +950,12 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
   // diagonal's registers costs the compiler 4x the VGPRs)
   P xr = P{T(0), T(0)};
   if (EPI && r < a.n) xr = ld_pair(a.x, r);
+  P dvv[DV ? KM : 1];
+  if constexpr (DV) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k)  // rows < the padded rows: in bounds
+      dvv[k] = k < a.ndiag ? ld_pair(a.dval + (size_t)k * a.dvs, r) : P{T(0), T(0)};
+  }
   if (t < a.ndiag * 16) lv[t] = tv;
   __syncthreads();
   T a0 = T(0), a1 = T(0);
@@ -955,7 +963,9 @@ __global__ __launch_bounds__(256) void k_spmv_dia(SpmvArgs<T> a) {
   for (int k = 0; k < KM; ++k) {
     if (k < a.ndiag) {
       const unsigned n0 = fld(a, c0, k), n1 = fld(a, c1, k);
-      const T p0 = lv[k * 16 + n0] * xv[k].x, p1 = lv[k * 16 + n1] * xv[k].y;
+      const T w0 = DV ? dvv[DV ? k : 0].x : lv[k * 16 + n0];
+      const T w1 = DV ? dvv[DV ? k : 0].y : lv[k * 16 + n1];
+      const T p0 = w0 * xv[k].x, p1 = w1 * xv[k].y;
       a0 = n0 != a.cmask[k] ? a0 + p0 : a0;
       a1 = n1 != a.cmask[k] ? a1 + p1 : a1;
     }
@@ -1478,7 +1488,9 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
 // ghost rows hold no p_k yet, so s of the edge rows (Sr1Args::elo / ehi:
 // those whose row reaches a ghost column) is provisional and stays out of
 // the (p.s, s.s) sums -- k_sr1_edge recomputes it after the halo.
-template <typename T, int SB, int NF, int CB>
+// DV (DIA-V, CB 1): the values of step m's rows stream in beside its codes
+// (one pair load per diagonal, issued a step ahead) instead of the table.
+template <typename T, int SB, int NF, int CB, bool DV>
 __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
@@ -1654,13 +1666,21 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     }
   };
   typedef typename CodeRaw<CB>::type CR;
-  auto codes_at = [&](int m, CR &cw) {
-    const int r = base_of(m) + 2 * t;
-    cw = ld_code_raw<CB>(a.dcode, r < padn ? r : base_of(m));
+  constexpr int KV = DV ? kDiaVMax : 1, KL = DV ? kDiaVMax : kDiaMax;
+  typedef P VS[KV];
+  auto codes_at = [&](int m, CR &cw, VS &vs) {
+    const int r = base_of(m) + 2 * t, rr = r < padn ? r : base_of(m);
+    cw = ld_code_raw<CB>(a.dcode, rr);
+    if constexpr (DV) {
+#pragma unroll
+      for (int kk = 0; kk < KV; ++kk)
+        vs[kk] = kk < a.ndiag ? ld_pair(a.dval + (size_t)kk * a.dvs, rr) : P{T(0), T(0)};
+    }
   };
   const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
   CR cw, cwn{};
-  codes_at(m0, cw);
+  VS vc, vn;
+  codes_at(m0, cw, vc);
   if (xup) load_x(m0, xc);
   load_win(m0 - 1);
   store_win(m0 - 1);
@@ -1668,7 +1688,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   store_win(m0);
   load_win(m0 + 1);
   if (t < a.ndiag * 16) lv[t] = tv;
-  auto step = [&](int m, const CR &ccw, XOps &cx, CR &ncw, XOps &nx) {
+  auto step = [&](int m, const CR &ccw, const VS &cvs, XOps &cx, CR &ncw, VS &nvs, XOps &nx) {
     store_win(m + 1);
     // depth 4's two more p operands of step m's rows: issued before this
     // step's other loads, used after its compute (no wait on the prefetch)
@@ -1678,7 +1698,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       qa = ld_pair(f.pa, rs);
       qb = ld_pair(f.pb, rs);
     }
-    codes_at(min(m + 1, m1 - 1), ncw);
+    codes_at(min(m + 1, m1 - 1), ncw, nvs);
     load_win(min(m + 2, m1));  // in flight during step m
     if (xup && m + 1 < m1) load_x(m + 1, nx);
     __syncthreads();
@@ -1691,7 +1711,7 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     code_split<CB>(ccw, cc0, cc1);
     T a0 = T(0), a1 = T(0);
 #pragma unroll
-    for (int kk = 0; kk < kDiaMax; ++kk) {
+    for (int kk = 0; kk < KL; ++kk) {
       if (kk < a.ndiag) {
         const int d = a.doff[kk];
         const T *src = (a.near >> kk) & 1u ? cur : d < 0 ? prv : nxt;
@@ -1703,7 +1723,9 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
           v1 = src[i + 1];
         }
         const unsigned n0 = fld(a, cc0, kk), n1 = fld(a, cc1, kk);
-        const T p0 = lv[kk * 16 + n0] * v0, p1 = lv[kk * 16 + n1] * v1;
+        const T w0 = DV ? cvs[DV ? kk : 0].x : lv[kk * 16 + n0];
+        const T w1 = DV ? cvs[DV ? kk : 0].y : lv[kk * 16 + n1];
+        const T p0 = w0 * v0, p1 = w1 * v1;
         a0 = n0 != a.cmask[kk] ? a0 + p0 : a0;
         a1 = n1 != a.cmask[kk] ? a1 + p1 : a1;
       }
@@ -1733,8 +1755,8 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     __syncthreads();  // every read of window m - 1's slot (and r slot m) is done before step m + 1 refills it
   };
   for (int m = m0; m < m1; m += 2) {
-    step(m, cw, xc, cwn, xn);
-    if (m + 1 < m1) step(m + 1, cwn, xn, cw, xc);
+    step(m, cw, vc, xc, cwn, vn, xn);
+    if (m + 1 < m1) step(m + 1, cwn, vn, xn, cw, vc, xc);
   }
   publish();
 }
@@ -3150,8 +3172,14 @@ static void launch_dc_w(const SpmvArgs<T> &a, int g, hipStream_t st, const Launc
 
 template <typename T, int KW, bool EPI, bool NT>
 static void launch_dia_w(const SpmvArgs<T> &a, int g, hipStream_t st, const LaunchEv &ev) {
-  if (a.items.list) launch_k(CGX_K(k_spmv_dia<T, KW, EPI, NT, true>), g, st, ev, a);
-  else launch_k(CGX_K(k_spmv_dia<T, KW, EPI, NT, false>), g, st, ev, a);
+  if (a.items.list) launch_k(CGX_K(k_spmv_dia<T, KW, EPI, NT, true, false>), g, st, ev, a);
+  else launch_k(CGX_K(k_spmv_dia<T, KW, EPI, NT, false, false>), g, st, ev, a);
+}
+
+template <typename T, bool EPI, bool NT>
+static void launch_dia_v(const SpmvArgs<T> &a, int g, hipStream_t st, const LaunchEv &ev) {
+  if (a.items.list) launch_k(CGX_K(k_spmv_dia<T, 1, EPI, NT, true, true>), g, st, ev, a);
+  else launch_k(CGX_K(k_spmv_dia<T, 1, EPI, NT, false, true>), g, st, ev, a);
 }
 
 template <typename T, bool EPI, bool NT>
@@ -3187,7 +3215,10 @@ static hipError_t launch_spmv_en(const SpmvArgs<T> &a, int g, hipStream_t st, co
       break;
     }
     case L_DIA:
-      if (a.ndiag <= 8) launch_dia_w<T, 1, EPI, NT>(a, g, st, ev);
+      if (a.dval) {
+        if (a.ndiag > kDiaVMax || a.cb != 1) return hipErrorInvalidValue;
+        launch_dia_v<T, EPI, NT>(a, g, st, ev);
+      } else if (a.ndiag <= 8) launch_dia_w<T, 1, EPI, NT>(a, g, st, ev);
       else launch_dia_w<T, 2, EPI, NT>(a, g, st, ev);
       break;
     case L_STENCIL:
@@ -3290,10 +3321,16 @@ static hipError_t launch_march(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipSt
 }
 
 template <typename T, int SB, int NF>
-static const void *sr1_kernel(int cb) {
-  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1>))
-         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2>))
-                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4>));
+static const void *sr1_kernel(int cb, bool dv) {
+  // DIA-V: no four-slice step (its value registers exceed a 1,024-thread
+  // workgroup's 128 VGPRs)
+  if (dv) {
+    if constexpr (SB == 4) return nullptr;
+    else return cb == 1 ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, true>)) : nullptr;
+  }
+  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, false>))
+         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2, false>))
+                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4, false>));
 }
 
 // The plan k_sr1_dia_m runs on the matrix's march plan (mq slices between
@@ -3306,7 +3343,8 @@ static const void *sr1_kernel(int cb) {
 template <typename T>
 static SpmvArgs<T> sr1_args(const SpmvArgs<T> &a0, int sb = 0) {
   SpmvArgs<T> a = a0;
-  if (sb <= 0 && a.msb == 2 && a.mq % 4 == 0 && 4 * kDiaSliceRows + a.hl + a.hr <= 2 * 2 * 1024)
+  if (sb <= 0 && !a.dval && a.msb == 2 && a.mq % 4 == 0 &&
+      4 * kDiaSliceRows + a.hl + a.hr <= 2 * 2 * 1024)
     sb = 4;
   if (sb > 0) {
     a.msb = sb;
@@ -3362,12 +3400,12 @@ static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
   // the three-window ring and two slots of own-row r
   lds = ((size_t)3 * a.mws + (size_t)2 * sb * kDiaSliceRows) * sizeof(T) + 16;
   switch (sb * 10 + nfc) {
-    case 12: return sr1_kernel<T, 1, 2>(cb);
-    case 13: return sr1_kernel<T, 1, 3>(cb);
-    case 15: return sr1_kernel<T, 1, 5>(cb);
-    case 22: return sr1_kernel<T, 2, 2>(cb);
-    case 23: return sr1_kernel<T, 2, 3>(cb);
-    case 42: return sr1_kernel<T, 4, 2>(cb);
+    case 12: return sr1_kernel<T, 1, 2>(cb, a.dval != nullptr);
+    case 13: return sr1_kernel<T, 1, 3>(cb, a.dval != nullptr);
+    case 15: return sr1_kernel<T, 1, 5>(cb, a.dval != nullptr);
+    case 22: return sr1_kernel<T, 2, 2>(cb, a.dval != nullptr);
+    case 23: return sr1_kernel<T, 2, 3>(cb, a.dval != nullptr);
+    case 42: return sr1_kernel<T, 4, 2>(cb, a.dval != nullptr);
     default: return nullptr;
   }
 }
@@ -3486,7 +3524,7 @@ template <typename T>
 hipError_t launch_sr1_edge(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
                            const LaunchEv &ev) {
   if (a.layout != L_DIA || (f.elo & 1) || f.elo < 0 || f.elo > a.n + 1 || f.ehi < f.elo ||
-      (f.ehi < a.n && (f.ehi & 1)) || a.ndiag > kDiaMax)
+      (f.ehi < a.n && (f.ehi & 1)) || a.ndiag > kDiaMax || a.dval)
     return hipErrorInvalidValue;
   const int g = sr1_edge_grid(a.n, f);
   if (g <= 0) {  // no edge rows: the launch's events still bracket it
@@ -3507,6 +3545,7 @@ template <typename T>
 hipError_t launch_spmv_fused(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipStream_t st,
                              const LaunchEv &ev) {
   if (a.items.count <= 0) return hipSuccess;
+  if (a.dval) return hipErrorInvalidValue;  // DIA-V: the fused HS kernels read the value table
   if (march_applies(a, f)) return launch_march(a, f, st, ev);
   const int sb = fuse_slices(a.hl, a.hr);
   const int g = fused_grid(a);
@@ -3566,7 +3605,7 @@ hipError_t launch_cg1_fused(const SpmvArgs<T> &a, const Cg1Args<T> &f, hipStream
                             const LaunchEv &ev) {
   const int g = spmv_grid(a);
   if (g <= 0) return hipSuccess;
-  if (a.layout != L_DIA || a.cb > 4 || !a.part || !f.pg) return hipErrorInvalidValue;
+  if (a.layout != L_DIA || a.cb > 4 || !a.part || !f.pg || a.dval) return hipErrorInvalidValue;
   const int wn = kDiaSliceRows + a.hl + a.hr;
   const int nf = (wn + 511) / 512;
   int nfar = 0;

@@ -363,6 +363,57 @@ int dia_encode_host(int n, int npad, int col_lo, int ncols, const int *rp, const
   return e;
 }
 
+// DIA-V of every row on host threads: dia_encode_host's diagonal-order and
+// column checks, each diagonal's one-bit field 0 where the row has an entry
+// (1, all ones: none) and the entry's value at dval[k npad + r] (0 where
+// none, and in the padding rows).  Same return codes.
+template <typename T>
+int dia_v_encode_host(int n, int npad, int ncols, const int *rp, const int *col, const T *val,
+                      const DiaCand &c, std::vector<unsigned char> &code, std::vector<T> &dval) {
+  if (c.cbytes != 1 || c.ndiag > kDiaVMax) return 1;
+  unsigned empty = 0;
+  for (int q = 0; q < c.ndiag; ++q) empty |= 1u << c.csh[q];
+  code.assign((size_t)npad, (unsigned char)empty);
+  dval.assign((size_t)c.ndiag * npad, T(0));
+  const int nt = host_threads(rp[n]);
+  std::vector<int> res((size_t)nt, 0);
+  parallel_rows(n, rp[n], [&](int t, long long lo, long long hi) {
+    int doff[kDiaVMax], sh[kDiaVMax];
+    const int K = c.ndiag;
+    for (int q = 0; q < K; ++q) {
+      doff[q] = c.doff[q];
+      sh[q] = c.csh[q];
+    }
+    T *dv = dval.data();
+    int err = 0;
+    for (long long r = lo; r < hi && !err; ++r) {
+      unsigned w = empty;
+      int q = 0;
+      for (int k = rp[r]; k < rp[r + 1]; ++k) {
+        const int cl = col[k];
+        if ((unsigned)cl >= (unsigned)ncols) {
+          err = 2;
+          break;
+        }
+        const int off = cl - (int)r;
+        while (q < K && doff[q] != off) ++q;
+        if (q == K) {
+          err = 1;
+          break;
+        }
+        w &= ~(1u << sh[q]);
+        dv[(size_t)q * npad + r] = val[k];
+        ++q;
+      }
+      code[(size_t)r] = (unsigned char)w;
+    }
+    res[(size_t)t] = err;
+  });
+  int e = 0;
+  for (int x : res) e = std::max(e, x);
+  return e;
+}
+
 }  // namespace
 
 void dia_pack(DiaCand &c) {
@@ -458,6 +509,7 @@ void DevMatrix::release() {
   dev_free(&d_dict);
   dev_free(&d_dcode);
   dev_free(&d_vtab);
+  dev_free(&d_dval);
   dev_free(&d_order);
   dev_free(&d_fpairs);
   dev_free(&d_mpos);
@@ -603,6 +655,53 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
       return finish_upload(t0);
     }
     memset(&dia, 0, sizeof dia);
+  }
+
+  // ---- DIA-V (single GPU): the nonzeros on <= 8 diagonals with values no
+  // table indexes (general coefficients): one presence byte per row and the
+  // values diagonal-major -- 1 + s_v ndiag bytes per row against CSR-DC's
+  // (s_v + 1) per nonzero + 1 -- so the plane march, and with it the
+  // one-launch SR step, applies to them (k_sr1_dia_m<..., DV>)
+  if (!dia_ok && !gen && allow_panels && want_dia && col_lo == 0 && n > 0 && nnz > 0 &&
+      maxlen <= kDiaVMax) {
+    std::vector<int> voff;
+    std::vector<T> vzero, vt_unused;
+    DiaCand c{};
+    bool ok = find_pairs(n, rp, col, val, false, kDiaVMax, true, voff, vzero) &&
+              group_dia(n, rp, col, true, voff, vzero, c, vt_unused);
+    std::vector<unsigned char> hcode;
+    std::vector<T> hval;
+    int e = ok ? dia_v_encode_host(n, npad, ncols, rp, col, val, c, hcode, hval) : 1;
+    if (ok && e == 1) {  // the sample missed a diagonal: exact scan
+      ok = find_pairs(n, rp, col, val, false, kDiaVMax, false, voff, vzero) &&
+           group_dia(n, rp, col, false, voff, vzero, c, vt_unused);
+      if (ok) e = dia_v_encode_host(n, npad, ncols, rp, col, val, c, hcode, hval);
+    }
+    if (e == 2) {
+      release();
+      return bad_column();
+    }
+    const double dv_row = 1.0 + (double)ts * c.ndiag, dc_row = (ts + 1.0) * nnz / n + 1.0;
+    if (ok && e == 0 && dv_row <= dc_row) {
+      // a zero value table: the kernels' table loads stay in bounds
+      const std::vector<T> zt((size_t)kDiaMax * 16, T(0));
+      if ((rc = dev_alloc(&d_dcode, hcode.size() + 16, &dev_bytes)) ||
+          (rc = dev_alloc(&d_vtab, zt.size() * ts, &dev_bytes)) ||
+          (rc = dev_alloc(&d_dval, hval.size() * ts + 16, &dev_bytes))) {
+        release();
+        return rc;
+      }
+      CGX_HIP(hipMemcpyAsync(d_dcode, hcode.data(), hcode.size(), hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d_vtab, zt.data(), zt.size() * ts, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipMemcpyAsync(d_dval, hval.data(), hval.size() * ts, hipMemcpyHostToDevice, st));
+      CGX_HIP(hipStreamSynchronize(st));  // the host arrays go out of scope
+      dia = c;
+      dia_ok = true;
+      layout = L_DIA;
+      for (int k = 0; k < dia.ndiag; ++k)
+        if (dia.doff[k] == 0) kdiag = k;
+      return finish_upload(t0);
+    }
   }
   if (col_lo < 0) {  // the in-place numbering exists for the DIA step only
     release();
@@ -885,6 +984,12 @@ int DevMatrix::download_csr(int *row_ptr, int *col, double *val) const {
   std::vector<double> vt((size_t)kDiaMax * 16);
   CGX_HIP(hipMemcpy(code.data(), d_dcode, code.size(), hipMemcpyDeviceToHost));
   CGX_HIP(hipMemcpy(vt.data(), d_vtab, vt.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<double> dvv;  // DIA-V: the value of (row, diagonal) from the stream
+  const int npad = padded_rows();
+  if (dv()) {
+    dvv.resize((size_t)dia.ndiag * npad);
+    CGX_HIP(hipMemcpy(dvv.data(), d_dval, dvv.size() * 8, hipMemcpyDeviceToHost));
+  }
   long long k = 0;
   row_ptr[0] = 0;
   for (int r = 0; r < n; ++r) {
@@ -896,7 +1001,7 @@ int DevMatrix::download_csr(int *row_ptr, int *col, double *val) const {
       if (f == m) continue;
       if (k >= nnz) return CGX_EINVAL;
       col[k] = r + dia.doff[q];
-      val[k++] = vt[(size_t)q * 16 + f];
+      val[k++] = dv() ? dvv[(size_t)q * npad + r] : vt[(size_t)q * 16 + f];
     }
     row_ptr[r + 1] = (int)k;
   }
@@ -976,10 +1081,11 @@ int DevMatrix::plan_march() {
 
 bool DevMatrix::near_diag(int k) const { return std::abs(dia.doff[k]) <= kHaloMax; }
 
-bool DevMatrix::fusable() const { return fuse_block() == 0; }
+bool DevMatrix::fusable(bool sr1) const { return fuse_block(sr1) == 0; }
 
-int DevMatrix::fuse_block() const {
+int DevMatrix::fuse_block(bool sr1) const {
   if (layout != L_DIA) return CGX_FUSE_STATUS_NOT_DIA;
+  if (dv() && !sr1) return CGX_FUSE_STATUS_VALUE_STREAM;
   if (dia.cbytes > 4) return CGX_FUSE_STATUS_WIDE_CODES;
   int nfar = 0;
   for (int k = 0; k < dia.ndiag; ++k) nfar += !near_diag(k);
@@ -1002,7 +1108,7 @@ double DevMatrix::csr_bytes() const {
 double DevMatrix::layout_bytes() const {
   const double sv = dtype == CGX_F32 ? 4.0 : 8.0;
   switch (layout) {
-    case L_DIA: return (double)dia.cbytes * n + 2.0 * n * sv;
+    case L_DIA: return (double)dia.cbytes * n + (dv() ? sv * dia.ndiag * n : 0.0) + 2.0 * n * sv;
     case L_DC: return (double)nnz * (sv + 1) + 1.0 * n + 2.0 * n * sv + 4.0 * ndict;
     case L_STENCIL: return 2.0 * n * sv;
     default:
@@ -1040,6 +1146,8 @@ SpmvArgs<T> DevMatrix::args(const T *x, T *y, double *part, const int *done, Ite
     a.cmask[k] = (1u << dia.cbits[k]) - 1u;
   }
   a.vtab = (const T *)d_vtab;
+  a.dval = (const T *)d_dval;
+  a.dvs = padded_rows();
   a.ndiag = dia.ndiag;
   a.kdiag = kdiag;
   for (int k = 0; k < kDiaMax; ++k) a.doff[k] = dia.doff[k];

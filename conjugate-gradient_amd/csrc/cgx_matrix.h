@@ -8,7 +8,8 @@
 // that layout's arrays are resident (DIA: codes and value tables, no CSR):
 //   auto: DIA-VI when the nonzeros lie on <= 16 diagonals (col - row) with
 //         <= 15 distinct values each and every row's columns ascend; else
-//         CSR-DC when they use <= 256 distinct offsets (rows <= 255
+//         (single GPU) DIA-V when they lie on <= 8 diagonals and its 1 + 8
+//         ndiag bytes per row (fp64) do not exceed CSR-DC's; else CSR-DC when they use <= 256 distinct offsets (rows <= 255
 //         entries); else plain CSR, with column panels when the gathers
 //         have no locality (C5).
 // Candidates (pairs / offsets) come from a sample of rows on the host; an
@@ -51,6 +52,10 @@ struct DevMatrix {
   // DIA
   unsigned char *d_dcode = nullptr;  // per row dia.cbytes bytes of packed value indices
   void *d_vtab = nullptr;       // [16][16] values
+  // DIA-V (single GPU, general coefficients on <= kDiaVMax diagonals): the
+  // values diagonal-major, [ndiag][padded rows]; nullptr: DIA-VI
+  void *d_dval = nullptr;
+  bool dv() const { return d_dval != nullptr; }
   DiaCand dia{};
   int kdiag = -1;               // main diagonal's index, -1: none
   int gath = 8;                 // CSR / DC: gathers per row chunk
@@ -86,9 +91,11 @@ struct DevMatrix {
   std::vector<int> item_rows() const;
   // The fused HS step applies (DIA, <= 4 code bytes per row, at most 4
   // far diagonals, |d| > kHaloMax): k_spmv_dia_h's window and far slots.
-  bool fusable() const;
-  // why not: 0 fusable, else CGX_FUSE_STATUS_NOT_DIA / _WIDE_CODES / _FAR_DIAGS
-  int fuse_block() const;
+  // sr1: the one-launch SR step (k_sr1_dia_m), which also runs on DIA-V.
+  bool fusable(bool sr1 = false) const;
+  // why not: 0 fusable, else CGX_FUSE_STATUS_NOT_DIA / _WIDE_CODES /
+  // _FAR_DIAGS / _VALUE_STREAM
+  int fuse_block(bool sr1 = false) const;
   bool near_diag(int k) const;  // read from k_spmv_dia_h's LDS window
   // rows covered by the items (DIA pads to whole 512-row slices)
   int padded_rows() const;

@@ -171,7 +171,7 @@ void drop_graph(cgx_solver *s) {
 // (k_sr1_dia_m): it needs a march plan, whatever the cache rule says.
 bool fused(const cgx_solver *s) {
   if (s->alg == CGX_ALG_SR)
-    return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
+    return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable(true) &&
            s->A.mq > 0 && s->march != 0;
   return s->fuse != CGX_FUSE_OFF && s->mode == CGX_MODE_FAST && s->A.fusable() &&
          (s->fuse == CGX_FUSE_ON || s->A.nt);
@@ -1039,6 +1039,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->tile_bands = A.tile_bands;
   info->nt = A.nt ? 1 : 0;
   info->code_bytes_per_row = A.layout == L_DIA ? A.dia.cbytes : 0;
+  info->dia_value_stream = A.layout == L_DIA && A.dv() ? 1 : 0;
   for (int k = 0; k < A.dia.ndiag; ++k) info->n_values += A.dia.nval[k];
   info->gathers_per_chunk = A.layout == L_CSR || A.layout == L_DC ? A.gath : 0;
   info->setup_host_ms = A.setup_host_ms;
@@ -1051,7 +1052,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
   info->fuse_status = !s->have_matrix ? CGX_FUSE_STATUS_NOT_DIA
                       : s->mode == CGX_MODE_EXACT ? CGX_FUSE_STATUS_EXACT
                       : s->fuse == CGX_FUSE_OFF   ? CGX_FUSE_STATUS_OFF
-                      : A.fuse_block()            ? A.fuse_block()
+                      : A.fuse_block(sr)          ? A.fuse_block(sr)
                       : sr && (A.mq == 0 || s->march == 0) ? CGX_FUSE_STATUS_NO_MARCH
                       : (!sr && s->fuse == CGX_FUSE_AUTO && !A.nt) ? CGX_FUSE_STATUS_CACHED
                                                                    : CGX_FUSE_STATUS_RUNS;

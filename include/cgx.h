@@ -144,7 +144,10 @@ enum { CGX_F64 = 0, CGX_F32 = 1 };
  *            columns ascending; a 1-4 bit field per (row, diagonal) names
  *            the entry's value or "no entry" (a Laplacian: one byte per
  *            row) -- no column or value stream
- *            (stencils, banded matrices with few coefficients)
+ *            (stencils, banded matrices with few coefficients); on one
+ *            GPU, values no table indexes on <= 8 diagonals are DIA-V: a
+ *            presence bit per (row, diagonal) and the values streamed
+ *            (cgx_info.dia_value_stream) when that is no more bytes than DC
  *   PANEL    CSR split into column panels (one SpMV pass per panel)
  *   STENCIL  matrix-free Laplacian (cgx_solver_set_stencil; info only)
  * A requested layout that does not apply falls back DIA -> DC -> CSR;
@@ -196,6 +199,10 @@ typedef struct {
   int fuse_march;       /* > 0: the fused HS / SR step runs as a plane
                            march (cgx_solver_set_march), this many steps per
                            workgroup (the longest segment); 0: it does not  */
+  int dia_value_stream; /* DIA: 1 = DIA-V, the values streamed per (row,
+                           diagonal) beside one presence byte per row (one
+                           GPU, general coefficients on <= 8 diagonals);
+                           0 = DIA-VI (value-indexed codes, no value stream) */
 } cgx_info;
 
 /* cgx_info.fuse_status / cgx_dist_stats.fuse_status */
@@ -212,9 +219,12 @@ enum { CGX_FUSE_STATUS_RUNS = 0,        /* the fused step runs                  
                                            refused (all ranks or none)           */
        CGX_FUSE_STATUS_CG1_AUTO = 8,    /* partitioned CG1: fused only when
                                            forced on (slower on a rank's slab)   */
-       CGX_FUSE_STATUS_NO_MARCH = 9 };  /* CGX_ALG_SR on one GPU: the matrix has
+       CGX_FUSE_STATUS_NO_MARCH = 9,    /* CGX_ALG_SR on one GPU: the matrix has
                                            no plane-march plan, or
                                            cgx_solver_set_march(0)               */
+       CGX_FUSE_STATUS_VALUE_STREAM = 10 }; /* DIA-V (cgx_info.dia_value_stream):
+                                           only the one-launch SR step fuses;
+                                           HS / CG1 run unfused                  */
 
 int  cgx_solver_create(int device, cgx_solver **out);
 void cgx_solver_destroy(cgx_solver *s);

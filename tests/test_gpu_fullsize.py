@@ -238,22 +238,35 @@ def varcoef_c3():
     return rp, col, val, b
 
 
-@pytest.mark.parametrize("layout", ["auto", "csr"])
+@pytest.mark.parametrize("layout", ["auto", "dc", "csr"])
 def test_general_coefficients_c3(varcoef_c3, layout):
     """A general CSR at the C3 shape (mv_ops.h:17-23 carries arbitrary
-    values): every off-diagonal value distinct, so DIA-VI cannot apply and
-    AUTO stores coded columns + the value stream (DC); the SpMV is bit-exact
-    in both layouts and 20 CG iterations stay within 1e-12 of the oracle."""
+    values): every off-diagonal value distinct, so DIA-VI cannot apply; AUTO
+    streams the values beside a presence byte per row (DIA-V, round 5; 57
+    bytes per row against DC's 63), DC codes the columns.  In every layout
+    the SpMV is bit-exact, 20 HS iterations stay within 1e-12 of
+    oracle_conj_grad and 20 SR iterations (AUTO: the one-launch plane march
+    on DIA-V; DC / CSR: the unfused SR step) within 1e-10 of oracle_solve_sr."""
     rp, col, val, b = varcoef_c3
     with cgx.Solver(0, layout=layout) as s:
         s.set_matrix(rp, col, val)
-        assert s.info()["layout_name"] == {"auto": "dc"}.get(layout, layout)
+        i = s.info()
+        assert i["layout_name"] == {"auto": "dia"}.get(layout, layout)
+        assert i["dia_value_stream"] == (1 if layout == "auto" else 0)
         assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
         s.set_rhs(b)
         s.run(20)
         x = s.x()
     x_ref, _ = H.o_conj_grad(20, rp, col, val, b)
     assert rel(x, x_ref) <= 1e-12
+    with cgx.Solver(0, layout=layout, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["fused"] == (1 if layout == "auto" else 0)
+        s.set_rhs(b)
+        assert s.run(20) == 21
+        x = s.x()
+    x_sr, its_sr, _ = H.o_solve(20, 0.0, rp, col, val, b, sr=True)
+    assert its_sr == 21 and rel(x, x_sr) <= 1e-10
 
 
 def its_close(a, b):

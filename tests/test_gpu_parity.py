@@ -57,11 +57,13 @@ def same32(a, b):
 
 
 def expect_layout(rp, col, val, want="auto"):
-    """The layout libcgx must pick (cgx_matrix.h): DIA when the nonzeros lie
-    on <= 16 diagonals (col - row) with <= 15 distinct values (bit patterns)
-    each and one order of the diagonals is followed by every row; else DC when <= 256
-    distinct offsets and rows <= 255 entries; else CSR.  A forced layout
-    falls back DIA -> DC -> CSR."""
+    """The layout libcgx must pick on one GPU (cgx_matrix.h): DIA when the
+    nonzeros lie on <= 16 diagonals (col - row) with <= 15 distinct values
+    (bit patterns) each and one order of the diagonals is followed by every
+    row; else DIA-V (layout "dia", dia_value_stream) on <= 8 such diagonals
+    with any values when 1 + s_v ndiag bytes per row do not exceed DC's
+    (s_v + 1) nnz / n + 1; else DC when <= 256 distinct offsets and rows <=
+    255 entries; else CSR.  A forced layout falls back DIA -> DC -> CSR."""
     rp, col = np.asarray(rp), np.asarray(col)
     n = len(rp) - 1
     if want == "panel":  # column panels need x wider than one 3.5 MiB panel
@@ -75,18 +77,22 @@ def expect_layout(rp, col, val, want="auto"):
     v = np.asarray(val)
     bits = v.view(np.uint64 if v.dtype == np.float64 else np.uint32).astype(np.uint64)
     doffs = np.unique(off)
-    dia_ok = len(doffs) <= 16 and all(len(np.unique(bits[off == d])) <= 15 for d in doffs)
-    if dia_ok:  # the diagonals need one order that every row's entries follow
+    order_ok = len(doffs) <= 16
+    if order_ok:  # the diagonals need one order that every row's entries follow
         same = np.diff(rows) == 0
         edges = set(zip(off[:-1][same].tolist(), off[1:][same].tolist()))
         pred = {d: {a for a, b in edges if b == d} for d in doffs.tolist()}
         placed = set()
-        while len(placed) < len(doffs) and dia_ok:
+        while len(placed) < len(doffs) and order_ok:
             ready = [d for d in doffs.tolist() if d not in placed and pred[d] <= placed]
-            dia_ok = bool(ready)
+            order_ok = bool(ready)
             placed |= set(ready[:1])
+    dia_ok = order_ok and all(len(np.unique(bits[off == d])) <= 15 for d in doffs)
+    ts = v.itemsize
+    dv_ok = (order_ok and len(doffs) <= 8 and lens.max() <= 8 and
+             1.0 + ts * len(doffs) <= (ts + 1.0) * len(col) / n + 1.0)
     dc_ok = len(doffs) <= 256 and lens.max() <= 255
-    if want in ("auto", "dia") and dia_ok:
+    if want in ("auto", "dia") and (dia_ok or dv_ok):
         return "dia"
     if want in ("auto", "dia", "dc") and dc_ok:
         return "dc"
@@ -658,7 +664,7 @@ def test_sr_unfused_graph_and_bench():
     b = np.random.default_rng(9).standard_normal(len(rp) - 1)
     xs = []
     for graph in (True, False):
-        with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        with cgx.Solver(0, alg=cgx.CGX_ALG_SR, layout="dc") as s:
             s.set_matrix(rp, col, val)
             assert s.info()["fused"] == 0
             s.set_rhs(b)
@@ -667,7 +673,7 @@ def test_sr_unfused_graph_and_bench():
             xs.append(s.x())
     assert H.same_bits_or_both_nan(xs[0], xs[1])
     assert np.all(np.isfinite(xs[0]))
-    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR, layout="dc") as s:
         s.set_matrix(rp, col, val)
         s.set_rhs(b)
         s.bench_prepare(3)
@@ -963,6 +969,108 @@ def test_sr_single_launch_vs_oracle(case):
                 s.bench_run(35, graph=graph)
                 out.append(s.x())
             assert H.same_bits_or_both_nan(out[0], out[1])
+
+
+@pytest.mark.parametrize("shape", [(32, 48, 20), (13, 11, 9), (64, 48, 10), (40, 30, 24)])
+def test_dia_v_general_coefficients(shape):
+    """DIA-V (round 5): general coefficients on <= 8 diagonals
+    (cgx_gen_varcoef3d: every off-diagonal value distinct, mv_ops.h:17-23's
+    arbitrary values) keep a presence byte per row and stream the values
+    diagonal-major on one GPU.  The SpMV bit-exact to the oracle
+    (mv_ops.c:187-197) and the matrix read back identical; HS runs unfused
+    (fuse_status VALUE_STREAM: the fused HS kernels read value tables)
+    within 1e-12 of oracle_conj_grad; the one-launch SR step
+    (k_sr1_dia_m<..., DV>) at every segment shape as
+    test_sr_single_launch_vs_oracle: within 1e-10 of oracle_solve_sr at
+    fixed maxit, within 1e-9 of both oracles at a tolerance stop, graph and
+    eager replays bit-identical.  Without a plane-march plan (a plane of <=
+    1,024 rows has no far diagonal; 40 x 30 = 1,200 rows lie 176 rows off
+    two slices, outside the 40-row halo) SR runs unfused (k_spmv_dia's
+    (p.s, s.s) pairs + k_update_sr) to the same bars."""
+    rp, col, val = cgx.varcoef3d(*shape, seed=11)
+    march_plan = shape[:2] in ((32, 48), (64, 48))  # planes of 3 and 6 slices
+    n = len(rp) - 1
+    b = np.random.default_rng(23).standard_normal(n)
+    with cgx.Solver(0, fused=True) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert (i["layout_name"], i["dia_value_stream"], i["code_bytes_per_row"]) == ("dia", 1, 1)
+        assert i["fused"] == 0 and i["fuse_status"] == cgx.CGX_FUSE_STATUS_VALUE_STREAM
+        assert H.same_bits_or_both_nan(s.spmv(b), H.o_spmv(rp, col, val, b))
+        rp2, col2, val2 = s.matrix()
+        assert np.array_equal(rp2, rp) and np.array_equal(col2, col)
+        assert H.same_bits_or_both_nan(val2, val)
+        s.set_rhs(b)
+        s.run(20)
+        x = s.x()
+    x_ref, _ = H.o_conj_grad(20, rp, col, val, b)
+    assert rel(x, x_ref) <= 1e-12
+    shapes = ((-1, 0), (1, 1), (100000, 0), (-1, 458), (2, 1000)) if march_plan else ((-1, 0),)
+    for march, chain in shapes:
+        with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+            s.set_march(march)
+            s.set_sr_chain(chain)
+            s.set_matrix(rp, col, val)
+            info = s.info()
+            assert info["dia_value_stream"] == 1
+            assert info["fused"] == int(march_plan) and (info["fuse_march"] > 0) == march_plan, info
+            for maxit in (0, 1, 16, 17, 40):
+                s.set_rhs(b)
+                its = s.run(maxit)
+                x, h = s.x(), s.history(its)
+                x_ref, its_ref, h_ref = H.o_solve(maxit, 0.0, rp, col, val, b, sr=True)
+                assert its == its_ref == maxit + 1, (march, chain, maxit)
+                assert rel(x, x_ref) <= 1e-10, (march, chain, maxit)
+                assert np.allclose(h, h_ref, rtol=1e-6, atol=0), (march, chain, maxit)
+            s.set_rhs(b)
+            its = s.run(3000, 1e-10)
+            x = s.x()
+            x_sr, its_sr, _ = H.o_solve(3000, 1e-10, rp, col, val, b, sr=True)
+            x_hs, its_hs, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+            assert abs(its - its_sr) <= 1 and abs(its - its_hs) <= 1 and its < 3000
+            assert rel(x, x_sr) <= 1e-9 and rel(x, x_hs) <= 1e-9
+            out = []
+            for graph in (True, False):
+                s.set_rhs(b)
+                s.bench_prepare(0)
+                s.bench_run(35, graph=graph)
+                out.append(s.x())
+            assert H.same_bits_or_both_nan(out[0], out[1])
+
+
+def test_dia_v_layout_rules():
+    """DIA-V only where it applies: a forced DC stays DC; more than 8
+    diagonals (a 9-point 2-D pattern of general values) -> DC; a row whose
+    columns descend -> not DIA; fp32 general coefficients -> DIA-V too; the
+    partitioned solver never builds it (its ranks' kernels read value
+    tables) -- every one bit-exact."""
+    rng = np.random.default_rng(31)
+    rp, col, val = cgx.varcoef3d(20, 18, 16, seed=2)
+    n = len(rp) - 1
+    x = rng.standard_normal(n)
+    with cgx.Solver(0, layout="dc") as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == "dc"
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+    with cgx.Solver(0) as s:
+        v32 = val.astype(np.float32)
+        s.set_matrix(rp, col, v32)
+        i = s.info()
+        assert (i["layout_name"], i["dia_value_stream"]) == ("dia", 1)
+        x32 = x.astype(np.float32)
+        assert same32(s.spmv(x32), H.o_spmv_f32(rp, col, v32, x32))
+        rp9, col9, val9 = banded_spd(5000, [1, 69, 70, 71], 3)
+        s.set_matrix(rp9, col9, val9)
+        assert s.info()["layout_name"] == expect_layout(rp9, col9, val9) == "dc"
+        x9 = rng.standard_normal(5000)
+        assert H.same_bits_or_both_nan(s.spmv(x9), H.o_spmv(rp9, col9, val9, x9))
+        col_d = col.copy()
+        col_d[rp[40]:rp[41]] = col_d[rp[40]:rp[41]][::-1]
+        val_d = val.copy()
+        val_d[rp[40]:rp[41]] = val_d[rp[40]:rp[41]][::-1]
+        s.set_matrix(rp, col_d, val_d)
+        assert s.info()["layout_name"] == expect_layout(rp, col_d, val_d) == "dc"
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col_d, val_d, x))
 
 
 @pytest.mark.parametrize("name", ["lap2d_32", "lap3d_12", "rand_spd_2000", "dense128"])
