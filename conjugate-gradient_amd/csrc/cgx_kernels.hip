@@ -1667,6 +1667,9 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
   };
   typedef typename CodeRaw<CB>::type CR;
   constexpr int KV = DV ? kDiaVMax : 1, KL = DV ? kDiaVMax : kDiaMax;
+  // DIA-V: the values load a step ahead into a second register set (181
+  // VGPRs, 2 waves per SIMD); loaded at the step instead (one set), C3 ran
+  // 243 against 235 us per iteration (profiles/r05_ab_dia_v.log)
   typedef P VS[KV];
   auto codes_at = [&](int m, CR &cw, VS &vs) {
     const int r = base_of(m) + 2 * t, rr = r < padn ? r : base_of(m);
