@@ -611,6 +611,18 @@ def test_dropin_sr_every_matrix():
             x_hs, its_hs, _ = H.o_solve(maxit, tol, rp, col, val, bv)
             assert its == its_sr and abs(its - its_hs) <= 1, (tol, its, its_sr, its_hs)
             assert rel(x, x_sr) <= 1e-10 and rel(x, x_hs) <= 1e-9, tol
+        # general coefficients (round 5): the drop-in's matrix on DIA-V, the
+        # one-launch SR step over streamed values
+        rp, col, val = cgx.varcoef3d(32, 48, 20, seed=4)
+        bv = np.random.default_rng(29).standard_normal(len(rp) - 1)
+        A, b = cgx.Mv(val, col, rp), cgx.Mv(bv)
+        for tol, maxit in ((0.0, 25), (1e-9, 3000)):
+            x, its = cgx.solve(A, b, tol, maxit)
+            assert cgx.ops_last_timing()["alg"] == cgx.CGX_ALG_SR
+            x_sr, its_sr, _ = H.o_solve(maxit, tol, rp, col, val, bv, sr=True)
+            x_hs, its_hs, _ = H.o_solve(maxit, tol, rp, col, val, bv)
+            assert its == its_sr and abs(its - its_hs) <= 1, (tol, its, its_sr, its_hs)
+            assert rel(x, x_sr) <= 1e-10 and rel(x, x_hs) <= 1e-9, tol
     finally:
         cgx.ops_set_mode(cgx.CGX_MODE_FAST, cgx.CGX_ALG_HS)
 

@@ -11,6 +11,8 @@
 #   python tools/pmc_summary.py r05c3csr r05 c3_csr 1044721156 "k_spmv_csr<double, 456, 7, true"
 #   python tools/pmc_summary.py r05c4csr r05 c4_csr 6644480004 "k_spmv_csr<double, 456, 7, true"
 #   python tools/pmc_summary.py r05c5 r05 c5_panel <bytes> "k_spmv_csr<float" r05 sum
+#   python tools/pmc_summary.py r05c3dv r05 c3dv_sr1 <bytes> "k_sr1_dia_m<double, 2"
+#   (C3 general coefficients on DIA-V: 1,159 MB = 115 B per row x 10,077,696)
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -26,6 +28,7 @@ for what in $steps; do
     c3csr) bash tools/profile.sh r05c3csr $B --workload c3 --layout csr --alg hs || exit $? ;;
     c4csr) bash tools/profile.sh r05c4csr $B --layout csr --alg hs || exit $? ;;
     c5)    bash tools/profile.sh r05c5 $B --workload c5 || exit $? ;;
+    c3dv)  bash tools/profile.sh r05c3dv python3 tools/dv_probe.py || exit $? ;;
   esac
 done
 echo "r05 profiles done"
