@@ -404,12 +404,16 @@ def general_coefficients(steps, warmup, device=0):
         i = leg["info"]
         own_gbs, own_frac = spmv_roofline(i["spmv_iter_bytes"], leg["spmv_us"] * 1e-3)
         csr_gbs, csr_frac = spmv_roofline(i["spmv_bytes"], leg["spmv_us"] * 1e-3)
+        one_launch = kernel_key(i) == "sr1"  # DIA-V (round 5): the one-launch SR step
         out[name] = dict(layout=layout_desc(i), layout_name=i["layout_name"], value=leg["value"],
-                         unit="it/s", alg=ALG_DESC[alg] if alg == "hs" else ALG_DESC["sr_unfused"],
+                         unit="it/s",
+                         alg=(ALG_DESC[alg] if alg == "hs" or one_launch else ALG_DESC["sr_unfused"]),
                          spmv_us=leg["spmv_us"], b2b_spmv_us=leg["b2b_spmv_us"],
                          own_bytes_gbs=own_gbs, own_bytes_frac=own_frac,
                          csr_basis_equiv_rate=csr_gbs, csr_basis_frac=csr_frac,
                          kernel=kernel_name(i))
+        if one_launch:  # PMC of k_sr1_dia_m<..., DV> on this system (profiles/r05_c3dv.md)
+            out[name].update(traffic_fields("c3dv", "sr1", i["spmv_iter_bytes"]))
     ok = [k for k in ("auto", "auto_sr") if "value" in out.get(k, {})]
     out["best_auto"] = max(ok, key=lambda k: out[k]["value"])
     return out
