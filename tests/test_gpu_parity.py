@@ -1015,8 +1015,24 @@ def test_dia_v_general_coefficients(shape):
         s.set_rhs(b)
         s.run(20)
         x = s.x()
-    x_ref, _ = H.o_conj_grad(20, rp, col, val, b)
+    x_ref, h_ref = H.o_conj_grad(20, rp, col, val, b)
     assert rel(x, x_ref) <= 1e-12
+    # exact mode (the reference's sequential dots): bit-identical x and history
+    with cgx.Solver(0, mode=cgx.CGX_MODE_EXACT) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["dia_value_stream"] == 1
+        s.set_rhs(b)
+        assert s.run(20) == 21
+        assert H.same_bits_or_both_nan(s.x(), x_ref)
+        assert H.same_bits_or_both_nan(s.history(21), h_ref)
+    # CG1 (unfused on DIA-V) at a tolerance stop
+    with cgx.Solver(0, alg=cgx.CGX_ALG_CG1) as s:
+        s.set_matrix(rp, col, val)
+        s.set_rhs(b)
+        its = s.run(3000, 1e-10)
+        x = s.x()
+    x_o, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b, cg1=True)
+    assert abs(its - its_o) <= 1 and rel(x, x_o) <= 1e-9
     shapes = ((-1, 0), (1, 1), (100000, 0), (-1, 458), (2, 1000)) if march_plan else ((-1, 0),)
     for march, chain in shapes:
         with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
