@@ -1066,6 +1066,47 @@ def test_dia_v_general_coefficients(shape):
             assert H.same_bits_or_both_nan(out[0], out[1])
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_dia_v_random_patterns(seed):
+    """DIA-V's encoder and kernel on random patterns: n not a multiple of 512,
+    ragged and empty rows, 1-7 random offsets out to +-3000 (far diagonals,
+    no plane-march plan), values drawn from a distinct-valued set with signed
+    zeros, a denormal-range value and stored explicit zeros -- the layout is
+    DIA-V when its bytes do not exceed DC's (else DC) and y is bit-identical
+    to the oracle."""
+    rng = np.random.default_rng(700 + seed)
+    n = int(rng.integers(600, 7000))
+    nd = int(rng.integers(1, 8))
+    offs = np.sort(rng.choice(np.arange(-3000, 3001), size=nd, replace=False))
+    rows = []
+    for r in range(n):
+        cand = r + offs
+        cand = cand[(cand >= 0) & (cand < n)]
+        keep = cand[rng.random(len(cand)) < 0.97] if rng.random() > 0.02 else cand[:0]
+        rows.append(keep)
+    rp = np.zeros(n + 1, dtype=np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.standard_normal(len(col))
+    special = rng.random(len(col))
+    val[special < 0.01] = -0.0
+    val[(special >= 0.01) & (special < 0.02)] = 0.0
+    val[(special >= 0.02) & (special < 0.025)] = 1e-310
+    x = rng.standard_normal(n)
+    x[rng.random(n) < 0.01] = -0.0
+    with cgx.Solver(0) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        want = expect_layout(rp, col, val)
+        assert i["layout_name"] == want, (i["layout_name"], want)
+        if want == "dia":
+            assert i["dia_value_stream"] == 1
+        assert H.same_bits_or_both_nan(s.spmv(x), H.o_spmv(rp, col, val, x))
+        rp2, col2, val2 = s.matrix()
+        assert np.array_equal(rp2, rp) and np.array_equal(col2, col)
+        assert H.same_bits_or_both_nan(val2, val)
+
+
 def test_dia_v_layout_rules():
     """DIA-V only where it applies: a forced DC stays DC; more than 8
     diagonals (a 9-point 2-D pattern of general values) -> DC; a row whose
