@@ -424,7 +424,7 @@ int build_inplace(cgx_dist *d, int n_loc, int nnz, const int *rp, const int *col
   for (size_t k = 0; k < (size_t)nnz; ++k) ci[k] = (int)(col_global[k] - rb);
   const int g_hi = d->n_ghost - nb;
   const int rc = d->Ai.upload<double>(n_loc, n_loc + g_hi, nnz, rp, ci.data(), val,
-                                      CGX_LAYOUT_DIA, false, nullptr, -nb);
+                                      CGX_LAYOUT_DIA, false, nullptr, -nb, true);
   if (rc || d->Ai.layout != L_DIA || d->Ai.mq == 0) {
     d->Ai.release();
     set_error("%s", "");

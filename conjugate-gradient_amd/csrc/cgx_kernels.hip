@@ -1800,6 +1800,15 @@ __global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
       v1[kk] = p[min(max(rl + 1 + d, a.xlo), a.ncols - 1)];
     }
   }
+  // DIA-V: the two rows' values on each diagonal (rows < the padded rows)
+  T w0[kDiaVMax], w1[kDiaVMax];
+  if (a.dval) {
+#pragma unroll
+    for (int kk = 0; kk < kDiaVMax; ++kk) {
+      w0[kk] = kk < a.ndiag ? a.dval[(size_t)kk * a.dvs + rl] : T(0);
+      w1[kk] = kk < a.ndiag ? a.dval[(size_t)kk * a.dvs + rl + 1] : T(0);
+    }
+  }
   const T p0 = p[rl], p1 = p[two ? rl + 1 : rl];
   // the state after the loads are out (its loads would otherwise go first)
   const Sr1Now sn = sr1_now(f.st, f.g);
@@ -1810,7 +1819,10 @@ __global__ __launch_bounds__(256) void k_sr1_edge(SpmvArgs<T> a, Sr1Args<T> f) {
   for (int kk = 0; kk < kDiaMax; ++kk) {
     if (kk < a.ndiag) {
       const unsigned n0 = fld(a, c0, kk), n1 = fld(a, c1, kk);
-      const T q0 = lv[kk * 16 + n0] * v0[kk], q1 = lv[kk * 16 + n1] * v1[kk];
+      const bool dv = a.dval && kk < kDiaVMax;
+      const T e0 = dv ? w0[kk < kDiaVMax ? kk : 0] : lv[kk * 16 + n0];
+      const T e1 = dv ? w1[kk < kDiaVMax ? kk : 0] : lv[kk * 16 + n1];
+      const T q0 = e0 * v0[kk], q1 = e1 * v1[kk];
       a0 = n0 != a.cmask[kk] ? a0 + q0 : a0;
       a1 = n1 != a.cmask[kk] ? a1 + q1 : a1;
     }
@@ -3527,7 +3539,7 @@ template <typename T>
 hipError_t launch_sr1_edge(const SpmvArgs<T> &a, const Sr1Args<T> &f, hipStream_t st,
                            const LaunchEv &ev) {
   if (a.layout != L_DIA || (f.elo & 1) || f.elo < 0 || f.elo > a.n + 1 || f.ehi < f.elo ||
-      (f.ehi < a.n && (f.ehi & 1)) || a.ndiag > kDiaMax || a.dval)
+      (f.ehi < a.n && (f.ehi & 1)) || a.ndiag > kDiaMax || (a.dval && a.ndiag > kDiaVMax))
     return hipErrorInvalidValue;
   const int g = sr1_edge_grid(a.n, f);
   if (g <= 0) {  // no edge rows: the launch's events still bracket it

@@ -368,8 +368,9 @@ int dia_encode_host(int n, int npad, int col_lo, int ncols, const int *rp, const
 // (1, all ones: none) and the entry's value at dval[k npad + r] (0 where
 // none, and in the padding rows).  Same return codes.
 template <typename T>
-int dia_v_encode_host(int n, int npad, int ncols, const int *rp, const int *col, const T *val,
-                      const DiaCand &c, std::vector<unsigned char> &code, std::vector<T> &dval) {
+int dia_v_encode_host(int n, int npad, int col_lo, int ncols, const int *rp, const int *col,
+                      const T *val, const DiaCand &c, std::vector<unsigned char> &code,
+                      std::vector<T> &dval) {
   if (c.cbytes != 1 || c.ndiag > kDiaVMax) return 1;
   unsigned empty = 0;
   for (int q = 0; q < c.ndiag; ++q) empty |= 1u << c.csh[q];
@@ -391,7 +392,7 @@ int dia_v_encode_host(int n, int npad, int ncols, const int *rp, const int *col,
       int q = 0;
       for (int k = rp[r]; k < rp[r + 1]; ++k) {
         const int cl = col[k];
-        if ((unsigned)cl >= (unsigned)ncols) {
+        if ((unsigned)(cl - col_lo) >= (unsigned)(ncols - col_lo)) {
           err = 2;
           break;
         }
@@ -553,7 +554,8 @@ int DevMatrix::set_stencil(const LapSpec &g) {
 
 template <typename T>
 int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *col, const T *val,
-                      int want, bool allow_panels, const LapSpec *gen, int col_lo_) {
+                      int want, bool allow_panels, const LapSpec *gen, int col_lo_,
+                      bool allow_dv) {
   const double t0 = now_ms();
   if (n_ < 0 || nnz_ < 0 || ncols_ < n_ || col_lo_ > 0 || (col_lo_ < 0 && (gen || !col)) ||
       (n_ > 0 && (!rp || (nnz_ > 0 && !gen && (!col || !val))))) {
@@ -657,13 +659,12 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
     memset(&dia, 0, sizeof dia);
   }
 
-  // ---- DIA-V (single GPU): the nonzeros on <= 8 diagonals with values no
+  // ---- DIA-V (allow_dv): the nonzeros on <= 8 diagonals with values no
   // table indexes (general coefficients): one presence byte per row and the
   // values diagonal-major -- 1 + s_v ndiag bytes per row against CSR-DC's
   // (s_v + 1) per nonzero + 1 -- so the plane march, and with it the
   // one-launch SR step, applies to them (k_sr1_dia_m<..., DV>)
-  if (!dia_ok && !gen && allow_panels && want_dia && col_lo == 0 && n > 0 && nnz > 0 &&
-      maxlen <= kDiaVMax) {
+  if (!dia_ok && !gen && allow_dv && want_dia && n > 0 && nnz > 0 && maxlen <= kDiaVMax) {
     std::vector<int> voff;
     std::vector<T> vzero, vt_unused;
     DiaCand c{};
@@ -671,11 +672,11 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
               group_dia(n, rp, col, true, voff, vzero, c, vt_unused);
     std::vector<unsigned char> hcode;
     std::vector<T> hval;
-    int e = ok ? dia_v_encode_host(n, npad, ncols, rp, col, val, c, hcode, hval) : 1;
+    int e = ok ? dia_v_encode_host(n, npad, col_lo, ncols, rp, col, val, c, hcode, hval) : 1;
     if (ok && e == 1) {  // the sample missed a diagonal: exact scan
       ok = find_pairs(n, rp, col, val, false, kDiaVMax, false, voff, vzero) &&
            group_dia(n, rp, col, false, voff, vzero, c, vt_unused);
-      if (ok) e = dia_v_encode_host(n, npad, ncols, rp, col, val, c, hcode, hval);
+      if (ok) e = dia_v_encode_host(n, npad, col_lo, ncols, rp, col, val, c, hcode, hval);
     }
     if (e == 2) {
       release();
@@ -913,9 +914,9 @@ int DevMatrix::upload(int n_, int ncols_, int nnz_, const int *rp, const int *co
 }
 
 template int DevMatrix::upload<double>(int, int, int, const int *, const int *, const double *,
-                                       int, bool, const LapSpec *, int);
+                                       int, bool, const LapSpec *, int, bool);
 template int DevMatrix::upload<float>(int, int, int, const int *, const int *, const float *,
-                                      int, bool, const LapSpec *, int);
+                                      int, bool, const LapSpec *, int, bool);
 
 // The item order, the non-temporal choice and the setup times, once the
 // layout's arrays are on the device.

@@ -77,9 +77,12 @@ struct DevMatrix {
   // device (rp is the host closed form).  allow_panels: single-GPU only.
   // col_lo < 0: columns in [col_lo, ncols) (a partition's in-place ghost
   // rows); DIA-VI only -- CGX_EINVAL when it does not apply.
+  // allow_dv: DIA-V may be built (the single-GPU solver; a partition's
+  // in-place matrix for the one-launch SR step)
   template <typename T>
   int upload(int n, int ncols, int nnz, const int *rp, const int *col, const T *val, int want,
-             bool allow_panels, const LapSpec *gen = nullptr, int col_lo = 0);
+             bool allow_panels, const LapSpec *gen = nullptr, int col_lo = 0,
+             bool allow_dv = false);
   int finish_upload(double t0);
   int set_stencil(const LapSpec &g);
   // The matrix as CSR on the host (fp64; DIA decodes its codes).

@@ -307,7 +307,7 @@ int upload_matrix(cgx_solver *s, int n, int nnz, const int *rp, const int *col, 
                   const LapSpec *gen = nullptr) {
   CGX_HIP(hipSetDevice(s->device));
   free_system(s);
-  int rc = s->A.upload<T>(n, n, nnz, rp, col, val, s->want_layout, true, gen);
+  int rc = s->A.upload<T>(n, n, nnz, rp, col, val, s->want_layout, true, gen, 0, true);
   if (rc) return rc;
   return alloc_vectors(s);
 }

@@ -668,6 +668,60 @@ def test_sr_unfused_partitions(layout, fused, P):
     assert np.linalg.norm(b - H.o_spmv(rp, col, val, x)) <= 2e-10 * np.linalg.norm(b)
 
 
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_sr_one_launch_partitions_general_coefficients(P):
+    """Round 5: general coefficients (cgx_gen_varcoef3d, every value distinct)
+    on partitioned ranks run the one-launch SR step too -- each rank's
+    in-place matrix is DIA-V (values streamed beside a presence byte per row),
+    k_sr1_dia_m<..., DV> marches the slab and k_sr1_edge reads the values of
+    the edge rows.  Against oracle_solve_sr within 1e-10 at fixed max_iter
+    (every residue of the depth-4 x deferral at the stop) and within 1e-9 with
+    the stop iteration within 1 (and of the HS oracle) at a tolerance."""
+    rp, col, val = cgx.varcoef3d(32, 48, 20, seed=9)
+    b = np.random.default_rng(41).standard_normal(len(rp) - 1)
+    runs = [(0, 0.0), (1, 0.0), (2, 0.0), (17, 0.0), (40, 0.0), (3000, 1e-10)]
+    out, st = _sr_group(rp, col, val, b, P, runs)
+    assert all(s["march"] > 0 and s["inplace"] == 1 and s["fused"] == 1 for s in st), \
+        [(s["march"], s["inplace"], s["fused"], s["layout_name"]) for s in st]
+    for (its, x, _), (maxit, tol) in zip(out[:-1], runs[:-1]):
+        x_sr, its_sr, _ = H.o_solve(maxit, tol, rp, col, val, b, sr=True)
+        assert its == its_sr == maxit + 1, (maxit, its, its_sr)
+        assert np.linalg.norm(x - x_sr) <= 1e-10 * np.linalg.norm(x_sr), maxit
+    its, x, _ = out[-1]
+    x_sr, its_sr, _ = H.o_solve(3000, 1e-10, rp, col, val, b, sr=True)
+    x_hs, its_hs, _ = H.o_solve(3000, 1e-10, rp, col, val, b)
+    assert abs(its - its_sr) <= 1 and abs(its - its_hs) <= 1 and its < 3000
+    assert np.linalg.norm(x - x_sr) <= 1e-9 * np.linalg.norm(x_sr)
+    assert np.linalg.norm(x - x_hs) <= 1e-9 * np.linalg.norm(x_hs)
+
+
+def test_sr_one_launch_rccl_one_rank_general_coefficients():
+    """The same over a 1-rank RCCL communicator (pack, all-reduce, the sums
+    applied privately), graph-replayed and eager bit-identical, within 1e-10
+    of oracle_solve_sr."""
+    rp, col, val = cgx.varcoef3d(32, 48, 20, seed=13)
+    n = len(rp) - 1
+    b = np.random.default_rng(5).standard_normal(n)
+    res = {}
+    for graph in (True, False):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+        try:
+            d.set_alg(cgx.CGX_ALG_SR)
+            d.set_graph(graph)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            its = d.run(25)
+            i = d.info()
+            assert i["fused"] == 1 and i["march"] > 0 and i["inplace"] == 1, i
+            res[graph] = (its, d.x())
+        finally:
+            d.close()
+    assert res[True][0] == res[False][0] == 26
+    assert H.same_bits_or_both_nan(res[True][1], res[False][1])
+    x_sr, _, _ = H.o_solve(25, 0.0, rp, col, val, b, sr=True)
+    assert np.linalg.norm(res[True][1] - x_sr) <= 1e-10 * np.linalg.norm(x_sr)
+
+
 def test_sr_unfused_rccl_one_rank_graph_parity():
     """The unfused SR step over a 1-rank RCCL communicator (every transport
     phase: pack, all-reduce of the three sums, the privately applied scalar
