@@ -163,10 +163,11 @@ std::vector<int> lap_offsets(const LapSpec &g);
 //              per diagonal (value index, all ones = no entry) in a 1-8
 //              byte word, no column or value stream; two rows per thread,
 //              pair loads of x (k_spmv_dia; fused step k_spmv_dia_h)
-//              DIA-V, its single-GPU variant for values no table indexes
-//              (general coefficients): <= 8 diagonals, a one-bit presence
-//              field per diagonal, the values streamed diagonal-major
-//              (SpmvArgs::dval; k_spmv_dia and the one-launch SR step)
+//              DIA-V, its variant for values no table indexes (general
+//              coefficients; one GPU and the ranks' one-launch SR matrix):
+//              <= 8 diagonals, a one-bit presence field per diagonal, the
+//              values streamed diagonal-major (SpmvArgs::dval; k_spmv_dia,
+//              the one-launch SR step and its edge launch)
 //   L_STENCIL  matrix-free 5/7-point Laplacian                (k_stencil)
 // Every kernel sums each row sequentially in column order from 0.0 with
 // separately rounded products: y is bit-identical across layouts and to the

@@ -8,10 +8,11 @@
 // that layout's arrays are resident (DIA: codes and value tables, no CSR):
 //   auto: DIA-VI when the nonzeros lie on <= 16 diagonals (col - row) with
 //         <= 15 distinct values each and every row's columns ascend; else
-//         (single GPU) DIA-V when they lie on <= 8 diagonals and its 1 + 8
-//         ndiag bytes per row (fp64) do not exceed CSR-DC's; else CSR-DC when they use <= 256 distinct offsets (rows <= 255
-//         entries); else plain CSR, with column panels when the gathers
-//         have no locality (C5).
+//         (allow_dv: one GPU, a partition's in-place SR matrix) DIA-V when
+//         they lie on <= 8 diagonals and its 1 + 8 ndiag bytes per row
+//         (fp64) do not exceed CSR-DC's; else CSR-DC when they use <= 256
+//         distinct offsets (rows <= 255 entries); else plain CSR, with
+//         column panels when the gathers have no locality (C5).
 // Candidates (pairs / offsets) come from a sample of rows on the host; an
 // encoder then checks every nonzero against them (DIA: host threads, so only
 // the 1-8 code bytes per row cross PCIe; DC: the device, over the uploaded
@@ -52,8 +53,9 @@ struct DevMatrix {
   // DIA
   unsigned char *d_dcode = nullptr;  // per row dia.cbytes bytes of packed value indices
   void *d_vtab = nullptr;       // [16][16] values
-  // DIA-V (single GPU, general coefficients on <= kDiaVMax diagonals): the
-  // values diagonal-major, [ndiag][padded rows]; nullptr: DIA-VI
+  // DIA-V (general coefficients on <= kDiaVMax diagonals; upload's
+  // allow_dv): the values diagonal-major, [ndiag][padded rows]; nullptr:
+  // DIA-VI
   void *d_dval = nullptr;
   bool dv() const { return d_dval != nullptr; }
   DiaCand dia{};

@@ -145,8 +145,9 @@ enum { CGX_F64 = 0, CGX_F32 = 1 };
  *            the entry's value or "no entry" (a Laplacian: one byte per
  *            row) -- no column or value stream
  *            (stencils, banded matrices with few coefficients); on one
- *            GPU, values no table indexes on <= 8 diagonals are DIA-V: a
- *            presence bit per (row, diagonal) and the values streamed
+ *            GPU (and in a partition's one-launch SR matrix), values no
+ *            table indexes on <= 8 diagonals are DIA-V: a presence bit per
+ *            (row, diagonal) and the values streamed
  *            (cgx_info.dia_value_stream) when that is no more bytes than DC
  *   PANEL    CSR split into column panels (one SpMV pass per panel)
  *   STENCIL  matrix-free Laplacian (cgx_solver_set_stencil; info only)
