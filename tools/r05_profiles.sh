@@ -13,6 +13,8 @@
 #   python tools/pmc_summary.py r05c5 r05 c5_panel <bytes> "k_spmv_csr<float" r05 sum
 #   python tools/pmc_summary.py r05c3dv r05 c3dv_sr1 <bytes> "k_sr1_dia_m<double, 2"
 #   (C3 general coefficients on DIA-V: 1,159 MB = 115 B per row x 10,077,696)
+#   python tools/pmc_summary.py r05c3sr r05 c3_sr1 594584064 "k_sr1_dia_m<double, 2"
+#   (C3's headline launch: 59 B per row x 10,077,696)
 set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -29,6 +31,7 @@ for what in $steps; do
     c4csr) bash tools/profile.sh r05c4csr $B --layout csr --alg hs || exit $? ;;
     c5)    bash tools/profile.sh r05c5 $B --workload c5 || exit $? ;;
     c3dv)  bash tools/profile.sh r05c3dv python3 tools/dv_probe.py || exit $? ;;
+    c3sr)  bash tools/profile.sh r05c3sr $B --workload c3 --alg sr || exit $? ;;
   esac
 done
 echo "r05 profiles done"
