@@ -180,6 +180,7 @@ _SIGS = {
     "cgx_dist_set_alg": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_layout": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_graph": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cgx_dist_debug_refuse_capture": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_march": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_sr_chain": (ctypes.c_int, [_vp, ctypes.c_int]),
     "cgx_dist_set_fused": (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -708,6 +709,12 @@ class DistSolver:
 
     def set_graph(self, on):
         check(lib().cgx_dist_set_graph(self._h, 1 if on else 0), "dist_set_graph")
+
+    def debug_refuse_capture(self, mode):
+        """Test hook (cgx_dist_debug_refuse_capture): 1 refuse this rank's
+        captures before any RCCL call is recorded (all ranks go eager), 2
+        after (fatal for the communicator: CGX_ECOMM), 0 off."""
+        check(lib().cgx_dist_debug_refuse_capture(self._h, int(mode)), "dist_debug_refuse_capture")
 
     def set_march(self, steps):
         """CGX_ALG_SR as one k_sr1_dia_m step per iteration on the in-place

@@ -168,6 +168,12 @@ struct cgx_dist {
   int graph_batch = 16;
   bool use_graph = true;
   int graph_state = 0;  // 1 captured, -1 capture failed (eager from then on)
+  // RCCL calls enqueued (or recorded under capture) by this rank: a capture
+  // that fails after it recorded one leaves RCCL's host-side state advanced
+  // for ops that will never run -- fatal for the communicator (comm_fatal)
+  long long nccl_calls = 0;
+  bool comm_fatal = false;
+  int dbg_refuse = 0;  // cgx_dist_debug_refuse_capture: 1 before, 2 after the RCCL ops
 };
 
 namespace {
@@ -623,13 +629,16 @@ int connect_local(Group *g) {
   return 0;
 }
 
-// Every rank's layout takes the fused step: MIN over the ranks (RCCL).
-int agree_fusable(cgx_dist *d, int mine, int *all) {
+// MIN of an int over the ranks (RCCL): every rank's layout takes the fused
+// step (ensure_fused_known), every rank's graph capture succeeded
+// (ensure_graphs).  The value itself below two ranks.
+int agree_min(cgx_dist *d, int mine, int *all) {
   *all = mine;
   if (d->comm == nullptr || d->nranks < 2) return 0;
   int *d_f = nullptr;
   CGX_HIP(hipMalloc((void **)&d_f, 2 * sizeof(int)));
   CGX_HIP(hipMemcpy(d_f, &mine, sizeof(int), hipMemcpyHostToDevice));
+  ++d->nccl_calls;
   ncclResult_t r = ncclAllReduce(d_f, d_f + 1, 1, ncclInt32, ncclMin, d->comm, d->st);
   hipError_t e = r == ncclSuccess ? hipStreamSynchronize(d->st) : hipSuccess;
   if (r == ncclSuccess && e == hipSuccess) e = hipMemcpy(all, d_f + 1, sizeof(int), hipMemcpyDeviceToHost);
@@ -656,8 +665,8 @@ int ensure_fused_known(Group *g) {
   } else {
     cgx_dist *d = g->parts[0];
     int all = 0, mall = 0;
-    int rc = agree_fusable(d, part_fusable(d) ? 1 : 0, &all);
-    if (rc == 0) rc = agree_fusable(d, part_marchable(d) ? 1 : 0, &mall);
+    int rc = agree_min(d, part_fusable(d) ? 1 : 0, &all);
+    if (rc == 0) rc = agree_min(d, part_marchable(d) ? 1 : 0, &mall);
     if (rc) return rc;
     d->fz_all = all != 0;
     d->mi_all = mall != 0;
@@ -818,6 +827,7 @@ int phase_halo(cgx_dist *d) {
                              d->st_comm));
     }
   } else {
+    ++d->nccl_calls;
     CGX_NCCL(ncclGroupStart());
     for (int q = 0; q < d->nranks; ++q) {
       if (q == d->rank) continue;
@@ -1004,6 +1014,7 @@ int allreduce(cgx_dist *d, int i, int count) {
                              d->st, i));
     CGX_HIP(hipEventRecord(d->ev_red, d->st));
   } else {
+    ++d->nccl_calls;
     CGX_NCCL(ncclAllReduce(d->d_sums + i, d->d_gsums + i, count, ncclFloat64, ncclSum, d->comm,
                            d->st));
   }
@@ -1208,24 +1219,37 @@ int run_phases_eager(Group *g, bool init, long long iters) {
 
 // Capture `nit` iterations (kernels, halo send/recv on the comm stream
 // forked and joined by events, all-reduces) into *out, without running them.
+// Returns 1 when captured, 0 when the capture was refused before any RCCL
+// call was recorded (nothing reached the communicator: eager is safe), -1
+// when it was refused after RCCL calls were recorded.  Every outcome comes
+// back as one of these (never as an early error return), so every rank
+// reaches ensure_graphs' agreement.
 int capture(cgx_dist *d, Group *g, int nit, int parity, hipGraphExec_t *out) {
   hipGraph_t gr = nullptr;
-  CGX_HIP(hipSetDevice(d->device));
+  *out = nullptr;
+  if (hipSetDevice(d->device) != hipSuccess ||
+      hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
   const int saved = d->pbuf;
+  const long long calls0 = d->nccl_calls;
   d->pbuf = parity;
-  CGX_HIP(hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal));
-  const int rc = run_phases_eager(g, false, nit);
+  // cgx_dist_debug_refuse_capture(1): refused before the first phase
+  const int rc = d->dbg_refuse == 1 ? CGX_ENODEV : run_phases_eager(g, false, nit);
   const hipError_t e = hipStreamEndCapture(d->st, &gr);
   d->pbuf = saved;
   hipError_t ei = hipSuccess;
-  if (rc == 0 && e == hipSuccess) ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
+  const bool refused = rc || e != hipSuccess || d->dbg_refuse == 2;
+  if (!refused) ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
   if (gr) (void)hipGraphDestroy(gr);
-  if (rc || e != hipSuccess || ei != hipSuccess) {
+  if (refused || ei != hipSuccess) {
+    if (*out) (void)hipGraphExecDestroy(*out);
     *out = nullptr;
     (void)hipGetLastError();
-    return CGX_ENODEV;
+    return d->nccl_calls > calls0 ? -1 : 0;
   }
-  return 0;
+  return 1;
 }
 
 bool graphs_on(const cgx_dist *d) {
@@ -1234,8 +1258,20 @@ bool graphs_on(const cgx_dist *d) {
 
 // The replayed graphs of the current recurrence: graph_batch iterations and
 // one iteration (remainders), captured once -- by bench_prepare, so a timed
-// region only replays.  A capture the transport refuses leaves the solver
-// eager (graph_state -1); nothing was enqueued on the stream.
+// region only replays.  Graph or eager is a COLLECTIVE decision: each rank's
+// capture result is MIN-all-reduced, and
+//   every rank captured               -> every rank replays its graphs;
+//   some rank refused before any RCCL
+//   call was recorded                 -> every rank drops its graphs and runs
+//                                        eager (graph_state -1 on all ranks:
+//                                        their send/recv sequences stay equal);
+//   some rank refused after recording
+//   RCCL calls                        -> CGX_ECOMM on every rank, and the
+//                                        communicator is marked unusable
+//                                        (comm_fatal): its host-side state may
+//                                        be out of step with the peers'.
+// Nothing captured is ever enqueued, so the decision costs one all-reduce of
+// an int per capture (once per recurrence).
 int ensure_graphs(Group *g) {
   cgx_dist *d = g->parts[0];
   if (!graphs_on(d)) return 0;
@@ -1243,12 +1279,26 @@ int ensure_graphs(Group *g) {
   if (d->gexec[0] && d->gexec1[0] && d->gexec_alg == key) return 0;
   drop_graph(d);
   const int nq = sr1(d) ? 4 : fz(d) || fz1(d) ? 2 : 1;
-  for (int q = 0; q < nq; ++q)
-    if (capture(d, g, d->graph_batch, q, &d->gexec[q]) || capture(d, g, 1, q, &d->gexec1[q])) {
-      drop_graph(d);
-      d->graph_state = -1;
-      return 0;
-    }
+  int mine = 1;
+  for (int q = 0; q < nq && mine == 1; ++q) {
+    mine = capture(d, g, d->graph_batch, q, &d->gexec[q]);
+    if (mine == 1) mine = capture(d, g, 1, q, &d->gexec1[q]);
+  }
+  int all = mine;
+  const int rc = agree_min(d, mine, &all);
+  if (rc || all < 1) drop_graph(d);
+  if (rc) return rc;
+  if (all < 0) {
+    d->comm_fatal = true;
+    d->graph_state = -1;
+    set_error("dist: a rank's hipGraph capture failed after RCCL calls were recorded; "
+              "the communicator is no longer usable");
+    return CGX_ECOMM;
+  }
+  if (all == 0) {
+    d->graph_state = -1;  // every rank: eager from now on
+    return 0;
+  }
   d->gexec_alg = key;
   d->graph_state = 1;
   return 0;
@@ -1256,6 +1306,10 @@ int ensure_graphs(Group *g) {
 
 int run_phases(Group *g, bool init, long long iters) {
   cgx_dist *d = g->parts[0];
+  if (d->comm_fatal) {
+    set_error("dist: the communicator is unusable after a failed capture (ensure_graphs)");
+    return CGX_ECOMM;
+  }
   if (!init && graphs_on(d)) {
     int rc = ensure_graphs(g);
     if (rc) return rc;
@@ -1617,6 +1671,14 @@ int cgx_dist_set_graph(cgx_dist *d, int on) {
   if (!d) return CGX_EINVAL;
   d->use_graph = on != 0;
   d->graph_state = 0;  // (re)try a capture at the next run
+  drop_graph(d);
+  return 0;
+}
+
+int cgx_dist_debug_refuse_capture(cgx_dist *d, int mode) {
+  if (!d || mode < 0 || mode > 2) return CGX_EINVAL;
+  d->dbg_refuse = mode;
+  d->graph_state = 0;  // the next run captures (and is refused) anew
   drop_graph(d);
   return 0;
 }

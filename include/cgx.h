@@ -489,6 +489,14 @@ int  cgx_dist_set_sr_chain(cgx_dist *d, int rows);
 /* hipGraph replay of the iteration batches (RCCL calls included); on by
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
 int  cgx_dist_set_graph(cgx_dist *d, int on);
+/* Test hook: make this rank's next hipGraph captures fail.  mode 1: refused
+ * before any RCCL call is recorded -- every rank then agrees (one MIN
+ * all-reduce) to drop its graphs and run eager (cgx_dist_stats.graph -1),
+ * with the same results; mode 2: refused after the iteration's RCCL calls
+ * were recorded -- every rank's run returns CGX_ECOMM and the communicator
+ * is unusable from then on (its host-side state may be out of step with
+ * the peers'); 0: off.  Call on the ranks to be refused only. */
+int  cgx_dist_debug_refuse_capture(cgx_dist *d, int mode);
 int  cgx_dist_run(cgx_dist *d, int maxit, double tol, int *iters);
 int  cgx_dist_get_x(cgx_dist *d, double *x_local);
 int  cgx_dist_get_history(cgx_dist *d, double *rr, int cap);

@@ -605,6 +605,56 @@ def test_sr_one_launch_rccl_one_rank_graph_parity():
             assert np.linalg.norm(s.x() - x) <= 1e-12 * np.linalg.norm(x)
 
 
+@pytest.mark.parametrize("alg", [cgx.CGX_ALG_SR, cgx.CGX_ALG_HS])
+def test_capture_refusal_is_collective(alg):
+    """Graph or eager is decided by all ranks together (ensure_graphs: the
+    capture results MIN-all-reduced).  On a 1-rank RCCL communicator with a
+    capture refused BEFORE any RCCL call was recorded the rank drops its
+    graphs and runs eager -- x, iteration counts and histories bit-identical
+    to the replayed graphs; refused AFTER the iteration's RCCL calls were
+    recorded, the run fails with CGX_ECOMM and the communicator stays
+    unusable (no eager run on a possibly desynchronised comm)."""
+    rp, col, val = cgx.laplacian3d(32, 48, 20)
+    b = np.random.default_rng(31).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    res = {}
+    for mode in (0, 1):
+        d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+        try:
+            d.set_alg(alg)
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(b)
+            if mode:
+                d.debug_refuse_capture(mode)
+            out = []
+            for maxit in (17, 40):
+                its = d.run(maxit, 0.0)
+                out.append((its, d.x(), d.history(its)))
+            its = d.run(3000, 1e-10)
+            out.append((its, d.x(), d.history(its)))
+            assert d.info()["graph"] == (1 if mode == 0 else -1), mode
+        finally:
+            d.close()
+        res[mode] = out
+    for (i0, x0, h0), (i1, x1, h1) in zip(res[0], res[1]):
+        assert i0 == i1
+        assert H.same_bits_or_both_nan(x0, x1)
+        assert H.same_bits_or_both_nan(h0, h1)
+    d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
+    try:
+        d.set_alg(alg)
+        d.set_matrix(n, rp, col, val)
+        d.set_rhs(b)
+        d.debug_refuse_capture(2)
+        with pytest.raises(cgx.CgxError, match="RCCL calls were recorded"):
+            d.run(17, 0.0)
+        d.debug_refuse_capture(0)
+        with pytest.raises(cgx.CgxError, match="unusable"):
+            d.run(17, 0.0)
+    finally:
+        d.close()
+
+
 def test_sr_rccl_one_rank_graph_parity():
     """SR through a 1-rank RCCL communicator (the all-reduce of three doubles
     in the replayed graphs), eager, and without a communicator (local sums

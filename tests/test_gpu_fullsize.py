@@ -80,6 +80,35 @@ def test_c3_fused_fast_path_vs_oracle(c3):
     assert np.allclose(hist, h_ref[:21], rtol=1e-10, atol=0)
 
 
+@pytest.mark.parametrize("alg", ["hs", "sr"])
+def test_c3_b_ones_fast_mode_bar(alg):
+    """The fast-mode bar that holds on the BASELINE system itself (VERDICT
+    r05 #6): C3 (216^3) with b = 1 -- bench.py's oracle gate system -- 20
+    iterations (21 SpMVs), HS (the fused plane march) and SR (one launch per
+    iteration) against oracle_conj_grad(20), the reference's HS order.
+    Stated bound 1e-10 relative; measured 3.05e-11 (HS, round 5's line).
+    Why not the fixtures' 1e-12: the oracle's dot products are sequential
+    sums of 10 M terms (rounding bound n u = 2.2e-9 of the sum of |terms|)
+    and with b = 1 every r.r term is positive and alike, so the oracle's own
+    alpha and beta carry ~1e-12-1e-11 relative error that the 20-step
+    recurrence then amplifies; the GPU's tree sums (log2(n) u) are the more
+    accurate of the two."""
+    rp, col, val = cgx.laplacian3d(216, 216, 216)
+    b = np.ones(len(rp) - 1)
+    a = cgx.CGX_ALG_SR if alg == "sr" else cgx.CGX_ALG_HS
+    with cgx.Solver(0, alg=a) as s:
+        s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["layout_name"] == "dia" and i["fused"] == 1 and i["fuse_march"] > 0
+        s.set_rhs(b)
+        s.run(20)
+        x = s.x()
+    x_ref, _ = H.o_conj_grad(20, rp, col, val, b)
+    err = rel(x, x_ref)
+    print(f"C3 b=1 maxit 20 {alg}: rel err vs oracle_conj_grad {err:.3e}")
+    assert err <= 1e-10
+
+
 def test_c3_march_bit_identical_to_unfused(c3):
     """The headline kernel at full C3 size: the plane-marching fused step
     (chains of slices 91 apart over the L2-tiled item order's partial

@@ -32,15 +32,23 @@ def py_partition(n, G, g, rp, col):
     return ghosts, np.array(local, np.int32), counts
 
 
-def matrices():
-    yield "lap3d_9x7x8", (*cgx.laplacian3d(9, 7, 8),)
-    yield "lap2d_40x30", (*cgx.laplacian2d(40, 30),)
-    rp, col, val = cgx.random_spd(1500, 6, 5)
-    yield "rand1500", (rp, col, val)
-    yield "tiny5", (*cgx.laplacian2d(5, 1),)
+_MAKERS = {
+    "lap3d_9x7x8": lambda: cgx.laplacian3d(9, 7, 8),
+    "lap2d_40x30": lambda: cgx.laplacian2d(40, 30),
+    "rand1500": lambda: cgx.random_spd(1500, 6, 5),
+    "tiny5": lambda: cgx.laplacian2d(5, 1),
+}
+MAT_NAMES = sorted(_MAKERS)
+_CACHE = {}
 
 
-MATS = dict(matrices())
+def mat(name):
+    """Built on first use, not at import: the generators call libcgx, which
+    the session fixture in conftest.py builds only after collection (a fresh
+    checkout has no libcgx.so when this module is imported)."""
+    if name not in _CACHE:
+        _CACHE[name] = tuple(_MAKERS[name]())
+    return _CACHE[name]
 
 
 @pytest.mark.parametrize("n,G", [(10, 3), (64_000_000, 8), (80_621_568, 8), (7, 8),
@@ -57,10 +65,10 @@ def test_rows_and_owner_64bit(n, G):
         assert cgx.lib().cgx_partition_owner(n, G, c) == py_owner(n, G, c)
 
 
-@pytest.mark.parametrize("name", sorted(MATS))
+@pytest.mark.parametrize("name", MAT_NAMES)
 @pytest.mark.parametrize("G", [1, 2, 3, 4, 8])
 def test_partition_bit_exact_vs_restatement(name, G):
-    rp, col, val = MATS[name]
+    rp, col, val = mat(name)
     n = len(rp) - 1
     for g in range(G):
         rb, re_ = py_rows(n, G, g)
@@ -75,13 +83,13 @@ def test_partition_bit_exact_vs_restatement(name, G):
         assert list(P.recv_counts()) == counts
 
 
-@pytest.mark.parametrize("name", sorted(MATS))
+@pytest.mark.parametrize("name", MAT_NAMES)
 @pytest.mark.parametrize("G", [2, 3, 5, 8])
 def test_halo_exchange_reproduces_global_spmv(name, G):
     """Exchange requests between G simulated ranks, move halo values by the
     send lists, and check every rank's local SpMV against the global one bit
     for bit (same products, same order)."""
-    rp, col, val = MATS[name]
+    rp, col, val = mat(name)
     n = len(rp) - 1
     x = np.random.default_rng(1).standard_normal(n)
     y_ref = H.o_spmv(rp, col, val, x)
@@ -118,7 +126,7 @@ def test_halo_exchange_reproduces_global_spmv(name, G):
 
 
 def test_partition_rejects_wrong_range():
-    rp, col, _ = MATS["lap2d_40x30"]
+    rp, col, _ = mat("lap2d_40x30")
     with pytest.raises(cgx.CgxError):
         cgx.Partition(len(rp) - 1, 4, 1, rp[:11] - rp[0], col[:rp[10]])
 
