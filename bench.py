@@ -393,7 +393,7 @@ def general_coefficients(steps, warmup, device=0):
     sysm = dict(rp=rp, col=col, val=val, b=np.ones(len(rp) - 1))
     out = dict(matrix="7-point pattern of C3 (216^3), a_ij = a_ji = -(0.5 + U(0,1]) per edge, "
                       "diagonal = sum |a_ij| + 0.01 (cgx_gen_varcoef3d, seed 7), b = 1")
-    gate = sr_gate(sysm, ("auto", "csr"))
+    gate = sr_gate(sysm, ("auto", "csr"), device=device)
     out["sr_gate"] = gate
     for name, layout, alg in (("auto", "auto", "hs"), ("auto_sr", "auto", "sr"),
                               ("csr", "csr", "hs"), ("csr_sr", "csr", "sr")):
@@ -419,16 +419,17 @@ def general_coefficients(steps, warmup, device=0):
     return out
 
 
-def sr_gate(sysm, layouts, maxit=20):
+def sr_gate(sysm, layouts, maxit=20, device=0):
     """The SR parity gate of a leg (as alg_trial's): SR x of `maxit`
-    iterations within 1e-10 of HS x in each layout."""
+    iterations within 1e-10 of HS x in each layout, on the device whose legs
+    are timed."""
     import numpy as np
     import cgx
     out = {}
     for layout in layouts:
         xs = {}
         for alg in ("hs", "sr"):
-            with cgx.Solver(0, layout=layout, alg=ALGS[alg]) as s:
+            with cgx.Solver(device, layout=layout, alg=ALGS[alg]) as s:
                 s.set_matrix(sysm["rp"], sysm["col"], sysm["val"])
                 s.set_rhs(sysm["b"])
                 s.run(maxit)

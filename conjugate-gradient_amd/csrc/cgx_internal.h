@@ -348,6 +348,16 @@ struct Sr1Args {
   // no scalar launch between the all-reduce and this one; nullptr: *st is
   // current (single GPU, transport-free)
   const double *g = nullptr;
+  // single GPU, the scalar step folded into the launch (no k_finalize): the
+  // state is read from *st and handed to the next launch in *st_out
+  // (workgroup 0, with the history entry in hist); when st->sr_pend, every
+  // workgroup first runs FIN_SR1's step on the last launch's pq_in / pc_in
+  // (np_in workgroups) -- the launches alternate two states and two sets of
+  // partials; nullptr: off
+  CgState *st_out = nullptr;
+  const double *pq_in = nullptr, *pc_in = nullptr;
+  int np_in = 0;
+  double *hist = nullptr;
 };
 
 // The fused CG1 step (Chronopoulos-Gear, DIA layout, k_cg1_dia_h): one
@@ -394,7 +404,8 @@ int sr1_grid(const SpmvArgs<T> &a, const Sr1Args<T> &f);
 // width (rows), the pair whose launch takes the fewest window-times in the
 // resident-workgroup model (ceil(chains nseg / slots) rounds of ceil(L /
 // nseg) + 2 windows, L the longest chain; slots from the kernel's
-// occupancy).  cw_force > 0: that chain width, only nseg picked.  An
+// occupancy; fold: the single GPU's kernel with the folded scalar step,
+// Sr1Args::st_out).  cw_force > 0: that chain width, only nseg picked.  An
 // explicit march length (> 0) is used as given instead (nseg 0).
 struct Sr1Shape {
   int nseg, cw, sb;
@@ -404,7 +415,7 @@ struct Sr1Shape {
 // launch_sr1_march keep to it
 inline int sr1_max_grid(int slices) { return 4 * slices + 64; }
 template <typename T>
-Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a, int cus, int cw_force = 0);
+Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a, int cus, int cw_force = 0, bool fold = false);
 // workgroups (= partial pairs) of k_sr1_edge over f's edge rows of n rows
 template <typename T>
 int sr1_edge_grid(int n, const Sr1Args<T> &f);

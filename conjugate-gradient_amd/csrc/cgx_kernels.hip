@@ -32,6 +32,7 @@
 #define CGX_EXP 0
 #endif
 
+
 namespace cgx {
 
 namespace {
@@ -1490,8 +1491,9 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
 // the (p.s, s.s) sums -- k_sr1_edge recomputes it after the halo.
 // DV (DIA-V, CB 1): the values of step m's rows stream in beside its codes
 // (one pair load per diagonal, issued a step ahead) instead of the table.
-template <typename T, int SB, int NF, int CB, bool DV>
-__global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
+template <typename T, int SB, int NF, int CB, bool DV, bool FOLD>
+__global__ __launch_bounds__(256 * SB)
+void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   constexpr int BS = 256 * SB, SR = kDiaSliceRows * SB;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_lds[];
   T *ring = reinterpret_cast<T *>(dyn_lds);
@@ -1518,25 +1520,27 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     m0 = seg * f.march;
     m1 = min(m0 + f.march, msteps);
   }
-  const Sr1Now sn = sr1_now(f.st, f.g);
-  if (sn.done > 1) return;  // uniform
-  const int k = sn.k_u;  // the last finalized iteration (-1: none)
-  const bool first = k < 0, stop = sn.done == 1;
+  // The launch's scalars: without FOLD the state as the last k_finalize (or
+  // the ranks' all-reduce, applied privately) left it, resolved here; with
+  // FOLD (f.st_out: the single GPU, no k_finalize) resolved below, after the
+  // prologue's loads are in flight, so that the folded scalar step overlaps
+  // them.  (FOLD is a template parameter so that the ranks' kernels carry
+  // none of its code: with it as a runtime branch their launch took 3-4 us
+  // longer, profiles/r06_ab_sr1.log.)
+  Sr1Now sn{};
+  if constexpr (!FOLD) {
+    sn = sr1_now(f.st, f.g);
+    if (sn.done > 1) return;  // uniform
+  }
+  int k = 0;  // the last finalized iteration (-1: none)
+  bool first = false, stop = false, odd = false, xup = false;
   // x deferral: depth 2 (x += alpha p for two iterations in odd launches)
   // or depth 4 (f.pa: four iterations in every launch with k % 4 == 3,
   // p_{k-3} / p_{k-2} / p_{k-1} from pnew / pa / pb, their alphas from
   // alpha_q) -- the same roundings in the same order as one update per
   // iteration (cg.c:115-116)
   const bool d4 = f.pa != nullptr;
-  const bool odd = d4 ? (k & 3) == 3 : (k & 1) != 0;  // this launch updates x
-  const bool xup = !first && odd;
-  const T alpha = (T)sn.alpha, beta = (T)sn.beta, alpha_d = (T)f.st->alpha_def;
-  if (!first && !odd && !stop && blockIdx.x == 0 && t == 0) {
-    if (d4) const_cast<CgState *>(f.st)->alpha_q[k & 3] = sn.alpha;
-    else const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
-  }
-  const T aq0 = d4 ? (T)f.st->alpha_q[0] : T(0), aq1 = d4 ? (T)f.st->alpha_q[1] : T(0),
-          aq2 = d4 ? (T)f.st->alpha_q[2] : T(0);
+  T alpha = T(0), beta = T(0), alpha_d = T(0), aq0 = T(0), aq1 = T(0), aq2 = T(0);
   const int padn = a.mslices * kDiaSliceRows;
   const bool nt = a.nt != 0;
   const int wn = wc + a.hl + a.hr, ws = a.mws;
@@ -1596,6 +1600,168 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
       f.pc[blockIdx.x] = p2;
     }
   };
+  P wr[NF], wp[NF], wsv[NF];
+  // a wave whose pairs of pass q all lie past the window skips that pass
+  // (wave-uniform: the wave's first pair; SB = 4 at C4: 9 of 16 waves skip
+  // pass 1 -- round 5, with the four-slice steps 812 -> 783 us per C4 launch)
+  const int wfirst = 2 * __builtin_amdgcn_readfirstlane(wid * kWave);
+  for (int q = 0; q < NF; ++q) wr[q] = wp[q] = wsv[q] = P{T(0), T(0)};
+  typedef P WinSet[NF];
+  // window m's r, p, s pairs into (vr, vp, vs); `all`: every pass, also
+  // those past the window (the prologue's loads, which must not sit under a
+  // branch) -- a pair past the window loads the window's first pair
+  // (unused; one line per wave instruction, an L1 hit)
+  auto load_win_to = [&](int m, WinSet &vr, WinSet &vp, WinSet &vs, bool all) {
+    const int w0 = base_of(m) - a.hl;
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      if (!all && q > 0 && wfirst + q * 2 * BS >= wn) continue;
+      const int i = 2 * t + q * 2 * BS;
+      const int j = min(max(i < wn ? w0 + i : w0, a.xlo), a.ncols - 1);
+      vr[q] = ld_pair(f.rold, j);
+      vp[q] = ld_pair(f.pold, j);
+      vs[q] = ld_pair(f.sold, j);
+    }
+  };
+  auto load_win = [&](int m) { load_win_to(m, wr, wp, wsv, false); };
+  auto store_win_from = [&](int m, const WinSet &vr, const WinSet &vp, const WinSet &vs) {
+    T *win = slot(m), *rb = rslot(m);
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+      const int i = 2 * t + q * 2 * BS;
+      P rk = vr[q], pk = vr[q];
+      if (!first) {
+        const T as0 = alpha * vs[q].x, as1 = alpha * vs[q].y;
+        rk.x = vr[q].x - as0;
+        rk.y = vr[q].y - as1;
+        pk = p_next<T>(rk, vp[q], beta);
+      }
+      if (i + 1 < wn) lds_st2(win, i, pk.x, pk.y);  // wn even (march plan)
+      else if (i < wn) win[i] = pk.x;
+      const int o = i - a.hl;  // hl even: a pair is in the own rows or not
+      if (o >= 0 && o < SR) lds_st2(rb, o, rk.x, rk.y);
+    }
+  };
+  auto store_win = [&](int m) { store_win_from(m, wr, wp, wsv); };
+  typedef typename CodeRaw<CB>::type CR;
+  constexpr int KV = DV ? kDiaVMax : 1, KL = DV ? kDiaVMax : kDiaMax;
+  // DIA-V: the values load a step ahead into a second register set (181
+  // VGPRs, 2 waves per SIMD); loaded at the step instead (one set), C3 ran
+  // 243 against 235 us per iteration (profiles/r05_ab_dia_v.log)
+  typedef P VS[KV];
+  auto codes_at = [&](int m, CR &cw, VS &vs) {
+    const int r = base_of(m) + 2 * t, rr = r < padn ? r : base_of(m);
+    cw = ld_code_raw<CB>(a.dcode, rr);
+    if constexpr (DV) {
+#pragma unroll
+      for (int kk = 0; kk < KV; ++kk)
+        vs[kk] = kk < a.ndiag ? ld_pair(a.dval + (size_t)kk * a.dvs, rr) : P{T(0), T(0)};
+    }
+  };
+  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
+  CR cw, cwn{};
+  VS vc, vn;
+  const bool has_steps = m0 < m1;
+  // FOLD: the segment's prologue loads windows m0 - 1, m0 and m0 + 1 at
+  // once, before the scalar step (one memory round trip under it, not three
+  // after it: each store waits only for its own set, vector loads retiring
+  // in order; m0 + 1 goes into the loop's set).  Without FOLD the windows
+  // load one after the other, after the scalars (the ranks: the three at
+  // once, with no scalar step to hide, measured 2-4 us longer per launch on
+  // C4's 8 M-row slab, profiles/r06_ab_sr1.log).
+  WinSet r1, p1, s1, r2, p2, s2;
+  if constexpr (FOLD) {
+    if (has_steps) {
+      codes_at(m0, cw, vc);
+      load_win_to(m0 - 1, r1, p1, s1, true);
+      load_win_to(m0, r2, p2, s2, true);
+      load_win_to(m0 + 1, wr, wp, wsv, true);
+    }
+    // the scalar step of the last launch (FIN_SR1's), run here on its (p.s,
+    // s.s) pairs and r.r partials (wave 0: lane l sums entries l, l + 64,
+    // ... in order, then the wave tree; every workgroup the same sums),
+    // fin_sr1 on a private copy of *f.st; workgroup 0 hands the state (with
+    // this launch's alpha_q / alpha_def) over to the next launch in
+    // *f.st_out with the history entry
+    __shared__ double fbc[4];
+#if CGX_EXP & 16
+    if (!f.st_out) {
+      sn = sr1_now(f.st, f.g);
+    } else
+#endif
+    if (wid == 0) {
+      const bool fold = f.st->sr_pend != 0;
+      double ps = 0.0, ss = 0.0, rr = 0.0;
+      if (fold) {
+        constexpr int U = 4;
+        const double2 *q2 = reinterpret_cast<const double2 *>(f.pq_in);
+        for (int i = lane; i < f.np_in; i += kWave * U) {
+          double2 v[U];
+          double w[U];
+#pragma unroll
+          for (int j = 0; j < U; ++j) {
+            const int ii = i + j * kWave;
+            v[j] = ii < f.np_in ? q2[ii] : make_double2(0.0, 0.0);
+            w[j] = ii < f.np_in ? f.pc_in[ii] : 0.0;
+          }
+#pragma unroll
+          for (int j = 0; j < U; ++j) {
+            ps = ps + v[j].x;
+            ss = ss + v[j].y;
+            rr = rr + w[j];
+          }
+        }
+        ps = wave_sum(ps);
+        ss = wave_sum(ss);
+        rr = wave_sum(rr);
+      }
+      if (lane == 0) {
+        CgState c = *f.st;
+        if (fold) fin_sr1(ps, ss, rr, &c, blockIdx.x == 0 ? f.hist : nullptr);
+        if (blockIdx.x == 0) {
+          CgState o = c;
+          const int kk = c.k_u;
+          const bool od = d4 ? (kk & 3) == 3 : (kk & 1) != 0;
+          if (kk >= 0 && !od && c.done == 0) {
+            if (d4) o.alpha_q[kk & 3] = c.alpha;
+            else o.alpha_def = c.alpha;
+          }
+          o.sr_pend = 1;
+          *f.st_out = o;
+        }
+        fbc[0] = c.alpha;
+        fbc[1] = c.beta;
+        fbc[2] = (double)c.k_u;
+        fbc[3] = (double)c.done;
+      }
+    }
+#if CGX_EXP & 16
+    if (f.st_out) {
+#endif
+    __syncthreads();
+    sn = Sr1Now{(int)fbc[2], (int)fbc[3], fbc[0], fbc[1]};
+#if CGX_EXP & 16
+    }
+#endif
+    if (sn.done > 1) return;  // uniform
+  }
+  k = sn.k_u;
+  first = k < 0;
+  stop = sn.done == 1;
+  odd = d4 ? (k & 3) == 3 : (k & 1) != 0;  // this launch updates x
+  xup = !first && odd;
+  alpha = (T)sn.alpha;
+  beta = (T)sn.beta;
+  alpha_d = (T)f.st->alpha_def;
+  if (!FOLD && !first && !odd && !stop && blockIdx.x == 0 && t == 0) {
+    if (d4) const_cast<CgState *>(f.st)->alpha_q[k & 3] = sn.alpha;
+    else const_cast<CgState *>(f.st)->alpha_def = sn.alpha;
+  }
+  if (d4) {
+    aq0 = (T)f.st->alpha_q[0];
+    aq1 = (T)f.st->alpha_q[1];
+    aq2 = (T)f.st->alpha_q[2];
+  }
   if (stop) {
     // fin_sr1 stopped at iteration k (k_u) with x updates pending.  Depth 2
     // (k even): alpha_k p_k, p_k in the p_new buffer of this launch.  Depth
@@ -1626,70 +1792,22 @@ __global__ __launch_bounds__(256 * SB) void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T
     }
     return;
   }
-  if (m0 >= m1) {  // no steps: zero sums (k_finalize adds every workgroup's)
+  if (!has_steps) {  // no steps: zero sums (k_finalize adds every workgroup's)
     publish();
     return;
   }
-  P wr[NF], wp[NF], wsv[NF];
-  // a wave whose pairs of pass q all lie past the window skips that pass
-  // (wave-uniform: the wave's first pair; SB = 4 at C4: 9 of 16 waves skip
-  // pass 1 -- round 5, with the four-slice steps 812 -> 783 us per C4 launch)
-  const int wfirst = 2 * __builtin_amdgcn_readfirstlane(wid * kWave);
-  for (int q = 0; q < NF; ++q) wr[q] = wp[q] = wsv[q] = P{T(0), T(0)};
-  auto load_win = [&](int m) {
-    const int w0 = base_of(m) - a.hl;
-#pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      if (q > 0 && wfirst + q * 2 * BS >= wn) continue;
-      const int j = min(max(w0 + 2 * t + q * 2 * BS, a.xlo), a.ncols - 1);
-      wr[q] = ld_pair(f.rold, j);
-      wp[q] = ld_pair(f.pold, j);
-      wsv[q] = ld_pair(f.sold, j);
-    }
-  };
-  auto store_win = [&](int m) {
-    T *win = slot(m), *rb = rslot(m);
-#pragma unroll
-    for (int q = 0; q < NF; ++q) {
-      const int i = 2 * t + q * 2 * BS;
-      P rk = wr[q], pk = wr[q];
-      if (!first) {
-        const T as0 = alpha * wsv[q].x, as1 = alpha * wsv[q].y;
-        rk.x = wr[q].x - as0;
-        rk.y = wr[q].y - as1;
-        pk = p_next<T>(rk, wp[q], beta);
-      }
-      if (i + 1 < wn) lds_st2(win, i, pk.x, pk.y);  // wn even (march plan)
-      else if (i < wn) win[i] = pk.x;
-      const int o = i - a.hl;  // hl even: a pair is in the own rows or not
-      if (o >= 0 && o < SR) lds_st2(rb, o, rk.x, rk.y);
-    }
-  };
-  typedef typename CodeRaw<CB>::type CR;
-  constexpr int KV = DV ? kDiaVMax : 1, KL = DV ? kDiaVMax : kDiaMax;
-  // DIA-V: the values load a step ahead into a second register set (181
-  // VGPRs, 2 waves per SIMD); loaded at the step instead (one set), C3 ran
-  // 243 against 235 us per iteration (profiles/r05_ab_dia_v.log)
-  typedef P VS[KV];
-  auto codes_at = [&](int m, CR &cw, VS &vs) {
-    const int r = base_of(m) + 2 * t, rr = r < padn ? r : base_of(m);
-    cw = ld_code_raw<CB>(a.dcode, rr);
-    if constexpr (DV) {
-#pragma unroll
-      for (int kk = 0; kk < KV; ++kk)
-        vs[kk] = kk < a.ndiag ? ld_pair(a.dval + (size_t)kk * a.dvs, rr) : P{T(0), T(0)};
-    }
-  };
-  const T tv = t < a.ndiag * 16 ? a.vtab[t] : T(0);
-  CR cw, cwn{};
-  VS vc, vn;
-  codes_at(m0, cw, vc);
+  if constexpr (!FOLD) codes_at(m0, cw, vc);
   if (xup) load_x(m0, xc);
-  load_win(m0 - 1);
-  store_win(m0 - 1);
-  load_win(m0);
-  store_win(m0);
-  load_win(m0 + 1);
+  if constexpr (FOLD) {
+    store_win_from(m0 - 1, r1, p1, s1);
+    store_win_from(m0, r2, p2, s2);
+  } else {
+    load_win(m0 - 1);
+    store_win(m0 - 1);
+    load_win(m0);
+    store_win(m0);
+    load_win(m0 + 1);
+  }
   if (t < a.ndiag * 16) lv[t] = tv;
   auto step = [&](int m, const CR &ccw, const VS &cvs, XOps &cx, CR &ncw, VS &nvs, XOps &nx) {
     store_win(m + 1);
@@ -3335,17 +3453,22 @@ static hipError_t launch_march(const SpmvArgs<T> &a, const FuseArgs<T> &f, hipSt
   return hipGetLastError();
 }
 
-template <typename T, int SB, int NF>
-static const void *sr1_kernel(int cb, bool dv) {
+template <typename T, int SB, int NF, bool FOLD>
+static const void *sr1_kernel_f(int cb, bool dv) {
   // DIA-V: no four-slice step (its value registers exceed a 1,024-thread
   // workgroup's 128 VGPRs)
   if (dv) {
     if constexpr (SB == 4) return nullptr;
-    else return cb == 1 ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, true>)) : nullptr;
+    else return cb == 1 ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, true, FOLD>)) : nullptr;
   }
-  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, false>))
-         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2, false>))
-                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4, false>));
+  return cb == 1   ? CGX_K((k_sr1_dia_m<T, SB, NF, 1, false, FOLD>))
+         : cb == 2 ? CGX_K((k_sr1_dia_m<T, SB, NF, 2, false, FOLD>))
+                   : CGX_K((k_sr1_dia_m<T, SB, NF, 4, false, FOLD>));
+}
+
+template <typename T, int SB, int NF>
+static const void *sr1_kernel(int cb, bool dv, bool fold) {
+  return fold ? sr1_kernel_f<T, SB, NF, true>(cb, dv) : sr1_kernel_f<T, SB, NF, false>(cb, dv);
 }
 
 // The plan k_sr1_dia_m runs on the matrix's march plan (mq slices between
@@ -3402,7 +3525,7 @@ int sr1_edge_grid(int n, const Sr1Args<T> &f) {
 
 // the kernel instance for the matrix's march plan (nullptr: none) and its LDS
 template <typename T>
-static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
+static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds, bool fold) {
   const int sb = a.msb;
   const int wn = sb * kDiaSliceRows + a.hl + a.hr;
   const int nf = (wn + 2 * 256 * sb - 1) / (2 * 256 * sb);
@@ -3415,12 +3538,12 @@ static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
   // the three-window ring and two slots of own-row r
   lds = ((size_t)3 * a.mws + (size_t)2 * sb * kDiaSliceRows) * sizeof(T) + 16;
   switch (sb * 10 + nfc) {
-    case 12: return sr1_kernel<T, 1, 2>(cb, a.dval != nullptr);
-    case 13: return sr1_kernel<T, 1, 3>(cb, a.dval != nullptr);
-    case 15: return sr1_kernel<T, 1, 5>(cb, a.dval != nullptr);
-    case 22: return sr1_kernel<T, 2, 2>(cb, a.dval != nullptr);
-    case 23: return sr1_kernel<T, 2, 3>(cb, a.dval != nullptr);
-    case 42: return sr1_kernel<T, 4, 2>(cb, a.dval != nullptr);
+    case 12: return sr1_kernel<T, 1, 2>(cb, a.dval != nullptr, fold);
+    case 13: return sr1_kernel<T, 1, 3>(cb, a.dval != nullptr, fold);
+    case 15: return sr1_kernel<T, 1, 5>(cb, a.dval != nullptr, fold);
+    case 22: return sr1_kernel<T, 2, 2>(cb, a.dval != nullptr, fold);
+    case 23: return sr1_kernel<T, 2, 3>(cb, a.dval != nullptr, fold);
+    case 42: return sr1_kernel<T, 4, 2>(cb, a.dval != nullptr, fold);
     default: return nullptr;
   }
 }
@@ -3447,7 +3570,7 @@ static const void *sr1_pick(const SpmvArgs<T> &a, size_t &lds) {
 // (set_march > 0) callers use cw_force's width or the matrix's sb and its
 // width: the auto shape assumes the auto segment count.
 template <typename T>
-Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force) {
+Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force, bool fold) {
   Sr1Shape best{1, 0, 0};
   if (a_in.mq <= 0) return best;
   const int QR = a_in.mq * kDiaSliceRows;
@@ -3457,7 +3580,7 @@ Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force) {
   auto consider_sb = [&](int sb, int cw_only) {
     const SpmvArgs<T> a = sr1_args(a_in, sb);
     size_t lds = 0;
-    const void *k = sr1_pick(a, lds);
+    const void *k = sr1_pick(a, lds, fold);
     if (!k) return;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * sb, lds) != hipSuccess ||
@@ -3505,6 +3628,12 @@ Sr1Shape sr1_pick_shape(const SpmvArgs<T> &a_in, int cus, int cw_force) {
         consider_sb(sb, cw);
         if (best_cost >= 0) break;
       }
+    // no step that wide has a kernel for this matrix (DIA-V has no four-slice
+    // step; a wide halo none of four slices): the widest step that runs,
+    // the width clamped to it -- never the silent one-segment fallback
+    // 
+    for (int sb : {2, 1})
+      if (best_cost < 0 && cw > sb * kDiaSliceRows) consider_sb(sb, sb * kDiaSliceRows);
     return best;
   }
   for (int sb : {1, 2, 4})
@@ -3524,7 +3653,11 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStr
       sr1_grid(a, f) > sr1_max_grid(a.mslices))
     return hipErrorInvalidValue;
   size_t lds = 0;
-  const void *k = sr1_pick(a, lds);
+#if CGX_EXP & 16
+  const void *k = sr1_pick(a, lds, true);
+#else
+  const void *k = sr1_pick(a, lds, f.st_out != nullptr);
+#endif
   if (!k) return hipErrorInvalidValue;
   const int g = sr1_grid(a, f);
   void *args[] = {(void *)&a, (void *)&f};
@@ -3893,7 +4026,7 @@ hipError_t launch_dia_encode(int n, int npad, const int *rp, const int *col, con
   template int fused_grid<T>(const SpmvArgs<T> &);                                               \
   template int march_grid<T>(const SpmvArgs<T> &, int);                                         \
   template int sr1_grid<T>(const SpmvArgs<T> &, const Sr1Args<T> &);                            \
-  template Sr1Shape sr1_pick_shape<T>(const SpmvArgs<T> &, int, int);                           \
+  template Sr1Shape sr1_pick_shape<T>(const SpmvArgs<T> &, int, int, bool);                           \
   template int sr1_edge_grid<T>(int, const Sr1Args<T> &);                                       \
   template hipError_t launch_sr1_edge<T>(const SpmvArgs<T> &, const Sr1Args<T> &, hipStream_t,   \
                                          const LaunchEv &);                                      \

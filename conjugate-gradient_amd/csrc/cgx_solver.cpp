@@ -200,6 +200,14 @@ bool alternating(const cgx_solver *s) {
 // 739.0 us per iteration (launch 694 against 730), C3 134.4-135.9 against
 // 139.4-140.1.
 bool sr_x4(const cgx_solver *s) { return fused(s) && s->alg == CGX_ALG_SR; }
+// The one-launch SR step runs its scalar step folded into the next launch
+// (round 6): no k_finalize between the launches; each launch
+// sums the last one's (p.s, s.s) pairs and r.r partials under its
+// prologue's window loads, and two CgState slots alternate (the launch
+// reads one and hands the state over in the other).  Same box, alternating
+// (profiles/r06_ab_sr1.log): C3 126.0-131.1 against 134.9-135.6 us per
+// iteration, C4 666.8-676.7 against 679.5-685.9.
+bool sr1_fold(const cgx_solver *s) { return sr_x4(s); }
 
 int prot(const cgx_solver *s) { return sr_x4(s) ? 4 : alternating(s) ? 2 : 1; }
 
@@ -236,7 +244,8 @@ int alloc_vectors(cgx_solver *s) {
   s->part_cap = std::max(s->A.partials(s->A.all_items()), s->vec_grid) + 1;
   // CGX_ALG_SR: one (p.s, s.s) pair per march workgroup, at most
   // kSr1MaxGrid(items) (sr1_pick_shape keeps chains x segments within it)
-  if (s->A.mq > 0) s->part_cap = std::max(s->part_cap, 2 * sr1_max_grid(s->A.items()) + 2);
+  // (folded scalar step: two sets of pairs and r.r partials, 3 per workgroup)
+  if (s->A.mq > 0) s->part_cap = std::max(s->part_cap, 3 * sr1_max_grid(s->A.items()) + 2);
   // unfused CGX_ALG_SR: the SpMV's (p.s, s.s) pair per workgroup
   s->part_cap = std::max(s->part_cap, 2 * s->A.partials(s->A.all_items()) + 2);
   int rc;
@@ -361,7 +370,7 @@ int enqueue_init(cgx_solver *s) {
 // one (with the step width it needs)
 template <typename T>
 void sr1_shape(const cgx_solver *s, const SpmvArgs<T> &a, Sr1Args<T> &f) {
-  const Sr1Shape sh = sr1_pick_shape(a, s->cus, s->sr_chain);
+  const Sr1Shape sh = sr1_pick_shape(a, s->cus, s->sr_chain, true);
   if (s->march <= 0) f.nseg = sh.nseg;
   if (s->march <= 0 || s->sr_chain > 0) {
     f.cw = sh.cw;
@@ -399,9 +408,10 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     return 0;
   }
   if (s->alg == CGX_ALG_SR) {
-    // k_sr1_dia_m: r = r - alpha s, p = r + beta p (window rows), x update,
-    // s = A p, (p.s, s.s) pairs + r.r per workgroup; k_finalize FIN_SR1: the
-    // scalar step (oracle_solve_sr's recurrence, one reduction)
+    // k_sr1_dia_m: the scalar step of the last launch (FIN_SR1's:
+    // oracle_solve_sr's recurrence, one reduction), r = r - alpha s, p = r +
+    // beta p (window rows), x update, s = A p, (p.s, s.s) pairs + r.r per
+    // workgroup -- ONE launch per iteration
     // p rotates over four buffers (sr_x4: p_{k-3}, p_{k-2}, p_{k-1} in pn,
     // pa, pb) or alternates over two; r and s alternate
     const int q = s->pbuf, rq = q & 1;
@@ -419,10 +429,21 @@ int enqueue_iter(cgx_solver *s, hipEvent_t ev0, hipEvent_t ev1) {
     }
     sr1_shape(s, a, f);
     const int g = sr1_grid(a, f);
-    if (2 * g > s->part_cap) return CGX_EINVAL;
+    if (3 * g > s->part_cap) return CGX_EINVAL;
+    // the scalar step folded into the next launch (sr1_fold): launch q reads
+    // state slot q & 1 and the other parity's partials, writes its own
+    // partials and hands the state over in slot (q + 1) & 1
+    const int par = q & 1;
+    double *pq[2] = {s->d_pa, s->d_pr2}, *pc[2] = {s->d_pb, s->d_pr2 + 2 * g};
+    f.st = s->d_st + par;
+    f.st_out = s->d_st + (par ^ 1);
+    f.pq = pq[par];
+    f.pc = pc[par];
+    f.pq_in = pq[par ^ 1];
+    f.pc_in = pc[par ^ 1];
+    f.np_in = g;
+    f.hist = s->d_hist;
     CGX_HIP(launch_sr1_march<T>(a, f, st, LaunchEv{ev0, ev1}));
-    CGX_HIP(launch_finalize(FIN_SR1, s->d_pa, g, nullptr, 0, s->d_st, s->d_hist, nullptr, st,
-                            s->d_pb, g));
     s->pbuf = (q + 1) % nr;
     return 0;
   }
@@ -604,7 +625,9 @@ int prepare_state(cgx_solver *s, int maxit, double tol, int hist_cap) {
 }
 
 int read_state(cgx_solver *s) {
-  CGX_HIP(hipMemcpyAsync(s->h_st, s->d_st, sizeof(CgState), hipMemcpyDeviceToHost, s->stream));
+  // the folded SR step: the state the next launch reads (slot pbuf & 1)
+  const CgState *cur = s->d_st + (sr1_fold(s) ? (s->pbuf & 1) : 0);
+  CGX_HIP(hipMemcpyAsync(s->h_st, cur, sizeof(CgState), hipMemcpyDeviceToHost, s->stream));
   CGX_HIP(hipStreamSynchronize(s->stream));
   return 0;
 }
@@ -619,8 +642,10 @@ int run_t(cgx_solver *s, int maxit, double tol, int *iters) {
   // the fused step does an iteration's x update in the next launch: one
   // more step carries the last one (and finds the stop); SR tests the stop
   // of iteration k on the exact r.r that launch k + 1 computes: one more
+  // (the folded SR step: the launch after the finalize's would-be place
+  // runs it -- one more)
   const long long total = (long long)maxit + 1 + (fused(s) && s->alg != CGX_ALG_CG1 ? 1 : 0) +
-                          (s->alg == CGX_ALG_SR ? 1 : 0);
+                          (s->alg == CGX_ALG_SR ? 1 : 0) + (sr1_fold(s) ? 1 : 0);
   // SR: complete once the finalize after the last x update marks done = 2
   const int fin_done = s->alg == CGX_ALG_SR ? 2 : 1;
   if (tol <= 0.0) {
@@ -821,7 +846,7 @@ int cgx_solver_create(int device, cgx_solver **out) {
   s->cus = cus;
   s->A.device = device;
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void **)&s->d_st, sizeof(CgState)) != hipSuccess ||
+      hipMalloc((void **)&s->d_st, 2 * sizeof(CgState)) != hipSuccess ||
       hipMalloc((void **)&s->d_tick, kTickRegion * sizeof(unsigned)) != hipSuccess ||
       hipMemset(s->d_tick, 0, kTickRegion * sizeof(unsigned)) != hipSuccess ||
       hipHostMalloc((void **)&s->h_st, sizeof(CgState), hipHostMallocDefault) != hipSuccess) {
@@ -1064,7 +1089,7 @@ int cgx_solver_info(cgx_solver *s, cgx_info *info) {
         s->A.args<double>(nullptr, nullptr, nullptr, nullptr, s->A.all_items());
     const long long QR = (long long)a.mq * kDiaSliceRows;
     const int steps = (int)((a.n + QR - 1) / QR);
-    const int ns = sr1_pick_shape(a, s->cus, s->sr_chain).nseg;
+    const int ns = sr1_pick_shape(a, s->cus, s->sr_chain, true).nseg;
     info->fuse_march = (steps + ns - 1) / std::max(1, ns);
   }
   return 0;

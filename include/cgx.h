@@ -261,9 +261,10 @@ int  cgx_solver_set_march(cgx_solver *s, int steps);
 /* CGX_ALG_SR's one-launch plane march (k_sr1_dia_m): the width, in rows, of
  * the chains a step of the march is cut into.  0 auto (default): the width
  * and segment count whose chains x segments fill the device's resident
- * workgroup slots best; > 0 that width (even, at most one step's 2,048 /
- * 1,024 / 512 rows; larger values are clamped), the segment count still
- * picked.  Results do not depend on it beyond the grouping of the partial
+ * workgroup slots best; > 0 that width, the segment count still picked.
+ * The width is made even and clamped to [128, 2,048] rows, and then to the
+ * widest step that has a kernel for the matrix (1,024 rows on DIA-V, which
+ * has no four-slice step; likewise when a wide halo rules four slices out).  Results do not depend on it beyond the grouping of the partial
  * sums (tolerance, as every SR launch shape). */
 int  cgx_solver_set_sr_chain(cgx_solver *s, int rows);
 /* Layout for the next set_matrix / gen_laplacian (CGX_LAYOUT_AUTO..PANEL). */

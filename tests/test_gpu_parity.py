@@ -958,7 +958,7 @@ def test_sr_single_launch_vs_oracle(case):
             s.set_matrix(rp, col, val)
             info = s.info()
             assert info["fused"] == 1 and info["fuse_march"] > 0
-            for maxit in (0, 1, 16, 17, 40):
+            for maxit in (0, 1, 2, 3, 16, 17, 18, 19, 40):  # every k % 4 at the stop
                 s.set_rhs(b)
                 its = s.run(maxit)
                 x, h = s.x(), s.history(its)
@@ -1033,7 +1033,10 @@ def test_dia_v_general_coefficients(shape):
         x = s.x()
     x_o, its_o, _ = H.o_solve(3000, 1e-10, rp, col, val, b, cg1=True)
     assert abs(its - its_o) <= 1 and rel(x, x_o) <= 1e-9
-    shapes = ((-1, 0), (1, 1), (100000, 0), (-1, 458), (2, 1000)) if march_plan else ((-1, 0),)
+    # (-1, 2048): wider than DIA-V's widest step (two slices, no four-slice
+    # kernel) -- clamped to 1,024-row chains with balanced segments (ADVICE
+    # r05), not one segment per chain
+    shapes = ((-1, 0), (1, 1), (100000, 0), (-1, 458), (2, 1000), (-1, 2048)) if march_plan else ((-1, 0),)
     for march, chain in shapes:
         with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
             s.set_march(march)
@@ -1042,7 +1045,9 @@ def test_dia_v_general_coefficients(shape):
             info = s.info()
             assert info["dia_value_stream"] == 1
             assert info["fused"] == int(march_plan) and (info["fuse_march"] > 0) == march_plan, info
-            for maxit in (0, 1, 16, 17, 40):
+            if chain == 2048:  # segments (steps each) shorter than a whole chain (nz steps)
+                assert info["fuse_march"] < shape[2], info
+            for maxit in (0, 1, 2, 3, 16, 17, 18, 19, 40):  # every k % 4 at the stop
                 s.set_rhs(b)
                 its = s.run(maxit)
                 x, h = s.x(), s.history(its)
