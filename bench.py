@@ -178,7 +178,8 @@ KERNELS = {
     "dia_march": "k_spmv_dia_m (fused HS step on DIA-VI as a plane march: a workgroup walks "
                  "slices nx*ny apart, p of three consecutive slices + halos in an LDS ring, "
                  "x / p update, s = A p, p.s partials)",
-    "sr1": "k_sr1_dia_m (one-launch SR iteration on DIA-VI as a plane march: r = r - alpha s "
+    "sr1": "k_sr1_dia_m (one-launch SR iteration on DIA-VI as a plane march: the scalar step "
+           "of the previous launch folded in (single GPU: no k_finalize), r = r - alpha s "
            "and p = r + beta p of the previous iteration for each window row, x update, "
            "s = A p from an LDS ring of three windows, (p.s, s.s, r.r) per workgroup)",
     "dc": "k_spmv_dc (LDS-DMA code window + value window per 64-row block, dictionary-coded columns)",
@@ -702,6 +703,7 @@ def c3_legs(steps, warmup):
                ms_per_step=round(1e3 * h["wall"] / steps, 4), layout=layout_desc(h["info"]),
                layout_name=h["info"]["layout_name"],
                default_layout=layout_roofline(h["info"], h["spmv_ms"], "c3"),
+               outside_launch_us=round(1e3 * h["dev_ms"] / steps - 1e3 * h["spmv_ms"], 2),
                csr_roofline=csr_roofline(csr, "c3"),
                csr_plain=dict(value=csr["value"], unit="it/s", spmv_us=csr["spmv_us"],
                               b2b_spmv_us=csr["b2b_spmv_us"], kernel=KERNELS["csr"],
@@ -797,6 +799,12 @@ def run_single(args, wl_name):
     mix = max(ceil["copy"], ceil["copy_nt"], ceil["mix33"], ceil["mix33_nt"])
     headline_kernel["rw_mix_ceiling_gbs"] = mix
     headline_kernel["frac_of_rw_mix_ceiling"] = round(headline_kernel["achieved"] / mix, 4)
+    # the per-iteration time outside the headline launch --
+    # the graph-replayed period minus the launch itself (HIP events); with the
+    # one-launch SR step's scalar step folded into the launch (round 6) that
+    # is the kernel boundary alone, no k_finalize
+    headline_kernel["outside_launch_us"] = round(1e3 * h["dev_ms"] / args.steps - hk["spmv_us"], 2)
+    headline_kernel["launches_per_iteration"] = 1 if kernel_key(info) == "sr1" else None
 
     extra = {}
     if "hs" in legs:
