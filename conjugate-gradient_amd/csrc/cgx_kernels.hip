@@ -1684,11 +1684,6 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
     // this launch's alpha_q / alpha_def) over to the next launch in
     // *f.st_out with the history entry
     __shared__ double fbc[4];
-#if CGX_EXP & 16
-    if (!f.st_out) {
-      sn = sr1_now(f.st, f.g);
-    } else
-#endif
     if (wid == 0) {
       const bool fold = f.st->sr_pend != 0;
       double ps = 0.0, ss = 0.0, rr = 0.0;
@@ -1735,14 +1730,8 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
         fbc[3] = (double)c.done;
       }
     }
-#if CGX_EXP & 16
-    if (f.st_out) {
-#endif
     __syncthreads();
     sn = Sr1Now{(int)fbc[2], (int)fbc[3], fbc[0], fbc[1]};
-#if CGX_EXP & 16
-    }
-#endif
     if (sn.done > 1) return;  // uniform
   }
   k = sn.k_u;
@@ -3653,11 +3642,7 @@ hipError_t launch_sr1_march(const SpmvArgs<T> &a_in, const Sr1Args<T> &f, hipStr
       sr1_grid(a, f) > sr1_max_grid(a.mslices))
     return hipErrorInvalidValue;
   size_t lds = 0;
-#if CGX_EXP & 16
-  const void *k = sr1_pick(a, lds, true);
-#else
   const void *k = sr1_pick(a, lds, f.st_out != nullptr);
-#endif
   if (!k) return hipErrorInvalidValue;
   const int g = sr1_grid(a, f);
   void *args[] = {(void *)&a, (void *)&f};
