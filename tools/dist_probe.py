@@ -69,9 +69,18 @@ for name in cases:
         d.bench_prepare(5)
         ms, _ = d.bench_run(100)
         _, sp = d.bench_run(30, graph=False, spmv_events=True)
+        ph = d.bench_phases()
         i = d.info()
         print("%-9s n %d  %.1f us/iter  spmv(launches) %.1f us  fused %d march %d layout %s" %
               (name, n, 1e3 * ms / 100, 1e3 * sp, i["fused"], i["march"], i["layout"]), flush=True)
+        # the eager iteration's phases (HIP events): first launch, gap to the
+        # second (halo wait), second launch (edge / boundary), tail to the next iteration's
+        # first launch (local sums, all-reduce, pack, launch gaps), period
+        if ph:
+            print("          phases (eager, us): " + "  ".join(
+                "%s %.1f" % (k, 1e3 * ph[k]) for k in ("first_launch", "halo_wait_gap",
+                                                        "second_launch", "tail", "period")),
+                  flush=True)
     finally:
         d.close()
 
