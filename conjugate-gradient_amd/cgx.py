@@ -711,9 +711,11 @@ class DistSolver:
         check(lib().cgx_dist_set_graph(self._h, 1 if on else 0), "dist_set_graph")
 
     def debug_refuse_capture(self, mode):
-        """Test hook (cgx_dist_debug_refuse_capture): 1 refuse this rank's
-        captures before any RCCL call is recorded (all ranks go eager), 2
-        after (fatal for the communicator: CGX_ECOMM), 0 off."""
+        """Test hook (cgx_dist_debug_refuse_capture): refuse this rank's
+        captures 1 before / 2 after the RCCL calls are recorded (eager when
+        every rank is refused at the same point, CGX_ECOMM and an unusable
+        communicator on a mix); 3 as 2 with the peers taken to have captured
+        (the mix on one rank); 0 off."""
         check(lib().cgx_dist_debug_refuse_capture(self._h, int(mode)), "dist_debug_refuse_capture")
 
     def set_march(self, steps):

@@ -1237,10 +1237,11 @@ int capture(cgx_dist *d, Group *g, int nit, int parity, hipGraphExec_t *out) {
   d->pbuf = parity;
   // cgx_dist_debug_refuse_capture(1): refused before the first phase
   const int rc = d->dbg_refuse == 1 ? CGX_ENODEV : run_phases_eager(g, false, nit);
+  // (modes 2 and 3: refused after the phases recorded their RCCL calls)
   const hipError_t e = hipStreamEndCapture(d->st, &gr);
   d->pbuf = saved;
   hipError_t ei = hipSuccess;
-  const bool refused = rc || e != hipSuccess || d->dbg_refuse == 2;
+  const bool refused = rc || e != hipSuccess || d->dbg_refuse >= 2;
   if (!refused) ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
   if (gr) (void)hipGraphDestroy(gr);
   if (refused || ei != hipSuccess) {
@@ -1259,19 +1260,24 @@ bool graphs_on(const cgx_dist *d) {
 // The replayed graphs of the current recurrence: graph_batch iterations and
 // one iteration (remainders), captured once -- by bench_prepare, so a timed
 // region only replays.  Graph or eager is a COLLECTIVE decision: each rank's
-// capture result is MIN-all-reduced, and
-//   every rank captured               -> every rank replays its graphs;
-//   some rank refused before any RCCL
-//   call was recorded                 -> every rank drops its graphs and runs
-//                                        eager (graph_state -1 on all ranks:
-//                                        their send/recv sequences stay equal);
-//   some rank refused after recording
-//   RCCL calls                        -> CGX_ECOMM on every rank, and the
-//                                        communicator is marked unusable
-//                                        (comm_fatal): its host-side state may
-//                                        be out of step with the peers'.
-// Nothing captured is ever enqueued, so the decision costs one all-reduce of
-// an int per capture (once per recurrence).
+// capture result (1 captured, 0 refused before any RCCL call was recorded,
+// -1 refused after) is MIN- and MAX-all-reduced, and
+//   every rank captured            -> every rank replays its graphs;
+//   every rank refused at the same
+//   point (all 0, or all -1)       -> every rank drops its graphs and runs
+//                                     eager (graph_state -1 on all ranks:
+//                                     the same RCCL calls, or none, were
+//                                     recorded everywhere, so their send /
+//                                     recv sequences stay equal -- e.g. a
+//                                     refusal inside RCCL itself, which hits
+//                                     every rank alike);
+//   a mix (some ranks recorded RCCL
+//   calls that others did not)     -> CGX_ECOMM on every rank, and the
+//                                     communicator is marked unusable
+//                                     (comm_fatal): the ranks' host-side
+//                                     RCCL state may be out of step.
+// Nothing captured is ever enqueued, so the decision costs two all-reduces
+// of an int per capture (once per recurrence).
 int ensure_graphs(Group *g) {
   cgx_dist *d = g->parts[0];
   if (!graphs_on(d)) return 0;
@@ -1284,20 +1290,23 @@ int ensure_graphs(Group *g) {
     mine = capture(d, g, d->graph_batch, q, &d->gexec[q]);
     if (mine == 1) mine = capture(d, g, 1, q, &d->gexec1[q]);
   }
-  int all = mine;
-  const int rc = agree_min(d, mine, &all);
-  if (rc || all < 1) drop_graph(d);
+  int lo = mine, neg_hi = -mine;
+  int rc = agree_min(d, mine, &lo);
+  if (rc == 0) rc = agree_min(d, -mine, &neg_hi);
+  // cgx_dist_debug_refuse_capture(3): as if the peers had captured (the mix)
+  const int hi = d->dbg_refuse == 3 ? 1 : -neg_hi;
+  if (rc || lo < 1) drop_graph(d);
   if (rc) return rc;
-  if (all < 0) {
-    d->comm_fatal = true;
-    d->graph_state = -1;
-    set_error("dist: a rank's hipGraph capture failed after RCCL calls were recorded; "
-              "the communicator is no longer usable");
-    return CGX_ECOMM;
-  }
-  if (all == 0) {
+  if (lo < 1 && lo == hi) {
     d->graph_state = -1;  // every rank: eager from now on
     return 0;
+  }
+  if (lo < 1) {
+    d->comm_fatal = true;
+    d->graph_state = -1;
+    set_error("dist: a rank's hipGraph capture failed after RCCL calls were recorded (or "
+              "the ranks' captures disagree); the communicator is no longer usable");
+    return CGX_ECOMM;
   }
   d->gexec_alg = key;
   d->graph_state = 1;
@@ -1676,7 +1685,7 @@ int cgx_dist_set_graph(cgx_dist *d, int on) {
 }
 
 int cgx_dist_debug_refuse_capture(cgx_dist *d, int mode) {
-  if (!d || mode < 0 || mode > 2) return CGX_EINVAL;
+  if (!d || mode < 0 || mode > 3) return CGX_EINVAL;
   d->dbg_refuse = mode;
   d->graph_state = 0;  // the next run captures (and is refused) anew
   drop_graph(d);

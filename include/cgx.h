@@ -491,12 +491,15 @@ int  cgx_dist_set_sr_chain(cgx_dist *d, int rows);
  * default; 0 runs every iteration eagerly.  Resets a failed capture. */
 int  cgx_dist_set_graph(cgx_dist *d, int on);
 /* Test hook: make this rank's next hipGraph captures fail.  mode 1: refused
- * before any RCCL call is recorded -- every rank then agrees (one MIN
- * all-reduce) to drop its graphs and run eager (cgx_dist_stats.graph -1),
- * with the same results; mode 2: refused after the iteration's RCCL calls
- * were recorded -- every rank's run returns CGX_ECOMM and the communicator
- * is unusable from then on (its host-side state may be out of step with
- * the peers'); 0: off.  Call on the ranks to be refused only. */
+ * before any RCCL call is recorded; mode 2: refused after the iteration's
+ * RCCL calls were recorded.  When every rank is refused at the same point
+ * the ranks agree (MIN / MAX all-reduce of the capture results) to drop
+ * their graphs and run eager (cgx_dist_stats.graph -1), with the same
+ * results; a mix -- ranks that recorded RCCL calls beside ranks that did
+ * not -- makes every rank's run return CGX_ECOMM, the communicator unusable
+ * from then on (the ranks' host-side RCCL state may be out of step).
+ * mode 3: as 2, and this rank takes its peers to have captured (the mix,
+ * testable on one rank).  0: off. */
 int  cgx_dist_debug_refuse_capture(cgx_dist *d, int mode);
 int  cgx_dist_run(cgx_dist *d, int maxit, double tol, int *iters);
 int  cgx_dist_get_x(cgx_dist *d, double *x_local);

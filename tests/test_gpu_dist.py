@@ -608,17 +608,20 @@ def test_sr_one_launch_rccl_one_rank_graph_parity():
 @pytest.mark.parametrize("alg", [cgx.CGX_ALG_SR, cgx.CGX_ALG_HS])
 def test_capture_refusal_is_collective(alg):
     """Graph or eager is decided by all ranks together (ensure_graphs: the
-    capture results MIN-all-reduced).  On a 1-rank RCCL communicator with a
-    capture refused BEFORE any RCCL call was recorded the rank drops its
-    graphs and runs eager -- x, iteration counts and histories bit-identical
-    to the replayed graphs; refused AFTER the iteration's RCCL calls were
-    recorded, the run fails with CGX_ECOMM and the communicator stays
-    unusable (no eager run on a possibly desynchronised comm)."""
+    capture results MIN- and MAX-all-reduced).  On a 1-rank RCCL
+    communicator: a capture refused before any RCCL call was recorded (mode
+    1), or after the iteration's RCCL calls were (mode 2) -- every rank
+    refused at the same point -- drops the graphs and runs eager, with x,
+    iteration counts and histories bit-identical to the replayed graphs; a
+    mix of ranks that recorded RCCL calls and ranks that did not (mode 3:
+    this rank refused after recording, its peers taken to have captured)
+    fails with CGX_ECOMM and leaves the communicator unusable (no eager run
+    on a possibly desynchronised comm)."""
     rp, col, val = cgx.laplacian3d(32, 48, 20)
     b = np.random.default_rng(31).standard_normal(len(rp) - 1)
     n = len(rp) - 1
     res = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
         try:
             d.set_alg(alg)
@@ -636,16 +639,17 @@ def test_capture_refusal_is_collective(alg):
         finally:
             d.close()
         res[mode] = out
-    for (i0, x0, h0), (i1, x1, h1) in zip(res[0], res[1]):
-        assert i0 == i1
-        assert H.same_bits_or_both_nan(x0, x1)
-        assert H.same_bits_or_both_nan(h0, h1)
+    for mode in (1, 2):
+        for (i0, x0, h0), (i1, x1, h1) in zip(res[0], res[mode]):
+            assert i0 == i1, mode
+            assert H.same_bits_or_both_nan(x0, x1), mode
+            assert H.same_bits_or_both_nan(h0, h1), mode
     d = cgx.DistSolver(0, 1, 0, cgx.dist_unique_id())
     try:
         d.set_alg(alg)
         d.set_matrix(n, rp, col, val)
         d.set_rhs(b)
-        d.debug_refuse_capture(2)
+        d.debug_refuse_capture(3)
         with pytest.raises(cgx.CgxError, match="RCCL calls were recorded"):
             d.run(17, 0.0)
         d.debug_refuse_capture(0)

@@ -101,3 +101,50 @@ def test_two_rank_rccl_bit_identical_to_local_group(tmp_path):
             assert (march > 0) == (shape == SHAPE1), (alg, shape)
             x = np.load(tmp_path / f"x_{tag}.npy")
             assert np.array_equal(x.view(np.uint64), xs_l[rank].view(np.uint64)), (alg, fused, shape)
+
+
+def _worker_refuse(rank, world, uid, out_dir):
+    """Both ranks' captures refused before any RCCL call is recorded: the
+    MIN / MAX agreement sends both eager with the results of the replayed
+    graphs.  (The mixed case -- one rank refused, its peer captured, RCCL
+    calls recorded on one side only -- is fatal by the same rule and is
+    checked on a 1-rank communicator in test_gpu_dist.py: over real peers a
+    one-sided capture may block in RCCL's lazy connection setup before the
+    agreement is reached.)"""
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo / "conjugate-gradient_amd"))
+    import cgx as c
+    rp, col, val = c.laplacian3d(*SHAPE1)
+    b = np.random.default_rng(11).standard_normal(len(rp) - 1)
+    n = len(rp) - 1
+    rb, re_ = c.partition_rows(n, world, rank)
+    d = c.DistSolver(rank, world, rank, uid)
+    try:
+        d.set_matrix(n, rp[rb:re_ + 1] - rp[rb], col[rp[rb]:rp[re_]], val[rp[rb]:rp[re_]])
+        d.set_rhs(b[rb:re_])
+        d.set_alg(c.CGX_ALG_SR)
+        d.debug_refuse_capture(1)
+        its = d.run(3000, 1e-10)
+        np.save(os.path.join(out_dir, f"x_refused_{rank}.npy"), d.x())
+        np.save(os.path.join(out_dir, f"its_refused_{rank}.npy"), np.array([its, d.info()["graph"]]))
+    finally:
+        d.close()
+
+
+def test_two_rank_capture_refusal_goes_eager_together(tmp_path):
+    """VERDICT r05 #3 over real peers: graph or eager is one decision of all
+    ranks (ensure_graphs' MIN / MAX all-reduce of the capture results)."""
+    if cgx.lib().cgx_device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+    world = 2
+    uid = cgx.dist_unique_id()
+    mp.start_processes(_worker_refuse, args=(world, uid, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    its_l, xs_l = _local("sr", "auto", world, SHAPE1)
+    for rank in range(world):
+        its, graph = np.load(tmp_path / f"its_refused_{rank}.npy")
+        assert its == its_l and graph == -1
+        x = np.load(tmp_path / f"x_refused_{rank}.npy")
+        assert np.array_equal(x.view(np.uint64), xs_l[rank].view(np.uint64))
