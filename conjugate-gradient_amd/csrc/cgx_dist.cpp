@@ -431,7 +431,9 @@ int build_inplace(cgx_dist *d, int n_loc, int nnz, const int *rp, const int *col
   const int g_hi = d->n_ghost - nb;
   const int rc = d->Ai.upload<double>(n_loc, n_loc + g_hi, nnz, rp, ci.data(), val,
                                       CGX_LAYOUT_DIA, false, nullptr, -nb, true);
-  if (rc || d->Ai.layout != L_DIA || d->Ai.mq == 0) {
+  // (a near-only plan, DevMatrix::mfar 0, is the single GPU's: ranks whose
+  // slabs have no far diagonals keep the two-launch step)
+  if (rc || d->Ai.layout != L_DIA || d->Ai.mq == 0 || !d->Ai.mfar) {
     d->Ai.release();
     set_error("%s", "");
     return 0;

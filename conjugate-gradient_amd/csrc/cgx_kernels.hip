@@ -1662,6 +1662,10 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   CR cw, cwn{};
   VS vc, vn;
   const bool has_steps = m0 < m1;
+  // a near-only plan (DevMatrix::mfar 0: every diagonal within the halo):
+  // no step reads its neighbours' windows, so the segment skips window
+  // m0 - 1 and never prefetches window m1 past its end
+  const bool nearonly = (a.near & ((1u << a.ndiag) - 1u)) == ((1u << a.ndiag) - 1u);
   // FOLD: the segment's prologue loads windows m0 - 1, m0 and m0 + 1 at
   // once, before the scalar step (one memory round trip under it, not three
   // after it: each store waits only for its own set, vector loads retiring
@@ -1673,7 +1677,7 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   if constexpr (FOLD) {
     if (has_steps) {
       codes_at(m0, cw, vc);
-      load_win_to(m0 - 1, r1, p1, s1, true);
+      if (!nearonly) load_win_to(m0 - 1, r1, p1, s1, true);
       load_win_to(m0, r2, p2, s2, true);
       load_win_to(m0 + 1, wr, wp, wsv, true);
     }
@@ -1788,16 +1792,19 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   if constexpr (!FOLD) codes_at(m0, cw, vc);
   if (xup) load_x(m0, xc);
   if constexpr (FOLD) {
-    store_win_from(m0 - 1, r1, p1, s1);
+    if (!nearonly) store_win_from(m0 - 1, r1, p1, s1);
     store_win_from(m0, r2, p2, s2);
   } else {
-    load_win(m0 - 1);
-    store_win(m0 - 1);
+    if (!nearonly) {
+      load_win(m0 - 1);
+      store_win(m0 - 1);
+    }
     load_win(m0);
     store_win(m0);
     load_win(m0 + 1);
   }
   if (t < a.ndiag * 16) lv[t] = tv;
+  const int mlast = nearonly ? max(m0, m1 - 1) : m1;  // the last window any step reads
   auto step = [&](int m, const CR &ccw, const VS &cvs, XOps &cx, CR &ncw, VS &nvs, XOps &nx) {
     store_win(m + 1);
     // depth 4's two more p operands of step m's rows: issued before this
@@ -1809,7 +1816,7 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
       qb = ld_pair(f.pb, rs);
     }
     codes_at(min(m + 1, m1 - 1), ncw, nvs);
-    load_win(min(m + 2, m1));  // in flight during step m
+    load_win(min(m + 2, mlast));  // in flight during step m
     if (xup && m + 1 < m1) load_x(m + 1, nx);
     __syncthreads();
     const int base = base_of(m), r = base + 2 * t;

@@ -515,7 +515,7 @@ void DevMatrix::release() {
   dev_free(&d_fpairs);
   dev_free(&d_mpos);
   n_fpairs = 0;
-  mq = mchains = mws = mlen = 0;
+  mq = mchains = mws = mlen = mfar = 0;
   msb = 1;
   order.clear();
   blk_row.clear();
@@ -1029,7 +1029,7 @@ int DevMatrix::padded_rows() const { return padded_rows_for(n); }
 // recomputed at a segment's ends at C3 / C4.
 int DevMatrix::plan_march() {
   dev_free(&d_mpos);
-  mq = mchains = mws = mlen = 0;
+  mq = mchains = mws = mlen = mfar = 0;
   msb = 1;
   if (layout != L_DIA || dia.cbytes > 4 || n == 0) return 0;
   int hl = 0, hr = 0, F = 0;
@@ -1046,8 +1046,32 @@ int DevMatrix::plan_march() {
     }
   }
   hl = (hl + 1) & ~1;  // as args()
-  if (F == 0) return 0;
   const int sb = hl + hr > kDiaSliceRows ? 2 : 1;
+  if (F == 0) {
+    // Near-only (round 6): every diagonal within the halo.  The one-launch SR
+    // step still runs as a "march" whose steps are Q slices apart and share
+    // nothing (no far diagonal reads the ring's other windows): chains of
+    // about 16 steps, Q a multiple of 4 (four-slice steps), one window per
+    // step plus one per segment.  One launch per iteration instead of the
+    // SpMV + k_update_sr pair (C2, 2-D 1000^2: 2,000-row halos, cache-resident)
+    const int ns = items();
+    const int wn = sb * kDiaSliceRows + hl + hr;
+    if ((wn + 2 * 256 * sb - 1) / (2 * 256 * sb) > (sb == 1 ? 5 : 3)) return 0;
+    const int Q = std::max(4, ((ns + 15) / 16 + 3) & ~3);
+    mq = Q;
+    msb = sb;
+    mchains = (Q + sb - 1) / sb;
+    mws = (wn + 3) & ~1;
+    mlen = std::max(1, (ns + Q - 1) / Q);
+    if (!order.empty()) {
+      std::vector<int> p((size_t)ns);
+      for (int i = 0; i < ns; ++i) p[(size_t)order[(size_t)i]] = i;
+      int rc;
+      if ((rc = dev_alloc(&d_mpos, p.size() * 4, &dev_bytes))) return rc;
+      CGX_HIP(hipMemcpy(d_mpos, p.data(), p.size() * 4, hipMemcpyHostToDevice));
+    }
+    return 0;
+  }
   auto fits = [&](long long q) {
     const long long e = F - q * kDiaSliceRows;
     if (q < 1) return false;
@@ -1067,6 +1091,7 @@ int DevMatrix::plan_march() {
   msb = sb;
   mchains = Q / sb;
   mws = (wn + 3) & ~1;
+  mfar = 1;
   const int steps = (ns + Q - 1) / Q;
   const int nseg = std::max(1, std::min(steps, (2048 + mchains / 2) / mchains));
   mlen = (steps + nseg - 1) / nseg;

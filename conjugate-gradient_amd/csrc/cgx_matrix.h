@@ -119,6 +119,11 @@ struct DevMatrix {
   // stride mws, mlen steps per segment (the default), d_mpos: slice ->
   // position in d_order (nullptr: natural order)
   int mq = 0, msb = 1, mchains = 0, mws = 0, mlen = 0;
+  // 1: the plan marches across far diagonals (+-F from the ring); 0 with mq >
+  // 0: a near-only plan (every diagonal within the window's halo: 2-D grids,
+  // small planes) -- steps mq slices apart share nothing, only the one-launch
+  // SR step (single GPU) runs it
+  int mfar = 0;
   int *d_mpos = nullptr;
   int plan_march();
   Items all_items() const { return Items{d_order, 0, items(), d_fpairs, n_fpairs}; }

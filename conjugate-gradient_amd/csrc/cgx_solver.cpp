@@ -182,6 +182,8 @@ bool fused(const cgx_solver *s) {
 // cgx_solver_set_march has not turned it off.
 int march_len(const cgx_solver *s) {
   if (!fused(s) || s->alg == CGX_ALG_CG1 || s->A.mq == 0 || s->march == 0) return 0;
+  // a near-only plan (DevMatrix::mfar 0) is the one-launch SR step's alone
+  if (!s->A.mfar && s->alg != CGX_ALG_SR) return 0;
   return s->march > 0 ? s->march : s->A.mlen;
 }
 

@@ -697,7 +697,10 @@ def test_sr_unfused_graph_and_bench():
 def test_sr_fuse_status():
     """cgx_info.fuse_status follows fused()'s SR rules -- SR
     ignores the Infinity Cache rule (a cache-resident system runs it) and
-    needs the march plan (NO_MARCH after set_march(0) or without a plan)."""
+    needs the march plan (NO_MARCH after set_march(0) or without a plan).
+    Round 6: a matrix whose diagonals all lie within the window's halo (a
+    2-D grid) has a near-only plan and runs the one-launch step; one whose
+    far diagonals are two distances (1,500 and 3,000) has none."""
     rp, col, val = H.laplacian3d(64, 64, 10)
     with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
         s.set_matrix(rp, col, val)
@@ -711,6 +714,13 @@ def test_sr_fuse_status():
     rp, col, val = H.laplacian2d(300, 200)
     with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
         s.set_matrix(rp, col, val)
+        i = s.info()
+        assert i["fused"] == 1 and i["fuse_status"] == cgx.CGX_FUSE_STATUS_RUNS
+        assert i["fuse_march"] > 0
+    rp, col, val, _ = band_sym_rhs(20000, [1, 1500, 3000], 8)
+    with cgx.Solver(0, alg=cgx.CGX_ALG_SR) as s:
+        s.set_matrix(rp, col, val)
+        assert s.info()["layout_name"] == "dia"
         assert s.info()["fuse_status"] == cgx.CGX_FUSE_STATUS_NO_MARCH
 
 
@@ -890,6 +900,13 @@ def march_cases():
     yield "band_1_200_1100", band_sym_rhs(20000, [1, 200, 1100], 8), False  # 2 * 512 + 76
 
 
+def sr_march_cases():
+    # the one-launch SR step also runs near-only plans (round 6): a 2-D grid
+    # whose +-1000 diagonals lie within the window's halo, C2's shape in 60 rows
+    yield from march_cases()
+    yield "lap2d_1000x60", (*H.laplacian2d(1000, 60), None), False
+
+
 @pytest.mark.parametrize("case", list(march_cases()), ids=lambda c: c[0])
 def test_fused_march_bit_identical_to_unfused(case):
     """The plane march of the fused step (k_spmv_dia_m: a workgroup walks
@@ -933,7 +950,7 @@ def test_fused_march_bit_identical_to_unfused(case):
                 assert H.same_bits_or_both_nan(h0, h1), (march, j)
 
 
-@pytest.mark.parametrize("case", list(march_cases()), ids=lambda c: c[0])
+@pytest.mark.parametrize("case", list(sr_march_cases()), ids=lambda c: c[0])
 def test_sr_single_launch_vs_oracle(case):
     """CGX_ALG_SR on one GPU (k_sr1_dia_m: the r update of the previous
     iteration, the p update and s = A p in ONE plane-marched launch, one
@@ -995,12 +1012,13 @@ def test_dia_v_general_coefficients(shape):
     (k_sr1_dia_m<..., DV>) at every segment shape as
     test_sr_single_launch_vs_oracle: within 1e-10 of oracle_solve_sr at
     fixed maxit, within 1e-9 of both oracles at a tolerance stop, graph and
-    eager replays bit-identical.  Without a plane-march plan (a plane of <=
-    1,024 rows has no far diagonal; 40 x 30 = 1,200 rows lie 176 rows off
-    two slices, outside the 40-row halo) SR runs unfused (k_spmv_dia's
-    (p.s, s.s) pairs + k_update_sr) to the same bars."""
+    eager replays bit-identical.  A plane of <= 1,024 rows has no far
+    diagonal: 13 x 11 runs the near-only plan (round 6); without any plan
+    (40 x 30 = 1,200 rows lie 176 rows off two slices, outside the 40-row
+    halo) SR runs unfused (k_spmv_dia's (p.s, s.s) pairs + k_update_sr) to
+    the same bars."""
     rp, col, val = cgx.varcoef3d(*shape, seed=11)
-    march_plan = shape[:2] in ((32, 48), (64, 48))  # planes of 3 and 6 slices
+    march_plan = shape[:2] in ((32, 48), (64, 48), (13, 11))  # 3 and 6 slices; near-only
     n = len(rp) - 1
     b = np.random.default_rng(23).standard_normal(n)
     with cgx.Solver(0, fused=True) as s:
