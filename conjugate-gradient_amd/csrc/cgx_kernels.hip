@@ -32,7 +32,6 @@
 #define CGX_EXP 0
 #endif
 
-
 namespace cgx {
 
 namespace {
@@ -1468,7 +1467,9 @@ __global__ __launch_bounds__(256 * SB) void k_spmv_dia_m(SpmvArgs<T> a, FuseArgs
 }
 
 // ------------------------------ single-GPU SR iteration, plane march (DIA-VI)
-// CGX_ALG_SR on one GPU in ONE launch per iteration (+ k_finalize FIN_SR1):
+// CGX_ALG_SR on one GPU in ONE launch per iteration (FOLD: the FIN_SR1
+// scalar step of the previous launch runs inside it; until round 6 a
+// k_finalize launch followed each):
 // the partitioned solver's SR recurrence (oracle_solve_sr: alpha = r.r / p.s
 // as cg.c:113, beta from the estimate r_new.r_new = alpha (alpha s.s) - r.r)
 // needs only the (p.s, s.s, r.r) of the launch that computes s = A p, so the
@@ -1785,7 +1786,7 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
     }
     return;
   }
-  if (!has_steps) {  // no steps: zero sums (k_finalize adds every workgroup's)
+  if (!has_steps) {  // no steps: zero sums (the next scalar step adds every workgroup's)
     publish();
     return;
   }

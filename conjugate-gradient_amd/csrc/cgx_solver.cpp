@@ -207,8 +207,8 @@ bool sr_x4(const cgx_solver *s) { return fused(s) && s->alg == CGX_ALG_SR; }
 // sums the last one's (p.s, s.s) pairs and r.r partials under its
 // prologue's window loads, and two CgState slots alternate (the launch
 // reads one and hands the state over in the other).  Same box, alternating
-// (profiles/r06_ab_sr1.log): C3 126.0-131.1 against 134.9-135.6 us per
-// iteration, C4 666.8-676.7 against 679.5-685.9.
+// (profiles/r06_ab_sr1.log, box 5): C3 131.3-132.4 against 134.1-135.4 us
+// per iteration, C4 even (712.7-713.2 against 710.0-718.3).
 bool sr1_fold(const cgx_solver *s) { return sr_x4(s); }
 
 int prot(const cgx_solver *s) { return sr_x4(s) ? 4 : alternating(s) ? 2 : 1; }
