@@ -105,6 +105,11 @@ def parse_args(argv=None):
     ap.add_argument("--dist-rehearsal", action="store_true",
                     help="at one rank (under torch.distributed.run --nproc-per-node 1): run the "
                          "N > 1 path -- parity gate, RCCL communicator, C4 -- on one GPU")
+    ap.add_argument("--ranks-share-gpu", action="store_true",
+                    help="rehearsal on a box with fewer GPUs than ranks: every rank on GPU 0, "
+                         "each with a host id of its own (NCCL_HOSTID) so that RCCL connects "
+                         "them over its socket transport on the loopback interface -- the N > 1 "
+                         "path's RCCL calls between real peers, not an xGMI or scaling number")
     ap.add_argument("--no-legs", action="store_true",
                     help="N = 1: only the headline solve (no CSR/DC/stencil/C3/e2e legs)")
     ap.add_argument("--layout", default="auto", choices=["auto", "csr", "dc", "dia"],
@@ -871,11 +876,11 @@ def gather_x(x_local, n_global, world, rank):
     import cgx
     sizes = [cgx.partition_rows(n_global, world, q) for q in range(world)]
     m = max(e - b for b, e in sizes)
-    t = torch.zeros(m, dtype=torch.float64, device="cuda")
-    t[:len(x_local)] = torch.from_numpy(x_local).cuda()
+    t = torch.zeros(m, dtype=torch.float64)  # host tensors: the gloo group
+    t[:len(x_local)] = torch.from_numpy(x_local)
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
-    return np.concatenate([parts[q][:e - b].cpu().numpy() for q, (b, e) in enumerate(sizes)])
+    return np.concatenate([parts[q][:e - b].numpy() for q, (b, e) in enumerate(sizes)])
 
 
 def parity_gate(world, rank, local_rank, uid, tol=1e-10):
@@ -982,7 +987,12 @@ def dist_line(args, wl, world, m):
         upload_ms=round(m["upload_ms"], 1), iter_bytes_rank0=int(info["iter_bytes"]),
         roofline=m["roofline"], phases=m["phases"], cpu_baseline=m["cpu"], parity=parity,
         parity_ok=bool(parity.get("ok")),
-        gate_failed=[k for k, v in parity.items() if isinstance(v, dict) and not v.get("ok")])
+        gate_failed=[k for k, v in parity.items() if isinstance(v, dict) and not v.get("ok")],
+        runtime=dict(m["runtime"], orchestration="torch.distributed gloo (host); data path: "
+                                                 "libcgx's RCCL communicator"),
+        **(dict(rehearsal="--ranks-share-gpu: every rank on GPU 0, RCCL over loopback sockets "
+                          "-- a correctness rehearsal of the N > 1 path, not a scaling number")
+           if args.ranks_share_gpu else {}))
 
 
 def dist_traffic_key(alg, info):
@@ -995,19 +1005,36 @@ def dist_traffic_key(alg, info):
 
 
 def run_dist(args, wl_name, world, rank, local_rank):
+    """One rank.  The solver's data path is libcgx's RCCL communicator (the
+    halos, the all-reduces); torch.distributed only orchestrates (the ids,
+    barriers, max over ranks, the parity gate's x) over a host-side gloo
+    group, and this process never touches torch's GPU runtime: libcgx is
+    loaded BEFORE torch, so it binds the ROCm it was built against
+    (/opt/rocm: HIP and RCCL of the same release).  Loaded after `import
+    torch`, it would bind the older libamdhip64.so.7 / librccl.so.1 copies
+    PyTorch bundles (same sonames), whose hipStreamEndCapture crashed on the
+    ranks' captured halo (tools/rccl_pair_probe.py, profiles/r06_rccl_pair.log)."""
     import numpy as np
-    import torch
-    import torch.distributed as dist
     import cgx
 
     wl = WORKLOADS[wl_name]
     if wl["kind"] == "rand":
         raise SystemExit("bench: C5 (random SPD) is a single-GPU configuration (BASELINE.json)")
-    torch.cuda.set_device(local_rank)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if args.ranks_share_gpu:
+        # before the first RCCL call of this process (RCCL reads its
+        # environment once): a host of its own per rank, loopback sockets
+        os.environ.update(NCCL_HOSTID=f"cgx-rank{rank}", NCCL_SOCKET_IFNAME="lo",
+                          NCCL_IB_DISABLE="1")
+        local_rank = 0
+    cgx.lib()
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # one node: the ranks meet on loopback
+    dist.init_process_group("gloo")
+    runtime = cgx.runtime_versions()
 
     def allmax(v):
-        t = torch.tensor([float(v)], device="cuda", dtype=torch.float64)
+        t = torch.tensor([float(v)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -1082,11 +1109,11 @@ def run_dist(args, wl_name, world, rank, local_rank):
     if ok[0]:
         # ---- timed region: exactly K steps, barrier + sync on both sides
         s.bench_prepare(args.warmup)
-        torch.cuda.synchronize()
+        cgx.device_synchronize(local_rank)
         dist.barrier()
         t0 = time.perf_counter()
         dev_ms = s.bench_run(args.steps)[0]
-        torch.cuda.synchronize()
+        cgx.device_synchronize(local_rank)
         dist.barrier()
         wall = allmax(time.perf_counter() - t0)
         ms_per_step = 1e3 * wall / args.steps
@@ -1136,7 +1163,7 @@ def run_dist(args, wl_name, world, rank, local_rank):
         out = dist_line(args, wl, world, dict(
             value=value, ms_per_step=ms_per_step, dev=dev, n_global=sysm["n_global"], info=info,
             alg=alg, trial=trial, refused=refused, halo=halo, upload_ms=upload_ms,
-            roofline=roofline, phases=phase_out, cpu=cpu, parity=parity))
+            roofline=roofline, phases=phase_out, cpu=cpu, parity=parity, runtime=runtime))
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
     if not ok[0]:

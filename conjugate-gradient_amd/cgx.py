@@ -100,6 +100,8 @@ _SIGS = {
     "cgx_ops_last_timing": (ctypes.c_int, [_vp]),
     "cgx_last_error": (ctypes.c_char_p, []),
     "cgx_device_count": (ctypes.c_int, []),
+    "cgx_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
+    "cgx_runtime_versions": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)] * 3),
     "cgx_stream_bench": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "cgx_solver_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
@@ -650,6 +652,19 @@ class Partition:
 
 
 # ---------------------------------------------------------- multi-GPU solver
+
+def device_synchronize(device=0):
+    check(lib().cgx_device_synchronize(device), "device_synchronize")
+
+
+def runtime_versions():
+    """(HIP runtime, HIP compiled against, RCCL) versions libcgx runs with
+    (cgx_runtime_versions): `import torch` before libcgx binds it to the
+    ROCm copies PyTorch bundles."""
+    v = [ctypes.c_int(0) for _ in range(3)]
+    check(lib().cgx_runtime_versions(*[ctypes.byref(x) for x in v]), "runtime_versions")
+    return dict(hip_runtime=v[0].value, hip_compiled=v[1].value, rccl=v[2].value)
+
 
 def dist_unique_id():
     buf = ctypes.create_string_buffer(128)

@@ -1226,9 +1226,27 @@ int run_phases_eager(Group *g, bool init, long long iters) {
 // when it was refused after RCCL calls were recorded.  Every outcome comes
 // back as one of these (never as an early error return), so every rank
 // reaches ensure_graphs' agreement.
+// CGX_DIST_TRACE=1: the capture / replay steps on stderr (diagnosis of a
+// capture that fails inside the HIP runtime or RCCL)
+bool dist_trace() {
+  static const bool on = [] {
+    const char *e = getenv("CGX_DIST_TRACE");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+#define DIST_TRACE(...)                      \
+  do {                                       \
+    if (dist_trace()) {                      \
+      fprintf(stderr, "cgx_dist: " __VA_ARGS__); \
+      fflush(stderr);                        \
+    }                                        \
+  } while (0)
+
 int capture(cgx_dist *d, Group *g, int nit, int parity, hipGraphExec_t *out) {
   hipGraph_t gr = nullptr;
   *out = nullptr;
+  DIST_TRACE("rank %d capture of %d iterations, parity %d\n", d->rank, nit, parity);
   if (hipSetDevice(d->device) != hipSuccess ||
       hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     (void)hipGetLastError();
@@ -1239,12 +1257,15 @@ int capture(cgx_dist *d, Group *g, int nit, int parity, hipGraphExec_t *out) {
   d->pbuf = parity;
   // cgx_dist_debug_refuse_capture(1): refused before the first phase
   const int rc = d->dbg_refuse == 1 ? CGX_ENODEV : run_phases_eager(g, false, nit);
+  DIST_TRACE("rank %d phases recorded (rc %d)\n", d->rank, rc);
   // (modes 2 and 3: refused after the phases recorded their RCCL calls)
   const hipError_t e = hipStreamEndCapture(d->st, &gr);
+  DIST_TRACE("rank %d end capture: %s\n", d->rank, hipGetErrorString(e));
   d->pbuf = saved;
   hipError_t ei = hipSuccess;
   const bool refused = rc || e != hipSuccess || d->dbg_refuse >= 2;
   if (!refused) ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
+  DIST_TRACE("rank %d instantiate: %s\n", d->rank, hipGetErrorString(ei));
   if (gr) (void)hipGraphDestroy(gr);
   if (refused || ei != hipSuccess) {
     if (*out) (void)hipGraphExecDestroy(*out);
@@ -1312,6 +1333,7 @@ int ensure_graphs(Group *g) {
   }
   d->gexec_alg = key;
   d->graph_state = 1;
+  DIST_TRACE("rank %d graphs agreed\n", d->rank);
   return 0;
 }
 
@@ -1328,6 +1350,7 @@ int run_phases(Group *g, bool init, long long iters) {
       // the graph captured at the current buffer rotation; a batch
       // advances it by graph_batch, one iteration by one
       const int nr = sr1(d) ? 4 : fz(d) || fz1(d) ? 2 : 1;
+      DIST_TRACE("rank %d replay of %lld iterations\n", d->rank, iters);
       for (; iters >= d->graph_batch; iters -= d->graph_batch) {
         CGX_HIP(hipGraphLaunch(d->gexec[d->pbuf % nr], d->st));
         d->pbuf = (d->pbuf + d->graph_batch) % nr;
@@ -1550,6 +1573,19 @@ void destroy_one(cgx_dist *d) {
 // ------------------------------------------------------------------ C ABI
 
 extern "C" {
+
+int cgx_runtime_versions(int *hip_runtime, int *hip_compiled, int *rccl) {
+  if (hip_runtime) {
+    *hip_runtime = 0;
+    CGX_HIP(hipRuntimeGetVersion(hip_runtime));
+  }
+  if (hip_compiled) *hip_compiled = HIP_VERSION;
+  if (rccl) {
+    *rccl = 0;
+    CGX_NCCL(ncclGetVersion(rccl));
+  }
+  return 0;
+}
 
 int cgx_dist_unique_id(unsigned char id[128]) {
   if (!id) return CGX_EINVAL;

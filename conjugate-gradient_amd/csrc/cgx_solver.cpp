@@ -785,6 +785,14 @@ int cgx_device_count(void) {
   return cnt;
 }
 
+int cgx_device_synchronize(int device) {
+  int rc = check_device(device, nullptr);
+  if (rc) return rc;
+  CGX_HIP(hipSetDevice(device));
+  CGX_HIP(hipDeviceSynchronize());
+  return 0;
+}
+
 int cgx_stream_bench(int device, int kind, long long n, int reps, double *gbs) {
   int nr = 0, nw = 0;
   const bool rw = stream_rw_arrays(kind, &nr, &nw) == 0;

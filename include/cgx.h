@@ -91,6 +91,14 @@ int cgx_ops_counters(long long *uploads, long long *reuses);
 
 const char *cgx_last_error(void);
 int cgx_device_count(void);
+/* Waits for all work on `device` (the solver's streams included). */
+int cgx_device_synchronize(int device);
+/* The HIP runtime the library runs on (hipRuntimeGetVersion), the HIP it
+ * was compiled against (HIP_VERSION) and the RCCL it calls (ncclGetVersion).
+ * A process that loads an older ROCm's libamdhip64.so.7 / librccl.so.1
+ * before this library (PyTorch's bundled copies, `import torch` first) binds
+ * the library to those: report, so a caller can tell. */
+int cgx_runtime_versions(int *hip_runtime, int *hip_compiled, int *rccl);
 
 /* On-box HBM ceilings (SURVEY.md 8d "STREAM-triad ceiling"), fp64 arrays of
  * n elements on `device`, best of `reps` timed launches, 16 B per lane:

@@ -133,12 +133,20 @@ def test_dist_line_schema():
                 traffic=5.0e8, traffic_source="profiles/pmc_c4n8_sr1.json", traffic_ratio=1.02)
     m = dict(value=7000.0, ms_per_step=0.1428, dev=0.14, n_global=64_000_000, info=info,
              alg="sr", trial={"sr": 0.14}, refused={}, halo=2.56e6, upload_ms=900.0,
-             roofline=roof, phases=phases, cpu=cpu, parity=parity)
+             roofline=roof, phases=phases, cpu=cpu, parity=parity,
+             runtime=dict(hip_runtime=70226015, hip_compiled=70226015, rccl=22707))
     line = bench.dist_line(args, bench.WORKLOADS["c4"], 8, m)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
-              "roofline", "phases", "cpu_baseline", "parity", "parity_ok", "gate_failed"):
+              "roofline", "phases", "cpu_baseline", "parity", "parity_ok", "gate_failed",
+              "runtime"):
         assert k in line, k
+    assert "rehearsal" not in line
+    assert line["runtime"]["hip_runtime"] == line["runtime"]["hip_compiled"]
+    # --ranks-share-gpu labels its line a rehearsal
+    shared = bench.dist_line(bench.parse_args(["--gpus", "2", "--ranks-share-gpu"]),
+                             bench.WORKLOADS["c4"], 2, m)
+    assert "not a scaling number" in shared["rehearsal"]
     assert line["n_gpus"] == 8 and line["value"] == 7000.0
     assert line["cpu_baseline"]["cores"] == 1 and line["roofline"]["traffic"] == 5.0e8
     assert set(line["phases"]) >= {"first_launch", "halo_wait_gap", "second_launch", "tail",
