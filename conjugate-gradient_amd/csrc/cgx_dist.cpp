@@ -1219,13 +1219,6 @@ int run_phases_eager(Group *g, bool init, long long iters) {
   return rc;
 }
 
-// Capture `nit` iterations (kernels, halo send/recv on the comm stream
-// forked and joined by events, all-reduces) into *out, without running them.
-// Returns 1 when captured, 0 when the capture was refused before any RCCL
-// call was recorded (nothing reached the communicator: eager is safe), -1
-// when it was refused after RCCL calls were recorded.  Every outcome comes
-// back as one of these (never as an early error return), so every rank
-// reaches ensure_graphs' agreement.
 // CGX_DIST_TRACE=1: the capture / replay steps on stderr (diagnosis of a
 // capture that fails inside the HIP runtime or RCCL)
 bool dist_trace() {
@@ -1235,14 +1228,21 @@ bool dist_trace() {
   }();
   return on;
 }
-#define DIST_TRACE(...)                      \
-  do {                                       \
-    if (dist_trace()) {                      \
+#define DIST_TRACE(...)                          \
+  do {                                           \
+    if (dist_trace()) {                          \
       fprintf(stderr, "cgx_dist: " __VA_ARGS__); \
-      fflush(stderr);                        \
-    }                                        \
+      fflush(stderr);                            \
+    }                                            \
   } while (0)
 
+// Capture `nit` iterations (kernels, halo send/recv on the comm stream
+// forked and joined by events, all-reduces) into *out, without running them.
+// Returns 1 when captured, 0 when the capture was refused before any RCCL
+// call was recorded (nothing reached the communicator: eager is safe), -1
+// when it was refused after RCCL calls were recorded.  Every outcome comes
+// back as one of these (never as an early error return), so every rank
+// reaches ensure_graphs' agreement.
 int capture(cgx_dist *d, Group *g, int nit, int parity, hipGraphExec_t *out) {
   hipGraph_t gr = nullptr;
   *out = nullptr;
