@@ -167,3 +167,18 @@ def test_no_gbs_field_exceeds_peak():
     marked resident."""
     src = (REPO / "bench.py").read_text()
     assert "csr_equivalent_gbs" not in src and "csr_basis_gbs" not in src
+
+
+def test_ranks_load_libcgx_before_torch():
+    """Round 6: a rank process binds libcgx to the ROCm it was built against
+    only if libcgx is loaded before `import torch` (PyTorch bundles older
+    libamdhip64.so.7 / librccl.so.1 under the same sonames; with those the
+    ranks' first capture with real peers crashed, profiles/r06_rccl_pair.log),
+    and the rank's torch.distributed group is host-side gloo (no torch GPU
+    runtime in the rank)."""
+    import inspect
+    src = inspect.getsource(bench.run_dist)
+    assert src.index("cgx.lib()") < src.index("import torch")
+    assert 'init_process_group("gloo")' in src and "torch.cuda" not in src
+    g = inspect.getsource(bench.gather_x)
+    assert "cuda" not in g
