@@ -27,6 +27,7 @@ SHAPE = (40, 30, 24)   # plane-aligned slabs: the fused HS step applies
 SHAPE1 = (32, 48, 24)  # planes 3 slices apart: SR runs the one-launch march step
 CASES = [("hs", True, SHAPE), ("hs", False, SHAPE), ("sr", "auto", SHAPE), ("cg1", False, SHAPE),
          ("sr", "auto", SHAPE1)]
+C4_ITERS = 50  # mode "c4": fixed iterations of the row-partitioned 400^3 system
 
 
 def _cgx():
@@ -122,6 +123,29 @@ def child(rank, world, out, mode, share):
     out = Path(out)
     dev = 0 if share else rank
     uid, uid1 = _uids(cgx, rank, out)
+    if mode == "c4":
+        # C4 (400^3) row-partitioned over the ranks: SR (the one-launch step)
+        # and HS, 50 iterations each, b = 1
+        nx = 400
+        n = nx ** 3
+        rb, re_ = cgx.partition_rows(n, world, rank)
+        rp, col, val = cgx.laplacian3d(nx, nx, nx, rb, re_)
+        d = cgx.DistSolver(dev, world, rank, uid)
+        try:
+            d.set_matrix(n, rp, col, val)
+            d.set_rhs(np.ones(re_ - rb))
+            for alg in ("sr", "hs"):
+                d.set_alg(algs(cgx)[alg])
+                its = d.run(C4_ITERS, 0.0)
+                i = d.info()
+                np.save(out / f"x_c4_{alg}_{rank}.npy", d.x())
+                np.save(out / f"its_c4_{alg}_{rank}.npy",
+                        np.array([its, i["fused"], i["graph"], i["march"], rb, re_]))
+                print(f"rank {rank}: c4 {alg} its {its} graph {i['graph']} march {i['march']}",
+                      flush=True)
+        finally:
+            d.close()
+        return 0
     if mode == "versions":
         v = cgx.runtime_versions()
         np.save(out / f"versions_{rank}.npy", np.array([v["hip_runtime"], v["hip_compiled"],
