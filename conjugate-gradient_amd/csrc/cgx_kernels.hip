@@ -1670,17 +1670,23 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   // FOLD: the segment's prologue loads windows m0 - 1, m0 and m0 + 1 at
   // once, before the scalar step (one memory round trip under it, not three
   // after it: each store waits only for its own set, vector loads retiring
-  // in order; m0 + 1 goes into the loop's set).  Without FOLD the windows
+  // in order; m0 + 1 goes into the loop's set; four-slice steps: m0 + 1
+  // after it, P3LATE).  Without FOLD the windows
   // load one after the other, after the scalars (the ranks: the three at
   // once, with no scalar step to hide, measured 2-4 us longer per launch on
   // C4's 8 M-row slab, profiles/r06_ab_sr1.log).
   WinSet r1, p1, s1, r2, p2, s2;
+  // the four-slice step loads window m0 + 1 after the scalar step instead:
+  // the three sets at once left its 1,024-thread kernel 4 VGPRs of spill
+  // (C3 124.2-125.6 -> 121.4-122.8 us per iteration, C4 even; box 8,
+  // profiles/r06_ab_p3late.log)
+  constexpr bool P3LATE = SB == 4;
   if constexpr (FOLD) {
     if (has_steps) {
       codes_at(m0, cw, vc);
       if (!nearonly) load_win_to(m0 - 1, r1, p1, s1, true);
       load_win_to(m0, r2, p2, s2, true);
-      load_win_to(m0 + 1, wr, wp, wsv, true);
+      if (!P3LATE) load_win_to(m0 + 1, wr, wp, wsv, true);
     }
     // the scalar step of the last launch (FIN_SR1's), run here on its (p.s,
     // s.s) pairs and r.r partials (wave 0: lane l sums entries l, l + 64,
@@ -1795,6 +1801,7 @@ void k_sr1_dia_m(SpmvArgs<T> a, Sr1Args<T> f) {
   if constexpr (FOLD) {
     if (!nearonly) store_win_from(m0 - 1, r1, p1, s1);
     store_win_from(m0, r2, p2, s2);
+    if (P3LATE) load_win(m0 + 1);
   } else {
     if (!nearonly) {
       load_win(m0 - 1);
